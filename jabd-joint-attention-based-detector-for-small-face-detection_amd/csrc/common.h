@@ -1,0 +1,74 @@
+// Shared helpers for libjabd: status/error plumbing and launch checks.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/jabd.h"
+
+namespace jabd {
+
+// Thread-local last-error text (DataParallel threads / DDP ranks call
+// concurrently; each sees only its own message).
+void set_error(const char* fmt, ...);
+
+inline hipStream_t as_stream(jabd_stream_t s) {
+  return reinterpret_cast<hipStream_t>(s);
+}
+
+inline int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return JABD_EHIP;
+  }
+  return JABD_OK;
+}
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+// Bump allocator over a caller-provided workspace.
+struct Carve {
+  char* base;
+  size_t cap;
+  size_t used = 0;
+  Carve(void* p, size_t c) : base(static_cast<char*>(p)), cap(c) {}
+  template <typename T>
+  T* take(size_t count) {
+    size_t off = align_up(used);
+    used = off + align_up(count * sizeof(T));
+    return reinterpret_cast<T*>(base + off);
+  }
+  bool ok() const { return used <= cap; }
+};
+
+// Size-only twin of Carve, used by the *_workspace_size queries so the
+// query and the carve can never disagree.
+struct Sizer {
+  size_t used = 0;
+  template <typename T>
+  void take(size_t count) {
+    used = align_up(used) + align_up(count * sizeof(T));
+  }
+};
+
+}  // namespace jabd
+
+#define JABD_REQUIRE(cond, ...)      \
+  do {                               \
+    if (!(cond)) {                   \
+      ::jabd::set_error(__VA_ARGS__); \
+      return JABD_EINVAL;            \
+    }                                \
+  } while (0)
+
+#define JABD_HIP(call)                                                   \
+  do {                                                                   \
+    hipError_t e_ = (call);                                              \
+    if (e_ != hipSuccess) {                                              \
+      ::jabd::set_error("%s: %s", #call, hipGetErrorString(e_));        \
+      return JABD_EHIP;                                                  \
+    }                                                                    \
+  } while (0)

@@ -1,0 +1,202 @@
+"""Tensor-level wrappers over the libjabd C-ABI (box ops, NMS, match, loss).
+
+Each wrapper validates device/dtype/shape, allocates outputs and workspace
+through torch's caching allocator, and launches on torch's current HIP
+stream.  CPU tensors are rejected: there is no CPU fallback on the product
+path (the CPU restatement lives in oracle/ and is test-only).
+"""
+import math
+
+import torch
+
+from ._lib import call, c_size, lib
+import ctypes
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _dev(name, t, dtype=torch.float32):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a tensor")
+    if not t.is_cuda:
+        raise RuntimeError(f"{name}: the JABD HIP path needs a GPU tensor (got {t.device}); "
+                           "there is no CPU fallback")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    return t.contiguous()
+
+
+def _ws(nbytes, device):
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+def _size_query(fn, *args):
+    out = c_size(0)
+    call(fn, *args, ctypes.byref(out))
+    return out.value
+
+
+# --------------------------------------------------------------------------- decode
+def decode(loc, priors, variances):
+    """utils/utils_bbox.py:29-34 — loc [A,4] or [B,A,4] -> corner boxes."""
+    loc = _dev("decode.loc", loc)
+    priors = _dev("decode.priors", priors)
+    A = priors.shape[0]
+    if loc.shape[-2:] != (A, 4):
+        raise ValueError(f"decode: loc {tuple(loc.shape)} vs priors {tuple(priors.shape)}")
+    B = loc.numel() // (A * 4) if A else 0
+    out = torch.empty_like(loc)
+    call("jabd_decode_f32", _p(loc), _p(priors), B, A, float(variances[0]), float(variances[1]),
+         _p(out), _stream())
+    return out
+
+
+def decode_landm(pre, priors, variances):
+    """utils/utils_bbox.py:39-46 — pre [A,10] or [B,A,10]."""
+    pre = _dev("decode_landm.pre", pre)
+    priors = _dev("decode_landm.priors", priors)
+    A = priors.shape[0]
+    if pre.shape[-2:] != (A, 10):
+        raise ValueError(f"decode_landm: pre {tuple(pre.shape)} vs priors {tuple(priors.shape)}")
+    B = pre.numel() // (A * 10) if A else 0
+    out = torch.empty_like(pre)
+    call("jabd_decode_landm_f32", _p(pre), _p(priors), B, A, float(variances[0]), _p(out),
+         _stream())
+    return out
+
+
+# --------------------------------------------------------------------------- NMS
+def batched_nms(boxes, scores, iou_threshold, score_threshold=-math.inf, n_valid=None):
+    """Independent greedy NMS per image.
+
+    boxes [B,N,4] (or a [B,N,>=5] row tensor whose first 4 columns are boxes),
+    scores [B,N].  Returns (keep [B,N] int64, n_keep [B] int64), both on the
+    device; keep[b,:n_keep[b]] are row indices in decreasing-score order.
+    """
+    if boxes.dim() != 3 or boxes.shape[-1] < 4:
+        raise ValueError(f"batched_nms: boxes must be [B,N,>=4], got {tuple(boxes.shape)}")
+    boxes = _dev("nms.boxes", boxes)
+    scores = _dev("nms.scores", scores)
+    B, N = boxes.shape[0], boxes.shape[1]
+    if scores.shape != (B, N):
+        raise ValueError(f"batched_nms: scores {tuple(scores.shape)} != {(B, N)}")
+    dev = boxes.device
+    keep = torch.empty((B, N), dtype=torch.int64, device=dev)
+    n_keep = torch.zeros((B,), dtype=torch.int64, device=dev)
+    if n_valid is not None:
+        n_valid = _dev("nms.n_valid", n_valid, torch.int64)
+    ws = _ws(_size_query("jabd_nms_workspace_size", B, N), dev)
+    C = boxes.shape[-1]
+    call("jabd_batched_nms_f32", _p(boxes), C, N * C, _p(scores), 1, N, _p(n_valid), B, N,
+         float(iou_threshold), float(score_threshold), _p(keep), _p(n_keep), _p(ws),
+         ws.numel(), _stream())
+    return keep, n_keep
+
+
+def nms(boxes, scores, iou_threshold):
+    """torchvision.ops.nms(boxes[N,4], scores[N], iou_threshold) -> int64[K].
+
+    Returns a device tensor; reading K synchronises the stream once.
+    """
+    if boxes.dim() != 2 or boxes.shape[-1] != 4:
+        raise ValueError(f"nms: boxes must be [N,4], got {tuple(boxes.shape)}")
+    keep, n_keep = batched_nms(boxes.unsqueeze(0), scores.unsqueeze(0), iou_threshold)
+    return keep[0, : int(n_keep[0].item())]
+
+
+def detect(loc, conf, landm, priors, variances, conf_threshold=0.5, nms_threshold=0.3):
+    """predict.py:162-181 on device for a batch: decode + filter + NMS.
+
+    loc [B,A,4], conf [B,A,2] (eval softmax), landm [B,A,10].
+    Returns (rows [B,A,15], n_keep [B]); rows[b,:n_keep[b]] are the kept
+    detections (x1,y1,x2,y2,score,landmarks) in NMS order.
+    """
+    loc = _dev("detect.loc", loc)
+    conf = _dev("detect.conf", conf)
+    landm = _dev("detect.landm", landm)
+    priors = _dev("detect.priors", priors)
+    B, A = loc.shape[0], loc.shape[1]
+    if priors.shape != (A, 4) or conf.shape != (B, A, 2) or landm.shape != (B, A, 10):
+        raise ValueError("detect: shape mismatch")
+    dev = loc.device
+    out = torch.empty((B, A, 15), dtype=torch.float32, device=dev)
+    n_keep = torch.zeros((B,), dtype=torch.int64, device=dev)
+    ws = _ws(_size_query("jabd_detect_workspace_size", B, A), dev)
+    call("jabd_detect_f32", _p(loc), _p(conf), _p(landm), _p(priors), B, A,
+         float(variances[0]), float(variances[1]), float(conf_threshold), float(nms_threshold),
+         _p(out), _p(n_keep), _p(ws), ws.numel(), _stream())
+    return out, n_keep
+
+
+# --------------------------------------------------------------------------- match
+def match_encode(targets, priors, threshold, variances):
+    """Batched match()+encode() — nets/retinaface_training.py:93-162.
+
+    targets: list of B device tensors [n_i,15]; priors [A,4].
+    Returns loc_t [B,A,4], conf_t [B,A] int64, landm_t [B,A,10].
+    """
+    priors = _dev("match.priors", priors)
+    dev = priors.device
+    B, A = len(targets), priors.shape[0]
+    counts = [int(t.shape[0]) for t in targets]
+    if any(c == 0 for c in counts):
+        raise ValueError("match: an image has no targets (the reference's match() fails too)")
+    flat = _dev("match.targets", torch.cat([t.reshape(-1, 15) for t in targets], 0))
+    offs = [0]
+    for c in counts:
+        offs.append(offs[-1] + c)
+    offsets = torch.tensor(offs, dtype=torch.int64).to(dev, non_blocking=True)
+    loc_t = torch.empty((B, A, 4), dtype=torch.float32, device=dev)
+    conf_t = torch.empty((B, A), dtype=torch.int64, device=dev)
+    landm_t = torch.empty((B, A, 10), dtype=torch.float32, device=dev)
+    ws = _ws(_size_query("jabd_match_workspace_size", B, A), dev)
+    call("jabd_match_encode_f32", _p(flat), _p(offsets), B, max(counts) if counts else 0,
+         _p(priors), A, float(threshold), float(variances[0]), float(variances[1]), _p(loc_t),
+         _p(conf_t), _p(landm_t), _p(ws), ws.numel(), _stream())
+    return loc_t, conf_t, landm_t
+
+
+# --------------------------------------------------------------------------- loss
+def multibox_sums(loc, conf, landm, loc_t, conf_t, landm_t, neg_pos):
+    """Un-normalised MultiBoxLoss sums [3], counts [2] and the selection mask."""
+    loc, conf, landm = (_dev("loss.loc", loc), _dev("loss.conf", conf),
+                        _dev("loss.landm", landm))
+    loc_t, landm_t = _dev("loss.loc_t", loc_t), _dev("loss.landm_t", landm_t)
+    conf_t = _dev("loss.conf_t", conf_t, torch.int64)
+    B, A = loc.shape[0], loc.shape[1]
+    dev = loc.device
+    sums = torch.empty(3, dtype=torch.float32, device=dev)
+    counts = torch.empty(2, dtype=torch.int64, device=dev)
+    sel = torch.empty((B, A), dtype=torch.uint8, device=dev)
+    ws = _ws(_size_query("jabd_multibox_workspace_size", B, A), dev)
+    call("jabd_multibox_loss_fwd_f32", _p(loc), _p(conf), _p(landm), _p(loc_t), _p(conf_t),
+         _p(landm_t), B, A, int(neg_pos), _p(sums), _p(counts), _p(sel), _p(ws), ws.numel(),
+         _stream())
+    return sums, counts, sel
+
+
+def multibox_normalize(sums, counts):
+    loss = torch.empty(3, dtype=torch.float32, device=sums.device)
+    call("jabd_multibox_loss_finalize_f32", _p(sums), _p(counts), _p(loss), _stream())
+    return loss
+
+
+def multibox_backward(loc, conf, landm, loc_t, conf_t, landm_t, sel, gout, counts):
+    B, A = loc.shape[0], loc.shape[1]
+    gl = torch.empty_like(loc)
+    gc = torch.empty_like(conf)
+    glm = torch.empty_like(landm)
+    gout = _dev("loss.gout", gout)
+    call("jabd_multibox_loss_bwd_f32", _p(loc), _p(conf), _p(landm), _p(loc_t), _p(conf_t),
+         _p(landm_t), _p(sel), B, A, _p(gout), _p(counts), _p(gl), _p(gc), _p(glm), _stream())
+    return gl, gc, glm
+
+
+def version():
+    return lib().jabd_version().decode()

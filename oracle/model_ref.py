@@ -1,0 +1,210 @@
+"""ORACLE (test infrastructure only) — PyTorch-CPU fp32 restatement of the
+JABD detector forward (and, through autograd, its backward).
+
+Functional: every function takes a flat `state_dict`-style mapping `P`
+whose keys are the reference's own parameter names, so one set of weights
+drives both this restatement and the product module.  Paths are relative to
+/root/reference/JABD2080ti.
+
+  * JABD-MobileNetV3  — nets/retinaface_r.py:228-343 over
+    nets/mobilenetV3.py:452-522 (MobileNetV3_Large_eca, Block_eca :94-150,
+    in-block eca_block :332-348 with Hardsigmoid).
+  * RetinaFace-R50 + ECA + NLM — nets/retinaface_eca_nonlocal.py:235-359
+    over torchvision.models.resnet50 (layout identical to
+    nets/resnet_pytorch_r.py:87-303).
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+# (kernel, in, expand, out, act, se, stride) — nets/mobilenetV3.py:459-481
+MNV3_LAYERS = [
+    [(3, 16, 16, 16, "relu", False, 1), (3, 16, 64, 24, "relu", False, 2),
+     (3, 24, 72, 24, "relu", False, 1), (5, 24, 72, 40, "relu", True, 2),
+     (5, 40, 120, 40, "relu", True, 1), (5, 40, 120, 40, "relu", True, 1)],
+    [(3, 40, 240, 80, "hswish", False, 2), (3, 80, 200, 80, "hswish", False, 1),
+     (3, 80, 184, 80, "hswish", False, 1), (3, 80, 184, 80, "hswish", False, 1)],
+    [(3, 80, 480, 112, "hswish", True, 1), (3, 112, 672, 112, "hswish", True, 1),
+     (5, 112, 672, 160, "hswish", True, 2), (5, 160, 672, 160, "hswish", True, 1),
+     (5, 160, 960, 160, "hswish", True, 1)],
+]
+
+R50_LAYERS = [(64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)]  # (width, blocks, stride)
+
+
+def eca_kernel_size(channel, b=1, gamma=2):
+    """nets/mobilenetV3.py:335-336 / nets/retinaface_r.py:211-212."""
+    k = int(abs((math.log(channel, 2) + b) / gamma))
+    return k if k % 2 else k + 1
+
+
+def _act(x, kind):
+    if kind == "relu":
+        return F.relu(x)
+    if kind == "hswish":
+        return F.hardswish(x)
+    if kind is None:
+        return x
+    raise ValueError(kind)
+
+
+class Ctx:
+    """Batch-norm mode: eval (running stats) or train (batch stats + update)."""
+
+    def __init__(self, P, train=False, momentum=0.1, eps=1e-5):
+        self.P, self.train, self.momentum, self.eps = P, train, momentum, eps
+
+    def bn(self, x, name):
+        P = self.P
+        return F.batch_norm(x, P[name + ".running_mean"], P[name + ".running_var"],
+                            P[name + ".weight"], P[name + ".bias"], self.train, self.momentum,
+                            self.eps)
+
+    def conv(self, x, name, stride=1, padding=0, groups=1):
+        b = self.P.get(name + ".bias")
+        return F.conv2d(x, self.P[name + ".weight"], b, stride, padding, 1, groups)
+
+
+def eca(ctx, x, name, gate):
+    """ECA: global average pool -> Conv1d over channels -> gate -> x*y."""
+    w = ctx.P[name + ".conv.weight"]
+    k = w.shape[-1]
+    y = x.mean(dim=(2, 3))                                # AdaptiveAvgPool2d(1)
+    y = F.conv1d(y.unsqueeze(1), w, padding=(k - 1) // 2).squeeze(1)
+    y = torch.sigmoid(y) if gate == "sigmoid" else F.hardsigmoid(y)
+    return x * y[:, :, None, None]
+
+
+def block_eca(ctx, x, pre, spec):
+    """nets/mobilenetV3.py:94-150 (Block_eca.forward); SeModule never called."""
+    k, cin, exp, cout, act, _se, stride = spec
+    out = _act(ctx.bn(ctx.conv(x, pre + "conv1"), pre + "bn1"), act)
+    out = _act(ctx.bn(ctx.conv(out, pre + "conv2", stride, k // 2, exp), pre + "bn2"), act)
+    out = eca(ctx, out, pre + "eca", "hsigmoid")
+    out = ctx.bn(ctx.conv(out, pre + "conv3"), pre + "bn3")
+    skip = x
+    if stride == 1 and cin != cout:
+        skip = ctx.bn(ctx.conv(x, pre + "skip.0"), pre + "skip.1")
+    elif stride == 2 and cin != cout:
+        s = ctx.bn(ctx.conv(x, pre + "skip.0", 2, 1, cin), pre + "skip.1")
+        skip = ctx.bn(ctx.conv(s, pre + "skip.2"), pre + "skip.3")
+    elif stride == 2:
+        skip = ctx.bn(ctx.conv(x, pre + "skip.0", 2, 1, cin), pre + "skip.1")
+    return _act(out + skip, act)
+
+
+def mnv3_body(ctx, x):
+    """MobileNetV3_Large_eca stem + layer1..3 -> (C3, C4, C5)."""
+    x = F.hardswish(ctx.bn(ctx.conv(x, "body.conv1", 2, 1), "body.bn1"))
+    feats = []
+    for li, layer in enumerate(MNV3_LAYERS):
+        for bi, spec in enumerate(layer):
+            x = block_eca(ctx, x, f"body.layer{li + 1}.{bi}.", spec)
+        feats.append(x)
+    return feats
+
+
+def r50_body(ctx, x):
+    """torchvision resnet50 stem + layer1..4, returning layer2/3/4."""
+    x = F.relu(ctx.bn(ctx.conv(x, "body.conv1", 2, 3), "body.bn1"))
+    x = F.max_pool2d(x, 3, 2, 1)
+    feats = []
+    for li, (w, n, s) in enumerate(R50_LAYERS):
+        for bi in range(n):
+            pre = f"body.layer{li + 1}.{bi}."
+            st = s if bi == 0 else 1
+            out = F.relu(ctx.bn(ctx.conv(x, pre + "conv1"), pre + "bn1"))
+            out = F.relu(ctx.bn(ctx.conv(out, pre + "conv2", st, 1), pre + "bn2"))
+            out = ctx.bn(ctx.conv(out, pre + "conv3"), pre + "bn3")
+            idn = x
+            if bi == 0:
+                idn = ctx.bn(ctx.conv(x, pre + "downsample.0", st), pre + "downsample.1")
+            x = F.relu(out + idn)
+        if li >= 1:
+            feats.append(x)
+    return feats
+
+
+def psp(x, sizes):
+    """PSPModule.forward (nets/retinaface_r.py:100-104)."""
+    n, c = x.shape[:2]
+    return torch.cat([F.adaptive_avg_pool2d(x, s).view(n, c, -1) for s in sizes], -1)
+
+
+def nlm(ctx, x, pre, sizes=(1, 4, 8, 12)):
+    """NLM.forward (nets/retinaface_r.py:124-152), scale=1."""
+    B, _, h, w = x.shape
+    q = ctx.conv(x, pre + "f_query")
+    ch = q.shape[1]
+    q = q.view(B, ch, -1).permute(0, 2, 1)
+    k = psp(ctx.conv(x, pre + "f_key"), sizes)
+    v = psp(ctx.conv(x, pre + "f_value"), sizes).permute(0, 2, 1)
+    sim = F.softmax(torch.matmul(q, k) * (1 ** -.5), dim=-1)
+    ctxv = torch.matmul(sim, v).permute(0, 2, 1).contiguous().view(B, ch, h, w)
+    return ctx.conv(ctxv, pre + "W") + x
+
+
+def conv_bn_act(ctx, x, pre, leaky, padding=0, act=True):
+    y = ctx.bn(ctx.conv(x, pre + ".0", 1, padding), pre + ".1")
+    return F.leaky_relu(y, leaky) if act else y
+
+
+def fpn(ctx, feats, leaky, nlm_name):
+    """FPN.forward (nets/retinaface_r.py:169-207)."""
+    o1 = conv_bn_act(ctx, feats[0], "fpn.output1", leaky)
+    o2 = conv_bn_act(ctx, feats[1], "fpn.output2", leaky)
+    o3 = conv_bn_act(ctx, feats[2], "fpn.output3", leaky)
+    up3 = F.interpolate(o3, size=[o2.shape[2], o2.shape[3]], mode="nearest")
+    o2 = conv_bn_act(ctx, o2 + nlm(ctx, up3, nlm_name), "fpn.merge2", leaky, 1)
+    up2 = F.interpolate(o2, size=[o1.shape[2], o1.shape[3]], mode="nearest")
+    o1 = conv_bn_act(ctx, o1 + nlm(ctx, up2, nlm_name), "fpn.merge1", leaky, 1)
+    return [o1, o2, o3]
+
+
+def ssh(ctx, x, pre, leaky):
+    """SSH.forward (nets/layers.py:37-68)."""
+    a = conv_bn_act(ctx, x, pre + "conv3X3", leaky, 1, act=False)
+    b1 = conv_bn_act(ctx, x, pre + "conv5X5_1", leaky, 1)
+    b = conv_bn_act(ctx, b1, pre + "conv5X5_2", leaky, 1, act=False)
+    c1 = conv_bn_act(ctx, b1, pre + "conv7X7_2", leaky, 1)
+    c = conv_bn_act(ctx, c1, pre + "conv7x7_3", leaky, 1, act=False)
+    return F.relu(torch.cat([a, b, c], 1))
+
+
+def heads(ctx, feats, mode):
+    """Class/Bbox/Landmark heads + concat (nets/retinaface_r.py:17-57, 335-343)."""
+    def run(kind, k):
+        outs = []
+        for i, f in enumerate(feats):
+            o = ctx.conv(f, f"{kind}.{i}.conv1x1").permute(0, 2, 3, 1).contiguous()
+            outs.append(o.view(o.shape[0], -1, k))
+        return torch.cat(outs, 1)
+    loc = run("BboxHead", 4)
+    conf = run("ClassHead", 2)
+    landm = run("LandmarkHead", 10)
+    if mode != "train":
+        conf = F.softmax(conf, dim=-1)
+    return loc, conf, landm
+
+
+def retinaface_mnv3(P, x, mode="eval", train_bn=False):
+    """JABD-MobileNetV3 RetinaFace.forward (nets/retinaface_r.py:304-343)."""
+    ctx = Ctx(P, train_bn)
+    c3, c4, c5 = mnv3_body(ctx, x)
+    feats = [eca(ctx, c3, "eca_40", "sigmoid"), eca(ctx, c4, "eca_80", "sigmoid"),
+             eca(ctx, c5, "eca_160", "sigmoid")]
+    f = fpn(ctx, feats, 0.1, "fpn.nlm.")
+    f = [ssh(ctx, eca(ctx, f[i], "eca_fpn", "sigmoid"), f"ssh{i + 1}.", 0.1) for i in range(3)]
+    return heads(ctx, f, mode)
+
+
+def retinaface_r50(P, x, mode="eval", train_bn=False):
+    """RetinaFace-R50 + ECA + NLM (nets/retinaface_eca_nonlocal.py:314-359)."""
+    ctx = Ctx(P, train_bn)
+    c3, c4, c5 = r50_body(ctx, x)
+    feats = [eca(ctx, c3, "eca_64", "sigmoid"), eca(ctx, c4, "eca_128", "sigmoid"),
+             eca(ctx, c5, "eca_256", "sigmoid")]
+    f = fpn(ctx, feats, 0.0, "fpn.Nlm.")
+    f = [ssh(ctx, eca(ctx, f[i], "eca_fpn", "sigmoid"), f"ssh{i + 1}.", 0.0) for i in range(3)]
+    return heads(ctx, f, mode)

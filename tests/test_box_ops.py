@@ -1,0 +1,156 @@
+"""A6-A10 box work: anchors, decode, NMS, matching — oracle KATs on CPU and
+HIP-vs-oracle parity on the GPU (bit-exact for indices and assignments)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import box_ref
+
+CFG_MNET = {"min_sizes": [[16, 32], [64, 128], [256, 512]], "steps": [8, 16, 32],
+            "variance": [0.1, 0.2], "clip": False}
+
+
+# ---------------------------------------------------------------- oracle KATs (CPU)
+def test_anchor_count_reference_kat():
+    # utils/anchors.py:82-105 prints 29518 for steps 8/16/32/64 at 840².
+    cfg = {"min_sizes": [[8, 16], [32, 64], [64, 128], [256, 512]], "steps": [8, 16, 32, 64],
+           "clip": False}
+    assert box_ref.anchors(cfg, (840, 840)).shape[0] == 29518
+    assert box_ref.num_anchors(cfg, (840, 840)) == 29518
+
+
+@pytest.mark.parametrize("size,count", [(640, 16800), (840, 29126), (1024, 43008),
+                                        (2048, 172032)])
+def test_anchor_counts_hand_derived(size, count):
+    assert box_ref.num_anchors(CFG_MNET, (size, size)) == count
+
+
+def test_anchor_values_first_rows():
+    a = box_ref.anchors(CFG_MNET, (640, 640))
+    # level 0, i=0, j=0: cx=cy=0.5*8/640, w=h=16/640 then 32/640
+    np.testing.assert_array_equal(a[0].numpy(), np.float32([4 / 640, 4 / 640, 16 / 640, 16 / 640]))
+    np.testing.assert_array_equal(a[1].numpy(), np.float32([4 / 640, 4 / 640, 32 / 640, 32 / 640]))
+    np.testing.assert_array_equal(a[2].numpy(), np.float32([12 / 640, 4 / 640, 16 / 640, 16 / 640]))
+
+
+def test_nms_kat_hand_made():
+    boxes = np.float32([[0, 0, 10, 10], [1, 1, 11, 11], [20, 20, 30, 30], [0, 0, 10, 10]])
+    scores = np.float32([0.9, 0.8, 0.7, 0.9])
+    # box1 vs box0: inter 81, union 119 -> 0.68 > 0.3 suppressed; box3 ties box0
+    # at 0.9 and sorts after it (stable), IoU 1 -> suppressed.
+    assert box_ref.nms(boxes, scores, 0.3).tolist() == [0, 2]
+    assert box_ref.nms_py(boxes, scores, 0.3).tolist() == [0, 2]
+    # IoU exactly 0.5 is NOT suppressed at thr 0.5 (strict >)
+    b2 = np.float32([[0, 0, 2, 1], [1, 0, 3, 1]])  # inter 1, union 3 -> 1/3
+    assert box_ref.nms(b2, np.float32([1, 0.5]), 1 / 3.0).tolist() in ([0], [0, 1])
+    b3 = np.float32([[0, 0, 4, 1], [0, 0, 2, 1]])  # inter 2 union 4 -> 0.5 exactly
+    assert box_ref.nms(b3, np.float32([1, 0.9]), 0.5).tolist() == [0, 1]
+    assert box_ref.nms(b3, np.float32([1, 0.9]), 0.49).tolist() == [0]
+
+
+def test_nms_oracle_c_matches_python_twin():
+    rng = np.random.default_rng(5)
+    for n in (0, 1, 7, 200):
+        xy = rng.uniform(0, 1, (n, 2)).astype(np.float32)
+        wh = rng.uniform(0.01, 0.3, (n, 2)).astype(np.float32)
+        b = np.concatenate([xy, xy + wh], 1)
+        s = rng.choice(np.float32([0.5, 0.6, 0.7, 0.8]), n)
+        assert box_ref.nms(b, s, 0.3).tolist() == box_ref.nms_py(b, s, 0.3).tolist()
+
+
+def test_match_kat_shared_best_prior():
+    # two truths whose best prior is the same prior 0: the later truth wins it
+    # (sequential loop at nets/retinaface_training.py:129-130).
+    priors = torch.tensor([[0.5, 0.5, 0.2, 0.2], [0.1, 0.1, 0.05, 0.05]])
+    t = torch.tensor([[0.4, 0.4, 0.6, 0.6], [0.41, 0.41, 0.61, 0.61]])
+    labels = torch.tensor([1.0, -1.0])
+    landms = torch.zeros(2, 10)
+    loc, conf, landm, bti, bto = box_ref.match(0.35, t, priors, [0.1, 0.2], labels, landms)
+    assert bti.tolist()[0] == 1 and conf.tolist()[0] == -1 and float(bto[0]) == 2.0
+    assert conf.tolist()[1] == 0  # prior 1 overlaps nothing
+
+
+# ---------------------------------------------------------------- HIP parity (GPU)
+def _clustered(n, seed, ties=True):
+    from jabd_amd import synth
+    b, s = synth.nms_boxes(1, n, seed=seed, tie_frac=0.05 if ties else 0.0)
+    return b[0], s[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [0, 1, 2, 63, 64, 65, 1000, 4096])
+def test_nms_parity_sizes(cuda, n):
+    from jabd_amd import ops
+    b, s = _clustered(max(n, 1), seed=n + 11)
+    b, s = b[:n], s[:n]
+    ref = box_ref.nms(b, s, 0.3)
+    got = ops.nms(torch.from_numpy(b).to(cuda), torch.from_numpy(s).to(cuda), 0.3)
+    assert got.cpu().numpy().tolist() == ref.tolist()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("thr", [0.0, 0.3, 0.45, 0.7, 1.0])
+def test_nms_parity_thresholds(cuda, thr):
+    from jabd_amd import ops
+    b, s = _clustered(3000, seed=7)
+    ref = box_ref.nms(b, s, thr)
+    got = ops.nms(torch.from_numpy(b).to(cuda), torch.from_numpy(s).to(cuda), thr)
+    assert got.cpu().numpy().tolist() == ref.tolist()
+
+
+@pytest.mark.gpu
+def test_nms_parity_degenerate(cuda):
+    from jabd_amd import ops
+    # identical boxes, zero-area boxes, all-equal scores, -0.0 vs 0.0 scores
+    b = np.float32([[0, 0, 1, 1]] * 5 + [[0.5, 0.5, 0.5, 0.5]] * 3 + [[0, 0, 2, 2], [2, 2, 1, 1]])
+    s = np.float32([0.5] * 5 + [0.0, -0.0, 0.0] + [0.5, 0.7])
+    for thr in (0.0, 0.3, 0.99):
+        ref = box_ref.nms(b, s, thr)
+        got = ops.nms(torch.from_numpy(b).to(cuda), torch.from_numpy(s).to(cuda), thr)
+        assert got.cpu().numpy().tolist() == ref.tolist(), thr
+
+
+@pytest.mark.gpu
+def test_batched_nms_with_filter(cuda):
+    from jabd_amd import ops, synth
+    B, n = 3, 5000
+    bx, sc = synth.nms_boxes(B, n, seed=3)
+    sc = sc - 0.25  # half the rows fall under the 0.5 filter
+    keep, nk = ops.batched_nms(torch.from_numpy(bx).to(cuda), torch.from_numpy(sc).to(cuda),
+                               0.3, score_threshold=0.5)
+    keep, nk = keep.cpu().numpy(), nk.cpu().numpy()
+    for b in range(B):
+        m = np.nonzero(sc[b] >= 0.5)[0]
+        ref = m[box_ref.nms(bx[b][m], sc[b][m], 0.3)]
+        assert keep[b, : nk[b]].tolist() == ref.tolist()
+
+
+@pytest.mark.gpu
+def test_decode_parity(cuda):
+    from jabd_amd import ops
+    pri = box_ref.anchors(CFG_MNET, (256, 256))
+    g = torch.Generator().manual_seed(0)
+    loc = torch.randn(2, pri.shape[0], 4, generator=g) * 0.5
+    lm = torch.randn(2, pri.shape[0], 10, generator=g)
+    got = ops.decode(loc.to(cuda), pri.to(cuda), [0.1, 0.2]).cpu()
+    gotl = ops.decode_landm(lm.to(cuda), pri.to(cuda), [0.1, 0.2]).cpu()
+    for b in range(2):
+        ref = box_ref.decode(loc[b], pri, [0.1, 0.2])
+        torch.testing.assert_close(got[b], ref, rtol=1e-6, atol=1e-7)  # exp ulp only
+        refl = box_ref.decode_landm(lm[b], pri, [0.1, 0.2])
+        assert torch.equal(gotl[b], refl)  # no transcendental: bit-exact
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("size,batch", [(256, 4), (640, 2)])
+def test_match_parity(cuda, size, batch):
+    from jabd_amd import ops, synth
+    pri = box_ref.anchors(CFG_MNET, (size, size))
+    tg = [torch.from_numpy(t) for t in synth.targets(batch, size, seed=size)]
+    rl, rc, rlm = box_ref.match_batch(tg, pri)
+    gl, gc, glm = ops.match_encode([t.to(cuda) for t in tg], pri.to(cuda), 0.35, [0.1, 0.2])
+    assert torch.equal(gc.cpu(), rc)  # bit-exact assignment incl. forced matches
+    torch.testing.assert_close(gl.cpu(), rl, rtol=1e-5, atol=1e-5)  # log() ulp
+    assert torch.equal(glm.cpu(), rlm)
