@@ -1,0 +1,238 @@
+"""JABD hot-path benchmark on MI355X (contract: see README / DESIGN.md §Measurement).
+
+Step = one eval-mode forward of JABD-MobileNetV3 (nets/retinaface_r.py) on a
+synthetic bs32 1024x1024 batch already resident in HBM (BASELINE.json
+configs[1], "C2").  N GPUs run N independent replicas (inference does not
+shard further; no collective on the data path) -> weak scaling; value =
+images/sec over all ranks, timed as max over ranks between barriers.
+
+Extra fields on the one JSON line:
+  roofline     conv-GEMM stack (the dominant kernel family) vs the fp32 MFMA
+               peak: algorithmic FLOPs of every jabd conv launch in one step /
+               their summed HIP-event durations on the launch stream.
+  nms          C5 (configs[4]): batched NMS over 8 x 100k clustered boxes,
+               boxes/sec, bit-exact NMS kernel pipeline (sort+mask+scan).
+  cpu_baseline the oracle's PyTorch-CPU restatement of the same forward at
+               1024x1024, bs1, on this host (rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "jabd-joint-attention-based-detector-for-small-face-detection_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+METRIC = "images/sec at 1024x1024 bs32 (1/2/4/8 GPU); boxes/sec NMS"
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--size", type=int, default=1024)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-nms", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    return ap.parse_args()
+
+
+def build_model(device):
+    from nets.retinaface_r import RetinaFace
+    from nets.retinaface_training import weights_init
+    from utils.config import cfg_mnet
+    torch.manual_seed(0)
+    m = RetinaFace(cfg=cfg_mnet, mode="eval")
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        weights_init(m)   # the training scripts' init (nets/retinaface_training.py:305-323)
+    return m.eval().to(device)
+
+
+def conv_roofline(model, x, steps):
+    """Time every conv-GEMM launch of `steps` forwards with HIP events."""
+    from jabd_amd import functional as F
+    recs = []
+    orig = F.conv
+
+    def timed_conv(xx, pk, stride=1, pad=0, **kw):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        out = orig(xx, pk, stride=stride, pad=pad, **kw)
+        e.record()
+        o = out
+        M = o.shape[0] * o.shape[1] * o.shape[2]
+        K = pk.KH * pk.KW * pk.Cin + pk.Cin2
+        recs.append((s, e, 2.0 * M * K * pk.Cout))
+        return out
+
+    F.conv = timed_conv
+    try:
+        with torch.no_grad():
+            for _ in range(steps):
+                model(x)
+        torch.cuda.synchronize()
+    finally:
+        F.conv = orig
+    t_ms = sum(s.elapsed_time(e) for s, e, _ in recs)
+    flops = sum(f for _, _, f in recs)
+    n = len(recs) // steps
+    return flops / steps, t_ms / steps, n
+
+
+def forward_flops(model, size, batch):
+    """Algorithmic FLOPs (2*MAC) of the whole forward, from the layer shapes."""
+    from jabd_amd import functional as F
+    tot = [0.0]
+    orig_conv, orig_dw = F.conv, F.dwconv
+
+    def c(xx, pk, stride=1, pad=0, **kw):
+        out = orig_conv(xx, pk, stride=stride, pad=pad, **kw)
+        tot[0] += 2.0 * out.shape[0] * out.shape[1] * out.shape[2] * (
+            pk.KH * pk.KW * pk.Cin + pk.Cin2) * pk.Cout
+        return out
+
+    def d(xx, w, b, k, stride, **kw):
+        y, p = orig_dw(xx, w, b, k, stride, **kw)
+        tot[0] += 2.0 * y.numel() * k * k
+        return y, p
+
+    F.conv, F.dwconv = c, d
+    try:
+        with torch.no_grad():
+            model(torch.zeros(1, 3, size, size, device="cuda"))
+        torch.cuda.synchronize()
+    finally:
+        F.conv, F.dwconv = orig_conv, orig_dw
+    return tot[0]
+
+
+def nms_bench(device, reps=5):
+    from jabd_amd import ops, synth
+    from oracle import box_ref
+    B, n = 8, 100_000
+    bx, sc = synth.nms_boxes(B, n, seed=99)
+    b = torch.from_numpy(bx).to(device)
+    s = torch.from_numpy(sc).to(device)
+    keep, nk = ops.batched_nms(b, s, 0.3)   # warm-up + parity spot check (image 0)
+    torch.cuda.synchronize()
+    ref0 = box_ref.nms(bx[0], sc[0], 0.3)
+    exact = keep[0, : int(nk[0])].cpu().numpy().tolist() == ref0.tolist()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ops.batched_nms(b, s, 0.3)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    return {"config": "C5: 8 images x 100k clustered boxes, iou 0.3", "boxes_per_sec":
+            B * n / dt, "ms_per_call": dt * 1e3, "kept_img0": int(nk[0]),
+            "bit_exact_img0_vs_oracle": bool(exact)}
+
+
+def cpu_baseline(size, seconds):
+    from oracle import model_ref
+    from nets.retinaface_r import RetinaFace
+    from nets.retinaface_training import weights_init
+    from utils.config import cfg_mnet
+    import contextlib
+    import io
+    torch.manual_seed(0)
+    m = RetinaFace(cfg=cfg_mnet, mode="eval")
+    with contextlib.redirect_stdout(io.StringIO()):
+        weights_init(m)
+    sd = {k: v.float() for k, v in m.eval().state_dict().items()}
+    x = torch.randn(1, 3, size, size)
+    with torch.no_grad():
+        model_ref.retinaface_mnv3(sd, x)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            model_ref.retinaface_mnv3(sd, x)
+            n += 1
+            if time.perf_counter() - t0 > seconds:
+                break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "images/sec", "cores": torch.get_num_threads(),
+            "kind": "port", "sample": f"{n} images, bs1 {size}x{size}, oracle "
+            "model_ref.retinaface_mnv3 (PyTorch-CPU fp32 restatement)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    device = torch.device("cuda", local)
+    from jabd_amd import synth
+    model = build_model(device)
+    x = synth.images(args.batch, args.size, seed=1234 + rank, device=device)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            model(x)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        for _ in range(args.steps):
+            model(x)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    n_gpus = world
+    imgs = args.batch * args.steps * n_gpus
+    value = imgs / el
+
+    extra = {}
+    if rank == 0:
+        flops_step, t_ms, n_launch = conv_roofline(model, x, max(3, min(args.steps, 10)))
+        ach = flops_step / (t_ms * 1e-3) / 1e12
+        extra["roofline"] = {
+            "bound": "mfma", "kernel": f"conv_gemm_kernel (all {n_launch} launches per step)",
+            "achieved": ach, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+            "frac": ach / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
+            "conv_ms_per_step": t_ms, "conv_gflop_per_step": flops_step / 1e9}
+        extra["forward_gflop_per_image"] = forward_flops(model, args.size, 1) / 1e9
+        if not args.no_nms:
+            extra["nms"] = nms_bench(device)
+        if world == 1 and not args.no_cpu_baseline:
+            extra["cpu_baseline"] = cpu_baseline(args.size, args.cpu_seconds)
+        line = {
+            "metric": METRIC, "value": value, "unit": "images/sec", "n_gpus": n_gpus,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": "C2: JABD-MobileNetV3 RetinaFace (nets/retinaface_r.py) "
+                       "eval forward, weights_init weights", "global_batch": args.batch * n_gpus,
+                       "image_size": args.size, "parallelism": f"replicas x{n_gpus}"},
+        }
+        line.update(extra)
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -135,6 +135,109 @@ int jabd_multibox_loss_bwd_f32(const float* loc, const float* conf,
 int jabd_multibox_loss_finalize_f32(const float* sums, const int64_t* counts,
                                     float* loss, jabd_stream_t stream);
 
+/* ======================================================================== *
+ * Detector forward kernels (NHWC fp32).  Layouts: an activation tensor is
+ * addressed as base + b*bs + pixel*ps + c0 + c   (bs/ps in floats), so
+ * channel slices (SSH concat) and the head's [B, A, k] layout are plain
+ * strides.  Activation codes for `act`:
+ * ======================================================================== */
+enum {
+  JABD_ACT_NONE = 0,
+  JABD_ACT_RELU = 1,
+  JABD_ACT_LEAKY = 2,    /* LeakyReLU(slope) */
+  JABD_ACT_HSWISH = 3,   /* nn.Hardswish     */
+  JABD_ACT_HSIGMOID = 4, /* nn.Hardsigmoid   */
+  JABD_ACT_SIGMOID = 5,
+};
+
+/* A1/A4/A5 dense conv as implicit GEMM on fp32 MFMA — replaces nn.Conv2d
+ * (+ folded BatchNorm2d + activation) at nets/mobilenetV3.py:101,113,126-130,
+ * nets/retinaface_r.py:60-84,114-120, nets/layers.py:10-32 and torchvision
+ * resnet50.  w: packed weights (see jabd_amd/packing.py): float4
+ * [Kc][Ntiles][64], Kc = ceil(K/16), K = KH*KW*Cin (+ Cin2).
+ *   x2/Cin2:  optional K-concatenated second source read as a strided 1x1
+ *             conv (skip branch / ResNet downsample folded into the GEMM).
+ *   ascale:   optional per-(image, input channel) multiplier (ECA gate).
+ *   res:      optional residual added before the activation.
+ *   nchw_in:  x is NCHW [B,Cin,H,W] (network input); else NHWC strided. */
+typedef struct jabd_conv_args {
+  const float* x; int64_t x_bs; int32_t x_ps, x_c0;
+  int32_t B, H, W, Cin;
+  const float* x2; int64_t x2_bs; int32_t x2_ps, Cin2;
+  int32_t x2_W, x2_stride; /* x2 pixel of output (oh,ow) = (oh*x2_stride, ow*x2_stride) */
+  const float* ascale; int64_t ascale_bs;
+  const void* w; const float* bias;
+  const float* res; int64_t res_bs; int32_t res_ps, res_c0;
+  float* y; int64_t y_bs; int32_t y_ps, y_c0;
+  int32_t OH, OW, Cout, Ntiles, tn, Kc;
+  int32_t KH, KW, stride, pad;
+  int32_t act; float slope;
+  int32_t nchw_in, reserved0;
+  int64_t M; /* filled in by the library */
+} jabd_conv_args;
+/* N-tiles (16 output channels each) grouped per workgroup for a Cout. */
+int jabd_conv_pack_tn(int cout);
+int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t stream);
+
+/* A1 depthwise k x k conv (+ folded BN + act) — nets/mobilenetV3.py:105-108
+ * and the stride-2 skip branches :126-137.  w [k*k][C] (tap-major), bias [C].
+ * part (nullable): per-(image, block, channel) sums of the activated output,
+ * [B][nblk][C], consumed by jabd_eca_gate_f32 (the ECA average pool). */
+typedef struct jabd_dw_args {
+  const float* x; int64_t x_bs; int32_t x_ps, reserved0;
+  int32_t B, H, W, C;
+  const float* w; const float* bias;
+  float* y; int64_t y_bs; int32_t y_ps, reserved1;
+  int32_t OH, OW, k, stride, pad, act;
+  float slope; int32_t nblk;
+  float* part;
+} jabd_dw_args;
+/* Number of per-image partial-sum blocks the dw kernel uses (size of part). */
+int64_t jabd_dw_nblk(int64_t B, int64_t OH, int64_t OW, int64_t C);
+int jabd_dwconv_nhwc_f32(const jabd_dw_args* args, jabd_stream_t stream);
+
+/* Per-(image, block, channel) sums of an NHWC tensor (ECA pooling of a tensor
+ * not produced by the dw kernel: C3/C4/C5 and the FPN outputs). */
+int jabd_channel_sum_f32(const float* x, int64_t x_bs, int32_t x_ps, int64_t B, int64_t HW,
+                         int64_t C, int64_t nblk, float* part, jabd_stream_t stream);
+/* A2 ECA gate — nets/mobilenetV3.py:343-348 (gate=HSIGMOID) and
+ * nets/retinaface_r.py:219-224 (gate=SIGMOID): mean = sum(part)/HW,
+ * Conv1d(1,1,k,pad=(k-1)/2,no bias) over channels, gate -> scale [B][C]. */
+int jabd_eca_gate_f32(const float* part, int64_t nblk, int64_t B, int64_t C, int64_t hw,
+                      const float* w1d, int32_t k, int32_t gate, float* scale,
+                      jabd_stream_t stream);
+
+/* A3 CSAF non-local block — nets/retinaface_r.py:85-152 + the FPN's nearest
+ * up-sample and add (:192-203).  x = nearest(src [B,hs,ws,C] -> h x w).
+ * nlm_pool: kpool/vpool [B][S][ch] = PSP adaptive-avg-pools (sizes[]) of
+ *   f_key(x) / f_value(x)  (wk/wv [ch][C], bk/bv [ch]).
+ * nlm_apply: out = lateral + (W·softmax_S(q·k)·v + bW + x), q = f_query(x),
+ *   lateral/out [B,h,w,C] NHWC (may alias). */
+int jabd_nlm_pool_f32(const float* src, int64_t src_bs, int32_t src_ps, int32_t B, int32_t hs,
+                      int32_t ws, int32_t C, int32_t h, int32_t w, const float* wk,
+                      const float* bk, const float* wv, const float* bv, int32_t ch,
+                      const int32_t* sizes, int32_t nsizes, float* kpool, float* vpool,
+                      jabd_stream_t stream);
+int jabd_nlm_apply_f32(const float* src, int64_t src_bs, int32_t src_ps, int32_t B, int32_t hs,
+                       int32_t ws, int32_t C, int32_t h, int32_t w, const float* wq,
+                       const float* bq, const float* kpool, const float* vpool, int32_t S,
+                       int32_t ch, const float* wW, const float* bW, const float* lateral,
+                       float* out, jabd_stream_t stream);
+
+/* A4 detection heads — nets/retinaface_r.py:17-57,335-343: the Bbox (2x4),
+ * Class (2x2) and Landmark (2x10) 1x1 convs of one pyramid level, written
+ * straight into loc [B,A,4] / conf [B,A,2] / landm [B,A,10] at anchor offset
+ * a_off (the permute+view+cat layout); softmax over conf pairs if asked.
+ * wt [32][C] rows = 8 bbox, 4 class, 20 landmark out channels; bias [32]. */
+/* 3x3/stride-2/pad-1 max pool, NHWC (torchvision resnet50 stem maxpool). */
+int jabd_maxpool_nhwc_f32(const float* x, int32_t B, int32_t H, int32_t W, int32_t C,
+                          int32_t k, int32_t stride, int32_t pad, float* y,
+                          jabd_stream_t stream);
+int jabd_heads_f32(const float* x, int64_t x_bs, int32_t x_ps, int32_t B, int32_t HW,
+                   int32_t C, const float* wt, const float* bias, int64_t A, int64_t a_off,
+                   int32_t softmax, float* loc, float* conf, float* landm,
+                   jabd_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

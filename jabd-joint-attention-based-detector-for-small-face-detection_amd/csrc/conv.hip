@@ -1,0 +1,275 @@
+// A1/A4/A5 dense convolutions on gfx950 as NHWC implicit GEMM on the exact
+// fp32 MFMA (v_mfma_f32_16x16x4_f32).
+//
+//   Y[m, n] = act( sum_k A[m, k] * W[k, n] + bias[n] (+ R[m, n]) )
+//   m = (image, oh, ow) output pixel, n = output channel,
+//   k = (kh, kw, ci) tap-major, channel-minor (1x1: k = ci).
+//
+// Operand mapping.  The MFMA sums over its 4-wide k index (lane>>4).  Each
+// lane loads 16 contiguous bytes — channels 4g..4g+3 of its pixel (g = lane>>4)
+// — and feeds element e to MFMA step e, so one 16-channel K chunk is four
+// MFMAs whose logical k order is (4g + e).  Weights are pre-packed on the host
+// in exactly that order: Wp[kc][ntile][lane] = float4{W[16kc+4g+e][16nt+j]},
+// j = lane&15, so every B fragment is one coalesced float4 per lane.
+// Accumulator layout (16x16 f32): col = lane&15, row = 4*(lane>>4) + reg.
+//
+// Fusions: BN folded into W/bias (eval) or applied by the caller's BN
+// kernels (train); optional per-(image, k) A-scale (ECA gate of the
+// producing block, applied on load exactly as the reference's x*y);
+// optional K-concatenated second source (the block's skip branch folded into
+// the same GEMM); residual add; activation; channel-offset / strided output
+// (SSH concat, head layout).
+#include "common.h"
+#include "conv_args.h"
+
+namespace jabd {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float act_apply(float v, int act, float slope) {
+  switch (act) {
+    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_LEAKY: return v > 0.f ? v : v * slope;
+    case ACT_HSWISH: {
+      float r = fminf(fmaxf(v + 3.f, 0.f), 6.f);
+      return v * r / 6.f;
+    }
+    case ACT_HSIGMOID: return fminf(fmaxf(v + 3.f, 0.f), 6.f) / 6.f;
+    case ACT_SIGMOID: return 1.f / (1.f + expf(-v));
+    default: return v;
+  }
+}
+
+__device__ __forceinline__ float4 load_x2(const ConvArgs& p, int b, int oh, int ow, int c) {
+  const float* src = p.x2 + (int64_t)b * p.x2_bs +
+                     ((int64_t)oh * p.x2_stride * p.x2_W + (int64_t)ow * p.x2_stride) * p.x2_ps;
+  return *reinterpret_cast<const float4*>(src + c);
+}
+
+// Load the float4 of A for one lane: pixel (b, oh, ow) and k4 = first of 4 ks.
+template <bool VEC4>
+__device__ __forceinline__ float4 load_a(const ConvArgs& p, int b, int oh, int ow, bool mvalid,
+                                         int k4) {
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (!mvalid) return r;
+  if (p.KH == 1 && p.KW == 1 && p.stride == 1 && p.pad == 0) {
+    if (k4 < p.Cin) {
+      const float* src = p.x + (int64_t)b * p.x_bs + ((int64_t)oh * p.W + ow) * p.x_ps + p.x_c0;
+      if (VEC4) {
+        r = *reinterpret_cast<const float4*>(src + k4);
+      } else {
+        r.x = src[k4];
+        if (k4 + 1 < p.Cin) r.y = src[k4 + 1];
+        if (k4 + 2 < p.Cin) r.z = src[k4 + 2];
+        if (k4 + 3 < p.Cin) r.w = src[k4 + 3];
+      }
+      if (p.ascale) {
+        const float* s = p.ascale + (int64_t)b * p.ascale_bs + k4;
+        r.x *= s[0]; r.y *= s[1]; r.z *= s[2]; r.w *= s[3];
+      }
+    } else if (p.x2 && k4 < p.Cin + p.Cin2) {
+      r = load_x2(p, b, oh, ow, k4 - p.Cin);
+    }
+    return r;
+  }
+  // k x k taps (tap-major, channel-minor)
+  const int Ktot = p.KH * p.KW * p.Cin;
+  if (p.x2 && k4 >= Ktot) {
+    if (k4 < Ktot + p.Cin2) r = load_x2(p, b, oh, ow, k4 - Ktot);
+    return r;
+  }
+  if (VEC4) {
+    if (k4 >= Ktot) return r;
+    const int tap = k4 / p.Cin, ci = k4 - tap * p.Cin;
+    const int kh = tap / p.KW, kw = tap - kh * p.KW;
+    const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
+    if (ih < 0 || ih >= p.H || iw < 0 || iw >= p.W) return r;
+    const float* src = p.x + (int64_t)b * p.x_bs + ((int64_t)ih * p.W + iw) * p.x_ps + p.x_c0 + ci;
+    r = *reinterpret_cast<const float4*>(src);
+    if (p.ascale) {
+      const float* s = p.ascale + (int64_t)b * p.ascale_bs + ci;
+      r.x *= s[0]; r.y *= s[1]; r.z *= s[2]; r.w *= s[3];
+    }
+    return r;
+  }
+  float v[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] = 0.f;
+    const int k = k4 + e;
+    if (k >= Ktot) continue;
+    const int tap = k / p.Cin, ci = k - tap * p.Cin;
+    const int kh = tap / p.KW, kw = tap - kh * p.KW;
+    const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
+    if (ih < 0 || ih >= p.H || iw < 0 || iw >= p.W) continue;
+    float x;
+    if (p.nchw_in)
+      x = p.x[(int64_t)b * p.x_bs + ((int64_t)ci * p.H + ih) * p.W + iw];
+    else
+      x = p.x[(int64_t)b * p.x_bs + ((int64_t)ih * p.W + iw) * p.x_ps + p.x_c0 + ci];
+    if (p.ascale) x *= p.ascale[(int64_t)b * p.ascale_bs + ci];
+    v[e] = x;
+  }
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+template <int TM, int TN, bool VEC4>
+__global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int g = lane >> 4, j = lane & 15;
+  const int nblk_n = p.Ntiles / TN;
+  // blocks of the same M range are adjacent -> share A through L2
+  const int64_t bid = blockIdx.x;
+  const int nb = (int)(bid % nblk_n);
+  const int64_t mb = bid / nblk_n;
+  const int64_t m_wave = (mb * 4 + wave) * (16 * TM);
+  const int64_t OHW = (int64_t)p.OH * p.OW;
+
+  // per-lane A pixels (row = lane&15 of each 16-row subtile)
+  int pb[TM], poh[TM], pow_[TM];
+  bool pv[TM];
+#pragma unroll
+  for (int t = 0; t < TM; ++t) {
+    int64_t m = m_wave + t * 16 + j;
+    pv[t] = m < p.M;
+    int64_t mm = pv[t] ? m : 0;
+    pb[t] = (int)(mm / OHW);
+    int64_t r = mm - (int64_t)pb[t] * OHW;
+    poh[t] = (int)(r / p.OW);
+    pow_[t] = (int)(r - (int64_t)poh[t] * p.OW);
+  }
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int u = 0; u < TN; ++u) acc[t][u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const float4* wbase = reinterpret_cast<const float4*>(p.w) + ((int64_t)nb * TN) * 64 + lane;
+  const int64_t wstride_k = (int64_t)p.Ntiles * 64;
+
+  float4 a_cur[TM], b_cur[TN];
+#pragma unroll
+  for (int t = 0; t < TM; ++t) a_cur[t] = load_a<VEC4>(p, pb[t], poh[t], pow_[t], pv[t], 4 * g);
+#pragma unroll
+  for (int u = 0; u < TN; ++u) b_cur[u] = wbase[u * 64];
+
+  for (int kc = 0; kc < p.Kc; ++kc) {
+    float4 a_nxt[TM], b_nxt[TN];
+    const bool more = kc + 1 < p.Kc;
+    if (more) {
+      const int k4 = (kc + 1) * 16 + 4 * g;
+#pragma unroll
+      for (int t = 0; t < TM; ++t) a_nxt[t] = load_a<VEC4>(p, pb[t], poh[t], pow_[t], pv[t], k4);
+#pragma unroll
+      for (int u = 0; u < TN; ++u) b_nxt[u] = wbase[(kc + 1) * wstride_k + u * 64];
+    }
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+#pragma unroll
+      for (int u = 0; u < TN; ++u) {
+        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[t].x, b_cur[u].x, acc[t][u], 0, 0, 0);
+        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[t].y, b_cur[u].y, acc[t][u], 0, 0, 0);
+        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[t].z, b_cur[u].z, acc[t][u], 0, 0, 0);
+        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[t].w, b_cur[u].w, acc[t][u], 0, 0, 0);
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int t = 0; t < TM; ++t) a_cur[t] = a_nxt[t];
+#pragma unroll
+      for (int u = 0; u < TN; ++u) b_cur[u] = b_nxt[u];
+    }
+  }
+
+  // epilogue: acc[t][u][r] = Y[m_wave + 16t + 4g + r][16(nb*TN+u) + j]
+#pragma unroll
+  for (int u = 0; u < TN; ++u) {
+    const int n = (nb * TN + u) * 16 + j;
+    if (n >= p.Cout) continue;
+    const float bn = p.bias ? p.bias[n] : 0.f;
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m_wave + t * 16 + 4 * g + r;
+        if (m >= p.M) continue;
+        const int b = (int)(m / OHW);
+        const int64_t pix = m - (int64_t)b * OHW;
+        float v = acc[t][u][r] + bn;
+        if (p.res) v += p.res[(int64_t)b * p.res_bs + pix * p.res_ps + p.res_c0 + n];
+        v = act_apply(v, p.act, p.slope);
+        p.y[(int64_t)b * p.y_bs + pix * p.y_ps + p.y_c0 + n] = v;
+      }
+    }
+  }
+}
+
+template <int TM, int TN>
+static int launch_conv(const ConvArgs& a, bool vec4, hipStream_t st) {
+  const int64_t rows_per_blk = 4 * 16 * TM;
+  const int64_t mblk = cdiv(a.M, rows_per_blk);
+  const int64_t nblk = a.Ntiles / TN;
+  const int64_t grid = mblk * nblk;
+  JABD_REQUIRE(grid < (int64_t)0x7fffffff, "conv: grid too large");
+  if (vec4)
+    conv_gemm_kernel<TM, TN, true><<<(unsigned)grid, 256, 0, st>>>(a);
+  else
+    conv_gemm_kernel<TM, TN, false><<<(unsigned)grid, 256, 0, st>>>(a);
+  return check_launch("conv_gemm");
+}
+
+}  // namespace jabd
+
+using namespace jabd;
+
+extern "C" int jabd_conv_pack_tn(int cout) {
+  // N-tile group per launch: minimise padded columns, cap accumulators.
+  int tiles = (cout + 15) / 16;
+  if (tiles <= 5) return tiles;
+  int best = 4, waste = 1 << 30;
+  for (int tn : {4, 5, 8}) {
+    int grp = (tiles + tn - 1) / tn;
+    int w = grp * tn - tiles;
+    if (w < waste || (w == waste && tn > best)) { waste = w; best = tn; }
+  }
+  return best;
+}
+
+extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t stream) {
+  JABD_REQUIRE(args, "conv: null args");
+  ConvArgs a = *args;
+  JABD_REQUIRE(a.x && a.w && a.y, "conv: null pointer");
+  JABD_REQUIRE(a.B > 0 && a.Cin > 0 && a.Cout > 0 && a.KH > 0 && a.KW > 0 && a.stride > 0,
+               "conv: bad shape");
+  JABD_REQUIRE(a.OH == (a.H + 2 * a.pad - a.KH) / a.stride + 1 &&
+                   a.OW == (a.W + 2 * a.pad - a.KW) / a.stride + 1,
+               "conv: output size mismatch");
+  const bool is1x1 = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
+  JABD_REQUIRE(!a.x2 || ((a.KH * a.KW * a.Cin) % 4 == 0 && a.Cin2 % 4 == 0 && a.x2_ps % 4 == 0 &&
+                         a.x2_stride > 0 && !a.nchw_in),
+               "conv: K-concat needs K and Cin2 multiples of 4");
+  (void)is1x1;
+  const int Ktot = a.KH * a.KW * a.Cin + (a.x2 ? a.Cin2 : 0);
+  JABD_REQUIRE(a.Kc == (Ktot + 15) / 16, "conv: Kc=%d, expected %d", a.Kc, (Ktot + 15) / 16);
+  const int tiles = (a.Cout + 15) / 16;
+  JABD_REQUIRE(a.Ntiles >= tiles, "conv: Ntiles=%d < %d", a.Ntiles, tiles);
+  a.M = (int64_t)a.B * a.OH * a.OW;
+  const bool vec4 = !a.nchw_in && a.Cin % 4 == 0 && a.x_ps % 4 == 0 && a.x_c0 % 4 == 0 &&
+                    (reinterpret_cast<uintptr_t>(a.x) & 15) == 0;
+  hipStream_t st = as_stream(stream);
+  const int tn = a.tn;
+  JABD_REQUIRE(a.Ntiles % tn == 0, "conv: Ntiles %% tn != 0");
+  switch (tn) {
+    case 1: return launch_conv<4, 1>(a, vec4, st);
+    case 2: return launch_conv<4, 2>(a, vec4, st);
+    case 3: return launch_conv<4, 3>(a, vec4, st);
+    case 4: return launch_conv<4, 4>(a, vec4, st);
+    case 5: return launch_conv<4, 5>(a, vec4, st);
+    case 8: return launch_conv<2, 8>(a, vec4, st);
+    default:
+      set_error("conv: unsupported tn=%d", tn);
+      return JABD_EINVAL;
+  }
+}

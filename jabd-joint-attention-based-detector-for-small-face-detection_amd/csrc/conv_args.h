@@ -1,0 +1,16 @@
+// Kernel-side view of the C-ABI argument structs.
+#pragma once
+#include "../../include/jabd.h"
+
+namespace jabd {
+typedef jabd_conv_args ConvArgs;
+typedef jabd_dw_args DwArgs;
+enum {
+  ACT_NONE = JABD_ACT_NONE,
+  ACT_RELU = JABD_ACT_RELU,
+  ACT_LEAKY = JABD_ACT_LEAKY,
+  ACT_HSWISH = JABD_ACT_HSWISH,
+  ACT_HSIGMOID = JABD_ACT_HSIGMOID,
+  ACT_SIGMOID = JABD_ACT_SIGMOID,
+};
+}  // namespace jabd

@@ -1,0 +1,163 @@
+// A1 depthwise k x k convolution (NHWC, fp32 VALU) with folded BN, activation
+// and the ECA average-pool partial sums fused into the epilogue.
+//
+// Thread = 4 channels (one float4) x a strip of PW output pixels along W.
+// Each thread keeps its k*k float4 taps in registers across all strips it
+// computes, and loads each input row segment of a strip once (sliding
+// window), so input re-reads come from L1 instead of HBM.  The ECA partial
+// sums of the activated output are reduced per workgroup in fixed order and
+// written to part[b][blk][c] (deterministic; no atomics).
+#include "common.h"
+#include "conv_args.h"
+
+namespace jabd {
+
+__device__ __forceinline__ float dw_act(float v, int act, float slope) {
+  switch (act) {
+    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_LEAKY: return v > 0.f ? v : v * slope;
+    case ACT_HSWISH: {
+      float r = fminf(fmaxf(v + 3.f, 0.f), 6.f);
+      return v * r / 6.f;
+    }
+    default: return v;
+  }
+}
+
+constexpr int kDwThreads = 256;
+constexpr int kPW = 4;
+
+__device__ __forceinline__ float4 f4fma(float4 a, float4 w, float4 c) {
+  c.x = fmaf(a.x, w.x, c.x);
+  c.y = fmaf(a.y, w.y, c.y);
+  c.z = fmaf(a.z, w.z, c.z);
+  c.w = fmaf(a.w, w.w, c.w);
+  return c;
+}
+
+template <int K, int S>
+__global__ __launch_bounds__(kDwThreads) void dw_kernel(const DwArgs p, int strips_per_blk) {
+  constexpr int SPAN = (kPW - 1) * S + K;
+  const int CG = p.C >> 2;
+  const int SP = kDwThreads / CG;  // strips in flight per pass
+  const int tid = threadIdx.x;
+  const int cg = tid % CG, sp = tid / CG;
+  const bool active = sp < SP;
+  const int b = blockIdx.y;
+  const int OWs = (p.OW + kPW - 1) / kPW;
+  const int64_t nstrip = (int64_t)p.OH * OWs;
+  const int64_t s0 = (int64_t)blockIdx.x * strips_per_blk;
+  const float* xb = p.x + (int64_t)b * p.x_bs + 4 * cg;
+  float* yb = p.y + (int64_t)b * p.y_bs + 4 * cg;
+
+  float4 wr[K * K];
+  float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (active) {
+#pragma unroll
+    for (int t = 0; t < K * K; ++t) wr[t] = reinterpret_cast<const float4*>(p.w + t * p.C)[cg];
+    if (p.bias) bias = reinterpret_cast<const float4*>(p.bias)[cg];
+  }
+  float4 psum = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  for (int it = 0; active && it * SP < strips_per_blk; ++it) {
+    const int64_t s = s0 + it * SP + sp;
+    if (s >= nstrip || it * SP + sp >= strips_per_blk) break;
+    const int oh = (int)(s / OWs);
+    const int ow0 = (int)(s - (int64_t)oh * OWs) * kPW;
+    float4 acc[kPW];
+#pragma unroll
+    for (int o = 0; o < kPW; ++o) acc[o] = bias;
+    const int iw0 = ow0 * S - p.pad;
+#pragma unroll
+    for (int kh = 0; kh < K; ++kh) {
+      const int ih = oh * S - p.pad + kh;
+      if (ih < 0 || ih >= p.H) continue;
+      float4 row[SPAN];
+      const float* xr = xb + (int64_t)ih * p.W * p.x_ps;
+#pragma unroll
+      for (int c = 0; c < SPAN; ++c) {
+        const int iw = iw0 + c;
+        row[c] = (iw >= 0 && iw < p.W) ? *reinterpret_cast<const float4*>(xr + (int64_t)iw * p.x_ps)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int o = 0; o < kPW; ++o)
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw) acc[o] = f4fma(row[o * S + kw], wr[kh * K + kw], acc[o]);
+    }
+#pragma unroll
+    for (int o = 0; o < kPW; ++o) {
+      if (ow0 + o >= p.OW) break;
+      float4 v;
+      v.x = dw_act(acc[o].x, p.act, p.slope);
+      v.y = dw_act(acc[o].y, p.act, p.slope);
+      v.z = dw_act(acc[o].z, p.act, p.slope);
+      v.w = dw_act(acc[o].w, p.act, p.slope);
+      *reinterpret_cast<float4*>(yb + ((int64_t)oh * p.OW + ow0 + o) * p.y_ps) = v;
+      psum.x += v.x; psum.y += v.y; psum.z += v.z; psum.w += v.w;
+    }
+  }
+
+  if (p.part) {
+    __shared__ float4 red[kDwThreads];
+    red[tid] = psum;
+    __syncthreads();
+    if (tid < CG) {
+      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int q = 0; q < SP; ++q) {
+        float4 v = red[q * CG + tid];
+        t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+      }
+      reinterpret_cast<float4*>(p.part + ((int64_t)b * p.nblk + blockIdx.x) * p.C)[tid] = t;
+    }
+  }
+}
+
+static int64_t dw_strips_per_blk(int64_t B, int64_t OH, int64_t OW, int64_t C) {
+  const int64_t SP = kDwThreads / (C / 4);
+  const int64_t nstrip = OH * ((OW + kPW - 1) / kPW);
+  // aim for >= ~2048 workgroups over the batch, at least one pass per block
+  int64_t per = cdiv(nstrip * B, 2048);
+  per = cdiv(per, SP) * SP;
+  if (per < SP) per = SP;
+  return per;
+}
+
+}  // namespace jabd
+
+using namespace jabd;
+
+extern "C" int64_t jabd_dw_nblk(int64_t B, int64_t OH, int64_t OW, int64_t C) {
+  if (B <= 0 || OH <= 0 || OW <= 0 || C <= 0 || C % 4 || C / 4 > kDwThreads) return -1;
+  const int64_t nstrip = OH * ((OW + kPW - 1) / kPW);
+  return cdiv(nstrip, dw_strips_per_blk(B, OH, OW, C));
+}
+
+extern "C" int jabd_dwconv_nhwc_f32(const jabd_dw_args* args, jabd_stream_t stream) {
+  JABD_REQUIRE(args, "dw: null args");
+  const DwArgs& a = *args;
+  JABD_REQUIRE(a.x && a.w && a.y, "dw: null pointer");
+  JABD_REQUIRE(a.C % 4 == 0 && a.C / 4 <= kDwThreads, "dw: C=%d must be a multiple of 4, <= 1024",
+               a.C);
+  JABD_REQUIRE(a.x_ps % 4 == 0 && a.y_ps % 4 == 0, "dw: pixel strides must be multiples of 4");
+  JABD_REQUIRE(a.OH == (a.H + 2 * a.pad - a.k) / a.stride + 1 &&
+                   a.OW == (a.W + 2 * a.pad - a.k) / a.stride + 1,
+               "dw: output size mismatch");
+  const int64_t per = dw_strips_per_blk(a.B, a.OH, a.OW, a.C);
+  const int64_t nblk = jabd_dw_nblk(a.B, a.OH, a.OW, a.C);
+  JABD_REQUIRE(!a.part || a.nblk == nblk, "dw: nblk %d != %lld", a.nblk, (long long)nblk);
+  dim3 grid((unsigned)nblk, (unsigned)a.B);
+  hipStream_t st = as_stream(stream);
+#define DW_CASE(K, S)                                                        \
+  if (a.k == K && a.stride == S) {                                          \
+    dw_kernel<K, S><<<grid, kDwThreads, 0, st>>>(a, (int)per);             \
+    return check_launch("dwconv");                                          \
+  }
+  DW_CASE(3, 1)
+  DW_CASE(3, 2)
+  DW_CASE(5, 1)
+  DW_CASE(5, 2)
+#undef DW_CASE
+  set_error("dw: unsupported k=%d stride=%d", a.k, a.stride);
+  return JABD_EINVAL;
+}

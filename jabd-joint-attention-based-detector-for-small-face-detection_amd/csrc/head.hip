@@ -1,0 +1,390 @@
+// A2-A4 attention and head kernels on gfx950: ECA pooling + gate, the CSAF
+// non-local block (PSP-pooled keys/values, per-pixel softmax over S bins)
+// fused with the FPN's nearest up-sample and lateral add, and the three
+// detection heads written straight into the anchor-major output layout.
+// All HBM/latency-bound: one pass over each activation, fixed-order sums.
+#include "common.h"
+#include "conv_args.h"
+
+namespace jabd {
+
+// ---------------------------------------------------------------- ECA
+constexpr int kSumThreads = 256;
+
+// part[b][blk][c] = sum over this block's pixels of x[b, pix, c]
+__global__ __launch_bounds__(kSumThreads) void channel_sum_kernel(
+    const float* __restrict__ x, int64_t x_bs, int x_ps, int64_t HW, int C, int64_t per_blk,
+    int64_t nblk, float* __restrict__ part) {
+  const int b = blockIdx.y;
+  const int64_t p0 = blockIdx.x * per_blk;
+  const int64_t p1 = min(p0 + per_blk, HW);
+  const float* xb = x + (int64_t)b * x_bs;
+  extern __shared__ float red[];  // [rows][C]
+  const int rows = kSumThreads / C > 0 ? kSumThreads / C : 1;
+  for (int c0 = 0; c0 < C; c0 += kSumThreads) {
+    const int c = c0 + (threadIdx.x % min(C, kSumThreads));
+    const int r = threadIdx.x / min(C, kSumThreads);
+    const int nrows = C >= kSumThreads ? 1 : rows;
+    float s = 0.f;
+    if (r < nrows && c < C)
+      for (int64_t q = p0 + r; q < p1; q += nrows) s += xb[q * x_ps + c];
+    __syncthreads();
+    if (r < nrows && c < C) red[r * min(C, kSumThreads) + (c - c0)] = s;
+    __syncthreads();
+    if (threadIdx.x < min(C - c0, kSumThreads)) {
+      float t = 0.f;
+      for (int q = 0; q < nrows; ++q) t += red[q * min(C, kSumThreads) + threadIdx.x];
+      part[((int64_t)b * nblk + blockIdx.x) * C + c0 + threadIdx.x] = t;
+    }
+    __syncthreads();
+  }
+}
+
+// scale[b][c] = gate( sum_t w[t] * mean[b][c + t - (k-1)/2] )   (zero padded)
+__global__ void eca_gate_kernel(const float* __restrict__ part, int64_t nblk, int C, float inv_hw,
+                                const float* __restrict__ w1d, int k, int gate,
+                                float* __restrict__ scale) {
+  extern __shared__ float mean[];
+  const int b = blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float s = 0.f;
+    for (int64_t q = 0; q < nblk; ++q) s += part[((int64_t)b * nblk + q) * C + c];
+    mean[c] = s * inv_hw;
+  }
+  __syncthreads();
+  const int h = (k - 1) / 2;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float y = 0.f;
+    for (int t = 0; t < k; ++t) {
+      const int cc = c + t - h;
+      if (cc >= 0 && cc < C) y = fmaf(w1d[t], mean[cc], y);
+    }
+    float g = gate == ACT_SIGMOID ? 1.f / (1.f + expf(-y)) : fminf(fmaxf(y + 3.f, 0.f), 6.f) / 6.f;
+    scale[(int64_t)b * C + c] = g;
+  }
+}
+
+// ---------------------------------------------------------------- NLM
+// F.interpolate(mode='nearest', size=...) source index (ATen nearest_idx).
+__device__ __forceinline__ int nearest_src(int dst, int in, int out) {
+  if (out == in) return dst;
+  if (out == 2 * in) return dst >> 1;
+  const float scale = (float)in / (float)out;
+  const int s = (int)floorf((float)dst * scale);
+  return s < in - 1 ? s : in - 1;
+}
+
+constexpr int kNlmMaxCh = 64;
+struct NlmSizes {
+  int n;
+  int v[8];
+};
+constexpr int kNlmMaxC = 512;
+
+// One workgroup per (bin s, image b): mean over the bin of f_key / f_value.
+__global__ __launch_bounds__(256) void nlm_pool_kernel(
+    const float* __restrict__ src, int64_t src_bs, int src_ps, int hs, int ws, int C, int h,
+    int w, const float* __restrict__ wk, const float* __restrict__ bk,
+    const float* __restrict__ wv, const float* __restrict__ bv, int ch, const NlmSizes sizes,
+    int S, float* __restrict__ kpool, float* __restrict__ vpool) {
+  const int nsizes = sizes.n;
+  const int s = blockIdx.x, b = blockIdx.y;
+  // locate the level and bin (sizes are tiny; scan)
+  int base = 0, lvl = 0;
+  for (; lvl < nsizes; ++lvl) {
+    const int n = sizes.v[lvl] * sizes.v[lvl];
+    if (s < base + n) break;
+    base += n;
+  }
+  const int sz = sizes.v[lvl];
+  const int bi = (s - base) / sz, bj = (s - base) % sz;
+  const int h0 = (bi * h) / sz, h1 = ((bi + 1) * h + sz - 1) / sz;  // AdaptiveAvgPool bins
+  const int w0 = (bj * w) / sz, w1 = ((bj + 1) * w + sz - 1) / sz;
+  const int rw = w1 - w0;
+  const int npix = (h1 - h0) * rw;
+  __shared__ float sw[2 * kNlmMaxCh * 64];  // weights staged in LDS when they fit
+  const bool wlds = 2 * ch * C <= 2 * kNlmMaxCh * 64;
+  if (wlds) {
+    for (int t = threadIdx.x; t < ch * C; t += blockDim.x) {
+      sw[t] = wk[t];
+      sw[ch * C + t] = wv[t];
+    }
+  }
+  __syncthreads();
+  const float* WK = wlds ? sw : wk;
+  const float* WV = wlds ? sw + ch * C : wv;
+  float ak[kNlmMaxCh], av[kNlmMaxCh];
+  for (int o = 0; o < ch; ++o) { ak[o] = 0.f; av[o] = 0.f; }
+  const float* sb = src + (int64_t)b * src_bs;
+  for (int q = threadIdx.x; q < npix; q += blockDim.x) {
+    const int i = h0 + q / rw, jx = w0 + q % rw;
+    const float* xp = sb + ((int64_t)nearest_src(i, hs, h) * ws + nearest_src(jx, ws, w)) * src_ps;
+    for (int o = 0; o < ch; ++o) {
+      float kk = bk[o], vv = bv[o];
+      for (int c = 0; c < C; ++c) {
+        const float x = xp[c];
+        kk = fmaf(WK[o * C + c], x, kk);
+        vv = fmaf(WV[o * C + c], x, vv);
+      }
+      ak[o] += kk;
+      av[o] += vv;
+    }
+  }
+  __shared__ float red[256];
+  const float inv = 1.f / (float)npix;
+  for (int o = 0; o < ch; ++o) {
+    for (int pass = 0; pass < 2; ++pass) {
+      red[threadIdx.x] = pass ? av[o] : ak[o];
+      __syncthreads();
+      for (int st = 128; st > 0; st >>= 1) {
+        if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) {
+        float* dst = pass ? vpool : kpool;
+        dst[((int64_t)b * S + s) * ch + o] = red[0] * inv;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Per pixel: out = lateral + (W · softmax(q·K) V + bW + x)
+__global__ __launch_bounds__(256) void nlm_apply_kernel(
+    const float* __restrict__ src, int64_t src_bs, int src_ps, int hs, int ws, int C, int h,
+    int w, const float* __restrict__ wq, const float* __restrict__ bq,
+    const float* __restrict__ kpool, const float* __restrict__ vpool, int S, int ch,
+    const float* __restrict__ wW, const float* __restrict__ bW, const float* lateral,
+    float* out) {
+  extern __shared__ float sm[];  // K [S][ch], V [S][ch], wq [ch][C], wW [C][ch]
+  const int b = blockIdx.y;
+  float* sK = sm;
+  float* sV = sK + S * ch;
+  float* sWq = sV + S * ch;
+  float* sWW = sWq + ch * C;
+  for (int t = threadIdx.x; t < S * ch; t += blockDim.x) {
+    sK[t] = kpool[(int64_t)b * S * ch + t];
+    sV[t] = vpool[(int64_t)b * S * ch + t];
+  }
+  for (int t = threadIdx.x; t < ch * C; t += blockDim.x) {
+    sWq[t] = wq[t];
+    sWW[t] = wW[t];
+  }
+  __syncthreads();
+  const int64_t pix = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (pix >= (int64_t)h * w) return;
+  const int i = (int)(pix / w), jx = (int)(pix % w);
+  const float* xp = src + (int64_t)b * src_bs +
+                    ((int64_t)nearest_src(i, hs, h) * ws + nearest_src(jx, ws, w)) * src_ps;
+  float q[kNlmMaxCh];
+  for (int o = 0; o < ch; ++o) {
+    float a = bq[o];
+    for (int c = 0; c < C; ++c) a = fmaf(sWq[o * C + c], xp[c], a);
+    q[o] = a;
+  }
+  // softmax over S with running max (two passes over LDS)
+  float mx = -INFINITY;
+  for (int s = 0; s < S; ++s) {
+    float l = 0.f;
+    for (int o = 0; o < ch; ++o) l = fmaf(q[o], sK[s * ch + o], l);
+    mx = fmaxf(mx, l);
+  }
+  float den = 0.f;
+  float cx[kNlmMaxCh];
+  for (int o = 0; o < ch; ++o) cx[o] = 0.f;
+  for (int s = 0; s < S; ++s) {
+    float l = 0.f;
+    for (int o = 0; o < ch; ++o) l = fmaf(q[o], sK[s * ch + o], l);
+    const float e = expf(l - mx);
+    den += e;
+    for (int o = 0; o < ch; ++o) cx[o] = fmaf(e, sV[s * ch + o], cx[o]);
+  }
+  const float inv = 1.f / den;
+  for (int o = 0; o < ch; ++o) cx[o] *= inv;
+  const int64_t opix = ((int64_t)b * h * w + pix) * C;
+  for (int c = 0; c < C; ++c) {
+    float a = bW[c];
+    for (int o = 0; o < ch; ++o) a = fmaf(sWW[c * ch + o], cx[o], a);
+    const float v = a + xp[c];
+    out[opix + c] = lateral[opix + c] + v;
+  }
+}
+
+// ---------------------------------------------------------------- heads
+constexpr int kHeadOut = 32;  // 8 bbox + 4 class + 20 landmark channels
+
+__global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ x, int64_t x_bs,
+                                                    int x_ps, int HW, int C,
+                                                    const float* __restrict__ wt,
+                                                    const float* __restrict__ bias, int64_t A,
+                                                    int64_t a_off, int softmax,
+                                                    float* __restrict__ loc,
+                                                    float* __restrict__ conf,
+                                                    float* __restrict__ landm) {
+  extern __shared__ float sw[];  // [32][C]
+  for (int t = threadIdx.x; t < kHeadOut * C; t += blockDim.x) sw[t] = wt[t];
+  __syncthreads();
+  const int b = blockIdx.y;
+  const int64_t pix = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (pix >= HW) return;
+  const float* xp = x + (int64_t)b * x_bs + pix * x_ps;
+  float o[kHeadOut];
+#pragma unroll
+  for (int n = 0; n < kHeadOut; ++n) o[n] = bias[n];
+  for (int c = 0; c < C; c += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(xp + c);
+#pragma unroll
+    for (int n = 0; n < kHeadOut; ++n) {
+      const float* wr = sw + n * C + c;
+      o[n] = fmaf(wr[0], v.x, o[n]);
+      o[n] = fmaf(wr[1], v.y, o[n]);
+      o[n] = fmaf(wr[2], v.z, o[n]);
+      o[n] = fmaf(wr[3], v.w, o[n]);
+    }
+  }
+  const int64_t row = (int64_t)b * A + a_off + pix * 2;  // 2 anchors per position
+  float4* lp = reinterpret_cast<float4*>(loc + row * 4);
+  lp[0] = make_float4(o[0], o[1], o[2], o[3]);
+  lp[1] = make_float4(o[4], o[5], o[6], o[7]);
+  float c0 = o[8], c1 = o[9], c2 = o[10], c3 = o[11];
+  if (softmax) {  // F.softmax over each anchor's 2 logits
+    float m = fmaxf(c0, c1), e0 = expf(c0 - m), e1 = expf(c1 - m), s = e0 + e1;
+    c0 = e0 / s; c1 = e1 / s;
+    m = fmaxf(c2, c3); e0 = expf(c2 - m); e1 = expf(c3 - m); s = e0 + e1;
+    c2 = e0 / s; c3 = e1 / s;
+  }
+  reinterpret_cast<float4*>(conf + row * 2)[0] = make_float4(c0, c1, c2, c3);
+  float* lm = landm + row * 10;
+#pragma unroll
+  for (int n = 0; n < 20; ++n) lm[n] = o[12 + n];
+}
+
+}  // namespace jabd
+
+using namespace jabd;
+
+extern "C" int jabd_channel_sum_f32(const float* x, int64_t x_bs, int32_t x_ps, int64_t B,
+                                    int64_t HW, int64_t C, int64_t nblk, float* part,
+                                    jabd_stream_t stream) {
+  JABD_REQUIRE(x && part && B > 0 && HW > 0 && C > 0 && nblk > 0, "channel_sum: bad args");
+  const int64_t per = cdiv(HW, nblk);
+  const int cw = (int)(C < kSumThreads ? C : kSumThreads);
+  const int rows = C >= kSumThreads ? 1 : kSumThreads / (int)C;
+  dim3 g((unsigned)nblk, (unsigned)B);
+  channel_sum_kernel<<<g, kSumThreads, rows * cw * sizeof(float), as_stream(stream)>>>(
+      x, x_bs, x_ps, HW, (int)C, per, nblk, part);
+  return check_launch("channel_sum");
+}
+
+extern "C" int jabd_eca_gate_f32(const float* part, int64_t nblk, int64_t B, int64_t C,
+                                 int64_t hw, const float* w1d, int32_t k, int32_t gate,
+                                 float* scale, jabd_stream_t stream) {
+  JABD_REQUIRE(part && w1d && scale && B > 0 && C > 0 && hw > 0 && k > 0 && (k & 1),
+               "eca_gate: bad args");
+  JABD_REQUIRE(gate == ACT_SIGMOID || gate == ACT_HSIGMOID, "eca_gate: gate must be (h)sigmoid");
+  JABD_REQUIRE(C * sizeof(float) <= 64 * 1024, "eca_gate: C too large");
+  eca_gate_kernel<<<(unsigned)B, 256, C * sizeof(float), as_stream(stream)>>>(
+      part, nblk, (int)C, 1.f / (float)hw, w1d, k, gate, scale);
+  return check_launch("eca_gate");
+}
+
+extern "C" int jabd_nlm_pool_f32(const float* src, int64_t src_bs, int32_t src_ps, int32_t B,
+                                 int32_t hs, int32_t ws, int32_t C, int32_t h, int32_t w,
+                                 const float* wk, const float* bk, const float* wv,
+                                 const float* bv, int32_t ch, const int32_t* sizes,
+                                 int32_t nsizes, float* kpool, float* vpool,
+                                 jabd_stream_t stream) {
+  JABD_REQUIRE(src && wk && bk && wv && bv && sizes && kpool && vpool, "nlm_pool: null pointer");
+  JABD_REQUIRE(ch > 0 && ch <= kNlmMaxCh && C > 0 && C <= kNlmMaxC, "nlm_pool: ch/C out of range");
+  JABD_REQUIRE(nsizes > 0 && nsizes <= 8, "nlm_pool: nsizes");
+  NlmSizes sz;
+  sz.n = nsizes;
+  int S = 0;
+  for (int i = 0; i < 8; ++i) {
+    sz.v[i] = i < nsizes ? sizes[i] : 0;
+    if (i < nsizes) {
+      JABD_REQUIRE(sizes[i] > 0, "nlm_pool: bad PSP size");
+      S += sizes[i] * sizes[i];
+    }
+  }
+  dim3 g((unsigned)S, (unsigned)B);
+  nlm_pool_kernel<<<g, 256, 0, as_stream(stream)>>>(src, src_bs, src_ps, hs, ws, C, h, w, wk, bk,
+                                                    wv, bv, ch, sz, S, kpool, vpool);
+  return check_launch("nlm_pool");
+}
+
+extern "C" int jabd_nlm_apply_f32(const float* src, int64_t src_bs, int32_t src_ps, int32_t B,
+                                  int32_t hs, int32_t ws, int32_t C, int32_t h, int32_t w,
+                                  const float* wq, const float* bq, const float* kpool,
+                                  const float* vpool, int32_t S, int32_t ch, const float* wW,
+                                  const float* bW, const float* lateral, float* out,
+                                  jabd_stream_t stream) {
+  JABD_REQUIRE(src && wq && bq && kpool && vpool && wW && bW && lateral && out,
+               "nlm_apply: null pointer");
+  JABD_REQUIRE(ch > 0 && ch <= kNlmMaxCh && C > 0 && S > 0, "nlm_apply: bad sizes");
+  const size_t smem = (2 * (size_t)S * ch + 2 * (size_t)ch * C) * sizeof(float);
+  JABD_REQUIRE(smem <= 64 * 1024, "nlm_apply: LDS %zu > 64KiB", smem);
+  dim3 g((unsigned)cdiv((int64_t)h * w, 256), (unsigned)B);
+  nlm_apply_kernel<<<g, 256, smem, as_stream(stream)>>>(src, src_bs, src_ps, hs, ws, C, h, w, wq,
+                                                        bq, kpool, vpool, S, ch, wW, bW, lateral,
+                                                        out);
+  return check_launch("nlm_apply");
+}
+
+extern "C" int jabd_heads_f32(const float* x, int64_t x_bs, int32_t x_ps, int32_t B, int32_t HW,
+                              int32_t C, const float* wt, const float* bias, int64_t A,
+                              int64_t a_off, int32_t softmax, float* loc, float* conf,
+                              float* landm, jabd_stream_t stream) {
+  JABD_REQUIRE(x && wt && bias && loc && conf && landm, "heads: null pointer");
+  JABD_REQUIRE(C % 4 == 0 && x_ps % 4 == 0, "heads: C and pixel stride must be multiples of 4");
+  JABD_REQUIRE(a_off + 2 * (int64_t)HW <= A, "heads: anchor range out of bounds");
+  dim3 g((unsigned)cdiv(HW, 256), (unsigned)B);
+  heads_kernel<<<g, 256, kHeadOut * C * sizeof(float), as_stream(stream)>>>(
+      x, x_bs, x_ps, HW, C, wt, bias, A, a_off, softmax, loc, conf, landm);
+  return check_launch("heads");
+}
+
+namespace jabd {
+// torchvision resnet50 stem maxpool (F.max_pool2d(3, 2, 1)) on NHWC, float4 lanes.
+__global__ void maxpool_kernel(const float* __restrict__ x, int H, int W, int C, int OH, int OW,
+                               int k, int s, int pad, int64_t total4, float* __restrict__ y) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= total4) return;
+  const int C4 = C >> 2;
+  const int c4 = (int)(i % C4);
+  int64_t r = i / C4;
+  const int ow = (int)(r % OW);
+  r /= OW;
+  const int oh = (int)(r % OH);
+  const int b = (int)(r / OH);
+  float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+  for (int kh = 0; kh < k; ++kh) {
+    const int ih = oh * s - pad + kh;
+    if (ih < 0 || ih >= H) continue;
+    for (int kw = 0; kw < k; ++kw) {
+      const int iw = ow * s - pad + kw;
+      if (iw < 0 || iw >= W) continue;
+      const float4 v =
+          reinterpret_cast<const float4*>(x + (((int64_t)b * H + ih) * W + iw) * C)[c4];
+      // max_pool2d propagates NaN
+      m.x = (v.x > m.x || v.x != v.x) ? v.x : m.x;
+      m.y = (v.y > m.y || v.y != v.y) ? v.y : m.y;
+      m.z = (v.z > m.z || v.z != v.z) ? v.z : m.z;
+      m.w = (v.w > m.w || v.w != v.w) ? v.w : m.w;
+    }
+  }
+  reinterpret_cast<float4*>(y)[i] = m;
+}
+}  // namespace jabd
+
+extern "C" int jabd_maxpool_nhwc_f32(const float* x, int32_t B, int32_t H, int32_t W, int32_t C,
+                                     int32_t k, int32_t stride, int32_t pad, float* y,
+                                     jabd_stream_t stream) {
+  JABD_REQUIRE(x && y && B > 0 && H > 0 && W > 0 && C > 0 && C % 4 == 0 && k > 0 && stride > 0,
+               "maxpool: bad args");
+  const int OH = (H + 2 * pad - k) / stride + 1, OW = (W + 2 * pad - k) / stride + 1;
+  const int64_t total4 = (int64_t)B * OH * OW * (C / 4);
+  maxpool_kernel<<<(unsigned)cdiv(total4, 256), 256, 0, as_stream(stream)>>>(
+      x, H, W, C, OH, OW, k, stride, pad, total4, y);
+  return check_launch("maxpool");
+}

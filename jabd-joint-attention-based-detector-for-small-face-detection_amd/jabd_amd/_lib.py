@@ -26,6 +26,44 @@ c_size = ctypes.c_size_t
 c_vp = ctypes.c_void_p
 c_sizep = ctypes.POINTER(ctypes.c_size_t)
 
+c_i32 = ctypes.c_int32
+c_fp = ctypes.POINTER(ctypes.c_float)
+
+
+class ConvArgs(ctypes.Structure):
+    """Mirror of `jabd_conv_args` (include/jabd.h) — field order is the ABI."""
+    _fields_ = [
+        ("x", c_vp), ("x_bs", c_i64), ("x_ps", c_i32), ("x_c0", c_i32),
+        ("B", c_i32), ("H", c_i32), ("W", c_i32), ("Cin", c_i32),
+        ("x2", c_vp), ("x2_bs", c_i64), ("x2_ps", c_i32), ("Cin2", c_i32),
+        ("x2_W", c_i32), ("x2_stride", c_i32),
+        ("ascale", c_vp), ("ascale_bs", c_i64),
+        ("w", c_vp), ("bias", c_vp),
+        ("res", c_vp), ("res_bs", c_i64), ("res_ps", c_i32), ("res_c0", c_i32),
+        ("y", c_vp), ("y_bs", c_i64), ("y_ps", c_i32), ("y_c0", c_i32),
+        ("OH", c_i32), ("OW", c_i32), ("Cout", c_i32), ("Ntiles", c_i32), ("tn", c_i32),
+        ("Kc", c_i32),
+        ("KH", c_i32), ("KW", c_i32), ("stride", c_i32), ("pad", c_i32),
+        ("act", c_i32), ("slope", c_f32),
+        ("nchw_in", c_i32), ("reserved0", c_i32),
+        ("M", c_i64),
+    ]
+
+
+class DwArgs(ctypes.Structure):
+    """Mirror of `jabd_dw_args` (include/jabd.h)."""
+    _fields_ = [
+        ("x", c_vp), ("x_bs", c_i64), ("x_ps", c_i32), ("reserved0", c_i32),
+        ("B", c_i32), ("H", c_i32), ("W", c_i32), ("C", c_i32),
+        ("w", c_vp), ("bias", c_vp),
+        ("y", c_vp), ("y_bs", c_i64), ("y_ps", c_i32), ("reserved1", c_i32),
+        ("OH", c_i32), ("OW", c_i32), ("k", c_i32), ("stride", c_i32), ("pad", c_i32),
+        ("act", c_i32),
+        ("slope", c_f32), ("nblk", c_i32),
+        ("part", c_vp),
+    ]
+
+
 # name -> argtypes (every function returns int status unless listed in _RESTYPE)
 SIGNATURES = {
     "jabd_version": [],
@@ -47,8 +85,22 @@ SIGNATURES = {
     "jabd_multibox_loss_bwd_f32": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
                                    c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "jabd_multibox_loss_finalize_f32": [c_vp, c_vp, c_vp, c_vp],
+    "jabd_conv_pack_tn": [c_int],
+    "jabd_conv2d_nhwc_f32": [ctypes.POINTER(ConvArgs), c_vp],
+    "jabd_dw_nblk": [c_i64, c_i64, c_i64, c_i64],
+    "jabd_dwconv_nhwc_f32": [ctypes.POINTER(DwArgs), c_vp],
+    "jabd_channel_sum_f32": [c_vp, c_i64, c_i32, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp],
+    "jabd_eca_gate_f32": [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp],
+    "jabd_nlm_pool_f32": [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp,
+                          c_vp, c_vp, c_vp, c_i32, ctypes.POINTER(c_i32), c_i32, c_vp, c_vp,
+                          c_vp],
+    "jabd_nlm_apply_f32": [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp,
+                           c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "jabd_maxpool_nhwc_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp],
+    "jabd_heads_f32": [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i64, c_i64, c_i32,
+                       c_vp, c_vp, c_vp, c_vp],
 }
-_RESTYPE = {"jabd_version": ctypes.c_char_p}
+_RESTYPE = {"jabd_version": ctypes.c_char_p, "jabd_dw_nblk": ctypes.c_int64}
 
 _lock = threading.Lock()
 _lib = None

@@ -1,0 +1,219 @@
+"""NHWC fp32 layer primitives over libjabd (conv, depthwise, ECA, NLM, heads).
+
+Activations are torch tensors [B, H, W, C] (a channel slice of a wider
+tensor is described by (tensor, c0)).  Weights arrive pre-folded and
+pre-packed (see `pack_conv`); every call launches on torch's current stream
+and returns without synchronising.
+"""
+import ctypes
+
+import torch
+
+from ._lib import ConvArgs, DwArgs, call, lib
+
+ACT = {"none": 0, "relu": 1, "leaky": 2, "hswish": 3, "hsigmoid": 4, "sigmoid": 5}
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t):
+    return t.data_ptr() if t is not None else None
+
+
+def _check(name, t):
+    if not t.is_cuda or t.dtype != torch.float32:
+        raise RuntimeError(f"{name}: needs a float32 GPU tensor (no CPU fallback), got "
+                           f"{t.dtype} on {t.device}")
+
+
+# ----------------------------------------------------------------------------- packing
+class PackedConv:
+    """Weights of one implicit-GEMM conv in the MFMA fragment order.
+
+    w2d: [K, Cout] with k = (kh*KW + kw)*Cin + ci (+ K-concatenated rows).
+    Stored as float4 [Kc][Ntiles][64 lanes], lane = 16*g + j holding
+    W[16kc + 4g + e][16nt + j] for e = 0..3 (conv.hip header).
+    """
+
+    def __init__(self, w2d, bias, KH, KW, Cin, Cin2=0):
+        K, cout = w2d.shape
+        self.KH, self.KW, self.Cin, self.Cin2, self.Cout = KH, KW, Cin, Cin2, cout
+        self.tn = int(lib().jabd_conv_pack_tn(cout))
+        tiles = (cout + 15) // 16
+        self.Ntiles = (tiles + self.tn - 1) // self.tn * self.tn
+        self.Kc = (K + 15) // 16
+        wp = torch.zeros((self.Kc * 16, self.Ntiles * 16), dtype=torch.float32, device=w2d.device)
+        wp[:K, :cout] = w2d
+        # [Kc, g, e, Ntiles, j] -> [Kc, Ntiles, g, j, e]
+        wp = wp.view(self.Kc, 4, 4, self.Ntiles, 16).permute(0, 3, 1, 4, 2).contiguous()
+        self.w = wp
+        self.bias = bias.contiguous().float() if bias is not None else None
+
+
+def conv_weight_2d(weight):
+    """nn.Conv2d weight [Cout, Cin, KH, KW] -> [KH*KW*Cin, Cout] (tap-major)."""
+    cout, cin, kh, kw = weight.shape
+    return weight.permute(2, 3, 1, 0).reshape(kh * kw * cin, cout)
+
+
+def bn_fold(bn, conv_bias=None):
+    """Eval BatchNorm2d as (scale, shift) per channel; conv bias folded in."""
+    s = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+    t = bn.bias - bn.running_mean * s
+    if conv_bias is not None:
+        t = t + conv_bias * s
+    return s, t
+
+
+def pack_conv(conv, bn=None, extra=None):
+    """Fold (conv [+ bn]) [+ extra K-concatenated (w2d, shift)] into PackedConv."""
+    w2d = conv_weight_2d(conv.weight.detach().float())
+    cb = conv.bias.detach().float() if conv.bias is not None else None
+    if bn is not None:
+        s, t = bn_fold(bn, cb)
+        w2d = w2d * s[None, :]
+        bias = t
+    else:
+        bias = cb
+    cin = conv.weight.shape[1]
+    cin2 = 0
+    if extra is not None:
+        w2, t2 = extra
+        cin2 = w2.shape[0]
+        w2d = torch.cat([w2d, w2], 0)
+        bias = t2 if bias is None else bias + t2
+    kh, kw = conv.weight.shape[2], conv.weight.shape[3]
+    return PackedConv(w2d.detach(), bias.detach() if bias is not None else None, kh, kw, cin,
+                      cin2)
+
+
+def pack_dw(conv, bn):
+    """Depthwise conv + BN -> (w [k*k][C] tap-major, bias [C])."""
+    c, _, k, _ = conv.weight.shape
+    s, t = bn_fold(bn, conv.bias.detach().float() if conv.bias is not None else None)
+    w = (conv.weight.detach().float().view(c, k * k) * s[:, None]).t().contiguous()
+    return w, t.detach().contiguous()
+
+
+# ----------------------------------------------------------------------------- kernels
+def conv(x, pk, stride=1, pad=0, act="none", slope=0.0, ascale=None, x2=None, x2_stride=1,
+         res=None, out=None, out_c0=0, nchw_in=False, x_c0=0):
+    """Implicit-GEMM conv.  x [B,H,W,C*] NHWC (or NCHW input if nchw_in)."""
+    _check("conv.x", x)
+    if nchw_in:
+        B, cin, H, W = x.shape
+        x_bs, x_ps = cin * H * W, 1
+    else:
+        B, H, W, ctot = x.shape
+        x_bs, x_ps = H * W * ctot, ctot
+    OH = (H + 2 * pad - pk.KH) // stride + 1
+    OW = (W + 2 * pad - pk.KW) // stride + 1
+    if out is None:
+        out = torch.empty((B, OH, OW, pk.Cout), dtype=torch.float32, device=x.device)
+        out_c0 = 0
+    a = ConvArgs()
+    a.x, a.x_bs, a.x_ps, a.x_c0 = x.data_ptr(), x_bs, x_ps, x_c0
+    a.B, a.H, a.W, a.Cin = B, H, W, pk.Cin
+    if x2 is not None:
+        a.x2, a.x2_bs, a.x2_ps, a.Cin2 = x2.data_ptr(), x2.stride(0), x2.shape[3], pk.Cin2
+        a.x2_W, a.x2_stride = x2.shape[2], x2_stride
+    if ascale is not None:
+        a.ascale, a.ascale_bs = ascale.data_ptr(), ascale.shape[1]
+    a.w = pk.w.data_ptr()
+    a.bias = _ptr(pk.bias)
+    if res is not None:
+        a.res, a.res_bs, a.res_ps, a.res_c0 = res.data_ptr(), res.stride(0), res.shape[3], 0
+    a.y, a.y_bs, a.y_ps, a.y_c0 = out.data_ptr(), out.stride(0), out.shape[3], out_c0
+    a.OH, a.OW, a.Cout, a.Ntiles, a.tn, a.Kc = OH, OW, pk.Cout, pk.Ntiles, pk.tn, pk.Kc
+    a.KH, a.KW, a.stride, a.pad = pk.KH, pk.KW, stride, pad
+    a.act, a.slope = ACT[act], float(slope)
+    a.nchw_in = 1 if nchw_in else 0
+    call("jabd_conv2d_nhwc_f32", ctypes.byref(a), _stream())
+    return out
+
+
+def dw_nblk(B, OH, OW, C):
+    return int(lib().jabd_dw_nblk(B, OH, OW, C))
+
+
+def dwconv(x, w, bias, k, stride, act="none", slope=0.0, partials=False):
+    """Depthwise k x k conv (pad k//2) + folded BN + act; optional ECA partial sums."""
+    _check("dw.x", x)
+    B, H, W, C = x.shape
+    pad = k // 2
+    OH = (H + 2 * pad - k) // stride + 1
+    OW = (W + 2 * pad - k) // stride + 1
+    y = torch.empty((B, OH, OW, C), dtype=torch.float32, device=x.device)
+    part = None
+    a = DwArgs()
+    a.x, a.x_bs, a.x_ps = x.data_ptr(), x.stride(0), C
+    a.B, a.H, a.W, a.C = B, H, W, C
+    a.w, a.bias = w.data_ptr(), _ptr(bias)
+    a.y, a.y_bs, a.y_ps = y.data_ptr(), y.stride(0), C
+    a.OH, a.OW, a.k, a.stride, a.pad, a.act = OH, OW, k, stride, pad, ACT[act]
+    a.slope = float(slope)
+    if partials:
+        nb = dw_nblk(B, OH, OW, C)
+        part = torch.empty((B, nb, C), dtype=torch.float32, device=x.device)
+        a.nblk, a.part = nb, part.data_ptr()
+    call("jabd_dwconv_nhwc_f32", ctypes.byref(a), _stream())
+    return y, part
+
+
+def channel_sums(x, nblk=None):
+    B, H, W, C = x.shape
+    HW = H * W
+    if nblk is None:
+        nblk = max(1, min(64, HW // 256))
+    part = torch.empty((B, nblk, C), dtype=torch.float32, device=x.device)
+    call("jabd_channel_sum_f32", x.data_ptr(), x.stride(0), C, B, HW, C, nblk, part.data_ptr(),
+         _stream())
+    return part
+
+
+def eca_gate(part, hw, w1d, gate):
+    B, nblk, C = part.shape
+    scale = torch.empty((B, C), dtype=torch.float32, device=part.device)
+    call("jabd_eca_gate_f32", part.data_ptr(), nblk, B, C, hw, w1d.data_ptr(), w1d.numel(),
+         ACT[gate], scale.data_ptr(), _stream())
+    return scale
+
+
+def nlm_fused(src, lateral, nlm_w, sizes):
+    """lateral + NLM(nearest(src -> lateral's size)); all NHWC."""
+    B, hs, ws, C = src.shape
+    _, h, w, _ = lateral.shape
+    wq, bq, wk, bk, wv, bv, wW, bW = nlm_w
+    ch = wq.shape[0]
+    S = sum(s * s for s in sizes)
+    kp = torch.empty((B, S, ch), dtype=torch.float32, device=src.device)
+    vp = torch.empty_like(kp)
+    arr = (ctypes.c_int32 * len(sizes))(*sizes)
+    call("jabd_nlm_pool_f32", src.data_ptr(), src.stride(0), C, B, hs, ws, C, h, w,
+         wk.data_ptr(), bk.data_ptr(), wv.data_ptr(), bv.data_ptr(), ch, arr, len(sizes),
+         kp.data_ptr(), vp.data_ptr(), _stream())
+    out = torch.empty_like(lateral)
+    call("jabd_nlm_apply_f32", src.data_ptr(), src.stride(0), C, B, hs, ws, C, h, w,
+         wq.data_ptr(), bq.data_ptr(), kp.data_ptr(), vp.data_ptr(), S, ch, wW.data_ptr(),
+         bW.data_ptr(), lateral.data_ptr(), out.data_ptr(), _stream())
+    return out
+
+
+def maxpool(x, k=3, stride=2, pad=1):
+    B, H, W, C = x.shape
+    OH = (H + 2 * pad - k) // stride + 1
+    OW = (W + 2 * pad - k) // stride + 1
+    y = torch.empty((B, OH, OW, C), dtype=torch.float32, device=x.device)
+    call("jabd_maxpool_nhwc_f32", x.data_ptr(), B, H, W, C, k, stride, pad, y.data_ptr(),
+         _stream())
+    return y
+
+
+def heads(x, wt, bias, loc, conf, landm, a_off, softmax):
+    B, H, W, C = x.shape
+    A = loc.shape[1]
+    call("jabd_heads_f32", x.data_ptr(), x.stride(0), C, B, H * W, C, wt.data_ptr(),
+         bias.data_ptr(), A, a_off, 1 if softmax else 0, loc.data_ptr(), conf.data_ptr(),
+         landm.data_ptr(), _stream())

@@ -1,0 +1,121 @@
+"""JABD-MobileNetV3 RetinaFace — drop-in for the reference
+nets/retinaface_r.py:17-343 (same class names, constructor signature and
+state_dict keys).  `RetinaFace.forward(x[B,3,H,W] fp32 GPU)` runs the whole
+detector as one fused HIP plan (jabd_amd/engine.py) and returns
+(loc [B,A,4], conf [B,A,2] (softmaxed iff mode != 'train'), landm [B,A,10]).
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from nets._getter import IntermediateLayerGetter
+from nets.layers import SSH, conv_bn, conv_bn1X1, conv_bn_no_relu  # noqa: F401
+from nets.mobilenetV3 import MobileNetV3_Large_eca
+
+
+class ClassHead(nn.Module):
+    def __init__(self, inchannels=512, num_anchors=2):
+        super().__init__()
+        self.num_anchors = num_anchors
+        self.conv1x1 = nn.Conv2d(inchannels, num_anchors * 2, kernel_size=(1, 1), stride=1,
+                                 padding=0)
+
+
+class BboxHead(nn.Module):
+    def __init__(self, inchannels=512, num_anchors=2):
+        super().__init__()
+        self.conv1x1 = nn.Conv2d(inchannels, num_anchors * 4, kernel_size=(1, 1), stride=1,
+                                 padding=0)
+
+
+class LandmarkHead(nn.Module):
+    def __init__(self, inchannels=512, num_anchors=2):
+        super().__init__()
+        self.conv1x1 = nn.Conv2d(inchannels, num_anchors * 10, kernel_size=(1, 1), stride=1,
+                                 padding=0)
+
+
+class PSPModule(nn.Module):
+    """Adaptive-average pools at `sizes`, concatenated (reference :85-104)."""
+
+    def __init__(self, sizes=(1, 3, 6, 8), dimension=2):
+        super().__init__()
+        self.sizes = tuple(sizes)
+        self.stages = nn.ModuleList([nn.AdaptiveAvgPool2d((s, s)) for s in sizes])
+
+
+class NLM(nn.Module):
+    """PSP-pooled non-local block, the CSAF attention (reference :107-152)."""
+
+    def __init__(self, in_channels, scale=1, psp_size=(1, 4, 8, 12), ch=4):
+        super().__init__()
+        if scale != 1:
+            raise NotImplementedError("NLM scale > 1 is not used by any JABD model")
+        self.scale, self.in_channels, self.ch = scale, in_channels, ch
+        self.pool = nn.MaxPool2d(kernel_size=(scale, scale))
+        self.f_query = nn.Conv2d(in_channels, ch, kernel_size=1)
+        self.f_key = nn.Conv2d(in_channels, ch, kernel_size=1)
+        self.f_value = nn.Conv2d(in_channels, ch, kernel_size=1)
+        self.psp = PSPModule(psp_size)
+        self.W = nn.Conv2d(ch, in_channels, kernel_size=1)
+        nn.init.constant_(self.W.weight, 0)
+        nn.init.constant_(self.W.bias, 0)
+
+
+class FPN(nn.Module):
+    def __init__(self, in_channels_list, out_channels):
+        super().__init__()
+        self.leaky = 0.1 if out_channels <= 64 else 0.0
+        self.output1 = conv_bn1X1(in_channels_list[0], out_channels, stride=1, leaky=self.leaky)
+        self.output2 = conv_bn1X1(in_channels_list[1], out_channels, stride=1, leaky=self.leaky)
+        self.output3 = conv_bn1X1(in_channels_list[2], out_channels, stride=1, leaky=self.leaky)
+        self.merge1 = conv_bn(out_channels, out_channels, leaky=self.leaky)
+        self.merge2 = conv_bn(out_channels, out_channels, leaky=self.leaky)
+        self.nlm = NLM(40)
+
+
+class eca_block(nn.Module):
+    """Head ECA with a Sigmoid gate (reference :208-224)."""
+    gate = "sigmoid"
+
+    def __init__(self, channel, b=1, gamma=2):
+        super().__init__()
+        k = int(abs((math.log(channel, 2) + b) / gamma))
+        k = k if k % 2 else k + 1
+        self.avg_pool = nn.AdaptiveAvgPool2d(1)
+        self.conv = nn.Conv1d(1, 1, kernel_size=k, padding=(k - 1) // 2, bias=False)
+        self.sigmoid = nn.Sigmoid()
+        self.Hsigmoid = nn.Hardsigmoid()
+
+
+class RetinaFace(nn.Module):
+    def __init__(self, cfg=None, pretrained=False, mode="train"):
+        super().__init__()
+        if cfg["name"] != "mobilenet0.25":
+            raise ValueError("nets.retinaface_r.RetinaFace is the JABD-MobileNetV3 model "
+                             "(cfg_mnet); use nets.retinaface_eca_nonlocal for ResNet-50")
+        if pretrained:
+            raise RuntimeError("the reference's pretrained backbone checkpoint is not shipped")
+        backbone = MobileNetV3_Large_eca()
+        self.body = IntermediateLayerGetter(backbone, cfg["return_layers"])
+        c = cfg["in_channel"]
+        self.fpn = FPN([c * 2, c * 4, c * 8], cfg["out_channel"])
+        self.ssh1 = SSH(cfg["out_channel"], cfg["out_channel"])
+        self.ssh2 = SSH(cfg["out_channel"], cfg["out_channel"])
+        self.ssh3 = SSH(cfg["out_channel"], cfg["out_channel"])
+        oc = cfg["out_channel"]
+        self.ClassHead = nn.ModuleList([ClassHead(oc, 2) for _ in range(3)])
+        self.BboxHead = nn.ModuleList([BboxHead(oc, 2) for _ in range(3)])
+        self.LandmarkHead = nn.ModuleList([LandmarkHead(oc, 2) for _ in range(3)])
+        self.eca_40 = eca_block(40)
+        self.eca_80 = eca_block(80)
+        self.eca_160 = eca_block(160)
+        self.eca_fpn = eca_block(40)
+        self.mode = mode
+        self.cfg = cfg
+        self._engine = None
+
+    def forward(self, inputs):
+        from jabd_amd.engine import get_engine
+        return get_engine(self, "mnv3").forward(inputs)

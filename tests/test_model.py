@@ -1,0 +1,86 @@
+"""A1-A5 detector forward: product modules vs the oracle restatement.
+
+CPU: the product modules carry the reference's state_dict layout (the
+oracle, written from the reference text, finds every weight it needs).
+GPU: eval-mode forward of the fused HIP plan against the oracle in fp32
+(tolerance: max-abs error <= 1e-3 of the output's max magnitude, per
+north-star "logits within 1e-3 relative fp32").
+"""
+import pytest
+import torch
+
+from _util import init_for_parity, rel_err
+from oracle import model_ref
+
+TOL = 1e-3
+
+
+def _mnv3():
+    from nets.retinaface_r import RetinaFace
+    from utils.config import cfg_mnet
+    return init_for_parity(RetinaFace(cfg=cfg_mnet, mode="eval"), seed=1).eval()
+
+
+def _r50():
+    from nets.retinaface_eca_nonlocal import RetinaFace
+    from utils.config import cfg_re50
+    return init_for_parity(RetinaFace(cfg=cfg_re50, mode="eval"), seed=2).eval()
+
+
+def test_mnv3_state_dict_layout():
+    m = _mnv3()
+    sd = m.state_dict()
+    for k in ("body.conv1.weight", "body.layer1.0.conv1.weight", "body.layer1.3.se.se.1.weight",
+              "body.layer1.3.skip.2.bias", "body.layer3.4.eca.conv.weight",
+              "fpn.nlm.f_query.weight", "fpn.nlm.W.bias", "ssh3.conv7x7_3.1.running_var",
+              "ClassHead.2.conv1x1.bias", "eca_fpn.conv.weight", "eca_160.conv.weight"):
+        assert k in sd, k
+    assert not any(k.startswith("body.conv2") or k.startswith("body.linear") for k in sd)
+    with torch.no_grad():  # the oracle consumes exactly these keys
+        loc, conf, landm = model_ref.retinaface_mnv3(sd, torch.randn(1, 3, 64, 64))
+    assert loc.shape == (1, 2 * (8 * 8 + 4 * 4 + 2 * 2), 4)
+    assert conf.shape[-1] == 2 and landm.shape[-1] == 10
+
+
+def test_r50_state_dict_layout():
+    m = _r50()
+    sd = m.state_dict()
+    for k in ("body.layer2.0.downsample.0.weight", "body.layer4.2.bn3.running_mean",
+              "fpn.Nlm.f_key.bias", "Nlm.W.weight", "IouHead.2.conv1x1.weight",
+              "eca_256.conv.weight"):
+        assert k in sd, k
+    assert sd["eca_256.conv.weight"].shape[-1] == 7
+    with torch.no_grad():
+        loc, _, _ = model_ref.retinaface_r50(sd, torch.randn(1, 3, 64, 64))
+    assert loc.shape == (1, 2 * (8 * 8 + 4 * 4 + 2 * 2), 4)
+
+
+def _compare(model, fn, x, cuda, mode):
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    with torch.no_grad():
+        ref = fn(sd, x, mode)
+    model.mode = mode
+    mg = model.to(cuda)
+    with torch.no_grad():
+        got = mg(x.to(cuda))
+    for g, r, name in zip(got, ref, ("loc", "conf", "landm")):
+        assert g.shape == r.shape, name
+        e = rel_err(g, r)
+        assert e < TOL, f"{name}: rel err {e:.2e}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(2, 128, 128), (1, 96, 160), (1, 104, 136)])
+@pytest.mark.parametrize("mode", ["eval", "train"])
+def test_mnv3_forward_parity(cuda, shape, mode):
+    B, H, W = shape
+    x = torch.randn(B, 3, H, W, generator=torch.Generator().manual_seed(H)) * 50
+    _compare(_mnv3(), model_ref.retinaface_mnv3, x, cuda, mode)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(1, 128, 128), (2, 96, 160)])
+def test_r50_forward_parity(cuda, shape):
+    B, H, W = shape
+    x = torch.randn(B, 3, H, W, generator=torch.Generator().manual_seed(W)) * 50
+    _compare(_r50(), model_ref.retinaface_r50, x, cuda, "eval")
