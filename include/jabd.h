@@ -179,6 +179,12 @@ typedef struct jabd_conv_args {
 int jabd_conv_pack_tn(int cout);
 int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t stream);
 
+/* A1 MobileNetV3 stem — nets/mobilenetV3.py:455-457,511: conv3x3/s2/p1 3->16
+ * on the NCHW input [B,3,H,W] with folded BN (w [27][16] tap-major, bias [16])
+ * and activation, written NHWC [B,OH,OW,16]. */
+int jabd_stem_nchw_f32(const float* x, int32_t B, int32_t H, int32_t W, const float* w,
+                       const float* bias, int32_t act, float* y, jabd_stream_t stream);
+
 /* A1 depthwise k x k conv (+ folded BN + act) — nets/mobilenetV3.py:105-108
  * and the stride-2 skip branches :126-137.  w [k*k][C] (tap-major), bias [C].
  * part (nullable): per-(image, block, channel) sums of the activated output,
@@ -209,15 +215,16 @@ int jabd_eca_gate_f32(const float* part, int64_t nblk, int64_t B, int64_t C, int
 
 /* A3 CSAF non-local block — nets/retinaface_r.py:85-152 + the FPN's nearest
  * up-sample and add (:192-203).  x = nearest(src [B,hs,ws,C] -> h x w).
- * nlm_pool: kpool/vpool [B][S][ch] = PSP adaptive-avg-pools (sizes[]) of
- *   f_key(x) / f_value(x)  (wk/wv [ch][C], bk/bv [ch]).
+ * nlm_pool: kpool/vpool [B][S][ch] = PSP adaptive-avg-pools (sizes[], host
+ *   array) of f_key(x) / f_value(x)  (wk/wv [ch][C], bk/bv [ch]); kv_ws is
+ *   scratch [B][hs*ws][2*ch].  Built for ch == 4 (the JABD NLM).
  * nlm_apply: out = lateral + (W·softmax_S(q·k)·v + bW + x), q = f_query(x),
  *   lateral/out [B,h,w,C] NHWC (may alias). */
 int jabd_nlm_pool_f32(const float* src, int64_t src_bs, int32_t src_ps, int32_t B, int32_t hs,
                       int32_t ws, int32_t C, int32_t h, int32_t w, const float* wk,
                       const float* bk, const float* wv, const float* bv, int32_t ch,
                       const int32_t* sizes, int32_t nsizes, float* kpool, float* vpool,
-                      jabd_stream_t stream);
+                      float* kv_ws, jabd_stream_t stream);
 int jabd_nlm_apply_f32(const float* src, int64_t src_bs, int32_t src_ps, int32_t B, int32_t hs,
                        int32_t ws, int32_t C, int32_t h, int32_t w, const float* wq,
                        const float* bq, const float* kpool, const float* vpool, int32_t S,

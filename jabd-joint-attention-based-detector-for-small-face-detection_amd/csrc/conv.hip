@@ -120,26 +120,30 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
   const int g = lane >> 4, j = lane & 15;
   const int nblk_n = p.Ntiles / TN;
   // blocks of the same M range are adjacent -> share A through L2
-  const int64_t bid = blockIdx.x;
-  const int nb = (int)(bid % nblk_n);
-  const int64_t mb = bid / nblk_n;
-  const int64_t m_wave = (mb * 4 + wave) * (16 * TM);
-  const int64_t OHW = (int64_t)p.OH * p.OW;
+  const int bid = blockIdx.x;
+  const int nb = bid % nblk_n;
+  const int mb = bid / nblk_n;
+  const int m_wave = (mb * 4 + wave) * (16 * TM);
+  const int OHW = p.OH * p.OW;  // host guarantees M < 2^31
 
-  // per-lane A pixels (row = lane&15 of each 16-row subtile)
+  // per-lane pixel of each 16-pixel subtile (column j of the MFMA tile)
   int pb[TM], poh[TM], pow_[TM];
   bool pv[TM];
 #pragma unroll
   for (int t = 0; t < TM; ++t) {
-    int64_t m = m_wave + t * 16 + j;
+    const int m = m_wave + t * 16 + j;
     pv[t] = m < p.M;
-    int64_t mm = pv[t] ? m : 0;
-    pb[t] = (int)(mm / OHW);
-    int64_t r = mm - (int64_t)pb[t] * OHW;
-    poh[t] = (int)(r / p.OW);
-    pow_[t] = (int)(r - (int64_t)poh[t] * p.OW);
+    const int mm = pv[t] ? m : 0;
+    pb[t] = mm / OHW;
+    const int r = mm - pb[t] * OHW;
+    poh[t] = r / p.OW;
+    pow_[t] = r - poh[t] * p.OW;
   }
 
+  // acc[t][u] = MFMA tile with rows = output channels, columns = pixels:
+  // operand A = packed weights (row n = lane&15), operand B = activations
+  // (column m = lane&15), so each lane ends up holding 4 consecutive output
+  // channels of one pixel -> one 16-byte store per tile.
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int t = 0; t < TM; ++t)
@@ -169,10 +173,10 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
     for (int t = 0; t < TM; ++t) {
 #pragma unroll
       for (int u = 0; u < TN; ++u) {
-        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[t].x, b_cur[u].x, acc[t][u], 0, 0, 0);
-        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[t].y, b_cur[u].y, acc[t][u], 0, 0, 0);
-        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[t].z, b_cur[u].z, acc[t][u], 0, 0, 0);
-        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[t].w, b_cur[u].w, acc[t][u], 0, 0, 0);
+        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(b_cur[u].x, a_cur[t].x, acc[t][u], 0, 0, 0);
+        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(b_cur[u].y, a_cur[t].y, acc[t][u], 0, 0, 0);
+        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(b_cur[u].z, a_cur[t].z, acc[t][u], 0, 0, 0);
+        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(b_cur[u].w, a_cur[t].w, acc[t][u], 0, 0, 0);
       }
     }
     if (more) {
@@ -183,24 +187,71 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
     }
   }
 
-  // epilogue: acc[t][u][r] = Y[m_wave + 16t + 4g + r][16(nb*TN+u) + j]
-#pragma unroll
-  for (int u = 0; u < TN; ++u) {
-    const int n = (nb * TN + u) * 16 + j;
-    if (n >= p.Cout) continue;
-    const float bn = p.bias ? p.bias[n] : 0.f;
+  // epilogue: acc[t][u][r] = Y[pixel m_wave + 16t + j][channel 16(nb*TN+u) + 4g + r]
+  const bool v4 = (p.reserved0 & 1) != 0;  // host: every channel offset/stride % 4 == 0
+  if (v4) {
+    // Stage each 16-pixel x 16*TN-channel subtile through LDS so every store
+    // instruction writes whole 16*TN-float pixel rows (1 KB contiguous when
+    // the tile spans the full channel range) instead of 16 scattered 64-B pieces.
+    constexpr int LDW = 16 * TN + 4;
+    __shared__ float s_epi[4 * 16 * LDW];
+    float* sm = s_epi + wave * 16 * LDW;
 #pragma unroll
     for (int t = 0; t < TM; ++t) {
 #pragma unroll
+      for (int u = 0; u < TN; ++u)
+        *reinterpret_cast<f32x4*>(sm + j * LDW + 16 * u + 4 * g) = acc[t][u];
+      const int64_t pix = (int64_t)poh[t] * p.OW + pow_[t];
+      const long long yoff = pv[t] ? (long long)((int64_t)pb[t] * p.y_bs + pix * p.y_ps + p.y_c0) : -1;
+      const long long roff =
+          p.res ? (long long)((int64_t)pb[t] * p.res_bs + pix * p.res_ps + p.res_c0) : 0;
+      __syncthreads();
+#pragma unroll
+      for (int f0 = 0; f0 < 16 * 4 * TN; f0 += 64) {
+        const int f = f0 + lane;
+        const int q = f / (4 * TN), c4 = f - q * (4 * TN);
+        // shuffles stay outside the divergent branch (an inactive source lane reads as 0)
+        const long long yo = __shfl(yoff, q);
+        const long long ro = __shfl(roff, q);
+        const int n0 = nb * TN * 16 + 4 * c4;
+        if (yo >= 0 && n0 < p.Cout) {
+          float4 v = *reinterpret_cast<const float4*>(sm + q * LDW + 4 * c4);
+          if (p.bias) {
+            const float4 bb = *reinterpret_cast<const float4*>(p.bias + n0);
+            v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
+          }
+          if (p.res) {
+            const float4 rr = *reinterpret_cast<const float4*>(p.res + ro + n0);
+            v.x += rr.x; v.y += rr.y; v.z += rr.z; v.w += rr.w;
+          }
+          v.x = act_apply(v.x, p.act, p.slope);
+          v.y = act_apply(v.y, p.act, p.slope);
+          v.z = act_apply(v.z, p.act, p.slope);
+          v.w = act_apply(v.w, p.act, p.slope);
+          *reinterpret_cast<float4*>(p.y + yo + n0) = v;
+        }
+      }
+      __syncthreads();
+    }
+    return;
+  }
+#pragma unroll
+  for (int t = 0; t < TM; ++t) {
+    if (!pv[t]) continue;
+    const int64_t pix = (int64_t)poh[t] * p.OW + pow_[t];
+    float* yrow = p.y + (int64_t)pb[t] * p.y_bs + pix * p.y_ps + p.y_c0;
+    const float* rrow =
+        p.res ? p.res + (int64_t)pb[t] * p.res_bs + pix * p.res_ps + p.res_c0 : nullptr;
+#pragma unroll
+    for (int u = 0; u < TN; ++u) {
+      const int n0 = (nb * TN + u) * 16 + 4 * g;
+#pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t m = m_wave + t * 16 + 4 * g + r;
-        if (m >= p.M) continue;
-        const int b = (int)(m / OHW);
-        const int64_t pix = m - (int64_t)b * OHW;
-        float v = acc[t][u][r] + bn;
-        if (p.res) v += p.res[(int64_t)b * p.res_bs + pix * p.res_ps + p.res_c0 + n];
-        v = act_apply(v, p.act, p.slope);
-        p.y[(int64_t)b * p.y_bs + pix * p.y_ps + p.y_c0 + n] = v;
+        const int n = n0 + r;
+        if (n >= p.Cout) break;
+        float v = acc[t][u][r] + (p.bias ? p.bias[n] : 0.f);
+        if (rrow) v += rrow[n];
+        yrow[n] = act_apply(v, p.act, p.slope);
       }
     }
   }
@@ -256,6 +307,15 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
   const int tiles = (a.Cout + 15) / 16;
   JABD_REQUIRE(a.Ntiles >= tiles, "conv: Ntiles=%d < %d", a.Ntiles, tiles);
   a.M = (int64_t)a.B * a.OH * a.OW;
+  JABD_REQUIRE(a.M < (int64_t)0x7fffffff, "conv: B*OH*OW must be < 2^31");
+  {
+    const uintptr_t al = reinterpret_cast<uintptr_t>(a.y) | reinterpret_cast<uintptr_t>(a.bias) |
+                         reinterpret_cast<uintptr_t>(a.res);
+    const bool v4 = a.Cout % 4 == 0 && a.y_ps % 4 == 0 && a.y_c0 % 4 == 0 && a.y_bs % 4 == 0 &&
+                    (!a.res || (a.res_ps % 4 == 0 && a.res_c0 % 4 == 0 && a.res_bs % 4 == 0)) &&
+                    (al & 15) == 0;
+    a.reserved0 = v4 ? 1 : 0;
+  }
   const bool vec4 = !a.nchw_in && a.Cin % 4 == 0 && a.x_ps % 4 == 0 && a.x_c0 % 4 == 0 &&
                     (reinterpret_cast<uintptr_t>(a.x) & 15) == 0;
   hipStream_t st = as_stream(stream);
@@ -272,4 +332,64 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
       set_error("conv: unsupported tn=%d", tn);
       return JABD_EINVAL;
   }
+}
+
+// ---------------------------------------------------------------------------
+// MobileNetV3 stem: conv3x3/s2/p1, 3 -> 16 channels, read straight from the
+// NCHW network input (layout conversion fused), folded BN + activation,
+// NHWC output.  One thread per output pixel; weights broadcast from LDS.
+// Reference: nets/mobilenetV3.py:455-457,511 (conv1 + bn1 + hs1).
+// ---------------------------------------------------------------------------
+namespace jabd {
+constexpr int kStemOut = 16;
+
+__global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ x, int H, int W,
+                                                   int OH, int OW, const float* __restrict__ w,
+                                                   const float* __restrict__ bias, int act,
+                                                   float* __restrict__ y) {
+  __shared__ float sw[27 * kStemOut];
+  __shared__ float sb[kStemOut];
+  for (int t = threadIdx.x; t < 27 * kStemOut; t += blockDim.x) sw[t] = w[t];
+  if (threadIdx.x < kStemOut) sb[threadIdx.x] = bias[threadIdx.x];
+  __syncthreads();
+  const int b = blockIdx.z, oh = blockIdx.y;
+  const int ow = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ow >= OW) return;
+  float o[kStemOut];
+#pragma unroll
+  for (int n = 0; n < kStemOut; ++n) o[n] = sb[n];
+  const float* xb = x + (int64_t)b * 3 * H * W;
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int ih = 2 * oh - 1 + kh;
+    if (ih < 0 || ih >= H) continue;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int iw = 2 * ow - 1 + kw;
+      if (iw < 0 || iw >= W) continue;
+#pragma unroll
+      for (int ci = 0; ci < 3; ++ci) {
+        const float v = xb[((int64_t)ci * H + ih) * W + iw];
+        const float* wr = sw + ((kh * 3 + kw) * 3 + ci) * kStemOut;
+#pragma unroll
+        for (int n = 0; n < kStemOut; ++n) o[n] = fmaf(wr[n], v, o[n]);
+      }
+    }
+  }
+  float4* yp = reinterpret_cast<float4*>(y + (((int64_t)b * OH + oh) * OW + ow) * kStemOut);
+#pragma unroll
+  for (int q = 0; q < kStemOut / 4; ++q)
+    yp[q] = make_float4(act_apply(o[4 * q], act, 0.f), act_apply(o[4 * q + 1], act, 0.f),
+                        act_apply(o[4 * q + 2], act, 0.f), act_apply(o[4 * q + 3], act, 0.f));
+}
+}  // namespace jabd
+
+extern "C" int jabd_stem_nchw_f32(const float* x, int32_t B, int32_t H, int32_t W,
+                                  const float* w, const float* bias, int32_t act, float* y,
+                                  jabd_stream_t stream) {
+  JABD_REQUIRE(x && w && bias && y && B > 0 && H > 0 && W > 0, "stem: bad args");
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  dim3 g((unsigned)cdiv(OW, 128), (unsigned)OH, (unsigned)B);
+  stem_kernel<<<g, 128, 0, as_stream(stream)>>>(x, H, W, OH, OW, w, bias, act, y);
+  return check_launch("stem");
 }

@@ -26,8 +26,16 @@ __global__ __launch_bounds__(kSumThreads) void channel_sum_kernel(
     const int r = threadIdx.x / min(C, kSumThreads);
     const int nrows = C >= kSumThreads ? 1 : rows;
     float s = 0.f;
-    if (r < nrows && c < C)
-      for (int64_t q = p0 + r; q < p1; q += nrows) s += xb[q * x_ps + c];
+    if (r < nrows && c < C) {
+      float s4[4] = {0.f, 0.f, 0.f, 0.f};
+      int64_t q = p0 + r;
+      for (; q + 3 * nrows < p1; q += 4 * nrows) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s4[u] += xb[(q + u * nrows) * x_ps + c];
+      }
+      for (; q < p1; q += nrows) s4[0] += xb[q * x_ps + c];
+      s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    }
     __syncthreads();
     if (r < nrows && c < C) red[r * min(C, kSumThreads) + (c - c0)] = s;
     __syncthreads();
@@ -46,10 +54,17 @@ __global__ void eca_gate_kernel(const float* __restrict__ part, int64_t nblk, in
                                 float* __restrict__ scale) {
   extern __shared__ float mean[];
   const int b = blockIdx.x;
+  const float* pb = part + (int64_t)b * nblk * C;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float s = 0.f;
-    for (int64_t q = 0; q < nblk; ++q) s += part[((int64_t)b * nblk + q) * C + c];
-    mean[c] = s * inv_hw;
+    // 8 independent accumulators keep 8 loads in flight (fixed order -> deterministic)
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int64_t q = 0;
+    for (; q + 8 <= nblk; q += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s[u] += pb[(q + u) * C + c];
+    }
+    for (; q < nblk; ++q) s[0] += pb[q * C + c];
+    mean[c] = (((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]))) * inv_hw;
   }
   __syncthreads();
   const int h = (k - 1) / 2;
@@ -74,139 +89,176 @@ __device__ __forceinline__ int nearest_src(int dst, int in, int out) {
   return s < in - 1 ? s : in - 1;
 }
 
-constexpr int kNlmMaxCh = 64;
 struct NlmSizes {
   int n;
   int v[8];
 };
-constexpr int kNlmMaxC = 512;
 
-// One workgroup per (bin s, image b): mean over the bin of f_key / f_value.
-__global__ __launch_bounds__(256) void nlm_pool_kernel(
-    const float* __restrict__ src, int64_t src_bs, int src_ps, int hs, int ws, int C, int h,
-    int w, const float* __restrict__ wk, const float* __restrict__ bk,
-    const float* __restrict__ wv, const float* __restrict__ bv, int ch, const NlmSizes sizes,
-    int S, float* __restrict__ kpool, float* __restrict__ vpool) {
-  const int nsizes = sizes.n;
+// kv[b][pix][0:CH] = f_key(x), [CH:2CH] = f_value(x) on the SOURCE grid (the
+// nearest up-sample only repeats source pixels, so projecting before the
+// gather gives identical values at 1/4 of the work).
+template <int CH>
+__global__ __launch_bounds__(256) void nlm_kv_kernel(const float* __restrict__ src, int64_t src_bs,
+                                                     int src_ps, int hsws, int C,
+                                                     const float* __restrict__ wk,
+                                                     const float* __restrict__ bk,
+                                                     const float* __restrict__ wv,
+                                                     const float* __restrict__ bv,
+                                                     float* __restrict__ kv) {
+  extern __shared__ float sw[];  // [2CH][C]
+  for (int t = threadIdx.x; t < CH * C; t += blockDim.x) {
+    sw[t] = wk[t];
+    sw[CH * C + t] = wv[t];
+  }
+  __syncthreads();
+  const int b = blockIdx.y;
+  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= hsws) return;
+  const float* xp = src + (int64_t)b * src_bs + (int64_t)pix * src_ps;
+  float o[2 * CH];
+#pragma unroll
+  for (int q = 0; q < CH; ++q) { o[q] = bk[q]; o[CH + q] = bv[q]; }
+  for (int c = 0; c < C; c += 4) {
+    const float4 x = *reinterpret_cast<const float4*>(xp + c);
+#pragma unroll
+    for (int q = 0; q < 2 * CH; ++q) {
+      const float* w = sw + q * C + c;
+      o[q] = fmaf(w[0], x.x, o[q]);
+      o[q] = fmaf(w[1], x.y, o[q]);
+      o[q] = fmaf(w[2], x.z, o[q]);
+      o[q] = fmaf(w[3], x.w, o[q]);
+    }
+  }
+  float* dst = kv + ((int64_t)b * hsws + pix) * (2 * CH);
+#pragma unroll
+  for (int q = 0; q < 2 * CH; ++q) dst[q] = o[q];
+}
+
+// One workgroup per (bin s, image b): adaptive-avg-pool bin of the
+// up-sampled kv map -> kpool/vpool [B][S][CH].
+template <int CH>
+__global__ __launch_bounds__(256) void nlm_pool_kernel(const float* __restrict__ kv, int hs, int ws,
+                                                       int h, int w, const NlmSizes sizes, int S,
+                                                       float* __restrict__ kpool,
+                                                       float* __restrict__ vpool) {
   const int s = blockIdx.x, b = blockIdx.y;
-  // locate the level and bin (sizes are tiny; scan)
   int base = 0, lvl = 0;
-  for (; lvl < nsizes; ++lvl) {
+  for (; lvl < sizes.n; ++lvl) {
     const int n = sizes.v[lvl] * sizes.v[lvl];
     if (s < base + n) break;
     base += n;
   }
   const int sz = sizes.v[lvl];
   const int bi = (s - base) / sz, bj = (s - base) % sz;
-  const int h0 = (bi * h) / sz, h1 = ((bi + 1) * h + sz - 1) / sz;  // AdaptiveAvgPool bins
+  const int h0 = (bi * h) / sz, h1 = ((bi + 1) * h + sz - 1) / sz;  // AdaptiveAvgPool2d bins
   const int w0 = (bj * w) / sz, w1 = ((bj + 1) * w + sz - 1) / sz;
   const int rw = w1 - w0;
   const int npix = (h1 - h0) * rw;
-  __shared__ float sw[2 * kNlmMaxCh * 64];  // weights staged in LDS when they fit
-  const bool wlds = 2 * ch * C <= 2 * kNlmMaxCh * 64;
-  if (wlds) {
-    for (int t = threadIdx.x; t < ch * C; t += blockDim.x) {
-      sw[t] = wk[t];
-      sw[ch * C + t] = wv[t];
-    }
+  const float* kb = kv + (int64_t)b * hs * ws * (2 * CH);
+  float a[2 * CH];
+#pragma unroll
+  for (int q = 0; q < 2 * CH; ++q) a[q] = 0.f;
+  for (int p = threadIdx.x; p < npix; p += blockDim.x) {
+    const int i = h0 + p / rw, jx = w0 + p % rw;
+    const float* v = kb + ((int64_t)nearest_src(i, hs, h) * ws + nearest_src(jx, ws, w)) * (2 * CH);
+#pragma unroll
+    for (int q = 0; q < 2 * CH; ++q) a[q] += v[q];
   }
+  __shared__ float red[2 * CH][257];
+#pragma unroll
+  for (int q = 0; q < 2 * CH; ++q) red[q][threadIdx.x] = a[q];
   __syncthreads();
-  const float* WK = wlds ? sw : wk;
-  const float* WV = wlds ? sw + ch * C : wv;
-  float ak[kNlmMaxCh], av[kNlmMaxCh];
-  for (int o = 0; o < ch; ++o) { ak[o] = 0.f; av[o] = 0.f; }
-  const float* sb = src + (int64_t)b * src_bs;
-  for (int q = threadIdx.x; q < npix; q += blockDim.x) {
-    const int i = h0 + q / rw, jx = w0 + q % rw;
-    const float* xp = sb + ((int64_t)nearest_src(i, hs, h) * ws + nearest_src(jx, ws, w)) * src_ps;
-    for (int o = 0; o < ch; ++o) {
-      float kk = bk[o], vv = bv[o];
-      for (int c = 0; c < C; ++c) {
-        const float x = xp[c];
-        kk = fmaf(WK[o * C + c], x, kk);
-        vv = fmaf(WV[o * C + c], x, vv);
-      }
-      ak[o] += kk;
-      av[o] += vv;
-    }
-  }
-  __shared__ float red[256];
-  const float inv = 1.f / (float)npix;
-  for (int o = 0; o < ch; ++o) {
-    for (int pass = 0; pass < 2; ++pass) {
-      red[threadIdx.x] = pass ? av[o] : ak[o];
-      __syncthreads();
-      for (int st = 128; st > 0; st >>= 1) {
-        if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
-        __syncthreads();
-      }
-      if (threadIdx.x == 0) {
-        float* dst = pass ? vpool : kpool;
-        dst[((int64_t)b * S + s) * ch + o] = red[0] * inv;
-      }
-      __syncthreads();
-    }
+  if (threadIdx.x < 2 * CH) {
+    const int q = threadIdx.x;
+    float t = 0.f;
+    for (int u = 0; u < 256; ++u) t += red[q][u];
+    const float avg = t / (float)npix;
+    if (q < CH) kpool[((int64_t)b * S + s) * CH + q] = avg;
+    else vpool[((int64_t)b * S + s) * CH + (q - CH)] = avg;
   }
 }
 
-// Per pixel: out = lateral + (W · softmax(q·K) V + bW + x)
+// Per pixel: out = lateral + (W · softmax_S(q·K) V + bW + x)
+template <int CH>
 __global__ __launch_bounds__(256) void nlm_apply_kernel(
     const float* __restrict__ src, int64_t src_bs, int src_ps, int hs, int ws, int C, int h,
     int w, const float* __restrict__ wq, const float* __restrict__ bq,
-    const float* __restrict__ kpool, const float* __restrict__ vpool, int S, int ch,
-    const float* __restrict__ wW, const float* __restrict__ bW, const float* lateral,
-    float* out) {
-  extern __shared__ float sm[];  // K [S][ch], V [S][ch], wq [ch][C], wW [C][ch]
+    const float* __restrict__ kpool, const float* __restrict__ vpool, int S,
+    const float* __restrict__ wW, const float* __restrict__ bW, const float* __restrict__ lateral,
+    float* __restrict__ out) {
+  extern __shared__ float sm[];  // K [S][CH], V [S][CH], wq [CH][C], wW [C][CH], bW [C]
   const int b = blockIdx.y;
   float* sK = sm;
-  float* sV = sK + S * ch;
-  float* sWq = sV + S * ch;
-  float* sWW = sWq + ch * C;
-  for (int t = threadIdx.x; t < S * ch; t += blockDim.x) {
-    sK[t] = kpool[(int64_t)b * S * ch + t];
-    sV[t] = vpool[(int64_t)b * S * ch + t];
+  float* sV = sK + S * CH;
+  float* sWq = sV + S * CH;
+  float* sWW = sWq + CH * C;
+  float* sbW = sWW + C * CH;
+  for (int t = threadIdx.x; t < S * CH; t += blockDim.x) {
+    sK[t] = kpool[(int64_t)b * S * CH + t];
+    sV[t] = vpool[(int64_t)b * S * CH + t];
   }
-  for (int t = threadIdx.x; t < ch * C; t += blockDim.x) {
+  for (int t = threadIdx.x; t < CH * C; t += blockDim.x) {
     sWq[t] = wq[t];
     sWW[t] = wW[t];
   }
+  for (int t = threadIdx.x; t < C; t += blockDim.x) sbW[t] = bW[t];
   __syncthreads();
-  const int64_t pix = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (pix >= (int64_t)h * w) return;
-  const int i = (int)(pix / w), jx = (int)(pix % w);
+  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= h * w) return;
+  const int i = pix / w, jx = pix - (pix / w) * w;
   const float* xp = src + (int64_t)b * src_bs +
                     ((int64_t)nearest_src(i, hs, h) * ws + nearest_src(jx, ws, w)) * src_ps;
-  float q[kNlmMaxCh];
-  for (int o = 0; o < ch; ++o) {
-    float a = bq[o];
-    for (int c = 0; c < C; ++c) a = fmaf(sWq[o * C + c], xp[c], a);
-    q[o] = a;
+  float q[CH];
+#pragma unroll
+  for (int o = 0; o < CH; ++o) q[o] = bq[o];
+  for (int c = 0; c < C; c += 4) {
+    const float4 x = *reinterpret_cast<const float4*>(xp + c);
+#pragma unroll
+    for (int o = 0; o < CH; ++o) {
+      const float* wr = sWq + o * C + c;
+      q[o] = fmaf(wr[0], x.x, q[o]);
+      q[o] = fmaf(wr[1], x.y, q[o]);
+      q[o] = fmaf(wr[2], x.z, q[o]);
+      q[o] = fmaf(wr[3], x.w, q[o]);
+    }
   }
-  // softmax over S with running max (two passes over LDS)
   float mx = -INFINITY;
   for (int s = 0; s < S; ++s) {
     float l = 0.f;
-    for (int o = 0; o < ch; ++o) l = fmaf(q[o], sK[s * ch + o], l);
+#pragma unroll
+    for (int o = 0; o < CH; ++o) l = fmaf(q[o], sK[s * CH + o], l);
     mx = fmaxf(mx, l);
   }
-  float den = 0.f;
-  float cx[kNlmMaxCh];
-  for (int o = 0; o < ch; ++o) cx[o] = 0.f;
+  float den = 0.f, cx[CH];
+#pragma unroll
+  for (int o = 0; o < CH; ++o) cx[o] = 0.f;
   for (int s = 0; s < S; ++s) {
     float l = 0.f;
-    for (int o = 0; o < ch; ++o) l = fmaf(q[o], sK[s * ch + o], l);
-    const float e = expf(l - mx);
+#pragma unroll
+    for (int o = 0; o < CH; ++o) l = fmaf(q[o], sK[s * CH + o], l);
+    const float e = __expf(l - mx);
     den += e;
-    for (int o = 0; o < ch; ++o) cx[o] = fmaf(e, sV[s * ch + o], cx[o]);
+#pragma unroll
+    for (int o = 0; o < CH; ++o) cx[o] = fmaf(e, sV[s * CH + o], cx[o]);
   }
   const float inv = 1.f / den;
-  for (int o = 0; o < ch; ++o) cx[o] *= inv;
+#pragma unroll
+  for (int o = 0; o < CH; ++o) cx[o] *= inv;
   const int64_t opix = ((int64_t)b * h * w + pix) * C;
-  for (int c = 0; c < C; ++c) {
-    float a = bW[c];
-    for (int o = 0; o < ch; ++o) a = fmaf(sWW[c * ch + o], cx[o], a);
-    const float v = a + xp[c];
-    out[opix + c] = lateral[opix + c] + v;
+  for (int c = 0; c < C; c += 4) {
+    const float4 x = *reinterpret_cast<const float4*>(xp + c);
+    const float4 lt = *reinterpret_cast<const float4*>(lateral + opix + c);
+    float v[4] = {x.x, x.y, x.z, x.w};
+    float lv[4] = {lt.x, lt.y, lt.z, lt.w};
+    float r[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float a = sbW[c + e];
+#pragma unroll
+      for (int o = 0; o < CH; ++o) a = fmaf(sWW[(c + e) * CH + o], cx[o], a);
+      r[e] = lv[e] + (a + v[e]);
+    }
+    *reinterpret_cast<float4*>(out + opix + c) = make_float4(r[0], r[1], r[2], r[3]);
   }
 }
 
@@ -292,10 +344,12 @@ extern "C" int jabd_nlm_pool_f32(const float* src, int64_t src_bs, int32_t src_p
                                  int32_t hs, int32_t ws, int32_t C, int32_t h, int32_t w,
                                  const float* wk, const float* bk, const float* wv,
                                  const float* bv, int32_t ch, const int32_t* sizes,
-                                 int32_t nsizes, float* kpool, float* vpool,
+                                 int32_t nsizes, float* kpool, float* vpool, float* kv_ws,
                                  jabd_stream_t stream) {
-  JABD_REQUIRE(src && wk && bk && wv && bv && sizes && kpool && vpool, "nlm_pool: null pointer");
-  JABD_REQUIRE(ch > 0 && ch <= kNlmMaxCh && C > 0 && C <= kNlmMaxC, "nlm_pool: ch/C out of range");
+  JABD_REQUIRE(src && wk && bk && wv && bv && sizes && kpool && vpool && kv_ws,
+               "nlm_pool: null pointer");
+  JABD_REQUIRE(ch == 4, "nlm_pool: only ch=4 (the JABD NLM) is built");
+  JABD_REQUIRE(C > 0 && C % 4 == 0 && src_ps % 4 == 0, "nlm_pool: C must be a multiple of 4");
   JABD_REQUIRE(nsizes > 0 && nsizes <= 8, "nlm_pool: nsizes");
   NlmSizes sz;
   sz.n = nsizes;
@@ -307,9 +361,14 @@ extern "C" int jabd_nlm_pool_f32(const float* src, int64_t src_bs, int32_t src_p
       S += sizes[i] * sizes[i];
     }
   }
-  dim3 g((unsigned)S, (unsigned)B);
-  nlm_pool_kernel<<<g, 256, 0, as_stream(stream)>>>(src, src_bs, src_ps, hs, ws, C, h, w, wk, bk,
-                                                    wv, bv, ch, sz, S, kpool, vpool);
+  hipStream_t st = as_stream(stream);
+  const size_t smem = 2 * (size_t)ch * C * sizeof(float);
+  JABD_REQUIRE(smem <= 64 * 1024, "nlm_pool: C too large");
+  dim3 g1((unsigned)cdiv((int64_t)hs * ws, 256), (unsigned)B);
+  nlm_kv_kernel<4><<<g1, 256, smem, st>>>(src, src_bs, src_ps, hs * ws, C, wk, bk, wv, bv, kv_ws);
+  if (int e = check_launch("nlm_kv")) return e;
+  dim3 g2((unsigned)S, (unsigned)B);
+  nlm_pool_kernel<4><<<g2, 256, 0, st>>>(kv_ws, hs, ws, h, w, sz, S, kpool, vpool);
   return check_launch("nlm_pool");
 }
 
@@ -321,13 +380,14 @@ extern "C" int jabd_nlm_apply_f32(const float* src, int64_t src_bs, int32_t src_
                                   jabd_stream_t stream) {
   JABD_REQUIRE(src && wq && bq && kpool && vpool && wW && bW && lateral && out,
                "nlm_apply: null pointer");
-  JABD_REQUIRE(ch > 0 && ch <= kNlmMaxCh && C > 0 && S > 0, "nlm_apply: bad sizes");
-  const size_t smem = (2 * (size_t)S * ch + 2 * (size_t)ch * C) * sizeof(float);
+  JABD_REQUIRE(ch == 4, "nlm_apply: only ch=4 (the JABD NLM) is built");
+  JABD_REQUIRE(C > 0 && C % 4 == 0 && src_ps % 4 == 0 && S > 0, "nlm_apply: bad sizes");
+  const size_t smem = (2 * (size_t)S * ch + 2 * (size_t)ch * C + C) * sizeof(float);
   JABD_REQUIRE(smem <= 64 * 1024, "nlm_apply: LDS %zu > 64KiB", smem);
   dim3 g((unsigned)cdiv((int64_t)h * w, 256), (unsigned)B);
-  nlm_apply_kernel<<<g, 256, smem, as_stream(stream)>>>(src, src_bs, src_ps, hs, ws, C, h, w, wq,
-                                                        bq, kpool, vpool, S, ch, wW, bW, lateral,
-                                                        out);
+  nlm_apply_kernel<4><<<g, 256, smem, as_stream(stream)>>>(src, src_bs, src_ps, hs, ws, C, h, w,
+                                                           wq, bq, kpool, vpool, S, wW, bW,
+                                                           lateral, out);
   return check_launch("nlm_apply");
 }
 

@@ -9,9 +9,11 @@
 //                    order (ties by lower row index, as torch's stable sort).
 //   3. nms_gather    sorted boxes (float4) + areas + original row ids.
 //   4. nms_mask      upper-triangular IoU bitmask, 64x64 tiles, one lane per
-//                    row box, column boxes broadcast from LDS.
-//   5. nms_scan      one workgroup per image walks the bitmask on the device
-//                    (suppressed-set in LDS), writes kept rows + count.
+//                    row box, column boxes broadcast from LDS; stored sparse:
+//                    the in-block word per row + a list of non-zero words.
+//   5. nms_scan      one workgroup per image walks the row blocks on the
+//                    device (suppressed-set bitset in LDS, next block's lists
+//                    prefetched), writes kept rows + count.
 // Compile with -ffp-contract=off: IoU must round exactly like the CPU kernel
 // (no FMA in (x2-x1)*(y2-y1) or inter/(a+b-inter)).
 #include <hipcub/hipcub.hpp>
@@ -68,7 +70,8 @@ __global__ void nms_gather(const uint64_t* __restrict__ sorted, int64_t total,
                            const float* __restrict__ boxes, int64_t box_stride,
                            int64_t box_bstride, const int* __restrict__ counts,
                            int batch, int64_t n, int img0, float4* __restrict__ sbox,
-                           float* __restrict__ sarea, int* __restrict__ sidx) {
+                           float* __restrict__ sarea, int* __restrict__ sidx,
+                           int* __restrict__ nanflag) {
   int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (p >= total) return;
   uint64_t k = sorted[p];
@@ -83,21 +86,29 @@ __global__ void nms_gather(const uint64_t* __restrict__ sorted, int64_t total,
   sbox[(int64_t)img * n + r] = make_float4(x1, y1, x2, y2);
   sarea[(int64_t)img * n + r] = (x2 - x1) * (y2 - y1);
   sidx[(int64_t)img * n + r] = row;
+  if (x1 != x1 || y1 != y1 || x2 != x2 || y2 != y2) atomicOr(&nanflag[img], 1);
 }
 
-// Offset (in u64 words) of row block rb in the per-image triangular mask.
-__device__ __host__ __forceinline__ int64_t tri_base(int64_t rb, int64_t nb) {
-  return 64 * (rb * nb - rb * (rb - 1) / 2);
+// Per-row sparse suppression lists.  Row i (sorted rank) of row block rb can
+// suppress boxes in at most nb-rb-1 later column blocks; its non-zero 64-bit
+// words are appended (any order: the scan ORs them) at
+//   ent[ent_base(rb) + (i - 64 rb) * (nb - rb - 1) + slot],  slot < nzcnt[i],
+// and its in-block word (column block rb, bits j > i) is diag[i].
+__device__ __host__ __forceinline__ int64_t ent_base(int64_t rb, int64_t nb) {
+  return 64 * (rb * (nb - 1) - rb * (rb - 1) / 2);
 }
 
 static constexpr int kColBlocksPerWave = 4;
 static constexpr int kWaves = 4;
 static constexpr int kColBlocksPerWG = kColBlocksPerWave * kWaves;
 
-// IoU of sorted box i (registers) against sorted box j, torchvision CPU order.
+// IoU(i, j) > thr with torchvision's CPU rounding.  inter/union is only
+// divided out when the pair is within 1e-4 of the threshold: far from it
+// the comparison of inter with thr*union (fp32, margin >> 2 ulp) already
+// decides the exact result.
 __device__ __forceinline__ bool iou_gt(float ix1, float iy1, float ix2, float iy2,
-                                       float iarea, float4 bj, float aj,
-                                       double thr, bool thr_nonneg) {
+                                       float iarea, float4 bj, float aj, double thr,
+                                       float thrf, bool thr_nonneg) {
   float xx1 = (ix1 < bj.x) ? bj.x : ix1;  // std::max(ix1, x1[j])
   float yy1 = (iy1 < bj.y) ? bj.y : iy1;
   float xx2 = (bj.z < ix2) ? bj.z : ix2;  // std::min(ix2, x2[j])
@@ -106,16 +117,25 @@ __device__ __forceinline__ bool iou_gt(float ix1, float iy1, float ix2, float iy
   float w = (0.f < dw) ? dw : 0.f;        // std::max(0, xx2 - xx1)
   float h = (0.f < dh) ? dh : 0.f;
   float inter = w * h;
-  // inter == 0 (or NaN) gives ovr in {0, -0, NaN}: never > a threshold >= 0.
-  if (thr_nonneg && !(inter > 0.f)) return false;
-  float ovr = inter / (iarea + aj - inter);
+  float uni = iarea + aj - inter;
+  if (thr_nonneg) {
+    // inter == 0 (or NaN) gives ovr in {0, -0, NaN}: never > thr >= 0.
+    if (!(inter > 0.f)) return false;
+    if (uni > 1e-30f && uni < 3e38f) {
+      const float tu = thrf * uni;
+      if (inter < tu * 0.9999f) return false;
+      if (inter > tu * 1.0001f) return true;
+    }
+  }
+  float ovr = inter / uni;
   return (double)ovr > thr;
 }
 
 __global__ __launch_bounds__(256) void nms_mask(
     const float4* __restrict__ sbox, const float* __restrict__ sarea,
     const int* __restrict__ counts, int64_t n, int64_t nb, double thr,
-    uint64_t* __restrict__ mask) {
+    const int* __restrict__ nanflag, uint64_t* __restrict__ diag, int* __restrict__ nzcnt,
+    int* __restrict__ ent_cb, uint64_t* __restrict__ ent_bits) {
   const int b = blockIdx.z;
   const int64_t rb = blockIdx.y;
   const int64_t cbg = (int64_t)blockIdx.x * kColBlocksPerWG;
@@ -143,8 +163,11 @@ __global__ __launch_bounds__(256) void nms_mask(
   float4 bi = row_ok ? ib[row] : make_float4(0.f, 0.f, 0.f, 0.f);
   float ai = row_ok ? ia[row] : 0.f;
   const bool thr_nonneg = thr >= 0.0;
-  uint64_t* mrow = mask + (int64_t)b * tri_base(nb, nb) + tri_base(rb, nb) +
-                   (int64_t)lane * (nb - rb);
+  const float thrf = (float)thr;
+  const float thr_hi = thrf * 1.0001f, thr_lo = thrf * 0.9999f;
+  const bool fast = thr_nonneg && nanflag[b] == 0;
+  const int64_t rowcap = nb - rb - 1;
+  const int64_t eoff = (int64_t)b * ent_base(nb, nb) + ent_base(rb, nb) + (int64_t)lane * rowcap;
   for (int q = 0; q < kColBlocksPerWave; ++q) {
     const int64_t cb = cbg + wave * kColBlocksPerWave + q;
     if (cb < rb || cb >= nbv) continue;
@@ -154,57 +177,125 @@ __global__ __launch_bounds__(256) void nms_mask(
     int jstart = (cb == rb) ? lane + 1 : 0;  // strictly after row i on the diagonal
     uint64_t bits = 0;
     if (row_ok) {
-      for (int jj = jstart; jj < jmax; ++jj) {
-        if (iou_gt(bi.x, bi.y, bi.z, bi.w, ai, cbox[lbase + jj], carea[lbase + jj], thr,
-                   thr_nonneg))
-          bits |= (uint64_t)1 << jj;
+      if (fast) {
+        // Branch-free: fminf/fmaxf equal std::min/max on non-NaN boxes (NaN
+        // images take the exact loop below); pairs within 1e-4 of the
+        // threshold (or with an out-of-range union) are resolved exactly.
+        uint64_t amb = 0;
+#pragma unroll 16
+        for (int jj = 0; jj < 64; ++jj) {
+          const float4 bj = cbox[lbase + jj];
+          const float aj = carea[lbase + jj];
+          const float xx1 = fmaxf(bi.x, bj.x), yy1 = fmaxf(bi.y, bj.y);
+          const float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
+          const float w = fmaxf(0.f, xx2 - xx1), h = fmaxf(0.f, yy2 - yy1);
+          const float inter = w * h;
+          const float uni = ai + aj - inter;
+          const bool pos = inter > 0.f;
+          const bool oku = uni > 1e-30f && uni < 3e38f;
+          const bool above = inter > thr_hi * uni;
+          const bool below = inter < thr_lo * uni;
+          const uint64_t bit = (uint64_t)1 << jj;
+          bits |= (pos && oku && above) ? bit : 0ull;
+          amb |= (pos && (!oku || (!above && !below))) ? bit : 0ull;
+        }
+        const uint64_t vmask = (jmax >= 64 ? ~0ull : ((1ull << jmax) - 1)) &
+                               ~((jstart >= 64) ? ~0ull : ((1ull << jstart) - 1));
+        bits &= vmask;
+        amb &= vmask;
+        while (amb) {  // rare: exact division near the threshold
+          const int jj = __ffsll((unsigned long long)amb) - 1;
+          amb &= amb - 1;
+          if (iou_gt(bi.x, bi.y, bi.z, bi.w, ai, cbox[lbase + jj], carea[lbase + jj], thr, thrf,
+                     thr_nonneg))
+            bits |= (uint64_t)1 << jj;
+        }
+      } else {
+        for (int jj = jstart; jj < jmax; ++jj) {
+          if (iou_gt(bi.x, bi.y, bi.z, bi.w, ai, cbox[lbase + jj], carea[lbase + jj], thr, thrf,
+                     thr_nonneg))
+            bits |= (uint64_t)1 << jj;
+        }
       }
-      mrow[cb - rb] = bits;
+      if (cb == rb) {
+        diag[(int64_t)b * n + row] = bits;
+      } else if (bits) {
+        const int slot = atomicAdd(&nzcnt[(int64_t)b * n + row], 1);
+        ent_cb[eoff + slot] = (int)cb;
+        ent_bits[eoff + slot] = bits;
+      }
     }
   }
 }
 
+// One workgroup per image walks the row blocks in rank order.  Block c's
+// suppressed-set word comes from LDS; wave 0 resolves the block (only rows
+// with in-block suppressions need the ordered pass); then every kept row
+// ORs its sparse list into the LDS bitset.  The next block's row data is
+// prefetched into registers while the current one resolves.
+static constexpr int kPrefetchEnt = 4;  // list entries per row prefetched (256 threads / 64 rows)
+
 __global__ __launch_bounds__(256) void nms_scan(
-    const uint64_t* __restrict__ mask, const int* __restrict__ sidx,
-    const int* __restrict__ counts, int64_t n, int64_t nb, int img0,
+    const uint64_t* __restrict__ diag, const int* __restrict__ nzcnt,
+    const int* __restrict__ ent_cb, const uint64_t* __restrict__ ent_bits,
+    const int* __restrict__ sidx, const int* __restrict__ counts, int64_t n, int64_t nb, int img0,
     int64_t* __restrict__ keep, int64_t keep_bstride, int64_t* __restrict__ n_keep) {
-  extern __shared__ uint64_t removed[];
+  extern __shared__ unsigned long long removed[];
   __shared__ uint64_t s_kept;
   __shared__ int s_nkeep;
   const int b = blockIdx.x;
   const int cnt = counts[b];
   const int64_t nbv = (cnt + 63) / 64;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, e = tid >> 6;
   for (int64_t w = tid; w < nbv; w += blockDim.x) removed[w] = 0;
   if (tid == 0) s_nkeep = 0;
-  __syncthreads();
-  const uint64_t* mimg = mask + (int64_t)b * tri_base(nb, nb);
+  const uint64_t* dimg = diag + (int64_t)b * n;
+  const int* cimg = nzcnt + (int64_t)b * n;
+  const int64_t ebase = (int64_t)b * ent_base(nb, nb);
   const int* sid = sidx + (int64_t)b * n;
   int64_t* kout = keep + (int64_t)(b + img0) * keep_bstride;
 
+  // prefetch registers for block c: this thread's row = 64c + lane, entry e
+  auto prefetch = [&](int64_t c, uint64_t& pdiag, int& pcnt, int& pcb, uint64_t& pbits) {
+    const int64_t r = c * 64 + lane;
+    pdiag = 0; pcnt = 0; pcb = -1; pbits = 0;
+    if (c < nbv && r < cnt) {
+      pcnt = cimg[r];
+      if (e == 0) pdiag = dimg[r];
+      if (e < pcnt) {
+        const int64_t off = ebase + ent_base(c, nb) + (int64_t)lane * (nb - c - 1) + e;
+        pcb = ent_cb[off];
+        pbits = ent_bits[off];
+      }
+    }
+  };
+  uint64_t pdiag;
+  int pcnt, pcb;
+  uint64_t pbits;
+  prefetch(0, pdiag, pcnt, pcb, pbits);
+  __syncthreads();
+
   for (int64_t c = 0; c < nbv; ++c) {
-    const uint64_t* mblk = mimg + tri_base(c, nb);  // row block c, words cb >= c
-    const int64_t rowlen = nb - c;
-    if (wave == 0) {
-      uint64_t word = removed[c];
-      const int64_t row = c * 64 + lane;
-      uint64_t diag = (row < cnt) ? mblk[(int64_t)lane * rowlen] : 0;
-      uint32_t dlo = (uint32_t)diag, dhi = (uint32_t)(diag >> 32);
+    if (e == 0) {  // wave 0: resolve block c
       const int lim = (int)min((int64_t)64, (int64_t)cnt - c * 64);
-      uint64_t kept = 0;
-      for (int t = 0; t < lim; ++t) {
-        if (!((word >> t) & 1)) {
-          kept |= (uint64_t)1 << t;
-          uint32_t lo = __builtin_amdgcn_readlane(dlo, t);
-          uint32_t hi = __builtin_amdgcn_readlane(dhi, t);
-          word |= ((uint64_t)hi << 32) | lo;
+      const uint64_t valid = lim == 64 ? ~0ull : ((1ull << lim) - 1);
+      uint64_t rem = removed[c];
+      uint64_t todo = __ballot(pdiag != 0) & valid;
+      const uint32_t dlo = (uint32_t)pdiag, dhi = (uint32_t)(pdiag >> 32);
+      while (todo) {  // rows with in-block suppressions, in rank order
+        const int t = __ffsll((unsigned long long)todo) - 1;
+        todo &= todo - 1;
+        if (!((rem >> t) & 1)) {
+          const uint32_t lo = __builtin_amdgcn_readlane(dlo, t);
+          const uint32_t hi = __builtin_amdgcn_readlane(dhi, t);
+          rem |= ((uint64_t)hi << 32) | lo;
         }
       }
-      // One wave: its LDS read of s_nkeep retires before lane 0's write.
-      int base = s_nkeep;
+      const uint64_t kept = valid & ~rem;
+      const int base = s_nkeep;  // one wave: read retires before lane 0's write
       if ((kept >> lane) & 1) {
-        int pos = base + __popcll(kept & (((uint64_t)1 << lane) - 1));
-        kout[pos] = sid[row];
+        const int pos = base + __popcll(kept & ((1ull << lane) - 1));
+        kout[pos] = sid[c * 64 + lane];
       }
       if (lane == 0) {
         s_kept = kept;
@@ -213,18 +304,15 @@ __global__ __launch_bounds__(256) void nms_scan(
     }
     __syncthreads();
     const uint64_t kept = s_kept;
-    if (kept) {
-      for (int64_t w = c + 1 + tid; w < nbv; w += blockDim.x) {
-        uint64_t acc = 0;
-        uint64_t k = kept;
-        while (k) {
-          int t = __ffsll((unsigned long long)k) - 1;
-          k &= k - 1;
-          acc |= mblk[(int64_t)t * rowlen + (w - c)];
-        }
-        removed[w] |= acc;
+    if ((kept >> lane) & 1) {
+      if (e < pcnt) atomicOr(&removed[pcb], (unsigned long long)pbits);
+      if (e == 0 && pcnt > kPrefetchEnt) {  // long lists: rare slow path
+        const int64_t off = ebase + ent_base(c, nb) + (int64_t)lane * (nb - c - 1);
+        for (int q = kPrefetchEnt; q < pcnt; ++q)
+          atomicOr(&removed[ent_cb[off + q]], (unsigned long long)ent_bits[off + q]);
       }
     }
+    prefetch(c + 1, pdiag, pcnt, pcb, pbits);
     __syncthreads();
   }
   if (tid == 0) n_keep[b + img0] = s_nkeep;
@@ -249,7 +337,11 @@ static void carve_nms(A& a, int64_t batch, int64_t n) {
   a.template take<float>(bc * n);          // sorted areas
   a.template take<int>(bc * n);            // sorted row ids
   a.template take<int>(bc);                // counts
-  a.template take<uint64_t>(bc * 64 * (nb * (nb + 1) / 2));  // triangular mask
+  a.template take<int>(bc);                // NaN-box flags
+  a.template take<uint64_t>(bc * n);       // diag words
+  a.template take<int>(bc * n);            // list lengths
+  a.template take<int>(bc * 64 * (nb * (nb - 1) / 2 + 1));       // list column blocks
+  a.template take<uint64_t>(bc * 64 * (nb * (nb - 1) / 2 + 1));  // list bit words
 }
 
 size_t nms_ws_bytes(int64_t batch, int64_t n) {
@@ -288,12 +380,18 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
     float* sarea = cv.take<float>((size_t)bc * n);
     int* sidx = cv.take<int>((size_t)bc * n);
     int* counts = cv.take<int>(bc);
-    uint64_t* mask = cv.take<uint64_t>((size_t)bc * 64 * (nb * (nb + 1) / 2));
+    int* nanflag = cv.take<int>(bc);
+    uint64_t* diag = cv.take<uint64_t>((size_t)bc * n);
+    int* nzcnt = cv.take<int>((size_t)bc * n);
+    int* ent_cb = cv.take<int>((size_t)bc * 64 * (nb * (nb - 1) / 2 + 1));
+    uint64_t* ent_bits = cv.take<uint64_t>((size_t)bc * 64 * (nb * (nb - 1) / 2 + 1));
     if (!cv.ok()) {
       set_error("nms: workspace carve overflow");
       return JABD_EWS;
     }
     JABD_HIP(hipMemsetAsync(counts, 0, sizeof(int) * bc, st));
+    JABD_HIP(hipMemsetAsync(nanflag, 0, sizeof(int) * bc, st));
+    JABD_HIP(hipMemsetAsync(nzcnt, 0, sizeof(int) * bc * n, st));
     dim3 g1((unsigned)cdiv(n, 256), bc);
     nms_keys<<<g1, 256, 0, st>>>(scores, score_stride, score_bstride, n_valid, n, bc,
                                   score_thr, filter, (int)img0, kin, counts);
@@ -302,17 +400,18 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
                                                64, st));
     nms_gather<<<(unsigned)cdiv((int64_t)bc * n, 256), 256, 0, st>>>(
         kout, (int64_t)bc * n, boxes, box_stride, box_bstride, counts, bc, n, (int)img0,
-        sbox, sarea, sidx);
+        sbox, sarea, sidx, nanflag);
     if (int e = check_launch("nms_gather")) return e;
     dim3 g2((unsigned)cdiv(nb, kColBlocksPerWG), (unsigned)nb, (unsigned)bc);
-    nms_mask<<<g2, 256, 0, st>>>(sbox, sarea, counts, n, nb, iou_thr, mask);
+    nms_mask<<<g2, 256, 0, st>>>(sbox, sarea, counts, n, nb, iou_thr, nanflag, diag, nzcnt,
+                                 ent_cb, ent_bits);
     if (int e = check_launch("nms_mask")) return e;
     if (nb * sizeof(uint64_t) > 64 * 1024) {
       JABD_HIP(hipFuncSetAttribute((const void*)nms_scan,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     }
-    nms_scan<<<bc, 256, nb * sizeof(uint64_t), st>>>(mask, sidx, counts, n, nb, (int)img0,
-                                                      keep, n, n_keep);
+    nms_scan<<<bc, 256, nb * sizeof(uint64_t), st>>>(diag, nzcnt, ent_cb, ent_bits, sidx, counts,
+                                                      n, nb, (int)img0, keep, n, n_keep);
     if (int e = check_launch("nms_scan")) return e;
   }
   return JABD_OK;

@@ -87,13 +87,14 @@ SIGNATURES = {
     "jabd_multibox_loss_finalize_f32": [c_vp, c_vp, c_vp, c_vp],
     "jabd_conv_pack_tn": [c_int],
     "jabd_conv2d_nhwc_f32": [ctypes.POINTER(ConvArgs), c_vp],
+    "jabd_stem_nchw_f32": [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp],
     "jabd_dw_nblk": [c_i64, c_i64, c_i64, c_i64],
     "jabd_dwconv_nhwc_f32": [ctypes.POINTER(DwArgs), c_vp],
     "jabd_channel_sum_f32": [c_vp, c_i64, c_i32, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp],
     "jabd_eca_gate_f32": [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp],
     "jabd_nlm_pool_f32": [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp,
                           c_vp, c_vp, c_vp, c_i32, ctypes.POINTER(c_i32), c_i32, c_vp, c_vp,
-                          c_vp],
+                          c_vp, c_vp],
     "jabd_nlm_apply_f32": [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp,
                            c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
     "jabd_maxpool_nhwc_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp],

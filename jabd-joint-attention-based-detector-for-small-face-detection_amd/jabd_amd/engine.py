@@ -54,10 +54,15 @@ class _Head:
                       d(nlm.W.weight.view(C, ch)), d(nlm.W.bias))
         self.eca_fpn = _w1d(m.eca_fpn)
         self.ssh = []
+        q = m.ssh1.conv5X5_1[0].out_channels
+        qp = (q + 3) // 4 * 4 if q % 4 else None  # 10-channel branches stored as 12
         for s in (m.ssh1, m.ssh2, m.ssh3):
-            self.ssh.append(tuple(F.pack_conv(c[0], c[1]) for c in
-                                  (s.conv3X3, s.conv5X5_1, s.conv5X5_2, s.conv7X7_2,
-                                   s.conv7x7_3)))
+            self.ssh.append((F.pack_conv(s.conv3X3[0], s.conv3X3[1]),
+                             F.pack_conv(s.conv5X5_1[0], s.conv5X5_1[1], cout_pad=qp),
+                             F.pack_conv(s.conv5X5_2[0], s.conv5X5_2[1], cin_pad=qp),
+                             F.pack_conv(s.conv7X7_2[0], s.conv7X7_2[1], cin_pad=qp,
+                                         cout_pad=qp),
+                             F.pack_conv(s.conv7x7_3[0], s.conv7x7_3[1], cin_pad=qp)))
         self.heads = []
         for i in range(3):
             convs = (m.BboxHead[i].conv1x1, m.ClassHead[i].conv1x1, m.LandmarkHead[i].conv1x1)
@@ -173,7 +178,9 @@ class Engine:
         m = self.model
         with torch.no_grad():
             if self.kind == "mnv3":
-                self.stem = F.pack_conv(m.body.conv1, m.body.bn1)
+                s_, t_ = F.bn_fold(m.body.bn1)
+                self.stem = ((F.conv_weight_2d(m.body.conv1.weight.detach().float())
+                              * s_[None, :]).contiguous(), t_.detach().contiguous())
                 self.layers = [[_MNv3Block(b) for b in getattr(m.body, f"layer{i}")]
                                for i in (1, 2, 3)]
                 self.head = _Head(m, ("eca_40", "eca_80", "eca_160"), m.fpn.nlm)
@@ -200,7 +207,7 @@ class Engine:
         x = x.contiguous()
         with torch.no_grad():
             if self.kind == "mnv3":
-                s = F.conv(x, self.stem, stride=2, pad=1, act="hswish", nchw_in=True)
+                s = F.stem(x, self.stem[0], self.stem[1], "hswish")
                 feats = []
                 for layer in self.layers:
                     for blk in layer:

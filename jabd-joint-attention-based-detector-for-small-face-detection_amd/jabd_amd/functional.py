@@ -67,17 +67,29 @@ def bn_fold(bn, conv_bias=None):
     return s, t
 
 
-def pack_conv(conv, bn=None, extra=None):
-    """Fold (conv [+ bn]) [+ extra K-concatenated (w2d, shift)] into PackedConv."""
-    w2d = conv_weight_2d(conv.weight.detach().float())
+def pack_conv(conv, bn=None, extra=None, cin_pad=None, cout_pad=None):
+    """Fold (conv [+ bn]) [+ extra K-concatenated (w2d, shift)] into PackedConv.
+
+    cin_pad / cout_pad zero-extend the input / output channels (a 10-channel
+    SSH tensor stored as 12 channels takes the 16-byte vector path; the extra
+    output channels compute exactly 0)."""
+    wt = conv.weight.detach().float()
     cb = conv.bias.detach().float() if conv.bias is not None else None
     if bn is not None:
         s, t = bn_fold(bn, cb)
-        w2d = w2d * s[None, :]
+        wt = wt * s[:, None, None, None]
         bias = t
     else:
         bias = cb
-    cin = conv.weight.shape[1]
+    cout, cin = wt.shape[0], wt.shape[1]
+    if cin_pad is not None and cin_pad > cin:
+        wt = torch.cat([wt, wt.new_zeros((cout, cin_pad - cin) + tuple(wt.shape[2:]))], 1)
+        cin = cin_pad
+    if cout_pad is not None and cout_pad > cout:
+        wt = torch.cat([wt, wt.new_zeros((cout_pad - cout,) + tuple(wt.shape[1:]))], 0)
+        bias = torch.cat([bias if bias is not None else wt.new_zeros(cout),
+                          wt.new_zeros(cout_pad - cout)])
+    w2d = conv_weight_2d(wt)
     cin2 = 0
     if extra is not None:
         w2, t2 = extra
@@ -132,6 +144,17 @@ def conv(x, pk, stride=1, pad=0, act="none", slope=0.0, ascale=None, x2=None, x2
     a.nchw_in = 1 if nchw_in else 0
     call("jabd_conv2d_nhwc_f32", ctypes.byref(a), _stream())
     return out
+
+
+def stem(x, w, bias, act):
+    """MobileNetV3 stem: NCHW [B,3,H,W] -> NHWC [B,H/2,W/2,16] (w [27][16])."""
+    _check("stem.x", x)
+    B, _, H, W = x.shape
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    y = torch.empty((B, OH, OW, 16), dtype=torch.float32, device=x.device)
+    call("jabd_stem_nchw_f32", x.data_ptr(), B, H, W, w.data_ptr(), bias.data_ptr(), ACT[act],
+         y.data_ptr(), _stream())
+    return y
 
 
 def dw_nblk(B, OH, OW, C):
@@ -191,9 +214,10 @@ def nlm_fused(src, lateral, nlm_w, sizes):
     kp = torch.empty((B, S, ch), dtype=torch.float32, device=src.device)
     vp = torch.empty_like(kp)
     arr = (ctypes.c_int32 * len(sizes))(*sizes)
+    kv = torch.empty((B, hs * ws, 2 * ch), dtype=torch.float32, device=src.device)
     call("jabd_nlm_pool_f32", src.data_ptr(), src.stride(0), C, B, hs, ws, C, h, w,
          wk.data_ptr(), bk.data_ptr(), wv.data_ptr(), bv.data_ptr(), ch, arr, len(sizes),
-         kp.data_ptr(), vp.data_ptr(), _stream())
+         kp.data_ptr(), vp.data_ptr(), kv.data_ptr(), _stream())
     out = torch.empty_like(lateral)
     call("jabd_nlm_apply_f32", src.data_ptr(), src.stride(0), C, B, hs, ws, C, h, w,
          wq.data_ptr(), bq.data_ptr(), kp.data_ptr(), vp.data_ptr(), S, ch, wW.data_ptr(),

@@ -154,3 +154,37 @@ def test_match_parity(cuda, size, batch):
     assert torch.equal(gc.cpu(), rc)  # bit-exact assignment incl. forced matches
     torch.testing.assert_close(gl.cpu(), rl, rtol=1e-5, atol=1e-5)  # log() ulp
     assert torch.equal(glm.cpu(), rlm)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("thr", [0.3, 0.5, 0.45])
+def test_nms_parity_near_threshold(cuda, thr):
+    """Pairs whose IoU sits within a few ulp of the threshold exercise the
+    exact-division path of the branch-free mask kernel."""
+    from jabd_amd import ops
+    rng = np.random.default_rng(11)
+    rows, scores = [], []
+    for k in range(400):
+        x0, y0 = rng.uniform(0, 50, 2).astype(np.float32)
+        s = np.float32(thr) * np.float32(1 + rng.integers(-8, 9) * 2e-7)
+        # IoU([x0,y0,x0+1,y0+1], [x0,y0,x0+s,y0+1]) = s (nested boxes)
+        rows += [[x0, y0, x0 + 1, y0 + 1], [x0, y0, x0 + s, y0 + 1]]
+        scores += [1.0 - k * 1e-3, 0.5 - k * 1e-4]
+    b = np.asarray(rows, np.float32)
+    sc = np.asarray(scores, np.float32)
+    ref = box_ref.nms(b, sc, thr)
+    got = ops.nms(torch.from_numpy(b).to(cuda), torch.from_numpy(sc).to(cuda), thr)
+    assert got.cpu().numpy().tolist() == ref.tolist()
+    assert 0 < len(ref) < len(sc)  # the set really straddles the threshold
+
+
+@pytest.mark.gpu
+def test_nms_parity_nan_boxes(cuda):
+    from jabd_amd import ops
+    b, s = _clustered(500, seed=3)
+    b = b.copy()
+    b[7, 0] = np.nan
+    b[100, 3] = np.nan
+    ref = box_ref.nms(b, s, 0.3)
+    got = ops.nms(torch.from_numpy(b).to(cuda), torch.from_numpy(s).to(cuda), 0.3)
+    assert got.cpu().numpy().tolist() == ref.tolist()
