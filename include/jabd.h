@@ -172,7 +172,10 @@ typedef struct jabd_conv_args {
   int32_t OH, OW, Cout, Ntiles, tn, Kc;
   int32_t KH, KW, stride, pad;
   int32_t act; float slope;
-  int32_t nchw_in, reserved0;
+  int32_t nchw_in, tconv; /* tconv: transposed conv — the data gradient of a
+                             conv with this geometry: output (oh,ow) reads
+                             input ((oh+pad-kh)/stride, (ow+pad-kw)/stride) */
+  int32_t flags, reserved1; /* library-internal */
   int64_t M; /* filled in by the library */
 } jabd_conv_args;
 /* N-tiles (16 output channels each) grouped per workgroup for a Cout. */
@@ -210,7 +213,7 @@ int jabd_channel_sum_f32(const float* x, int64_t x_bs, int32_t x_ps, int64_t B, 
  * nets/retinaface_r.py:219-224 (gate=SIGMOID): mean = sum(part)/HW,
  * Conv1d(1,1,k,pad=(k-1)/2,no bias) over channels, gate -> scale [B][C]. */
 int jabd_eca_gate_f32(const float* part, int64_t nblk, int64_t B, int64_t C, int64_t hw,
-                      const float* w1d, int32_t k, int32_t gate, float* scale,
+                      const float* w1d, int32_t k, int32_t gate, float* scale, float* mean_out,
                       jabd_stream_t stream);
 
 /* A3 CSAF non-local block — nets/retinaface_r.py:85-152 + the FPN's nearest
@@ -219,7 +222,8 @@ int jabd_eca_gate_f32(const float* part, int64_t nblk, int64_t B, int64_t C, int
  *   array) of f_key(x) / f_value(x)  (wk/wv [ch][C], bk/bv [ch]); kv_ws is
  *   scratch [B][hs*ws][2*ch].  Built for ch == 4 (the JABD NLM).
  * nlm_apply: out = lateral + (W·softmax_S(q·k)·v + bW + x), q = f_query(x),
- *   lateral/out [B,h,w,C] NHWC (may alias). */
+ *   lateral/out [B,h,w,C] NHWC (may alias); q_out/ctx_out [B,h*w,ch]
+ *   (nullable) keep q and the attention context for the backward. */
 int jabd_nlm_pool_f32(const float* src, int64_t src_bs, int32_t src_ps, int32_t B, int32_t hs,
                       int32_t ws, int32_t C, int32_t h, int32_t w, const float* wk,
                       const float* bk, const float* wv, const float* bv, int32_t ch,
@@ -229,7 +233,7 @@ int jabd_nlm_apply_f32(const float* src, int64_t src_bs, int32_t src_ps, int32_t
                        int32_t ws, int32_t C, int32_t h, int32_t w, const float* wq,
                        const float* bq, const float* kpool, const float* vpool, int32_t S,
                        int32_t ch, const float* wW, const float* bW, const float* lateral,
-                       float* out, jabd_stream_t stream);
+                       float* out, float* q_out, float* ctx_out, jabd_stream_t stream);
 
 /* A4 detection heads — nets/retinaface_r.py:17-57,335-343: the Bbox (2x4),
  * Class (2x2) and Landmark (2x10) 1x1 convs of one pyramid level, written
@@ -244,6 +248,86 @@ int jabd_heads_f32(const float* x, int64_t x_bs, int32_t x_ps, int32_t B, int32_
                    int32_t C, const float* wt, const float* bias, int64_t A, int64_t a_off,
                    int32_t softmax, float* loc, float* conf, float* landm,
                    jabd_stream_t stream);
+
+/* ======================================================================== *
+ * A11 training (loss.backward() of train_*.py:532) — fp32 NHWC, row-major
+ * [M = B*H*W rows][C], ld = row stride in floats.  BatchNorm2d in training
+ * mode (batch statistics, momentum update of the running buffers).
+ * ======================================================================== */
+/* Partial-buffer size (blocks) of the BN reductions: part = [nblk][2][C]. */
+int64_t jabd_bn_nblk(int64_t M, int32_t C);
+/* mean/invstd of x over M rows (biased var); running stats updated in place
+ * (running_var with the unbiased estimate) when non-null. */
+int jabd_bn_stats_f32(const float* x, int32_t ldx, int64_t M, int32_t C, float* part,
+                      float* mean, float* invstd, float* running_mean, float* running_var,
+                      float momentum, float eps, jabd_stream_t stream);
+/* y[:, yc0:yc0+C] = act((x - mean) * invstd * gamma + beta [+ res]) */
+int jabd_bn_act_fwd_f32(const float* x, int32_t ldx, int64_t M, int32_t C, const float* mean,
+                        const float* invstd, const float* gamma, const float* beta,
+                        const float* res, int32_t ldr, int32_t act, float slope, float* y,
+                        int32_t ldy, int32_t yc0, jabd_stream_t stream);
+/* Backward of bn_act_fwd: dx [M][C] (dense), dres [M][C] (= dz, nullable),
+ * dgamma/dbeta [C].  dy is read at columns dyc0.. of rows of lddy floats. */
+int jabd_bn_act_bwd_f32(const float* dy, int32_t lddy, int32_t dyc0, const float* x, int32_t ldx,
+                        const float* res, int32_t ldr, int64_t M, int32_t C, const float* mean,
+                        const float* invstd, const float* gamma, const float* beta, int32_t act,
+                        float slope, float* part, float* dgamma, float* dbeta, float* dx,
+                        float* dres, jabd_stream_t stream);
+/* Conv weight gradient (fp32 MFMA): x/geometry as the forward jabd_conv_args
+ * with `y` pointing at dY; dw in torch layout [Cout][Cin][KH][KW]; part is
+ * scratch of jabd_conv_wgrad_part_floats() floats.  The data gradient is
+ * jabd_conv2d_nhwc_f32 with tconv=1 and the transposed weights. */
+int64_t jabd_conv_wgrad_part_floats(const jabd_conv_args* args);
+int jabd_conv_wgrad_f32(const jabd_conv_args* args, float* part, float* dw, jabd_stream_t stream);
+/* Depthwise gradients (nets/mobilenetV3.py:105-106): dx from dy and w
+ * [k*k][C]; dw in torch layout [C][1][k][k] (part: jabd_dw_wgrad_part_floats). */
+int jabd_dw_dgrad_f32(const float* dy, const float* w, int32_t B, int32_t H, int32_t W, int32_t C,
+                      int32_t OH, int32_t OW, int32_t k, int32_t stride, int32_t pad, float* dx,
+                      jabd_stream_t stream);
+int64_t jabd_dw_wgrad_part_floats(int64_t M, int32_t C, int32_t k);
+int jabd_dw_wgrad_f32(const float* x, const float* dy, int32_t B, int32_t H, int32_t W, int32_t C,
+                      int32_t OH, int32_t OW, int32_t k, int32_t stride, int32_t pad, float* part,
+                      float* dw, jabd_stream_t stream);
+/* ECA backward.  The consumer saw a = x * scale[b][c]; given da:
+ *   dx = da * scale + (d mean)/HW  through the gate, Conv1d and average pool,
+ *   dw1d [k] the Conv1d weight gradient.  mean/scale are the forward's
+ *   (jabd_eca_gate_f32 mean_out).  part [B][nblk][C], dmean_ws [B][C],
+ *   dw1d_ws [B][k] are scratch. */
+int jabd_eca_bwd_f32(const float* da, const float* x, int64_t B, int64_t HW, int32_t C,
+                     const float* scale, const float* mean, const float* w1d, int32_t k,
+                     int32_t gate, float* part, int32_t nblk, float* dmean_ws, float* dw1d_ws,
+                     float* dx, float* dw1d, jabd_stream_t stream);
+/* dx = da * scale[b][c] and part[b][blk][c] = sum da * x (scale gradient). */
+int jabd_scale_bwd_f32(const float* da, const float* x, int64_t B, int64_t HW, int32_t C,
+                       const float* scale, float* part, int32_t nblk, float* dx,
+                       jabd_stream_t stream);
+/* Heads backward input: d(loc|conf|landm) rows of one level -> [B][HW][32]. */
+int jabd_heads_gather_f32(const float* gloc, const float* gconf, const float* glandm, int32_t B,
+                          int64_t A, int64_t a_off, int32_t HW, float* dout,
+                          jabd_stream_t stream);
+/* Max-pool backward (F.max_pool2d first-max / NaN semantics), NHWC. */
+int jabd_maxpool_bwd_f32(const float* x, const float* dy, int32_t B, int32_t H, int32_t W,
+                         int32_t C, int32_t k, int32_t stride, int32_t pad, float* dx,
+                         jabd_stream_t stream);
+/* CSAF/NLM backward (nets/retinaface_r.py:124-152).  attn: from dOut (grad
+ * of lateral + NLM(x)) -> dq [M][4], dx_up [M][C] (= dOut + Wq^T dq), and
+ * dK/dV [B][S][4] (part: [B][ceil(h*w/256)][S][8] scratch).  proj: PSP
+ * backward -> dkv [M][8] and dx_up += Wk^T dk + Wv^T dv.  Up-sample backward
+ * gathers dx_up onto the source grid (accumulate=1 adds to dsrc). */
+int jabd_nlm_bwd_attn_f32(const float* dout, int32_t B, int32_t h, int32_t w, int32_t C,
+                          const float* q, const float* kpool, const float* vpool, int32_t S,
+                          const float* wW, const float* wq, float* dq, float* dxup, float* part,
+                          float* dk, float* dv, jabd_stream_t stream);
+int jabd_nlm_bwd_proj_f32(const float* dk, const float* dv, int32_t B, int32_t S,
+                          const int32_t* sizes, int32_t nsizes, int32_t h, int32_t w, int32_t C,
+                          const float* wk, const float* wv, float* dkv, float* dxup,
+                          jabd_stream_t stream);
+int jabd_upsample_nearest_bwd_f32(const float* dxup, int32_t B, int32_t h, int32_t w, int32_t hs,
+                                  int32_t ws, int32_t C, int32_t accumulate, float* dsrc,
+                                  jabd_stream_t stream);
+/* F.interpolate(mode='nearest', size=(h,w)) of an NHWC tensor. */
+int jabd_upsample_nearest_f32(const float* src, int32_t B, int32_t hs, int32_t ws, int32_t h,
+                              int32_t w, int32_t C, float* dst, jabd_stream_t stream);
 
 #ifdef __cplusplus
 }

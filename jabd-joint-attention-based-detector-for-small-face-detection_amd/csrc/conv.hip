@@ -52,7 +52,7 @@ __device__ __forceinline__ float4 load_a(const ConvArgs& p, int b, int oh, int o
                                          int k4) {
   float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
   if (!mvalid) return r;
-  if (p.KH == 1 && p.KW == 1 && p.stride == 1 && p.pad == 0) {
+  if (p.KH == 1 && p.KW == 1 && p.stride == 1 && p.pad == 0 && !p.tconv) {
     if (k4 < p.Cin) {
       const float* src = p.x + (int64_t)b * p.x_bs + ((int64_t)oh * p.W + ow) * p.x_ps + p.x_c0;
       if (VEC4) {
@@ -82,7 +82,16 @@ __device__ __forceinline__ float4 load_a(const ConvArgs& p, int b, int oh, int o
     if (k4 >= Ktot) return r;
     const int tap = k4 / p.Cin, ci = k4 - tap * p.Cin;
     const int kh = tap / p.KW, kw = tap - kh * p.KW;
-    const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
+    int ih, iw;
+    if (p.tconv) {
+      const int nh = oh + p.pad - kh, nw = ow + p.pad - kw;
+      if (nh < 0 || nw < 0 || nh % p.stride || nw % p.stride) return r;
+      ih = nh / p.stride;
+      iw = nw / p.stride;
+    } else {
+      ih = oh * p.stride - p.pad + kh;
+      iw = ow * p.stride - p.pad + kw;
+    }
     if (ih < 0 || ih >= p.H || iw < 0 || iw >= p.W) return r;
     const float* src = p.x + (int64_t)b * p.x_bs + ((int64_t)ih * p.W + iw) * p.x_ps + p.x_c0 + ci;
     r = *reinterpret_cast<const float4*>(src);
@@ -100,7 +109,16 @@ __device__ __forceinline__ float4 load_a(const ConvArgs& p, int b, int oh, int o
     if (k >= Ktot) continue;
     const int tap = k / p.Cin, ci = k - tap * p.Cin;
     const int kh = tap / p.KW, kw = tap - kh * p.KW;
-    const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
+    int ih, iw;
+    if (p.tconv) {
+      const int nh = oh + p.pad - kh, nw = ow + p.pad - kw;
+      if (nh < 0 || nw < 0 || nh % p.stride || nw % p.stride) continue;
+      ih = nh / p.stride;
+      iw = nw / p.stride;
+    } else {
+      ih = oh * p.stride - p.pad + kh;
+      iw = ow * p.stride - p.pad + kw;
+    }
     if (ih < 0 || ih >= p.H || iw < 0 || iw >= p.W) continue;
     float x;
     if (p.nchw_in)
@@ -188,7 +206,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
   }
 
   // epilogue: acc[t][u][r] = Y[pixel m_wave + 16t + j][channel 16(nb*TN+u) + 4g + r]
-  const bool v4 = (p.reserved0 & 1) != 0;  // host: every channel offset/stride % 4 == 0
+  const bool v4 = (p.flags & 1) != 0;  // host: every channel offset/stride % 4 == 0
   if (v4) {
     // Stage each 16-pixel x 16*TN-channel subtile through LDS so every store
     // instruction writes whole 16*TN-float pixel rows (1 KB contiguous when
@@ -294,9 +312,15 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
   JABD_REQUIRE(a.x && a.w && a.y, "conv: null pointer");
   JABD_REQUIRE(a.B > 0 && a.Cin > 0 && a.Cout > 0 && a.KH > 0 && a.KW > 0 && a.stride > 0,
                "conv: bad shape");
-  JABD_REQUIRE(a.OH == (a.H + 2 * a.pad - a.KH) / a.stride + 1 &&
-                   a.OW == (a.W + 2 * a.pad - a.KW) / a.stride + 1,
-               "conv: output size mismatch");
+  if (a.tconv) {  // data gradient: (OH, OW) is the forward input size, (H, W) its output
+    JABD_REQUIRE(a.H == (a.OH + 2 * a.pad - a.KH) / a.stride + 1 &&
+                     a.W == (a.OW + 2 * a.pad - a.KW) / a.stride + 1 && !a.nchw_in && !a.x2,
+                 "conv: transposed-conv size mismatch");
+  } else {
+    JABD_REQUIRE(a.OH == (a.H + 2 * a.pad - a.KH) / a.stride + 1 &&
+                     a.OW == (a.W + 2 * a.pad - a.KW) / a.stride + 1,
+                 "conv: output size mismatch");
+  }
   const bool is1x1 = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
   JABD_REQUIRE(!a.x2 || ((a.KH * a.KW * a.Cin) % 4 == 0 && a.Cin2 % 4 == 0 && a.x2_ps % 4 == 0 &&
                          a.x2_stride > 0 && !a.nchw_in),
@@ -314,7 +338,7 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
     const bool v4 = a.Cout % 4 == 0 && a.y_ps % 4 == 0 && a.y_c0 % 4 == 0 && a.y_bs % 4 == 0 &&
                     (!a.res || (a.res_ps % 4 == 0 && a.res_c0 % 4 == 0 && a.res_bs % 4 == 0)) &&
                     (al & 15) == 0;
-    a.reserved0 = v4 ? 1 : 0;
+    a.flags = v4 ? 1 : 0;
   }
   const bool vec4 = !a.nchw_in && a.Cin % 4 == 0 && a.x_ps % 4 == 0 && a.x_c0 % 4 == 0 &&
                     (reinterpret_cast<uintptr_t>(a.x) & 15) == 0;

@@ -51,7 +51,7 @@ __global__ __launch_bounds__(kSumThreads) void channel_sum_kernel(
 // scale[b][c] = gate( sum_t w[t] * mean[b][c + t - (k-1)/2] )   (zero padded)
 __global__ void eca_gate_kernel(const float* __restrict__ part, int64_t nblk, int C, float inv_hw,
                                 const float* __restrict__ w1d, int k, int gate,
-                                float* __restrict__ scale) {
+                                float* __restrict__ scale, float* __restrict__ mean_out) {
   extern __shared__ float mean[];
   const int b = blockIdx.x;
   const float* pb = part + (int64_t)b * nblk * C;
@@ -65,6 +65,7 @@ __global__ void eca_gate_kernel(const float* __restrict__ part, int64_t nblk, in
     }
     for (; q < nblk; ++q) s[0] += pb[q * C + c];
     mean[c] = (((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]))) * inv_hw;
+    if (mean_out) mean_out[(int64_t)b * C + c] = mean[c];
   }
   __syncthreads();
   const int h = (k - 1) / 2;
@@ -185,7 +186,7 @@ __global__ __launch_bounds__(256) void nlm_apply_kernel(
     int w, const float* __restrict__ wq, const float* __restrict__ bq,
     const float* __restrict__ kpool, const float* __restrict__ vpool, int S,
     const float* __restrict__ wW, const float* __restrict__ bW, const float* __restrict__ lateral,
-    float* __restrict__ out) {
+    float* __restrict__ out, float* __restrict__ q_out, float* __restrict__ ctx_out) {
   extern __shared__ float sm[];  // K [S][CH], V [S][CH], wq [CH][C], wW [C][CH], bW [C]
   const int b = blockIdx.y;
   float* sK = sm;
@@ -244,6 +245,14 @@ __global__ __launch_bounds__(256) void nlm_apply_kernel(
   const float inv = 1.f / den;
 #pragma unroll
   for (int o = 0; o < CH; ++o) cx[o] *= inv;
+  if (q_out) {  // training: saved for the backward
+    const int64_t mq = ((int64_t)b * h * w + pix) * CH;
+#pragma unroll
+    for (int o = 0; o < CH; ++o) {
+      q_out[mq + o] = q[o];
+      ctx_out[mq + o] = cx[o];
+    }
+  }
   const int64_t opix = ((int64_t)b * h * w + pix) * C;
   for (int c = 0; c < C; c += 4) {
     const float4 x = *reinterpret_cast<const float4*>(xp + c);
@@ -330,13 +339,13 @@ extern "C" int jabd_channel_sum_f32(const float* x, int64_t x_bs, int32_t x_ps, 
 
 extern "C" int jabd_eca_gate_f32(const float* part, int64_t nblk, int64_t B, int64_t C,
                                  int64_t hw, const float* w1d, int32_t k, int32_t gate,
-                                 float* scale, jabd_stream_t stream) {
+                                 float* scale, float* mean_out, jabd_stream_t stream) {
   JABD_REQUIRE(part && w1d && scale && B > 0 && C > 0 && hw > 0 && k > 0 && (k & 1),
                "eca_gate: bad args");
   JABD_REQUIRE(gate == ACT_SIGMOID || gate == ACT_HSIGMOID, "eca_gate: gate must be (h)sigmoid");
   JABD_REQUIRE(C * sizeof(float) <= 64 * 1024, "eca_gate: C too large");
   eca_gate_kernel<<<(unsigned)B, 256, C * sizeof(float), as_stream(stream)>>>(
-      part, nblk, (int)C, 1.f / (float)hw, w1d, k, gate, scale);
+      part, nblk, (int)C, 1.f / (float)hw, w1d, k, gate, scale, mean_out);
   return check_launch("eca_gate");
 }
 
@@ -377,7 +386,7 @@ extern "C" int jabd_nlm_apply_f32(const float* src, int64_t src_bs, int32_t src_
                                   const float* wq, const float* bq, const float* kpool,
                                   const float* vpool, int32_t S, int32_t ch, const float* wW,
                                   const float* bW, const float* lateral, float* out,
-                                  jabd_stream_t stream) {
+                                  float* q_out, float* ctx_out, jabd_stream_t stream) {
   JABD_REQUIRE(src && wq && bq && kpool && vpool && wW && bW && lateral && out,
                "nlm_apply: null pointer");
   JABD_REQUIRE(ch == 4, "nlm_apply: only ch=4 (the JABD NLM) is built");
@@ -387,7 +396,7 @@ extern "C" int jabd_nlm_apply_f32(const float* src, int64_t src_bs, int32_t src_
   dim3 g((unsigned)cdiv((int64_t)h * w, 256), (unsigned)B);
   nlm_apply_kernel<4><<<g, 256, smem, as_stream(stream)>>>(src, src_bs, src_ps, hs, ws, C, h, w,
                                                            wq, bq, kpool, vpool, S, wW, bW,
-                                                           lateral, out);
+                                                           lateral, out, q_out, ctx_out);
   return check_launch("nlm_apply");
 }
 

@@ -1,0 +1,331 @@
+// A3/A11 CSAF non-local block backward (nets/retinaface_r.py:124-152 and the
+// FPN's nearest up-sample :192-203).  Forward (training) saves q and ctx per
+// pixel and the pooled K/V; backward recomputes the attention row per pixel:
+//   dctx = W^T dOut;  dP = dctx . V;  dL = P (dP - sum P dP);  dq = dL K
+//   dK[s] += dL_s q,  dV[s] += P_s dctx      (wave shuffles -> block partials)
+//   dx_up = dOut + Wq^T dq + Wk^T dkproj + Wv^T dvproj,
+//   dkproj(pix) = sum over PSP bins containing pix of dK[bin] / |bin|
+// then the up-sample backward gathers dx_up onto the source grid.  Weight
+// gradients are 1x1-conv weight gradients (jabd_conv_wgrad_f32) of the saved
+// per-pixel tensors.
+#include "common.h"
+#include "conv_args.h"
+
+namespace jabd {
+
+__device__ __forceinline__ int nsrc(int dst, int in, int out) {
+  if (out == in) return dst;
+  if (out == 2 * in) return dst >> 1;
+  const float scale = (float)in / (float)out;
+  const int s = (int)floorf((float)dst * scale);
+  return s < in - 1 ? s : in - 1;
+}
+
+constexpr int CH = 4;
+
+// One thread per up-sampled pixel; block partials of dK/dV: part[b][blk][S][8].
+__global__ __launch_bounds__(256) void nlm_bwd_attn_kernel(
+    const float* __restrict__ dout, int h, int w, int C, const float* __restrict__ q,
+    const float* __restrict__ kpool, const float* __restrict__ vpool, int S,
+    const float* __restrict__ wW, const float* __restrict__ wq, float* __restrict__ dq_out,
+    float* __restrict__ dxup, float* __restrict__ part, int nblk) {
+  extern __shared__ float sm[];  // K[S][4], V[S][4], wW[C][4], wq[4][C], red[4 waves][S][8]
+  const int b = blockIdx.y;
+  float* sK = sm;
+  float* sV = sK + S * CH;
+  float* sWW = sV + S * CH;
+  float* sWq = sWW + C * CH;
+  float* red = sWq + CH * C;
+  for (int t = threadIdx.x; t < S * CH; t += blockDim.x) {
+    sK[t] = kpool[(int64_t)b * S * CH + t];
+    sV[t] = vpool[(int64_t)b * S * CH + t];
+  }
+  for (int t = threadIdx.x; t < C * CH; t += blockDim.x) {
+    sWW[t] = wW[t];
+    sWq[t] = wq[t];
+  }
+  __syncthreads();
+  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool ok = pix < h * w;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t m = (int64_t)b * h * w + (ok ? pix : 0);
+  float qv[CH], dctx[CH];
+  for (int o = 0; o < CH; ++o) { qv[o] = ok ? q[m * CH + o] : 0.f; dctx[o] = 0.f; }
+  const float* dop = dout + m * C;
+  if (ok) {
+    for (int c = 0; c < C; c += 4) {
+      const float4 g = *reinterpret_cast<const float4*>(dop + c);
+      const float gg[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int o = 0; o < CH; ++o) dctx[o] = fmaf(gg[e], sWW[(c + e) * CH + o], dctx[o]);
+    }
+  }
+  // recompute the softmax row
+  float mx = -INFINITY;
+  for (int s = 0; s < S; ++s) {
+    float l = 0.f;
+#pragma unroll
+    for (int o = 0; o < CH; ++o) l = fmaf(qv[o], sK[s * CH + o], l);
+    mx = fmaxf(mx, l);
+  }
+  float den = 0.f, sdp = 0.f;
+  for (int s = 0; s < S; ++s) {
+    float l = 0.f, dp = 0.f;
+#pragma unroll
+    for (int o = 0; o < CH; ++o) {
+      l = fmaf(qv[o], sK[s * CH + o], l);
+      dp = fmaf(dctx[o], sV[s * CH + o], dp);
+    }
+    const float e = __expf(l - mx);
+    den += e;
+    sdp = fmaf(e, dp, sdp);
+  }
+  const float inv = 1.f / den;
+  sdp *= inv;
+  float dq[CH] = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < S; ++s) {
+    float l = 0.f, dp = 0.f;
+#pragma unroll
+    for (int o = 0; o < CH; ++o) {
+      l = fmaf(qv[o], sK[s * CH + o], l);
+      dp = fmaf(dctx[o], sV[s * CH + o], dp);
+    }
+    const float P = ok ? __expf(l - mx) * inv : 0.f;
+    const float dL = P * (dp - sdp);
+    float v[2 * CH];
+#pragma unroll
+    for (int o = 0; o < CH; ++o) {
+      dq[o] = fmaf(dL, sK[s * CH + o], dq[o]);
+      v[o] = dL * qv[o];
+      v[CH + o] = P * dctx[o];
+    }
+#pragma unroll
+    for (int o = 0; o < 2 * CH; ++o) {
+      float a = v[o];
+      for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off);
+      v[o] = a;
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int o = 0; o < 2 * CH; ++o) red[(wave * S + s) * 2 * CH + o] = v[o];
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < S * 2 * CH; t += blockDim.x) {
+    float a = 0.f;
+    for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) a += red[wv * S * 2 * CH + t];
+    part[((int64_t)b * nblk + blockIdx.x) * S * 2 * CH + t] = a;
+  }
+  if (!ok) return;
+  for (int o = 0; o < CH; ++o) dq_out[m * CH + o] = dq[o];
+  float* dx = dxup + m * C;
+  for (int c = 0; c < C; c += 4) {
+    const float4 g = *reinterpret_cast<const float4*>(dop + c);
+    float r[4] = {g.x, g.y, g.z, g.w};  // the "+ x" path
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int o = 0; o < CH; ++o) r[e] = fmaf(sWq[o * C + c + e], dq[o], r[e]);
+    *reinterpret_cast<float4*>(dx + c) = make_float4(r[0], r[1], r[2], r[3]);
+  }
+}
+
+__global__ void nlm_bwd_kv_reduce_kernel(const float* __restrict__ part, int nblk, int S,
+                                         float* __restrict__ dk, float* __restrict__ dv) {
+  const int b = blockIdx.y;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= S * 2 * CH) return;
+  float a = 0.f;
+  for (int q = 0; q < nblk; ++q) a += part[((int64_t)b * nblk + q) * S * 2 * CH + t];
+  const int s = t / (2 * CH), o = t % (2 * CH);
+  if (o < CH) dk[((int64_t)b * S + s) * CH + o] = a;
+  else dv[((int64_t)b * S + s) * CH + (o - CH)] = a;
+}
+
+struct PspSizes {
+  int n;
+  int v[8];
+};
+
+// Per up-sampled pixel: dkproj/dvproj from every PSP bin containing it, then
+// dx_up += Wk^T dkproj + Wv^T dvproj.  dkv [M][8] is kept for the weight grads.
+__global__ __launch_bounds__(256) void nlm_bwd_proj_kernel(
+    const float* __restrict__ dk, const float* __restrict__ dv, int S, const PspSizes ps, int h,
+    int w, int C, const float* __restrict__ wk, const float* __restrict__ wv,
+    float* __restrict__ dkv, float* __restrict__ dxup) {
+  extern __shared__ float sm[];  // dK[S][4], dV[S][4], wk[4][C], wv[4][C]
+  const int b = blockIdx.y;
+  float* sK = sm;
+  float* sV = sK + S * CH;
+  float* sWk = sV + S * CH;
+  float* sWv = sWk + CH * C;
+  for (int t = threadIdx.x; t < S * CH; t += blockDim.x) {
+    sK[t] = dk[(int64_t)b * S * CH + t];
+    sV[t] = dv[(int64_t)b * S * CH + t];
+  }
+  for (int t = threadIdx.x; t < CH * C; t += blockDim.x) {
+    sWk[t] = wk[t];
+    sWv[t] = wv[t];
+  }
+  __syncthreads();
+  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= h * w) return;
+  const int i = pix / w, j = pix - (pix / w) * w;
+  float gk[CH] = {0.f, 0.f, 0.f, 0.f}, gv[CH] = {0.f, 0.f, 0.f, 0.f};
+  int base = 0;
+  for (int l = 0; l < ps.n; ++l) {
+    const int sz = ps.v[l];
+    // bins bi with floor(bi*h/sz) <= i < ceil((bi+1)*h/sz)
+    // bins containing row i: floor(bi*h/sz) <= i < ceil((bi+1)*h/sz); when
+    // sz > h several consecutive bins share a row, so scan the full range
+    const int bi_lo = max(0, ((i - 1) * sz) / h - 1), bi_hi = min(sz - 1, ((i + 1) * sz) / h);
+    for (int bi = bi_lo; bi <= bi_hi; ++bi) {
+      const int h0 = (bi * h) / sz, h1 = ((bi + 1) * h + sz - 1) / sz;
+      if (i < h0 || i >= h1) continue;
+      const int bj_lo = max(0, ((j - 1) * sz) / w - 1), bj_hi = min(sz - 1, ((j + 1) * sz) / w);
+      for (int bj = bj_lo; bj <= bj_hi; ++bj) {
+        const int w0 = (bj * w) / sz, w1 = ((bj + 1) * w + sz - 1) / sz;
+        if (j < w0 || j >= w1) continue;
+        const float invn = 1.f / (float)((h1 - h0) * (w1 - w0));
+        const int s = base + bi * sz + bj;
+#pragma unroll
+        for (int o = 0; o < CH; ++o) {
+          gk[o] = fmaf(sK[s * CH + o], invn, gk[o]);
+          gv[o] = fmaf(sV[s * CH + o], invn, gv[o]);
+        }
+      }
+    }
+    base += sz * sz;
+  }
+  const int64_t m = (int64_t)b * h * w + pix;
+#pragma unroll
+  for (int o = 0; o < CH; ++o) {
+    dkv[m * 2 * CH + o] = gk[o];
+    dkv[m * 2 * CH + CH + o] = gv[o];
+  }
+  float* dx = dxup + m * C;
+  for (int c = 0; c < C; c += 4) {
+    float4 r = *reinterpret_cast<float4*>(dx + c);
+    float rr[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int o = 0; o < CH; ++o)
+        rr[e] = fmaf(sWk[o * C + c + e], gk[o], fmaf(sWv[o * C + c + e], gv[o], rr[e]));
+    *reinterpret_cast<float4*>(dx + c) = make_float4(rr[0], rr[1], rr[2], rr[3]);
+  }
+}
+
+// Nearest up-sample backward: dsrc[si][sj] += sum of dx_up over its preimage
+// (a contiguous index range per axis; gather, no atomics).  dsrc may hold a
+// gradient already (accumulate=1).
+__global__ void upsample_bwd_kernel(const float* __restrict__ dxup, int h, int w, int hs, int ws,
+                                    int C, int accumulate, float* __restrict__ dsrc) {
+  const int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int C4 = C >> 2;
+  const int b = blockIdx.y;
+  if (idx >= (int64_t)hs * ws * C4) return;
+  const int c4 = (int)(idx % C4);
+  const int sp = (int)(idx / C4);
+  const int si = sp / ws, sj = sp - (sp / ws) * ws;
+  // preimage rows: dst i with nsrc(i) == si (monotone in i)
+  int i0 = (int)((int64_t)si * h / hs) - 2, j0 = (int)((int64_t)sj * w / ws) - 2;
+  if (i0 < 0) i0 = 0;
+  if (j0 < 0) j0 = 0;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = i0; i < h; ++i) {
+    const int ni = nsrc(i, hs, h);
+    if (ni < si) continue;
+    if (ni > si) break;
+    for (int j = j0; j < w; ++j) {
+      const int nj = nsrc(j, ws, w);
+      if (nj < sj) continue;
+      if (nj > sj) break;
+      const float4 g = reinterpret_cast<const float4*>(dxup + (((int64_t)b * h + i) * w + j) * C)[c4];
+      acc.x += g.x; acc.y += g.y; acc.z += g.z; acc.w += g.w;
+    }
+  }
+  float4* d = reinterpret_cast<float4*>(dsrc + (((int64_t)b * hs + si) * ws + sj) * C) + c4;
+  if (accumulate) {
+    const float4 o = *d;
+    acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+  }
+  *d = acc;
+}
+
+// Training forward helper: x_up = nearest(src) materialised (the NLM weight
+// gradients need it per pixel).
+__global__ void upsample_fwd_kernel(const float* __restrict__ src, int hs, int ws, int h, int w,
+                                    int C, float* __restrict__ dst) {
+  const int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int C4 = C >> 2;
+  const int b = blockIdx.y;
+  if (idx >= (int64_t)h * w * C4) return;
+  const int c4 = (int)(idx % C4);
+  const int p = (int)(idx / C4);
+  const int i = p / w, j = p - (p / w) * w;
+  reinterpret_cast<float4*>(dst + (((int64_t)b * h + i) * w + j) * C)[c4] =
+      reinterpret_cast<const float4*>(src + (((int64_t)b * hs + nsrc(i, hs, h)) * ws + nsrc(j, ws, w)) * C)[c4];
+}
+
+}  // namespace jabd
+
+using namespace jabd;
+
+extern "C" int jabd_nlm_bwd_attn_f32(const float* dout, int32_t B, int32_t h, int32_t w,
+                                     int32_t C, const float* q, const float* kpool,
+                                     const float* vpool, int32_t S, const float* wW,
+                                     const float* wq, float* dq, float* dxup, float* part,
+                                     float* dk, float* dv, jabd_stream_t stream) {
+  JABD_REQUIRE(dout && q && kpool && vpool && wW && wq && dq && dxup && part && dk && dv &&
+                   C % 4 == 0,
+               "nlm_bwd_attn: bad args");
+  const int nblk = (int)cdiv((int64_t)h * w, 256);
+  const size_t smem = (2 * (size_t)S * CH + 2 * (size_t)C * CH + 4 * (size_t)S * 2 * CH) * 4;
+  JABD_REQUIRE(smem <= 64 * 1024, "nlm_bwd_attn: LDS %zu > 64KiB", smem);
+  hipStream_t st = as_stream(stream);
+  dim3 g((unsigned)nblk, (unsigned)B);
+  nlm_bwd_attn_kernel<<<g, 256, smem, st>>>(dout, h, w, C, q, kpool, vpool, S, wW, wq, dq, dxup,
+                                            part, nblk);
+  if (int e = check_launch("nlm_bwd_attn")) return e;
+  dim3 g2((unsigned)cdiv(S * 2 * CH, 256), (unsigned)B);
+  nlm_bwd_kv_reduce_kernel<<<g2, 256, 0, st>>>(part, nblk, S, dk, dv);
+  return check_launch("nlm_bwd_kv_reduce");
+}
+
+extern "C" int jabd_nlm_bwd_proj_f32(const float* dk, const float* dv, int32_t B, int32_t S,
+                                     const int32_t* sizes, int32_t nsizes, int32_t h, int32_t w,
+                                     int32_t C, const float* wk, const float* wv, float* dkv,
+                                     float* dxup, jabd_stream_t stream) {
+  JABD_REQUIRE(dk && dv && sizes && wk && wv && dkv && dxup && nsizes > 0 && nsizes <= 8 &&
+                   C % 4 == 0,
+               "nlm_bwd_proj: bad args");
+  PspSizes ps;
+  ps.n = nsizes;
+  for (int i = 0; i < 8; ++i) ps.v[i] = i < nsizes ? sizes[i] : 0;
+  const size_t smem = (2 * (size_t)S * CH + 2 * (size_t)C * CH) * 4;
+  dim3 g((unsigned)cdiv((int64_t)h * w, 256), (unsigned)B);
+  nlm_bwd_proj_kernel<<<g, 256, smem, as_stream(stream)>>>(dk, dv, S, ps, h, w, C, wk, wv, dkv,
+                                                           dxup);
+  return check_launch("nlm_bwd_proj");
+}
+
+extern "C" int jabd_upsample_nearest_bwd_f32(const float* dxup, int32_t B, int32_t h, int32_t w,
+                                             int32_t hs, int32_t ws, int32_t C, int32_t accumulate,
+                                             float* dsrc, jabd_stream_t stream) {
+  JABD_REQUIRE(dxup && dsrc && C % 4 == 0 && hs <= h && ws <= w, "upsample_bwd: bad args");
+  dim3 g((unsigned)cdiv((int64_t)hs * ws * (C / 4), 256), (unsigned)B);
+  upsample_bwd_kernel<<<g, 256, 0, as_stream(stream)>>>(dxup, h, w, hs, ws, C, accumulate, dsrc);
+  return check_launch("upsample_bwd");
+}
+
+extern "C" int jabd_upsample_nearest_f32(const float* src, int32_t B, int32_t hs, int32_t ws,
+                                         int32_t h, int32_t w, int32_t C, float* dst,
+                                         jabd_stream_t stream) {
+  JABD_REQUIRE(src && dst && C % 4 == 0, "upsample: bad args");
+  dim3 g((unsigned)cdiv((int64_t)h * w * (C / 4), 256), (unsigned)B);
+  upsample_fwd_kernel<<<g, 256, 0, as_stream(stream)>>>(src, hs, ws, h, w, C, dst);
+  return check_launch("upsample");
+}

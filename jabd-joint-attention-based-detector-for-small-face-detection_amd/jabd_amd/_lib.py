@@ -45,7 +45,8 @@ class ConvArgs(ctypes.Structure):
         ("Kc", c_i32),
         ("KH", c_i32), ("KW", c_i32), ("stride", c_i32), ("pad", c_i32),
         ("act", c_i32), ("slope", c_f32),
-        ("nchw_in", c_i32), ("reserved0", c_i32),
+        ("nchw_in", c_i32), ("tconv", c_i32),
+        ("flags", c_i32), ("reserved1", c_i32),
         ("M", c_i64),
     ]
 
@@ -91,17 +92,49 @@ SIGNATURES = {
     "jabd_dw_nblk": [c_i64, c_i64, c_i64, c_i64],
     "jabd_dwconv_nhwc_f32": [ctypes.POINTER(DwArgs), c_vp],
     "jabd_channel_sum_f32": [c_vp, c_i64, c_i32, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp],
-    "jabd_eca_gate_f32": [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp],
+    "jabd_eca_gate_f32": [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp,
+                          c_vp],
     "jabd_nlm_pool_f32": [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp,
                           c_vp, c_vp, c_vp, c_i32, ctypes.POINTER(c_i32), c_i32, c_vp, c_vp,
                           c_vp, c_vp],
     "jabd_nlm_apply_f32": [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp,
-                           c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
+                           c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                           c_vp],
     "jabd_maxpool_nhwc_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp],
     "jabd_heads_f32": [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i64, c_i64, c_i32,
                        c_vp, c_vp, c_vp, c_vp],
+    # training (A11)
+    "jabd_bn_nblk": [c_i64, c_i32],
+    "jabd_bn_stats_f32": [c_vp, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32,
+                          c_vp],
+    "jabd_bn_act_fwd_f32": [c_vp, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32,
+                            c_i32, c_f32, c_vp, c_i32, c_i32, c_vp],
+    "jabd_bn_act_bwd_f32": [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_i64, c_i32, c_vp,
+                            c_vp, c_vp, c_vp, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "jabd_conv_wgrad_part_floats": [ctypes.POINTER(ConvArgs)],
+    "jabd_conv_wgrad_f32": [ctypes.POINTER(ConvArgs), c_vp, c_vp, c_vp],
+    "jabd_dw_dgrad_f32": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
+                          c_i32, c_vp, c_vp],
+    "jabd_dw_wgrad_part_floats": [c_i64, c_i32, c_i32],
+    "jabd_dw_wgrad_f32": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
+                          c_i32, c_vp, c_vp, c_vp],
+    "jabd_eca_bwd_f32": [c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp,
+                         c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "jabd_scale_bwd_f32": [c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp],
+    "jabd_heads_gather_f32": [c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp],
+    "jabd_nlm_bwd_attn_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp,
+                              c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "jabd_nlm_bwd_proj_f32": [c_vp, c_vp, c_i32, c_i32, ctypes.POINTER(c_i32), c_i32, c_i32,
+                              c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
+    "jabd_upsample_nearest_bwd_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
+                                      c_vp, c_vp],
+    "jabd_upsample_nearest_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp],
+    "jabd_maxpool_bwd_f32": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp,
+                             c_vp],
 }
-_RESTYPE = {"jabd_version": ctypes.c_char_p, "jabd_dw_nblk": ctypes.c_int64}
+_RESTYPE = {"jabd_version": ctypes.c_char_p, "jabd_dw_nblk": ctypes.c_int64,
+            "jabd_bn_nblk": ctypes.c_int64, "jabd_conv_wgrad_part_floats": ctypes.c_int64,
+            "jabd_dw_wgrad_part_floats": ctypes.c_int64}
 
 _lock = threading.Lock()
 _lib = None

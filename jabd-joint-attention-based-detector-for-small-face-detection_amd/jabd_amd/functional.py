@@ -196,16 +196,19 @@ def channel_sums(x, nblk=None):
     return part
 
 
-def eca_gate(part, hw, w1d, gate):
+def eca_gate(part, hw, w1d, gate, return_mean=False):
     B, nblk, C = part.shape
     scale = torch.empty((B, C), dtype=torch.float32, device=part.device)
+    mean = torch.empty((B, C), dtype=torch.float32, device=part.device) if return_mean else None
     call("jabd_eca_gate_f32", part.data_ptr(), nblk, B, C, hw, w1d.data_ptr(), w1d.numel(),
-         ACT[gate], scale.data_ptr(), _stream())
-    return scale
+         ACT[gate], scale.data_ptr(), _ptr(mean), _stream())
+    return (scale, mean) if return_mean else scale
 
 
-def nlm_fused(src, lateral, nlm_w, sizes):
-    """lateral + NLM(nearest(src -> lateral's size)); all NHWC."""
+def nlm_fused(src, lateral, nlm_w, sizes, save=False):
+    """lateral + NLM(nearest(src -> lateral's size)); all NHWC.
+
+    save=True also returns (q, ctx, kpool, vpool) for the backward."""
     B, hs, ws, C = src.shape
     _, h, w, _ = lateral.shape
     wq, bq, wk, bk, wv, bv, wW, bW = nlm_w
@@ -219,9 +222,15 @@ def nlm_fused(src, lateral, nlm_w, sizes):
          wk.data_ptr(), bk.data_ptr(), wv.data_ptr(), bv.data_ptr(), ch, arr, len(sizes),
          kp.data_ptr(), vp.data_ptr(), kv.data_ptr(), _stream())
     out = torch.empty_like(lateral)
+    q = ctx = None
+    if save:
+        q = torch.empty((B, h * w, ch), dtype=torch.float32, device=src.device)
+        ctx = torch.empty_like(q)
     call("jabd_nlm_apply_f32", src.data_ptr(), src.stride(0), C, B, hs, ws, C, h, w,
          wq.data_ptr(), bq.data_ptr(), kp.data_ptr(), vp.data_ptr(), S, ch, wW.data_ptr(),
-         bW.data_ptr(), lateral.data_ptr(), out.data_ptr(), _stream())
+         bW.data_ptr(), lateral.data_ptr(), out.data_ptr(), _ptr(q), _ptr(ctx), _stream())
+    if save:
+        return out, (q, ctx, kp, vp)
     return out
 
 

@@ -1,6 +1,642 @@
-"""Training-mode (batch-statistics BatchNorm) forward/backward — see DESIGN.md."""
+"""Training-mode forward/backward of the JABD detectors on the HIP path (A11).
+
+`train_forward(model, kind, x)` runs RetinaFace.forward in training mode
+(BatchNorm2d with batch statistics and running-buffer updates, as
+`loss.backward()` at train_mobilenetV3_ecagai.py:532 expects) as a graph of
+torch.autograd.Functions whose forward AND backward passes are libjabd
+kernels (fp32, NHWC):
+
+  ConvFn      implicit-GEMM conv (MFMA); dgrad = transposed-conv GEMM,
+              wgrad = MFMA weight-gradient kernel
+  EcaConvFn   conv(x * ECA(x)) — the ECA gate applied on the GEMM's operand
+              load; backward through the gate, Conv1d and average pool
+  BnActFn     batch-stat BN + activation (+ the block's residual add)
+  DwConvFn    depthwise conv; dgrad/wgrad kernels
+  NlmFn       CSAF non-local block fused with the up-sample and lateral add
+  SshTailFn   SSH's three BN branches written into one concatenated tensor
+  HeadsFn     the three 1x1 heads of all levels -> (loc, conf, landm)
+  MaxPoolFn   ResNet stem max pool
+
+Torch is used only for allocation, views and a few tiny reductions of
+kernel partials.  There is no CPU path.
+"""
+import ctypes
+import weakref
+
+import torch
+
+from . import functional as F
+from ._lib import ConvArgs, call, lib
+
+ACT = F.ACT
+
+
+def _st():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+    return t.data_ptr() if t is not None else None
+
+
+# ----------------------------------------------------------------------------- packing cache
+_PACK = {}  # id(Parameter) -> (weakref to it, {(version, ptr, transposed): PackedConv})
+
+
+def _packed(weight, transposed):
+    """PackedConv of a raw (unfolded) conv weight; transposed = data-gradient form.
+
+    Cached per live Parameter object (weak key, so a freed parameter's address
+    can never hit a stale entry) and per version (an optimizer step bumps it);
+    derived tensors are packed per call."""
+    cache = None
+    key = (weight._version, weight.data_ptr(), transposed)
+    if isinstance(weight, torch.nn.Parameter):
+        ent = _PACK.get(id(weight))
+        if ent is None or ent[0]() is not weight:  # new or recycled id: start fresh
+            ent = (weakref.ref(weight, lambda _r, i=id(weight): _PACK.pop(i, None)), {})
+            _PACK[id(weight)] = ent
+        cache = ent[1]
+        pk = cache.get(key)
+        if pk is not None:
+            return pk
+    w = weight.detach().float()
+    if transposed:
+        w = w.transpose(0, 1)  # [Cin][Cout][KH][KW]: the dgrad GEMM's "weight"
+    kh, kw = w.shape[2], w.shape[3]
+    pk = F.PackedConv(F.conv_weight_2d(w).contiguous(), None, kh, kw, w.shape[1])
+    if cache is not None:
+        if len(cache) > 4:  # stale versions
+            cache.clear()
+        cache[key] = pk
+    return pk
+
+
+def _conv_args(x, pk, y, stride, pad, nchw_in=False, ascale=None, tconv=False, OH=None, OW=None):
+    a = ConvArgs()
+    if nchw_in:
+        B, cin, H, W = x.shape
+        a.x, a.x_bs, a.x_ps = x.data_ptr(), cin * H * W, 1
+    else:
+        B, H, W, ctot = x.shape
+        a.x, a.x_bs, a.x_ps = x.data_ptr(), H * W * ctot, ctot
+    a.B, a.H, a.W, a.Cin = B, H, W, pk.Cin
+    if ascale is not None:
+        a.ascale, a.ascale_bs = ascale.data_ptr(), ascale.shape[1]
+    a.w = pk.w.data_ptr()
+    a.y, a.y_bs, a.y_ps, a.y_c0 = y.data_ptr(), y.stride(0), y.shape[3], 0
+    a.OH = y.shape[1] if OH is None else OH
+    a.OW = y.shape[2] if OW is None else OW
+    a.Cout, a.Ntiles, a.tn, a.Kc = pk.Cout, pk.Ntiles, pk.tn, pk.Kc
+    a.KH, a.KW, a.stride, a.pad = pk.KH, pk.KW, stride, pad
+    a.nchw_in = 1 if nchw_in else 0
+    a.tconv = 1 if tconv else 0
+    return a
+
+
+def _wgrad(x, dy, weight, stride, pad, nchw_in=False, ascale=None):
+    """dW (torch layout) of conv(x[*ascale]) given dY (NHWC)."""
+    cout, cin, kh, kw = weight.shape
+    a = ConvArgs()
+    if nchw_in:
+        B, _, H, W = x.shape
+        a.x, a.x_bs, a.x_ps = x.data_ptr(), cin * H * W, 1
+    else:
+        B, H, W, ctot = x.shape
+        a.x, a.x_bs, a.x_ps = x.data_ptr(), H * W * ctot, ctot
+    a.B, a.H, a.W, a.Cin = B, H, W, cin
+    if ascale is not None:
+        a.ascale, a.ascale_bs = ascale.data_ptr(), ascale.shape[1]
+    a.y, a.y_bs, a.y_ps, a.y_c0 = dy.data_ptr(), dy.stride(0), dy.shape[3], 0
+    a.OH, a.OW, a.Cout = dy.shape[1], dy.shape[2], cout
+    a.KH, a.KW, a.stride, a.pad = kh, kw, stride, pad
+    a.nchw_in = 1 if nchw_in else 0
+    nparts = int(lib().jabd_conv_wgrad_part_floats(ctypes.byref(a)))
+    part = torch.empty(max(nparts, 1), dtype=torch.float32, device=dy.device)
+    dw = torch.empty_like(weight, dtype=torch.float32)
+    call("jabd_conv_wgrad_f32", ctypes.byref(a), part.data_ptr(), dw.data_ptr(), _st())
+    return dw
+
+
+def _chan_sum(t):
+    """Per-channel sum of an NHWC tensor (kernel partials, tiny torch reduce)."""
+    return F.channel_sums(t).sum(dim=(0, 1))
+
+
+def _dgrad(dy, weight, stride, pad, H, W):
+    pk = _packed(weight, transposed=True)
+    B = dy.shape[0]
+    dx = torch.empty((B, H, W, pk.Cout), dtype=torch.float32, device=dy.device)
+    a = _conv_args(dy, pk, dx, stride, pad, tconv=True, OH=H, OW=W)
+    call("jabd_conv2d_nhwc_f32", ctypes.byref(a), _st())
+    return dx
+
+
+# ----------------------------------------------------------------------------- functions
+class ConvFn(torch.autograd.Function):
+    """y = conv(x, weight) [+ bias]; x NHWC (or the NCHW network input)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, pad, nchw_in):
+        pk = _packed(weight, transposed=False)
+        if nchw_in:
+            B, _, H, W = x.shape
+        else:
+            B, H, W, _ = x.shape
+        OH = (H + 2 * pad - pk.KH) // stride + 1
+        OW = (W + 2 * pad - pk.KW) // stride + 1
+        y = torch.empty((B, OH, OW, pk.Cout), dtype=torch.float32, device=x.device)
+        if (nchw_in and pk.KH == 3 and stride == 2 and pad == 1 and pk.Cin == 3
+                and pk.Cout == 16):
+            wt = F.conv_weight_2d(weight.detach().float()).contiguous()
+            zb = torch.zeros(16, dtype=torch.float32, device=x.device)
+            call("jabd_stem_nchw_f32", x.data_ptr(), B, H, W, wt.data_ptr(), zb.data_ptr(),
+                 ACT["none"], y.data_ptr(), _st())
+        else:
+            a = _conv_args(x, pk, y, stride, pad, nchw_in=nchw_in)
+            if bias is not None:
+                b = bias.detach().float().contiguous()
+                a.bias = b.data_ptr()
+            call("jabd_conv2d_nhwc_f32", ctypes.byref(a), _st())
+        ctx.save_for_backward(x, weight)
+        ctx.cfg = (stride, pad, nchw_in, bias is not None, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        stride, pad, nchw_in, has_bias, H, W = ctx.cfg
+        dy = dy.contiguous()
+        dx = None
+        if ctx.needs_input_grad[0] and not nchw_in:
+            dx = _dgrad(dy, weight, stride, pad, H, W)
+        dw = _wgrad(x, dy, weight, stride, pad, nchw_in) if ctx.needs_input_grad[1] else None
+        db = _chan_sum(dy) if has_bias and ctx.needs_input_grad[2] else None
+        return dx, dw, db, None, None, None
+
+
+class EcaConvFn(torch.autograd.Function):
+    """y = conv(x * eca(x), weight): ECA (mean pool -> Conv1d -> gate) of x,
+    applied on the GEMM's operand load (nets/mobilenetV3.py:343-348 then the
+    consumer conv; nets/retinaface_r.py:219-224 for the head ECAs)."""
+
+    @staticmethod
+    def forward(ctx, x, w1d, weight, stride, pad, gate):
+        B, H, W, C = x.shape
+        w1 = w1d.detach().reshape(-1).float().contiguous()
+        scale, mean = F.eca_gate(F.channel_sums(x), H * W, w1, gate, return_mean=True)
+        pk = _packed(weight, transposed=False)
+        OH = (H + 2 * pad - pk.KH) // stride + 1
+        OW = (W + 2 * pad - pk.KW) // stride + 1
+        y = torch.empty((B, OH, OW, pk.Cout), dtype=torch.float32, device=x.device)
+        a = _conv_args(x, pk, y, stride, pad, ascale=scale)
+        call("jabd_conv2d_nhwc_f32", ctypes.byref(a), _st())
+        ctx.save_for_backward(x, w1d, weight, scale, mean)
+        ctx.cfg = (stride, pad, gate, H, W)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w1d, weight, scale, mean = ctx.saved_tensors
+        stride, pad, gate, H, W = ctx.cfg
+        dy = dy.contiguous()
+        B, _, _, C = x.shape
+        da = _dgrad(dy, weight, stride, pad, H, W)          # grad of x*scale
+        dw = _wgrad(x, dy, weight, stride, pad, ascale=scale)
+        w1 = w1d.detach().reshape(-1).float().contiguous()
+        k = w1.numel()
+        HW = H * W
+        nblk = max(1, min(64, HW // 256))
+        part = torch.empty((B, nblk, C), dtype=torch.float32, device=x.device)
+        dmean = torch.empty((B, C), dtype=torch.float32, device=x.device)
+        dw1_img = torch.empty((B, k), dtype=torch.float32, device=x.device)
+        dx = torch.empty_like(x)
+        dw1 = torch.empty(k, dtype=torch.float32, device=x.device)
+        call("jabd_eca_bwd_f32", da.data_ptr(), x.data_ptr(), B, HW, C, scale.data_ptr(),
+             mean.data_ptr(), w1.data_ptr(), k, ACT[gate], part.data_ptr(), nblk,
+             dmean.data_ptr(), dw1_img.data_ptr(), dx.data_ptr(), dw1.data_ptr(), _st())
+        return dx, dw1.view_as(w1d), dw, None, None, None
+
+
+class BnActFn(torch.autograd.Function):
+    """y = act(BN_train(x) [+ res]); updates the running buffers in place."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, res, rmean, rvar, act, slope, momentum, eps):
+        B, H, W, C = x.shape
+        M = B * H * W
+        nblk = int(lib().jabd_bn_nblk(M, C))
+        part = torch.empty((nblk, 2, C), dtype=torch.float32, device=x.device)
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        invstd = torch.empty_like(mean)
+        call("jabd_bn_stats_f32", x.data_ptr(), C, M, C, part.data_ptr(), mean.data_ptr(),
+             invstd.data_ptr(), _p(rmean), _p(rvar), float(momentum), float(eps), _st())
+        y = torch.empty_like(x)
+        g = gamma.detach().contiguous()
+        b = beta.detach().contiguous()
+        call("jabd_bn_act_fwd_f32", x.data_ptr(), C, M, C, mean.data_ptr(), invstd.data_ptr(),
+             g.data_ptr(), b.data_ptr(), _p(res), C, ACT[act], float(slope), y.data_ptr(), C, 0,
+             _st())
+        ctx.save_for_backward(x, g, b, res if res is not None else None, mean, invstd)
+        ctx.cfg = (act, slope, res is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, g, b, res, mean, invstd = ctx.saved_tensors
+        act, slope, has_res = ctx.cfg
+        dy = dy.contiguous()
+        B, H, W, C = x.shape
+        M = B * H * W
+        nblk = int(lib().jabd_bn_nblk(M, C))
+        part = torch.empty((nblk, 2, C), dtype=torch.float32, device=x.device)
+        dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
+        dbeta = torch.empty_like(dgamma)
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(x) if has_res else None
+        call("jabd_bn_act_bwd_f32", dy.data_ptr(), C, 0, x.data_ptr(), C, _p(res), C, M, C,
+             mean.data_ptr(), invstd.data_ptr(), g.data_ptr(), b.data_ptr(), ACT[act],
+             float(slope), part.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), dx.data_ptr(),
+             _p(dres), _st())
+        return dx, dgamma, dbeta, dres, None, None, None, None, None, None
+
+
+class DwConvFn(torch.autograd.Function):
+    """Depthwise k x k conv (pad k//2), no bias (nets/mobilenetV3.py:105-106)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride):
+        C, _, k, _ = weight.shape
+        wt = weight.detach().float().reshape(C, k * k).t().contiguous()
+        y, _ = F.dwconv(x, wt, None, k, stride)
+        ctx.save_for_backward(x, wt)
+        ctx.cfg = (k, stride)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wt = ctx.saved_tensors
+        k, stride = ctx.cfg
+        dy = dy.contiguous()
+        B, H, W, C = x.shape
+        OH, OW = dy.shape[1], dy.shape[2]
+        pad = k // 2
+        dx = torch.empty_like(x)
+        call("jabd_dw_dgrad_f32", dy.data_ptr(), wt.data_ptr(), B, H, W, C, OH, OW, k, stride,
+             pad, dx.data_ptr(), _st())
+        nparts = int(lib().jabd_dw_wgrad_part_floats(B * OH * OW, C, k))
+        part = torch.empty(nparts, dtype=torch.float32, device=x.device)
+        dw = torch.empty((C, 1, k, k), dtype=torch.float32, device=x.device)
+        call("jabd_dw_wgrad_f32", x.data_ptr(), dy.data_ptr(), B, H, W, C, OH, OW, k, stride,
+             pad, part.data_ptr(), dw.data_ptr(), _st())
+        return dx, dw, None
+
+
+class NlmFn(torch.autograd.Function):
+    """lateral + NLM(nearest(src -> lateral size)) (nets/retinaface_r.py:192-203)."""
+
+    @staticmethod
+    def forward(ctx, src, lateral, wq, bq, wk, bk, wv, bv, wW, bW, sizes):
+        B, hs, ws, C = src.shape
+        _, h, w, _ = lateral.shape
+        ch = wq.shape[0]
+        d = lambda t, *s: t.detach().float().reshape(*s).contiguous()  # noqa: E731
+        W = (d(wq, ch, C), d(bq, ch), d(wk, ch, C), d(bk, ch), d(wv, ch, C), d(bv, ch),
+             d(wW, C, ch), d(bW, C))
+        out, (q, cx, kp, vp) = F.nlm_fused(src, lateral.contiguous(), W, sizes, save=True)
+        xup = torch.empty((B, h, w, C), dtype=torch.float32, device=src.device)
+        call("jabd_upsample_nearest_f32", src.data_ptr(), B, hs, ws, h, w, C, xup.data_ptr(),
+             _st())
+        ctx.save_for_backward(xup, q, cx, kp, vp, *W)
+        ctx.cfg = (tuple(sizes), hs, ws)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        xup, q, cx, kp, vp, wq, bq, wk, bk, wv, bv, wW, bW = ctx.saved_tensors
+        sizes, hs, ws = ctx.cfg
+        dout = dout.contiguous()
+        B, h, w, C = dout.shape
+        ch = wq.shape[0]
+        S = kp.shape[1]
+        dev = dout.device
+        nblk = (h * w + 255) // 256
+        dq = torch.empty((B, h, w, ch), dtype=torch.float32, device=dev)
+        dxup = torch.empty((B, h, w, C), dtype=torch.float32, device=dev)
+        part = torch.empty((B, nblk, S, 2 * ch), dtype=torch.float32, device=dev)
+        dk = torch.empty((B, S, ch), dtype=torch.float32, device=dev)
+        dv = torch.empty_like(dk)
+        call("jabd_nlm_bwd_attn_f32", dout.data_ptr(), B, h, w, C, q.data_ptr(), kp.data_ptr(),
+             vp.data_ptr(), S, wW.data_ptr(), wq.data_ptr(), dq.data_ptr(), dxup.data_ptr(),
+             part.data_ptr(), dk.data_ptr(), dv.data_ptr(), _st())
+        dkv = torch.empty((B, h, w, 2 * ch), dtype=torch.float32, device=dev)
+        arr = (ctypes.c_int32 * len(sizes))(*sizes)
+        call("jabd_nlm_bwd_proj_f32", dk.data_ptr(), dv.data_ptr(), B, S, arr, len(sizes), h, w,
+             C, wk.data_ptr(), wv.data_ptr(), dkv.data_ptr(), dxup.data_ptr(), _st())
+        dsrc = torch.empty((B, hs, ws, C), dtype=torch.float32, device=dev)
+        call("jabd_upsample_nearest_bwd_f32", dxup.data_ptr(), B, h, w, hs, ws, C, 0,
+             dsrc.data_ptr(), _st())
+        # weight gradients = 1x1-conv weight gradients of the saved per-pixel tensors
+        ctxv = cx.view(B, h, w, ch)
+        dWW = _wgrad(ctxv, dout, torch.empty((C, ch, 1, 1), device=dev), 1, 0)
+        dWq = _wgrad(xup, dq, torch.empty((ch, C, 1, 1), device=dev), 1, 0)
+        dk_only = dkv[..., :ch].contiguous()
+        dv_only = dkv[..., ch:].contiguous()
+        dWk = _wgrad(xup, dk_only, torch.empty((ch, C, 1, 1), device=dev), 1, 0)
+        dWv = _wgrad(xup, dv_only, torch.empty((ch, C, 1, 1), device=dev), 1, 0)
+        g = (dWq, _chan_sum(dq), dWk, _chan_sum(dk_only), dWv, _chan_sum(dv_only), dWW,
+             _chan_sum(dout))
+        return (dsrc, dout) + g + (None,)
+
+
+class SshTailFn(torch.autograd.Function):
+    """relu(cat(BN(a), BN(b), BN(c))) of SSH (nets/layers.py:56-68)."""
+
+    @staticmethod
+    def forward(ctx, a, b, c, ga, ba, gb, bb, gc, bc, stats):
+        outs = []
+        B, H, W, _ = a.shape
+        Ctot = a.shape[3] + b.shape[3] + c.shape[3]
+        y = torch.empty((B, H, W, Ctot), dtype=torch.float32, device=a.device)
+        saved = []
+        c0 = 0
+        for x, g, bt, (rm, rv, mom, eps) in zip((a, b, c), (ga, gb, gc), (ba, bb, bc), stats):
+            C = x.shape[3]
+            M = B * H * W
+            nblk = int(lib().jabd_bn_nblk(M, C))
+            part = torch.empty((nblk, 2, C), dtype=torch.float32, device=x.device)
+            mean = torch.empty(C, dtype=torch.float32, device=x.device)
+            invstd = torch.empty_like(mean)
+            call("jabd_bn_stats_f32", x.data_ptr(), C, M, C, part.data_ptr(), mean.data_ptr(),
+                 invstd.data_ptr(), _p(rm), _p(rv), float(mom), float(eps), _st())
+            gg, bb_ = g.detach().contiguous(), bt.detach().contiguous()
+            call("jabd_bn_act_fwd_f32", x.data_ptr(), C, M, C, mean.data_ptr(),
+                 invstd.data_ptr(), gg.data_ptr(), bb_.data_ptr(), None, C, ACT["relu"], 0.0,
+                 y.data_ptr(), Ctot, c0, _st())
+            saved += [x, gg, bb_, mean, invstd]
+            outs.append(c0)
+            c0 += C
+        ctx.save_for_backward(*saved)
+        ctx.offs = outs
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        sv = ctx.saved_tensors
+        res = []
+        Ctot = dy.shape[3]
+        for i in range(3):
+            x, g, b, mean, invstd = sv[5 * i:5 * i + 5]
+            B, H, W, C = x.shape
+            M = B * H * W
+            nblk = int(lib().jabd_bn_nblk(M, C))
+            part = torch.empty((nblk, 2, C), dtype=torch.float32, device=x.device)
+            dg = torch.empty(C, dtype=torch.float32, device=x.device)
+            db = torch.empty_like(dg)
+            dx = torch.empty_like(x)
+            call("jabd_bn_act_bwd_f32", dy.data_ptr(), Ctot, ctx.offs[i], x.data_ptr(), C, None,
+                 C, M, C, mean.data_ptr(), invstd.data_ptr(), g.data_ptr(), b.data_ptr(),
+                 ACT["relu"], 0.0, part.data_ptr(), dg.data_ptr(), db.data_ptr(), dx.data_ptr(),
+                 None, _st())
+            res.append((dx, dg, db))
+        (da, dga, dba), (dbx, dgb, dbb), (dc, dgc, dbc) = res
+        return da, dbx, dc, dga, dba, dgb, dbb, dgc, dbc, None
+
+
+class HeadsFn(torch.autograd.Function):
+    """Bbox/Class/Landmark 1x1 heads of the 3 levels -> (loc, conf, landm) logits."""
+
+    @staticmethod
+    def forward(ctx, f1, f2, f3, *wb):
+        feats = (f1, f2, f3)
+        B = f1.shape[0]
+        A = sum(2 * f.shape[1] * f.shape[2] for f in feats)
+        dev = f1.device
+        loc = torch.empty((B, A, 4), dtype=torch.float32, device=dev)
+        conf = torch.empty((B, A, 2), dtype=torch.float32, device=dev)
+        landm = torch.empty((B, A, 10), dtype=torch.float32, device=dev)
+        a_off = 0
+        cat = []
+        for i, f in enumerate(feats):
+            ws = wb[6 * i:6 * i + 6]  # Wb, bb, Wc, bc, Wl, bl
+            C = f.shape[3]
+            wt = torch.cat([ws[0].detach().reshape(8, C), ws[2].detach().reshape(4, C),
+                            ws[4].detach().reshape(20, C)]).float().contiguous()
+            bs = torch.cat([ws[1].detach(), ws[3].detach(), ws[5].detach()]).float().contiguous()
+            F.heads(f, wt, bs, loc, conf, landm, a_off, softmax=False)
+            cat.append(wt)
+            a_off += 2 * f.shape[1] * f.shape[2]
+        ctx.save_for_backward(f1, f2, f3, *cat)
+        return loc, conf, landm
+
+    @staticmethod
+    def backward(ctx, gl, gc, glm):
+        f1, f2, f3, w1, w2, w3 = ctx.saved_tensors
+        dev = f1.device
+        B = f1.shape[0]
+        A = gl.shape[1]
+        gl = gl.contiguous() if gl is not None else torch.zeros((B, A, 4), device=dev)
+        gc = gc.contiguous() if gc is not None else torch.zeros((B, A, 2), device=dev)
+        glm = glm.contiguous() if glm is not None else torch.zeros((B, A, 10), device=dev)
+        a_off = 0
+        dfs, dws = [], []
+        for f, wt in zip((f1, f2, f3), (w1, w2, w3)):
+            _, h, w, C = f.shape
+            dout = torch.empty((B, h, w, 32), dtype=torch.float32, device=dev)
+            call("jabd_heads_gather_f32", gl.data_ptr(), gc.data_ptr(), glm.data_ptr(), B, A,
+                 a_off, h * w, dout.data_ptr(), _st())
+            wconv = wt.view(32, C, 1, 1)
+            dfs.append(_dgrad(dout, wconv, 1, 0, h, w))
+            dW = _wgrad(f, dout, wconv, 1, 0).view(32, C)
+            db = _chan_sum(dout)
+            dws += [dW[:8].reshape(8, C, 1, 1), db[:8], dW[8:12].reshape(4, C, 1, 1), db[8:12],
+                    dW[12:].reshape(20, C, 1, 1), db[12:]]
+            a_off += 2 * h * w
+        return tuple(dfs) + tuple(dws)
+
+
+class MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        y = F.maxpool(x, 3, 2, 1)
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        B, H, W, C = x.shape
+        dx = torch.empty_like(x)
+        call("jabd_maxpool_bwd_f32", x.data_ptr(), dy.data_ptr(), B, H, W, C, 3, 2, 1,
+             dx.data_ptr(), _st())
+        return dx
+
+
+# ----------------------------------------------------------------------------- graph helpers
+def _pad_to4(c):
+    return (c + 3) // 4 * 4
+
+
+def bn_act(x, bn, act="none", slope=0.0, res=None):
+    """BatchNorm2d module (training) + activation, padded channels allowed."""
+    C = x.shape[3]
+    g, b = bn.weight, bn.bias
+    rm, rv = bn.running_mean, bn.running_var
+    if C != g.shape[0]:  # zero-padded channels (10 -> 12): pad params/buffers
+        pad = C - g.shape[0]
+        g = torch.cat([g, g.new_zeros(pad)])
+        b = torch.cat([b, b.new_zeros(pad)])
+        rm_p = torch.cat([rm, rm.new_zeros(pad)])
+        rv_p = torch.cat([rv, rv.new_ones(pad)])
+        y = BnActFn.apply(x, g, b, res, rm_p, rv_p, act, slope, bn.momentum, bn.eps)
+        with torch.no_grad():
+            rm.copy_(rm_p[: rm.shape[0]])
+            rv.copy_(rv_p[: rv.shape[0]])
+    else:
+        y = BnActFn.apply(x, g, b, res, rm, rv, act, slope, bn.momentum, bn.eps)
+    if bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    return y
+
+
+def _padw(weight, cout=None, cin=None):
+    """Zero-pad a conv weight's out/in channels (autograd-tracked)."""
+    w = weight
+    if cout is not None and cout > w.shape[0]:
+        w = torch.cat([w, w.new_zeros((cout - w.shape[0],) + tuple(w.shape[1:]))], 0)
+    if cin is not None and cin > w.shape[1]:
+        w = torch.cat([w, w.new_zeros((w.shape[0], cin - w.shape[1]) + tuple(w.shape[2:]))], 1)
+    return w
+
+
+def conv(x, m, stride=1, pad=0, nchw_in=False):
+    return ConvFn.apply(x, m.weight, m.bias, stride, pad, nchw_in)
+
+
+def _mnv3_block(blk, s):
+    act = blk.act_name
+    e = bn_act(conv(s, blk.conv1), blk.bn1, act)
+    d = bn_act(DwConvFn.apply(e, blk.conv2.weight, blk.stride), blk.bn2, act)
+    p = EcaConvFn.apply(d, blk.eca.conv.weight, blk.conv3.weight, 1, 0, "hsigmoid")
+    sk = blk.skip
+    if sk is None:
+        res = s
+    elif blk.stride == 1:
+        res = bn_act(conv(s, sk[0]), sk[1])
+    elif len(sk) == 4:
+        t = bn_act(DwConvFn.apply(s, sk[0].weight, 2), sk[1])
+        res = bn_act(conv(t, sk[2]), sk[3])
+    else:
+        res = bn_act(DwConvFn.apply(s, sk[0].weight, 2), sk[1])
+    return bn_act(p, blk.bn3, act, res=res)
+
+
+def _r50_block(blk, x):
+    t = bn_act(conv(x, blk.conv1), blk.bn1, "relu")
+    t = bn_act(conv(t, blk.conv2, blk.stride, 1), blk.bn2, "relu")
+    t = conv(t, blk.conv3)
+    if blk.downsample is not None:
+        idn = bn_act(conv(x, blk.downsample[0], blk.stride), blk.downsample[1])
+    else:
+        idn = x
+    return bn_act(t, blk.bn3, "relu", res=idn)
+
+
+def _head(m, feats, eca_names, nlm):
+    fpn = m.fpn
+    lk = fpn.leaky
+    outs = (fpn.output1, fpn.output2, fpn.output3)
+    lat = [bn_act(EcaConvFn.apply(f, getattr(m, n).conv.weight, o[0].weight, 1, 0, "sigmoid"),
+                  o[1], "leaky", lk) for f, n, o in zip(feats, eca_names, outs)]
+    o1, o2, o3 = lat
+    nw = (nlm.f_query.weight, nlm.f_query.bias, nlm.f_key.weight, nlm.f_key.bias,
+          nlm.f_value.weight, nlm.f_value.bias, nlm.W.weight, nlm.W.bias)
+    sizes = tuple(nlm.psp.sizes)
+    m2 = NlmFn.apply(o3, o2, *nw, sizes)
+    o2 = bn_act(conv(m2, fpn.merge2[0], 1, 1), fpn.merge2[1], "leaky", lk)
+    m1 = NlmFn.apply(o2, o1, *nw, sizes)
+    o1 = bn_act(conv(m1, fpn.merge1[0], 1, 1), fpn.merge1[1], "leaky", lk)
+    feats_out = []
+    ew = m.eca_fpn.conv.weight
+    for o, ssh in zip((o1, o2, o3), (m.ssh1, m.ssh2, m.ssh3)):
+        q = ssh.conv5X5_1[0].out_channels
+        qp = _pad_to4(q)
+        a = EcaConvFn.apply(o, ew, ssh.conv3X3[0].weight, 1, 1, "sigmoid")
+        b1 = bn_act(EcaConvFn.apply(o, ew, _padw(ssh.conv5X5_1[0].weight, cout=qp), 1, 1,
+                                    "sigmoid"), ssh.conv5X5_1[1], "leaky", ssh.leaky)
+        b = ConvFn.apply(b1, _padw(ssh.conv5X5_2[0].weight, cout=qp, cin=qp), None, 1, 1, False)
+        c1 = bn_act(ConvFn.apply(b1, _padw(ssh.conv7X7_2[0].weight, cout=qp, cin=qp), None, 1, 1,
+                                 False), ssh.conv7X7_2[1], "leaky", ssh.leaky)
+        c = ConvFn.apply(c1, _padw(ssh.conv7x7_3[0].weight, cout=qp, cin=qp), None, 1, 1, False)
+        stats = []
+        bns = (ssh.conv3X3[1], ssh.conv5X5_2[1], ssh.conv7x7_3[1])
+        gb = []
+        for bn, t in zip(bns, (a, b, c)):
+            C = t.shape[3]
+            pad = C - bn.weight.shape[0]
+            if pad:
+                g = torch.cat([bn.weight, bn.weight.new_zeros(pad)])
+                bt = torch.cat([bn.bias, bn.bias.new_zeros(pad)])
+                stats.append((None, None, bn.momentum, bn.eps))  # updated below
+            else:
+                g, bt = bn.weight, bn.bias
+                stats.append((bn.running_mean, bn.running_var, bn.momentum, bn.eps))
+            gb += [g, bt]
+            if bn.num_batches_tracked is not None:
+                bn.num_batches_tracked.add_(1)
+        if qp != q:
+            # padded branches: track running stats on padded copies, then copy back
+            padded = []
+            for i, (bn, t) in enumerate(zip(bns, (a, b, c))):
+                if stats[i][0] is None:
+                    pad = t.shape[3] - bn.weight.shape[0]
+                    rm = torch.cat([bn.running_mean, bn.running_mean.new_zeros(pad)])
+                    rv = torch.cat([bn.running_var, bn.running_var.new_ones(pad)])
+                    stats[i] = (rm, rv, bn.momentum, bn.eps)
+                    padded.append((bn, rm, rv))
+            f = SshTailFn.apply(a, b, c, *gb, stats)
+            with torch.no_grad():
+                for bn, rm, rv in padded:
+                    bn.running_mean.copy_(rm[: bn.running_mean.shape[0]])
+                    bn.running_var.copy_(rv[: bn.running_var.shape[0]])
+            # drop the zero pad channels of the 10-channel branches
+            C = o.shape[3]
+            half, quarter = C // 2, q
+            f = torch.cat([f[..., :half], f[..., half:half + quarter],
+                           f[..., half + qp:half + qp + quarter]], -1)
+        else:
+            f = SshTailFn.apply(a, b, c, *gb, stats)
+        feats_out.append(f.contiguous())
+    wb = []
+    for i in range(3):
+        for h in (m.BboxHead[i], m.ClassHead[i], m.LandmarkHead[i]):
+            wb += [h.conv1x1.weight, h.conv1x1.bias]
+    return HeadsFn.apply(*feats_out, *wb)
 
 
 def train_forward(model, kind, x):
-    raise NotImplementedError(
-        "training-mode RetinaFace.forward on the HIP path is not built yet; call model.eval()")
+    if model.mode != "train":
+        raise NotImplementedError("training-mode forward returns logits (mode='train'); the "
+                                  "reference's training scripts construct RetinaFace that way")
+    x = x.contiguous()
+    if kind == "mnv3":
+        body = model.body
+        s = bn_act(conv(x, body.conv1, 2, 1, nchw_in=True), body.bn1, "hswish")
+        feats = []
+        for i in (1, 2, 3):
+            for blk in getattr(body, f"layer{i}"):
+                s = _mnv3_block(blk, s)
+            feats.append(s)
+        return _head(model, feats, ("eca_40", "eca_80", "eca_160"), model.fpn.nlm)
+    body = model.body
+    s = bn_act(conv(x, body.conv1, 2, 3, nchw_in=True), body.bn1, "relu")
+    s = MaxPoolFn.apply(s)
+    feats = []
+    for i in (1, 2, 3, 4):
+        for blk in getattr(body, f"layer{i}"):
+            s = _r50_block(blk, s)
+        if i >= 2:
+            feats.append(s)
+    return _head(model, feats, ("eca_64", "eca_128", "eca_256"), model.fpn.Nlm)

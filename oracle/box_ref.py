@@ -134,7 +134,7 @@ def multibox_loss(loc, conf, landm, loc_t, conf_t, landm_t, neg_pos=7, num_class
     mine = lse - bc.gather(1, conf_t.view(-1, 1))
     mine[pos.view(-1, 1)] = 0
     mine = mine.view(loc.shape[0], -1)
-    _, order = mine.sort(1, descending=True, stable=True)
+    _, order = torch.sort(mine, dim=1, descending=True, stable=True)
     _, rank = order.sort(1)
     num_pos = pos.long().sum(1, keepdim=True)
     num_neg = torch.clamp(neg_pos * num_pos, max=pos.shape[1] - 1)

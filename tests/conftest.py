@@ -20,3 +20,7 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     return torch.device("cuda:0")
+
+# spawned test workers import jabd_amd too
+os.environ["PYTHONPATH"] = os.pathsep.join(
+    [PKG, ROOT] + [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p])

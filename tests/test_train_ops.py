@@ -1,0 +1,208 @@
+"""Per-op backward parity of the training Functions (jabd_amd/train.py)
+against autograd of the same math in PyTorch-CPU float64 (test-only
+reference).  Tolerance: max-abs error <= 1e-4 of each tensor's magnitude."""
+import pytest
+import torch
+import torch.nn.functional as tF
+
+from _util import rel_err
+
+TOL = 1e-4
+
+
+def _nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def _nchw(t):
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+def _check(got_list, ref_list, names):
+    for g, r, n in zip(got_list, ref_list, names):
+        assert g is not None, n
+        e = rel_err(g, r)
+        assert e < TOL, f"{n}: rel err {e:.2e}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,k,s,h", [(16, 64, 1, 1, 12), (40, 40, 3, 1, 9), (256, 128, 3, 1, 4),
+                                            (64, 64, 3, 2, 11), (256, 512, 1, 2, 8),
+                                            (12, 10, 3, 1, 7), (1024, 256, 1, 1, 4)])
+def test_convfn_grads(cuda, cin, cout, k, s, h):
+    from jabd_amd.train import ConvFn
+    g = torch.Generator().manual_seed(cin + k)
+    x = torch.randn(2, cin, h, h + 1, generator=g)
+    w = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
+    dy_seed = torch.Generator().manual_seed(7)
+    xr, wr = x.double().requires_grad_(), w.double().requires_grad_()
+    y = tF.conv2d(xr, wr, None, s, k // 2)
+    dy = torch.randn(y.shape, generator=dy_seed, dtype=torch.float64)
+    (y * dy).sum().backward()
+    xg = _nhwc(x).to(cuda).requires_grad_()
+    wg = torch.nn.Parameter(w.to(cuda))
+    yg = ConvFn.apply(xg, wg, None, s, k // 2, False)
+    assert rel_err(_nchw(yg.detach()), y.detach()) < TOL
+    (yg * _nhwc(dy.float()).to(cuda)).sum().backward()
+    _check([_nchw(xg.grad), wg.grad], [xr.grad, wr.grad], ["dx", "dw"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,cout,k,gate,h", [(40, 40, 1, "sigmoid", 8), (256, 128, 3, "sigmoid", 4),
+                                             (72, 24, 1, "hsigmoid", 10), (2048, 256, 1, "sigmoid", 3)])
+def test_ecaconvfn_grads(cuda, c, cout, k, gate, h):
+    from jabd_amd.train import EcaConvFn
+    from oracle.model_ref import eca_kernel_size
+    g = torch.Generator().manual_seed(c)
+    x = torch.randn(2, c, h, h, generator=g)
+    ke = eca_kernel_size(c)
+    w1 = torch.randn(1, 1, ke, generator=g)
+    w = torch.randn(cout, c, k, k, generator=g) / (c * k * k) ** 0.5
+    xr, w1r, wr = (t.double().requires_grad_() for t in (x, w1, w))
+    yv = xr.mean(dim=(2, 3))
+    z = tF.conv1d(yv.unsqueeze(1), w1r, padding=(ke - 1) // 2).squeeze(1)
+    sc = torch.sigmoid(z) if gate == "sigmoid" else tF.hardsigmoid(z)
+    y = tF.conv2d(xr * sc[:, :, None, None], wr, None, 1, k // 2)
+    dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(3), dtype=torch.float64)
+    (y * dy).sum().backward()
+    xg = _nhwc(x).to(cuda).requires_grad_()
+    w1g = torch.nn.Parameter(w1.to(cuda))
+    wg = torch.nn.Parameter(w.to(cuda))
+    yg = EcaConvFn.apply(xg, w1g, wg, 1, k // 2, gate)
+    assert rel_err(_nchw(yg.detach()), y.detach()) < TOL
+    (yg * _nhwc(dy.float()).to(cuda)).sum().backward()
+    _check([_nchw(xg.grad), w1g.grad, wg.grad], [xr.grad, w1r.grad, wr.grad], ["dx", "dw1d", "dw"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,act,res", [(40, "relu", False), (24, "hswish", True), (2048, "relu", True),
+                                       (256, "leaky", False), (12, "none", False)])
+def test_bnactfn_grads(cuda, c, act, res):
+    from jabd_amd.train import BnActFn
+    g = torch.Generator().manual_seed(c)
+    x = torch.randn(3, c, 5, 6, generator=g) * 2 + 1
+    gam = 1 + 0.2 * torch.randn(c, generator=g)
+    bet = 0.1 * torch.randn(c, generator=g)
+    r = torch.randn(3, c, 5, 6, generator=g) if res else None
+    xr, gr, br = (t.double().requires_grad_() for t in (x, gam, bet))
+    rr = r.double().requires_grad_() if res else None
+    rm, rv = torch.zeros(c, dtype=torch.float64), torch.ones(c, dtype=torch.float64)
+    z = tF.batch_norm(xr, rm, rv, gr, br, True, 0.1, 1e-5)
+    if res:
+        z = z + rr
+    y = {"relu": tF.relu, "hswish": tF.hardswish, "leaky": lambda t: tF.leaky_relu(t, 0.1),
+         "none": lambda t: t}[act](z)
+    dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(4), dtype=torch.float64)
+    (y * dy).sum().backward()
+    xg = _nhwc(x).to(cuda).requires_grad_()
+    gg, bg = (torch.nn.Parameter(t.to(cuda)) for t in (gam, bet))
+    rg = _nhwc(r).to(cuda).requires_grad_() if res else None
+    rmg, rvg = torch.zeros(c, device=cuda), torch.ones(c, device=cuda)
+    yg = BnActFn.apply(xg, gg, bg, rg, rmg, rvg, act, 0.1, 0.1, 1e-5)
+    assert rel_err(_nchw(yg.detach()), y.detach()) < TOL
+    (yg * _nhwc(dy.float()).to(cuda)).sum().backward()
+    got = [_nchw(xg.grad), gg.grad, bg.grad] + ([_nchw(rg.grad)] if res else [])
+    ref = [xr.grad, gr.grad, br.grad] + ([rr.grad] if res else [])
+    _check(got, ref, ["dx", "dgamma", "dbeta", "dres"])
+    assert rel_err(rmg, rm) < TOL and rel_err(rvg, rv) < TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,k,s,h", [(16, 3, 1, 9), (64, 3, 2, 10), (72, 5, 2, 11), (120, 5, 1, 6)])
+def test_dwconvfn_grads(cuda, c, k, s, h):
+    from jabd_amd.train import DwConvFn
+    g = torch.Generator().manual_seed(c + k)
+    x = torch.randn(2, c, h, h + 2, generator=g)
+    w = torch.randn(c, 1, k, k, generator=g) / k
+    xr, wr = x.double().requires_grad_(), w.double().requires_grad_()
+    y = tF.conv2d(xr, wr, None, s, k // 2, 1, c)
+    dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(2), dtype=torch.float64)
+    (y * dy).sum().backward()
+    xg = _nhwc(x).to(cuda).requires_grad_()
+    wg = torch.nn.Parameter(w.to(cuda))
+    yg = DwConvFn.apply(xg, wg, s)
+    assert rel_err(_nchw(yg.detach()), y.detach()) < TOL
+    (yg * _nhwc(dy.float()).to(cuda)).sum().backward()
+    _check([_nchw(xg.grad), wg.grad], [xr.grad, wr.grad], ["dx", "dw"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,hs,h", [(40, 4, 8), (256, 2, 4), (40, 27, 53), (40, 6, 12)])
+def test_nlmfn_grads(cuda, C, hs, h):
+    from jabd_amd.train import NlmFn
+    from oracle.model_ref import Ctx, nlm
+    g = torch.Generator().manual_seed(C + h)
+    src = torch.randn(2, C, hs, hs, generator=g)
+    lat = torch.randn(2, C, h, h, generator=g)
+    P = {"n.f_query.weight": torch.randn(4, C, 1, 1, generator=g) / C ** 0.5,
+         "n.f_query.bias": 0.1 * torch.randn(4, generator=g),
+         "n.f_key.weight": torch.randn(4, C, 1, 1, generator=g) / C ** 0.5,
+         "n.f_key.bias": 0.1 * torch.randn(4, generator=g),
+         "n.f_value.weight": torch.randn(4, C, 1, 1, generator=g) / C ** 0.5,
+         "n.f_value.bias": 0.1 * torch.randn(4, generator=g),
+         "n.W.weight": torch.randn(C, 4, 1, 1, generator=g) / 2,
+         "n.W.bias": 0.1 * torch.randn(C, generator=g)}
+    Pr = {k: v.double().requires_grad_() for k, v in P.items()}
+    sr, lr = src.double().requires_grad_(), lat.double().requires_grad_()
+    up = tF.interpolate(sr, size=[h, h], mode="nearest")
+    y = lr + nlm(Ctx(Pr), up, "n.")
+    dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(8), dtype=torch.float64)
+    (y * dy).sum().backward()
+    Pg = {k: torch.nn.Parameter(v.to(cuda)) for k, v in P.items()}
+    sg, lg = _nhwc(src).to(cuda).requires_grad_(), _nhwc(lat).to(cuda).requires_grad_()
+    order = ["n.f_query.weight", "n.f_query.bias", "n.f_key.weight", "n.f_key.bias",
+             "n.f_value.weight", "n.f_value.bias", "n.W.weight", "n.W.bias"]
+    yg = NlmFn.apply(sg, lg, *[Pg[k] for k in order], (1, 4, 8, 12))
+    assert rel_err(_nchw(yg.detach()), y.detach()) < TOL
+    (yg * _nhwc(dy.float()).to(cuda)).sum().backward()
+    got = [_nchw(sg.grad), _nchw(lg.grad)] + [Pg[k].grad for k in order if k != "n.f_key.bias"]
+    ref = [sr.grad, lr.grad] + [Pr[k].grad for k in order if k != "n.f_key.bias"]
+    _check(got, ref, ["dsrc", "dlat"] + [k for k in order if k != "n.f_key.bias"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C", [40, 256])
+def test_headsfn_grads(cuda, C):
+    from jabd_amd.train import HeadsFn
+    g = torch.Generator().manual_seed(C)
+    feats = [torch.randn(2, C, s, s, generator=g) for s in (8, 4, 2)]
+    wb = []
+    for _ in range(3):
+        for n in (8, 4, 20):
+            wb += [torch.randn(n, C, 1, 1, generator=g) / C ** 0.5, 0.1 * torch.randn(n, generator=g)]
+    fr = [f.double().requires_grad_() for f in feats]
+    wr = [t.double().requires_grad_() for t in wb]
+    outs = []
+    for kind, (k, off) in enumerate(((4, 0), (2, 2), (10, 4))):
+        parts = []
+        for i, f in enumerate(fr):
+            o = tF.conv2d(f, wr[6 * i + off], wr[6 * i + off + 1]).permute(0, 2, 3, 1)
+            parts.append(o.reshape(2, -1, k))
+        outs.append(torch.cat(parts, 1))
+    dys = [torch.randn(o.shape, generator=torch.Generator().manual_seed(i), dtype=torch.float64)
+           for i, o in enumerate(outs)]
+    sum((o * d).sum() for o, d in zip(outs, dys)).backward()
+    fg = [_nhwc(f).to(cuda).requires_grad_() for f in feats]
+    wg = [torch.nn.Parameter(t.to(cuda)) for t in wb]
+    og = HeadsFn.apply(*fg, *wg)
+    for o, r in zip(og, outs):
+        assert rel_err(o.detach(), r.detach()) < TOL
+    sum((o * d.float().to(cuda)).sum() for o, d in zip(og, dys)).backward()
+    _check([_nchw(f.grad) for f in fg] + [w.grad for w in wg],
+           [f.grad for f in fr] + [w.grad for w in wr], [f"t{i}" for i in range(21)])
+
+
+@pytest.mark.gpu
+def test_maxpoolfn_grads(cuda):
+    from jabd_amd.train import MaxPoolFn
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(2, 64, 9, 10, generator=g)
+    xr = x.double().requires_grad_()
+    y = tF.max_pool2d(xr, 3, 2, 1)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (y * dy).sum().backward()
+    xg = _nhwc(x).to(cuda).requires_grad_()
+    yg = MaxPoolFn.apply(xg)
+    assert rel_err(_nchw(yg.detach()), y.detach()) < TOL
+    (yg * _nhwc(dy.float()).to(cuda)).sum().backward()
+    _check([_nchw(xg.grad)], [xr.grad], ["dx"])
