@@ -92,17 +92,50 @@ __global__ __launch_bounds__(kRedThreads) void bn_stats_part_kernel(
   }
 }
 
-__global__ void bn_stats_final_kernel(const float* __restrict__ x, const float* __restrict__ part,
-                                      int64_t nblk, int64_t M, int C, float momentum, float eps,
-                                      float* __restrict__ mean, float* __restrict__ invstd,
-                                      float* __restrict__ rmean, float* __restrict__ rvar) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double S = 0.0, Q = 0.0;  // 1024 partials: fp64 accumulation is free here
-  for (int64_t b = 0; b < nblk; ++b) {
-    S += part[b * 2 * C + c];
-    Q += part[b * 2 * C + C + c];
+// Deterministic fp64 sum over the nblk partial blocks of part[b][0|1][c] for
+// the `lanes` channels of this workgroup (rows of threads stride the blocks,
+// then a fixed-order LDS combine); valid in threads t < lanes.
+__device__ __forceinline__ void bn_final_sums(const float* __restrict__ part, int64_t nblk, int C,
+                                              int lanes, double& S, double& Q) {
+  __shared__ double ls[kRedThreads], lq[kRedThreads];
+  const int t = threadIdx.x;
+  const int rows = kRedThreads / lanes;
+  const int r = t / lanes;
+  const int c = blockIdx.x * lanes + t % lanes;
+  double s = 0.0, q = 0.0;
+  if (r < rows && c < C) {
+#pragma unroll 4
+    for (int64_t b = r; b < nblk; b += rows) {
+      s += part[b * 2 * C + c];
+      q += part[b * 2 * C + C + c];
+    }
   }
+  ls[t] = s;
+  lq[t] = q;
+  __syncthreads();
+  S = 0.0;
+  Q = 0.0;
+  if (t < lanes)
+    for (int k = 0; k < rows; ++k) {
+      S += ls[k * lanes + t];
+      Q += lq[k * lanes + t];
+    }
+}
+
+static int bn_fin_lanes(int C) {
+  int l = 1;
+  while (l < C && l < 64) l <<= 1;
+  return l;
+}
+
+__global__ __launch_bounds__(kRedThreads) void bn_stats_final_kernel(
+    const float* __restrict__ x, const float* __restrict__ part, int64_t nblk, int64_t M, int C,
+    int lanes, float momentum, float eps, float* __restrict__ mean, float* __restrict__ invstd,
+    float* __restrict__ rmean, float* __restrict__ rvar) {
+  double S, Q;
+  bn_final_sums(part, nblk, C, lanes, S, Q);
+  const int c = blockIdx.x * lanes + threadIdx.x;
+  if (threadIdx.x >= lanes || c >= C) return;
   const double ms = S / (double)M;
   double var = Q / (double)M - ms * ms;
   if (var < 0.0) var = 0.0;
@@ -116,36 +149,61 @@ __global__ void bn_stats_final_kernel(const float* __restrict__ x, const float* 
   }
 }
 
+// Elementwise BN kernels: workgroup = `lanes` float4 channel groups x
+// (256 / lanes) rows, `iters` row passes; per-channel parameters live in
+// registers (no per-element index division).
+constexpr int kEwIters = 8;
+
+struct EwMap {
+  int64_t m0;
+  int rows_pass, cg;
+  bool ok;
+};
+
+__device__ __forceinline__ EwMap ew_map(int lanes, int C4) {
+  EwMap e;
+  const int t = threadIdx.x;
+  e.rows_pass = kRedThreads / lanes;
+  const int r0 = t / lanes;
+  e.cg = blockIdx.y * lanes + t % lanes;
+  e.ok = r0 < e.rows_pass && e.cg < C4;
+  e.m0 = (int64_t)blockIdx.x * e.rows_pass * kEwIters + r0;
+  return e;
+}
+
 // y = act((x - mean) * invstd * gamma + beta [+ res])
-__global__ void bn_act_fwd_kernel(const float* __restrict__ x, int ldx, int64_t M, int C,
-                                  const float* __restrict__ mean, const float* __restrict__ invstd,
-                                  const float* __restrict__ gamma, const float* __restrict__ beta,
-                                  const float* __restrict__ res, int ldr, int act, float slope,
-                                  float* __restrict__ y, int ldy, int yc0) {
-  const int C4 = C >> 2;
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= M * C4) return;
-  const int64_t m = i / C4;
-  const int c = (int)(i - m * C4) * 4;
-  const float4 v = *reinterpret_cast<const float4*>(x + m * ldx + c);
+__global__ __launch_bounds__(kRedThreads) void bn_act_fwd_kernel(
+    const float* __restrict__ x, int ldx, int64_t M, int C, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ beta, const float* __restrict__ res, int ldr, int act, float slope,
+    float* __restrict__ y, int ldy, int yc0, int lanes) {
+  const EwMap e = ew_map(lanes, C >> 2);
+  if (!e.ok) return;
+  const int c = e.cg * 4;
   const float4 mu = *reinterpret_cast<const float4*>(mean + c);
   const float4 is = *reinterpret_cast<const float4*>(invstd + c);
   const float4 gm = *reinterpret_cast<const float4*>(gamma + c);
   const float4 bt = *reinterpret_cast<const float4*>(beta + c);
-  float4 o;
-  o.x = (v.x - mu.x) * is.x * gm.x + bt.x;
-  o.y = (v.y - mu.y) * is.y * gm.y + bt.y;
-  o.z = (v.z - mu.z) * is.z * gm.z + bt.z;
-  o.w = (v.w - mu.w) * is.w * gm.w + bt.w;
-  if (res) {
-    const float4 r = *reinterpret_cast<const float4*>(res + m * ldr + c);
-    o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+#pragma unroll 2
+  for (int k = 0; k < kEwIters; ++k) {
+    const int64_t m = e.m0 + (int64_t)k * e.rows_pass;
+    if (m >= M) break;
+    const float4 v = *reinterpret_cast<const float4*>(x + m * ldx + c);
+    float4 o;
+    o.x = (v.x - mu.x) * is.x * gm.x + bt.x;
+    o.y = (v.y - mu.y) * is.y * gm.y + bt.y;
+    o.z = (v.z - mu.z) * is.z * gm.z + bt.z;
+    o.w = (v.w - mu.w) * is.w * gm.w + bt.w;
+    if (res) {
+      const float4 r = *reinterpret_cast<const float4*>(res + m * ldr + c);
+      o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+    }
+    o.x = act_f(o.x, act, slope);
+    o.y = act_f(o.y, act, slope);
+    o.z = act_f(o.z, act, slope);
+    o.w = act_f(o.w, act, slope);
+    *reinterpret_cast<float4*>(y + m * ldy + yc0 + c) = o;
   }
-  o.x = act_f(o.x, act, slope);
-  o.y = act_f(o.y, act, slope);
-  o.z = act_f(o.z, act, slope);
-  o.w = act_f(o.w, act, slope);
-  *reinterpret_cast<float4*>(y + m * ldy + yc0 + c) = o;
 }
 
 // dz = dy * act'(z);  part[blk][0][c] = sum dz, part[blk][1][c] = sum dz * xhat
@@ -209,51 +267,68 @@ __global__ __launch_bounds__(kRedThreads) void bn_bwd_part_kernel(
   }
 }
 
-__global__ void bn_bwd_final_kernel(const float* __restrict__ part, int64_t nblk, int C,
-                                    float* __restrict__ dbeta, float* __restrict__ dgamma) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double S = 0.0, Q = 0.0;
-  for (int64_t b = 0; b < nblk; ++b) {
-    S += part[b * 2 * C + c];
-    Q += part[b * 2 * C + C + c];
-  }
+__global__ __launch_bounds__(kRedThreads) void bn_bwd_final_kernel(
+    const float* __restrict__ part, int64_t nblk, int C, int lanes, float* __restrict__ dbeta,
+    float* __restrict__ dgamma) {
+  double S, Q;
+  bn_final_sums(part, nblk, C, lanes, S, Q);
+  const int c = blockIdx.x * lanes + threadIdx.x;
+  if (threadIdx.x >= lanes || c >= C) return;
   dbeta[c] = (float)S;
   dgamma[c] = (float)Q;
 }
 
 // dx = gamma*invstd*(dz - sum(dz)/M - xhat*sum(dz*xhat)/M); dres = dz
-__global__ void bn_bwd_apply_kernel(const float* __restrict__ dy, int lddy, int dyc0,
-                                    const float* __restrict__ x, int ldx,
-                                    const float* __restrict__ res, int ldr, int64_t M, int C,
-                                    const float* __restrict__ mean,
-                                    const float* __restrict__ invstd,
-                                    const float* __restrict__ gamma,
-                                    const float* __restrict__ beta, int act, float slope,
-                                    const float* __restrict__ sdz, const float* __restrict__ sdzx,
-                                    float* __restrict__ dx, float* __restrict__ dres) {
-  const int C4 = C >> 2;
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= M * C4) return;
-  const int64_t m = i / C4;
-  const int c = (int)(i - m * C4) * 4;
+__global__ __launch_bounds__(kRedThreads) void bn_bwd_apply_kernel(
+    const float* __restrict__ dy, int lddy, int dyc0, const float* __restrict__ x, int ldx,
+    const float* __restrict__ res, int ldr, int64_t M, int C, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ beta, int act, float slope, const float* __restrict__ sdz,
+    const float* __restrict__ sdzx, float* __restrict__ dx, float* __restrict__ dres, int lanes) {
+  const EwMap e = ew_map(lanes, C >> 2);
+  if (!e.ok) return;
+  const int c = e.cg * 4;
   const float invM = 1.f / (float)M;
-  const float4 v = *reinterpret_cast<const float4*>(x + m * ldx + c);
-  const float4 g = *reinterpret_cast<const float4*>(dy + m * lddy + dyc0 + c);
-  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (res) r = *reinterpret_cast<const float4*>(res + m * ldr + c);
-  float vv[4] = {v.x, v.y, v.z, v.w}, gg[4] = {g.x, g.y, g.z, g.w}, rr[4] = {r.x, r.y, r.z, r.w};
-  float o[4], dzo[4];
+  float mu[4], is[4], gm[4], bt[4], a1[4], a2[4];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const float mu = mean[c + e], is = invstd[c + e], gm = gamma[c + e], bt = beta[c + e];
-    const float xh = (vv[e] - mu) * is;
-    const float dz = gg[e] * act_d(xh * gm + bt + rr[e], act, slope);
-    dzo[e] = dz;
-    o[e] = gm * is * (dz - sdz[c + e] * invM - xh * sdzx[c + e] * invM);
+  for (int j = 0; j < 4; ++j) {
+    mu[j] = mean[c + j];
+    is[j] = invstd[c + j];
+    gm[j] = gamma[c + j];
+    bt[j] = beta[c + j];
+    a1[j] = sdz[c + j] * invM;
+    a2[j] = sdzx[c + j] * invM;
   }
-  *reinterpret_cast<float4*>(dx + m * (int64_t)C + c) = make_float4(o[0], o[1], o[2], o[3]);
-  if (dres) *reinterpret_cast<float4*>(dres + m * (int64_t)C + c) = make_float4(dzo[0], dzo[1], dzo[2], dzo[3]);
+#pragma unroll 2
+  for (int k = 0; k < kEwIters; ++k) {
+    const int64_t m = e.m0 + (int64_t)k * e.rows_pass;
+    if (m >= M) break;
+    const float4 v = *reinterpret_cast<const float4*>(x + m * ldx + c);
+    const float4 g = *reinterpret_cast<const float4*>(dy + m * lddy + dyc0 + c);
+    float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (res) r = *reinterpret_cast<const float4*>(res + m * ldr + c);
+    const float vv[4] = {v.x, v.y, v.z, v.w}, gg[4] = {g.x, g.y, g.z, g.w},
+                rr[4] = {r.x, r.y, r.z, r.w};
+    float o[4], dzo[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float xh = (vv[j] - mu[j]) * is[j];
+      const float dz = gg[j] * act_d(xh * gm[j] + bt[j] + rr[j], act, slope);
+      dzo[j] = dz;
+      o[j] = gm[j] * is[j] * (dz - a1[j] - xh * a2[j]);
+    }
+    *reinterpret_cast<float4*>(dx + m * (int64_t)C + c) = make_float4(o[0], o[1], o[2], o[3]);
+    if (dres)
+      *reinterpret_cast<float4*>(dres + m * (int64_t)C + c) =
+          make_float4(dzo[0], dzo[1], dzo[2], dzo[3]);
+  }
+}
+
+static dim3 ew_grid(int64_t M, int C, int& lanes) {
+  const int C4 = C / 4;
+  lanes = C4 < 64 ? C4 : 64;
+  const int rows_pass = kRedThreads / lanes;
+  return dim3((unsigned)cdiv(M, (int64_t)rows_pass * kEwIters), (unsigned)cdiv(C4, lanes), 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -369,26 +444,203 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const ConvArgs p, int64
   }
 }
 
-// dW (torch layout [Cout][Cin][KH][KW]) = sum over chunks of part[chunk][k][n]
-__global__ void wgrad_reduce_kernel(const float* __restrict__ part, int64_t nchunk, int K, int Cout,
-                                    int Cin, int KHW, float* __restrict__ dw) {
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= (int64_t)K * Cout) return;
-  const int k = (int)(i / Cout), n = (int)(i - (int64_t)k * Cout);
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-  int64_t c = 0;
-  for (; c + 4 <= nchunk; c += 4) {
+// Vector wgrad (NHWC x with Cin % 4 == 0, contiguous dY with Cout % 4 == 0):
+// tile KT (im2col k) x NT (out channels) over a chunk of pixels.  X and dY
+// stage through LDS in their natural [pixel][channel] layout with float4
+// global loads and float4 LDS stores (no transposition); the MFMA reduction
+// index runs over pixels, lane (i, g) feeding pixel 16S + g + 4e of step e, so
+// the operand reads are conflict-free ds_read_b32 (row pitch = 16 mod 32
+// dwords).  Tiles smaller than 4 MFMA blocks split the pixels across waves
+// and combine in LDS in a fixed order.  Global loads of stage s+1 are issued
+// before the MFMAs of stage s (register prefetch).
+constexpr int kWvP = 64;  // pixels per stage
+
+template <int KT>
+struct WvPitch {
+  static constexpr int v = (KT % 32 == 16) ? KT : KT + 16;
+};
+
+template <int KT, int NT>
+__global__ __launch_bounds__(256) void conv_wgrad_v_kernel(const ConvArgs p, int px_per_wg,
+                                                           int fast1x1, float* __restrict__ part) {
+  constexpr int LDA = WvPitch<KT>::v, LDN = WvPitch<NT>::v;
+  constexpr int QA = KT / 16, QD = NT / 16;  // float4 loads per thread per stage
+  constexpr int NBK = KT / 16, NBN = NT / 16, NB = NBK * NBN;
+  constexpr int BPW = NB >= 4 ? NB / 4 : 1;  // MFMA blocks per wave
+  constexpr int WPB = NB >= 4 ? 1 : 4 / NB;  // waves sharing a block (pixel split)
+  __shared__ float Xs[kWvP * LDA];
+  __shared__ float Ds[kWvP * LDN];
+  const int K = p.KH * p.KW * p.Cin;
+  const int k0 = blockIdx.x * KT, n0 = blockIdx.y * NT;
+  const int chunk = blockIdx.z;
+  const int mbeg = chunk * px_per_wg;
+  const int mend = min(mbeg + px_per_wg, (int)p.M);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int OHW = p.OH * p.OW;
+
+  float4 ra[QA], rd[QD];
+  auto load_stage = [&](int px0) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) s[u] += part[(c + u) * K * Cout + i];
+    for (int q = 0; q < QA; ++q) {
+      const int idx = q * 256 + t;
+      const int px = idx / (KT / 4), c4 = (idx % (KT / 4)) * 4;
+      const int m = px0 + px;
+      const int k = k0 + c4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (m < mend && k < K) {
+        if (fast1x1) {
+          v = *reinterpret_cast<const float4*>(p.x + (int64_t)m * p.x_ps + p.x_c0 + k);
+          if (p.ascale) {
+            const int b = m / OHW;
+            const float4 s4 = *reinterpret_cast<const float4*>(p.ascale + (int64_t)b * p.ascale_bs + k);
+            v.x *= s4.x; v.y *= s4.y; v.z *= s4.z; v.w *= s4.w;
+          }
+        } else {
+          const int b = m / OHW, rr = m - b * OHW;
+          const int oh = rr / p.OW, ow = rr - oh * p.OW;
+          const int tap = k / p.Cin, ci = k - tap * p.Cin;
+          const int kh = tap / p.KW, kw = tap - kh * p.KW;
+          const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
+          if (ih >= 0 && ih < p.H && iw >= 0 && iw < p.W) {
+            v = *reinterpret_cast<const float4*>(p.x + (int64_t)b * p.x_bs +
+                                                 ((int64_t)ih * p.W + iw) * p.x_ps + p.x_c0 + ci);
+            if (p.ascale) {
+              const float4 s4 =
+                  *reinterpret_cast<const float4*>(p.ascale + (int64_t)b * p.ascale_bs + ci);
+              v.x *= s4.x; v.y *= s4.y; v.z *= s4.z; v.w *= s4.w;
+            }
+          }
+        }
+      }
+      ra[q] = v;
+    }
+#pragma unroll
+    for (int q = 0; q < QD; ++q) {
+      const int idx = q * 256 + t;
+      const int px = idx / (NT / 4), c4 = (idx % (NT / 4)) * 4;
+      const int m = px0 + px;
+      const int n = n0 + c4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (m < mend && n < p.Cout)
+        v = *reinterpret_cast<const float4*>(p.y + (int64_t)m * p.y_ps + p.y_c0 + n);
+      rd[q] = v;
+    }
+  };
+
+  f32x4 acc[BPW];
+#pragma unroll
+  for (int j = 0; j < BPW; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // this wave's blocks: NB >= 4 -> blocks wave*BPW + j; else block wave % NB
+  const int sub = NB >= 4 ? 0 : wave / NB;  // pixel-group residue (NB < 4)
+
+  load_stage(mbeg);
+  for (int px0 = mbeg; px0 < mend; px0 += kWvP) {
+#pragma unroll
+    for (int q = 0; q < QA; ++q) {
+      const int idx = q * 256 + t;
+      const int px = idx / (KT / 4), c4 = (idx % (KT / 4)) * 4;
+      *reinterpret_cast<float4*>(Xs + px * LDA + c4) = ra[q];
+    }
+#pragma unroll
+    for (int q = 0; q < QD; ++q) {
+      const int idx = q * 256 + t;
+      const int px = idx / (NT / 4), c4 = (idx % (NT / 4)) * 4;
+      *reinterpret_cast<float4*>(Ds + px * LDN + c4) = rd[q];
+    }
+    __syncthreads();
+    if (px0 + kWvP < mend) load_stage(px0 + kWvP);
+#pragma unroll
+    for (int S = 0; S < kWvP / 16; ++S) {
+      if (NB < 4 && (S % WPB) != sub) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = 16 * S + g + 4 * e;
+#pragma unroll
+        for (int j = 0; j < BPW; ++j) {
+          const int blk = NB >= 4 ? wave * BPW + j : wave % NB;
+          const int bk = blk / NBN, bn = blk % NBN;
+          const float a = Xs[row * LDA + 16 * bk + i];
+          const float b = Ds[row * LDN + 16 * bn + i];
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
   }
-  for (; c < nchunk; ++c) s[0] += part[c * K * Cout + i];
+  if (NB < 4) {  // combine the WPB waves of each block (fixed order), via LDS
+    f32x4* red = reinterpret_cast<f32x4*>(Xs);  // 4 waves x 64 lanes x f32x4 = 4 KB
+    red[wave * 64 + lane] = acc[0];
+    __syncthreads();
+    if (wave >= NB) return;
+    f32x4 s4 = red[wave * 64 + lane];
+    for (int w2 = 1; w2 < WPB; ++w2) {
+      const f32x4 o = red[(wave + w2 * NB) * 64 + lane];
+      s4[0] += o[0]; s4[1] += o[1]; s4[2] += o[2]; s4[3] += o[3];
+    }
+    acc[0] = s4;
+  }
+  float* pc = part + (int64_t)chunk * K * p.Cout;
+#pragma unroll
+  for (int j = 0; j < BPW; ++j) {
+    const int blk = NB >= 4 ? wave * BPW + j : wave % NB;
+    const int bk = blk / NBN, bn = blk % NBN;
+    const int n = n0 + 16 * bn + i;
+    if (n >= p.Cout) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = k0 + 16 * bk + 4 * g + r;
+      if (k < K) pc[(int64_t)k * p.Cout + n] = acc[j][r];
+    }
+  }
+}
+
+// dW[n][ci][tap] = sum over chunks of part[chunk][k = tap*Cin + ci][n]:
+// workgroup = `lanes` consecutive outputs x (256/lanes) chunk stripes, fixed
+// order combine (deterministic).
+__global__ __launch_bounds__(256) void wgrad_reduce2_kernel(const float* __restrict__ part,
+                                                            int64_t nchunk, int K, int Cout,
+                                                            int Cin, int KHW, int lanes,
+                                                            float* __restrict__ dw) {
+  __shared__ float red[256];
+  const int t = threadIdx.x;
+  const int rows = 256 / lanes, r = t / lanes;
+  const int64_t KN = (int64_t)K * Cout;
+  const int64_t o = (int64_t)blockIdx.x * lanes + t % lanes;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (r < rows && o < KN) {
+    int64_t c = r;
+    for (; c + 3 * rows < nchunk; c += 4 * rows) {
+      s0 += part[c * KN + o];
+      s1 += part[(c + rows) * KN + o];
+      s2 += part[(c + 2 * rows) * KN + o];
+      s3 += part[(c + 3 * rows) * KN + o];
+    }
+    for (; c < nchunk; c += rows) s0 += part[c * KN + o];
+  }
+  red[t] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (t >= lanes || o >= KN) return;
+  float s = 0.f;
+  for (int k = 0; k < rows; ++k) s += red[k * lanes + t];
+  const int k = (int)(o / Cout), n = (int)(o - (int64_t)k * Cout);
   const int tap = k / Cin, ci = k - tap * Cin;
-  dw[((int64_t)n * Cin + ci) * KHW + tap] = (s[0] + s[1]) + (s[2] + s[3]);
+  dw[((int64_t)n * Cin + ci) * KHW + tap] = s;
+}
+
+static int wv_tile(int64_t n) { return n <= 16 ? 16 : (n <= 32 ? 32 : 64); }
+
+static bool wgrad_vec_ok(const ConvArgs& a) {
+  return !a.nchw_in && a.Cin % 4 == 0 && a.x_ps % 4 == 0 && a.x_c0 % 4 == 0 && a.Cout % 4 == 0 &&
+         a.y_ps % 4 == 0 && a.y_c0 % 4 == 0 && a.y_bs == (int64_t)a.OH * a.OW * a.y_ps &&
+         a.x_bs == (int64_t)a.H * a.W * a.x_ps && (!a.ascale || a.ascale_bs % 4 == 0);
 }
 
 static int64_t wgrad_chunks(const ConvArgs& a) {
   const int64_t K = (int64_t)a.KH * a.KW * a.Cin;
-  const int64_t tiles = cdiv(K, kWgT) * cdiv(a.Cout, kWgT);
+  const bool vec = wgrad_vec_ok(a);
+  const int64_t tk = vec ? wv_tile(K) : kWgT, tn = vec ? wv_tile(a.Cout) : kWgT;
+  const int64_t tiles = cdiv(K, tk) * cdiv(a.Cout, tn);
   int64_t nchunk = cdiv(2048, tiles);
   const int64_t maxchunk = cdiv(a.M, kWgPx);
   if (nchunk > maxchunk) nchunk = maxchunk;
@@ -399,112 +651,136 @@ static int64_t wgrad_chunks(const ConvArgs& a) {
 }
 
 // ---------------------------------------------------------------------------
-// Depthwise gradients.  dgrad: dx[i] = sum_{taps with (i+pad-kh) % s == 0}
-// dy[(i+pad-kh)/s] * w[kh][kw]  (a gather, so no atomics).  wgrad: per tap
-// and channel, sum over pixels of dy * x (block partials, fixed order).
-// ---------------------------------------------------------------------------
-__global__ void dw_dgrad_kernel(const float* __restrict__ dy, const float* __restrict__ w,
-                                int H, int W, int C, int OH, int OW, int k, int s, int pad,
-                                int64_t total4, float* __restrict__ dx) {
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= total4) return;
-  const int C4 = C >> 2;
-  const int c4 = (int)(i % C4);
-  int64_t r = i / C4;
-  const int iw = (int)(r % W);
-  r /= W;
-  const int ih = (int)(r % H);
-  const int b = (int)(r / H);
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int kh = 0; kh < k; ++kh) {
-    const int nh = ih + pad - kh;
-    if (nh < 0 || nh % s) continue;
-    const int oh = nh / s;
-    if (oh >= OH) continue;
-    for (int kw = 0; kw < k; ++kw) {
-      const int nw = iw + pad - kw;
-      if (nw < 0 || nw % s) continue;
-      const int ow = nw / s;
-      if (ow >= OW) continue;
-      const float4 g = reinterpret_cast<const float4*>(dy + (((int64_t)b * OH + oh) * OW + ow) * C)[c4];
-      const float4 wv = reinterpret_cast<const float4*>(w + (kh * k + kw) * C)[c4];
-      acc.x = fmaf(g.x, wv.x, acc.x); acc.y = fmaf(g.y, wv.y, acc.y);
-      acc.z = fmaf(g.z, wv.z, acc.z); acc.w = fmaf(g.w, wv.w, acc.w);
-    }
-  }
-  reinterpret_cast<float4*>(dx)[i] = acc;
+// Depthwise gradients: dgrad is a gather (no atomics), wgrad per-block
+// partials reduced in a fixed order.  Register-strip kernels (3x3/5x5, stride 1/2, pad k/2).  A
+// thread owns one float4 channel group of a strip of PW consecutive pixels
+// of one row; workgroup = `lanes` channel groups x (256/lanes) strips.  Row
+// segments are loaded once per kernel row and reused across the k taps in
+// registers; no per-element index division.
+__device__ __forceinline__ void fma4(float4& a, const float4 x, const float4 y) {
+  a.x = fmaf(x.x, y.x, a.x); a.y = fmaf(x.y, y.y, a.y);
+  a.z = fmaf(x.z, y.z, a.z); a.w = fmaf(x.w, y.w, a.w);
 }
 
-// part[blk][tap][c]; block = (rows of output pixels) x (channel groups)
-template <int K>
-__global__ __launch_bounds__(256) void dw_wgrad_kernel(const float* __restrict__ x,
-                                                       const float* __restrict__ dy, int H, int W,
-                                                       int C, int OH, int OW, int s, int pad,
-                                                       int64_t M, int64_t px_per_blk,
-                                                       float* __restrict__ part) {
+__host__ __device__ constexpr int floordiv_c(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
+
+// dx strip iw0..iw0+PW-1 of input row ih: dx = sum_{kh,kw} dy[(ih+pad-kh)/S][(iw+pad-kw)/S] w[kh][kw]
+template <int K, int S, int PW>
+__global__ __launch_bounds__(256) void dw_dgrad_strip_kernel(
+    const float* __restrict__ dy, const float* __restrict__ w, int H, int W, int C, int OH, int OW,
+    int nstrip, int64_t items, int lanes, float* __restrict__ dx) {
+  constexpr int PAD = K / 2;
+  constexpr int OFF = floordiv_c(PAD - K + 1, S);   // ow0 = iw0/S + OFF
+  constexpr int L = (PW - 1 + PAD - S * OFF) / S + 1;
   const int C4 = C >> 2;
-  const int lanes = C4 < 256 ? C4 : 256;
-  const int rows_pass = 256 / lanes;
   const int t = threadIdx.x;
-  const int r0 = t / lanes;
-  const int64_t m0 = blockIdx.x * px_per_blk, m1 = min(m0 + px_per_blk, M);
-  __shared__ float4 red[256];
-  const int OHW = OH * OW;
-  for (int cgb = 0; cgb < C4; cgb += lanes) {  // uniform trip count (barriers inside)
-    const int cg = cgb + t % lanes;
-    const bool cv = cg < C4;
-    float4 acc[K * K];
+  const int rows_pass = 256 / lanes;
+  if (t / lanes >= rows_pass) return;
+  const int cg = blockIdx.y * lanes + t % lanes;
+  if (cg >= C4) return;
+  const int64_t it = (int64_t)blockIdx.x * rows_pass + t / lanes;
+  if (it >= items) return;
+  const int row = (int)(it / nstrip), strip = (int)(it - (int64_t)row * nstrip);
+  const int b = row / H, ih = row - b * H;
+  const int iw0 = strip * PW;
+  const int ow0 = iw0 / S + OFF;
+  float4 acc[PW];
 #pragma unroll
-    for (int q = 0; q < K * K; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (r0 < rows_pass && cv) {
-      for (int64_t m = m0 + r0; m < m1; m += rows_pass) {
-        const int b = (int)(m / OHW);
-        const int rr = (int)(m - (int64_t)b * OHW);
-        const int oh = rr / OW, ow = rr - (rr / OW) * OW;
-        const float4 g = reinterpret_cast<const float4*>(dy + m * C)[cg];
+  for (int q = 0; q < PW; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int kh = 0; kh < K; ++kh) {
-          const int ih = oh * s - pad + kh;
-          if (ih < 0 || ih >= H) continue;
+  for (int kh = 0; kh < K; ++kh) {
+    const int nh = ih + PAD - kh;
+    if (nh < 0 || (S == 2 && (nh & 1))) continue;
+    const int oh = nh / S;
+    if (oh >= OH) continue;
+    const float4* drow = reinterpret_cast<const float4*>(dy + (((int64_t)b * OH + oh) * OW) * C) + cg;
+    float4 seg[L];
 #pragma unroll
-          for (int kw = 0; kw < K; ++kw) {
-            const int iw = ow * s - pad + kw;
-            if (iw < 0 || iw >= W) continue;
-            const float4 v = reinterpret_cast<const float4*>(x + (((int64_t)b * H + ih) * W + iw) * C)[cg];
-            float4& a = acc[kh * K + kw];
-            a.x = fmaf(g.x, v.x, a.x); a.y = fmaf(g.y, v.y, a.y);
-            a.z = fmaf(g.z, v.z, a.z); a.w = fmaf(g.w, v.w, a.w);
-          }
-        }
-      }
+    for (int j = 0; j < L; ++j) {
+      const int ow = ow0 + j;
+      seg[j] = (ow >= 0 && ow < OW) ? drow[(int64_t)ow * C4] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    float4 wk[K];
 #pragma unroll
-    for (int q = 0; q < K * K; ++q) {
-      __syncthreads();
-      red[t] = acc[q];
-      __syncthreads();
-      if (t < lanes && cv) {
-        float4 S = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int r = 0; r < rows_pass; ++r) {
-          const float4 a = red[r * lanes + t];
-          S.x += a.x; S.y += a.y; S.z += a.z; S.w += a.w;
-        }
-        reinterpret_cast<float4*>(part + ((int64_t)blockIdx.x * K * K + q) * C)[cg] = S;
+    for (int kw = 0; kw < K; ++kw) wk[kw] = reinterpret_cast<const float4*>(w + (kh * K + kw) * C)[cg];
+#pragma unroll
+    for (int q = 0; q < PW; ++q)
+#pragma unroll
+      for (int kw = 0; kw < K; ++kw) {
+        if (((q + PAD - kw) % S + S) % S) continue;  // parity (iw0 % S == 0)
+        const int j = (q + PAD - kw - S * OFF) / S;
+        fma4(acc[q], seg[j], wk[kw]);
       }
+  }
+  float4* xrow = reinterpret_cast<float4*>(dx + (((int64_t)b * H + ih) * W) * C) + cg;
+#pragma unroll
+  for (int q = 0; q < PW; ++q)
+    if (iw0 + q < W) xrow[(int64_t)(iw0 + q) * C4] = acc[q];
+}
+
+// part[blk][tap][c] = sum over this block's output strips of dy * x(tap)
+template <int K, int S, int PW>
+__global__ __launch_bounds__(256) void dw_wgrad_strip_kernel(
+    const float* __restrict__ x, const float* __restrict__ dy, int H, int W, int C, int OH,
+    int OW, int nstrip, int64_t items, int64_t items_per_blk, int lanes,
+    float* __restrict__ part) {
+  constexpr int PAD = K / 2;
+  constexpr int L = (PW - 1) * S + K;
+  __shared__ float4 red[256];
+  const int C4 = C >> 2;
+  const int t = threadIdx.x;
+  const int rows_pass = 256 / lanes;
+  const int r0 = t / lanes;
+  const int cg = blockIdx.y * lanes + t % lanes;
+  const bool active = r0 < rows_pass && cg < C4;
+  float4 acc[K * K];
+#pragma unroll
+  for (int q = 0; q < K * K; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int64_t i0 = (int64_t)blockIdx.x * items_per_blk;
+  const int64_t i1 = min(i0 + items_per_blk, items);
+  for (int64_t it = i0 + r0; active && it < i1; it += rows_pass) {
+    const int row = (int)(it / nstrip), strip = (int)(it - (int64_t)row * nstrip);
+    const int b = row / OH, oh = row - b * OH;
+    const int ow0 = strip * PW;
+    const float4* drow = reinterpret_cast<const float4*>(dy + (((int64_t)b * OH + oh) * OW) * C) + cg;
+    float4 g[PW];
+#pragma unroll
+    for (int q = 0; q < PW; ++q)
+      g[q] = (ow0 + q < OW) ? drow[(int64_t)(ow0 + q) * C4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int iw0 = ow0 * S - PAD;
+#pragma unroll
+    for (int kh = 0; kh < K; ++kh) {
+      const int ih = oh * S - PAD + kh;
+      if (ih < 0 || ih >= H) continue;
+      const float4* xrow = reinterpret_cast<const float4*>(x + (((int64_t)b * H + ih) * W) * C) + cg;
+      float4 seg[L];
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const int iw = iw0 + j;
+        seg[j] = (iw >= 0 && iw < W) ? xrow[(int64_t)iw * C4] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+        for (int q = 0; q < PW; ++q) fma4(acc[kh * K + kw], g[q], seg[q * S + kw]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < K * K; ++q) {
+    __syncthreads();
+    red[t] = acc[q];
+    __syncthreads();
+    if (t < lanes && cg < C4) {
+      float4 Sm = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int r = 0; r < rows_pass; ++r) {
+        const float4 a = red[r * lanes + t];
+        Sm.x += a.x; Sm.y += a.y; Sm.z += a.z; Sm.w += a.w;
+      }
+      reinterpret_cast<float4*>(part + ((int64_t)blockIdx.x * K * K + q) * C)[cg] = Sm;
     }
   }
 }
 
-// dw torch layout [C][1][k][k] = sum over blocks of part[blk][tap][c]
-__global__ void dw_wgrad_reduce_kernel(const float* __restrict__ part, int64_t nblk, int KK, int C,
-                                       float* __restrict__ dw) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= KK * C) return;
-  const int tap = i / C, c = i - tap * C;
-  double s = 0.0;
-  for (int64_t b = 0; b < nblk; ++b) s += part[b * KK * C + i];
-  dw[c * KK + tap] = (float)s;
-}
 
 // ---------------------------------------------------------------------------
 // ECA-scaled operand backward.  The consumer conv saw a = x * s[b][c]; given
@@ -705,9 +981,9 @@ extern "C" int jabd_bn_stats_f32(const float* x, int32_t ldx, int64_t M, int32_t
   const int64_t per = bn_rows_per_blk(M, C), nblk = cdiv(M, per);
   bn_stats_part_kernel<<<(unsigned)nblk, kRedThreads, 0, st>>>(x, ldx, M, C, per, part);
   if (int e = check_launch("bn_stats_part")) return e;
-  bn_stats_final_kernel<<<(unsigned)cdiv(C, 256), 256, 0, st>>>(x, part, nblk, M, C, momentum, eps,
-                                                                mean, invstd, running_mean,
-                                                                running_var);
+  const int fl = bn_fin_lanes(C);
+  bn_stats_final_kernel<<<(unsigned)cdiv(C, fl), kRedThreads, 0, st>>>(
+      x, part, nblk, M, C, fl, momentum, eps, mean, invstd, running_mean, running_var);
   return check_launch("bn_stats_final");
 }
 
@@ -719,10 +995,11 @@ extern "C" int jabd_bn_act_fwd_f32(const float* x, int32_t ldx, int64_t M, int32
   JABD_REQUIRE(x && mean && invstd && gamma && beta && y && C % 4 == 0 && ldx % 4 == 0 &&
                    ldy % 4 == 0 && yc0 % 4 == 0 && (!res || ldr % 4 == 0),
                "bn_act_fwd: bad args");
-  const int64_t total = M * (C / 4);
-  if (total == 0) return JABD_OK;
-  bn_act_fwd_kernel<<<(unsigned)cdiv(total, 256), 256, 0, as_stream(stream)>>>(
-      x, ldx, M, C, mean, invstd, gamma, beta, res, ldr, act, slope, y, ldy, yc0);
+  if (M == 0 || C == 0) return JABD_OK;
+  int lanes;
+  const dim3 grid = ew_grid(M, C, lanes);
+  bn_act_fwd_kernel<<<grid, kRedThreads, 0, as_stream(stream)>>>(
+      x, ldx, M, C, mean, invstd, gamma, beta, res, ldr, act, slope, y, ldy, yc0, lanes);
   return check_launch("bn_act_fwd");
 }
 
@@ -741,12 +1018,15 @@ extern "C" int jabd_bn_act_bwd_f32(const float* dy, int32_t lddy, int32_t dyc0, 
                                                             C, mean, invstd, gamma, beta, act,
                                                             slope, per, part);
   if (int e = check_launch("bn_bwd_part")) return e;
-  bn_bwd_final_kernel<<<(unsigned)cdiv(C, 256), 256, 0, st>>>(part, nblk, C, dbeta, dgamma);
+  const int fl = bn_fin_lanes(C);
+  bn_bwd_final_kernel<<<(unsigned)cdiv(C, fl), kRedThreads, 0, st>>>(part, nblk, C, fl, dbeta,
+                                                                     dgamma);
   if (int e = check_launch("bn_bwd_final")) return e;
-  const int64_t total = M * (C / 4);
-  bn_bwd_apply_kernel<<<(unsigned)cdiv(total, 256), 256, 0, st>>>(
-      dy, lddy, dyc0, x, ldx, res, ldr, M, C, mean, invstd, gamma, beta, act, slope, dbeta, dgamma,
-      dx, dres);
+  int lanes;
+  const dim3 grid = ew_grid(M, C, lanes);
+  bn_bwd_apply_kernel<<<grid, kRedThreads, 0, st>>>(dy, lddy, dyc0, x, ldx, res, ldr, M, C, mean,
+                                                    invstd, gamma, beta, act, slope, dbeta,
+                                                    dgamma, dx, dres, lanes);
   return check_launch("bn_bwd_apply");
 }
 
@@ -769,22 +1049,49 @@ extern "C" int jabd_conv_wgrad_f32(const jabd_conv_args* args, float* part, floa
   const int64_t per = cdiv(cdiv(a.M, nchunk), kWgPx) * kWgPx;
   const int64_t nch = cdiv(a.M, per);
   hipStream_t st = as_stream(stream);
-  dim3 g((unsigned)cdiv(K, kWgT), (unsigned)cdiv(a.Cout, kWgT), (unsigned)nch);
-  conv_wgrad_kernel<<<g, 256, 0, st>>>(a, per, part);
+  if (wgrad_vec_ok(a)) {
+    const int tk = wv_tile(K), tn = wv_tile(a.Cout);
+    const int fast = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.H == a.OH &&
+                     a.W == a.OW;
+    dim3 g((unsigned)cdiv(K, tk), (unsigned)cdiv(a.Cout, tn), (unsigned)nch);
+#define WV_CASE(KT_, NT_)                                                         \
+  if (tk == KT_ && tn == NT_)                                                     \
+    conv_wgrad_v_kernel<KT_, NT_><<<g, 256, 0, st>>>(a, (int)per, fast, part);
+    WV_CASE(16, 16) WV_CASE(16, 32) WV_CASE(16, 64)
+    WV_CASE(32, 16) WV_CASE(32, 32) WV_CASE(32, 64)
+    WV_CASE(64, 16) WV_CASE(64, 32) WV_CASE(64, 64)
+#undef WV_CASE
+  } else {
+    dim3 g((unsigned)cdiv(K, kWgT), (unsigned)cdiv(a.Cout, kWgT), (unsigned)nch);
+    conv_wgrad_kernel<<<g, 256, 0, st>>>(a, per, part);
+  }
   if (int e = check_launch("conv_wgrad")) return e;
   const int64_t tot = (int64_t)K * a.Cout;
-  wgrad_reduce_kernel<<<(unsigned)cdiv(tot, 256), 256, 0, st>>>(part, nch, K, a.Cout, a.Cin,
-                                                                a.KH * a.KW, dw);
+  const int lanes = tot >= 64 * 512 ? 64 : 16;
+  wgrad_reduce2_kernel<<<(unsigned)cdiv(tot, lanes), 256, 0, st>>>(part, nch, K, a.Cout, a.Cin,
+                                                                   a.KH * a.KW, lanes, dw);
   return check_launch("wgrad_reduce");
 }
 
 extern "C" int jabd_dw_dgrad_f32(const float* dy, const float* w, int32_t B, int32_t H, int32_t W,
                                  int32_t C, int32_t OH, int32_t OW, int32_t k, int32_t stride,
                                  int32_t pad, float* dx, jabd_stream_t stream) {
-  JABD_REQUIRE(dy && w && dx && C % 4 == 0, "dw_dgrad: bad args");
-  const int64_t total4 = (int64_t)B * H * W * (C / 4);
-  dw_dgrad_kernel<<<(unsigned)cdiv(total4, 256), 256, 0, as_stream(stream)>>>(
-      dy, w, H, W, C, OH, OW, k, stride, pad, total4, dx);
+  JABD_REQUIRE(dy && w && dx && C % 4 == 0 && B > 0 && H > 0 && W > 0, "dw_dgrad: bad args");
+  JABD_REQUIRE((k == 3 || k == 5) && pad == k / 2 && (stride == 1 || stride == 2) &&
+                   OH == (H + 2 * pad - k) / stride + 1 && OW == (W + 2 * pad - k) / stride + 1,
+               "dw_dgrad: unsupported geometry");
+  const int C4 = C / 4, lanes = C4 < 64 ? C4 : 64, rows_pass = 256 / lanes;
+  hipStream_t st = as_stream(stream);
+#define DG_CASE(K_, S_, PW_)                                                                   \
+  if (k == K_ && stride == S_) {                                                               \
+    const int nstrip = (int)cdiv(W, PW_);                                                      \
+    const int64_t items = (int64_t)B * H * nstrip;                                             \
+    dim3 g((unsigned)cdiv(items, rows_pass), (unsigned)cdiv(C4, lanes));                       \
+    dw_dgrad_strip_kernel<K_, S_, PW_><<<g, 256, 0, st>>>(dy, w, H, W, C, OH, OW, nstrip, items, \
+                                                          lanes, dx);                          \
+  }
+  DG_CASE(3, 1, 8) DG_CASE(3, 2, 8) DG_CASE(5, 1, 8) DG_CASE(5, 2, 8)
+#undef DG_CASE
   return check_launch("dw_dgrad");
 }
 
@@ -795,25 +1102,31 @@ extern "C" int64_t jabd_dw_wgrad_part_floats(int64_t M, int32_t C, int32_t k) {
 extern "C" int jabd_dw_wgrad_f32(const float* x, const float* dy, int32_t B, int32_t H, int32_t W,
                                  int32_t C, int32_t OH, int32_t OW, int32_t k, int32_t stride,
                                  int32_t pad, float* part, float* dw, jabd_stream_t stream) {
-  JABD_REQUIRE(x && dy && part && dw && C % 4 == 0, "dw_wgrad: bad args");
-  const int64_t M = (int64_t)B * OH * OW;
-  int64_t per = cdiv(M, 1024);
-  if (per < 1) per = 1;
-  const int64_t nblk = cdiv(M, per);
+  JABD_REQUIRE(x && dy && part && dw && C % 4 == 0 && B > 0, "dw_wgrad: bad args");
+  JABD_REQUIRE((k == 3 || k == 5) && pad == k / 2 && (stride == 1 || stride == 2) &&
+                   OH == (H + 2 * pad - k) / stride + 1 && OW == (W + 2 * pad - k) / stride + 1,
+               "dw_wgrad: unsupported geometry");
+  const int C4 = C / 4, lanes = C4 < 64 ? C4 : 64, rows_pass = 256 / lanes;
   hipStream_t st = as_stream(stream);
-  if (k == 3)
-    dw_wgrad_kernel<3><<<(unsigned)nblk, 256, 0, st>>>(x, dy, H, W, C, OH, OW, stride, pad, M, per,
-                                                       part);
-  else if (k == 5)
-    dw_wgrad_kernel<5><<<(unsigned)nblk, 256, 0, st>>>(x, dy, H, W, C, OH, OW, stride, pad, M, per,
-                                                       part);
-  else {
-    set_error("dw_wgrad: k=%d unsupported", k);
-    return JABD_EINVAL;
+  int64_t nblk = 0;
+#define WG_CASE(K_, S_, PW_)                                                                    \
+  if (k == K_ && stride == S_) {                                                                \
+    const int nstrip = (int)cdiv(OW, PW_);                                                      \
+    const int64_t items = (int64_t)B * OH * nstrip;                                             \
+    int64_t per = cdiv(items, 1024);                                                            \
+    per = cdiv(per, rows_pass) * rows_pass;                                                     \
+    nblk = cdiv(items, per);                                                                    \
+    dim3 g((unsigned)nblk, (unsigned)cdiv(C4, lanes));                                          \
+    dw_wgrad_strip_kernel<K_, S_, PW_><<<g, 256, 0, st>>>(x, dy, H, W, C, OH, OW, nstrip, items, \
+                                                          per, lanes, part);                    \
   }
+  WG_CASE(3, 1, 8) WG_CASE(3, 2, 4) WG_CASE(5, 1, 4) WG_CASE(5, 2, 4)
+#undef WG_CASE
   if (int e = check_launch("dw_wgrad")) return e;
-  dw_wgrad_reduce_kernel<<<(unsigned)cdiv((int64_t)k * k * C, 256), 256, 0, st>>>(part, nblk, k * k,
-                                                                                C, dw);
+  const int64_t tot = (int64_t)k * k * C;
+  const int rl = tot >= 64 * 512 ? 64 : 16;
+  wgrad_reduce2_kernel<<<(unsigned)cdiv(tot, rl), 256, 0, st>>>(part, nblk, k * k, C, 1, k * k, rl,
+                                                                dw);
   return check_launch("dw_wgrad_reduce");
 }
 
