@@ -12,6 +12,12 @@ Extra fields on the one JSON line:
                their summed HIP-event durations on the launch stream.
   nms          C5 (configs[4]): batched NMS over 8 x 100k clustered boxes,
                boxes/sec, bit-exact NMS kernel pipeline (sort+mask+scan).
+  train        C4 (configs[3]): JABD-MobileNetV3 training step, 32 images/GPU
+               at 1024x1024 (forward, MultiBoxLoss with on-device matching,
+               backward, SUM gradient all-reduce over RCCL when N>1, Adam
+               wd 5e-4 as train_mobilenetV3_ecagai.py:564) on every rank ->
+               whole-job images/sec, data-parallel weak scaling; at N=1 also
+               C3 (configs[2]): R50 RetinaFace training step at bs64 1024x1024.
   cpu_baseline the oracle's PyTorch-CPU restatement of the same forward at
                1024x1024, bs1, on this host (rank 0, N=1 only).
 """
@@ -43,6 +49,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-nms", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--train-steps", type=int, default=10)
+    ap.add_argument("--r50-batch", type=int, default=64)
+    ap.add_argument("--pmc-forward-only", action="store_true",
+                    help="run exactly --steps eval forwards and nothing else (PMC passes)")
     return ap.parse_args()
 
 
@@ -74,7 +85,10 @@ def conv_roofline(model, x, steps):
         o = out
         M = o.shape[0] * o.shape[1] * o.shape[2]
         K = pk.KH * pk.KW * pk.Cin + pk.Cin2
-        recs.append((s, e, 2.0 * M * K * pk.Cout))
+        # algorithmic bytes: input read once, weights once, output written once
+        nbytes = 4.0 * (xx.numel() + (kw["x2"].numel() if kw.get("x2") is not None else 0)
+                        + K * pk.Cout + M * pk.Cout)
+        recs.append((s, e, 2.0 * M * K * pk.Cout, nbytes))
         return out
 
     F.conv = timed_conv
@@ -85,10 +99,11 @@ def conv_roofline(model, x, steps):
         torch.cuda.synchronize()
     finally:
         F.conv = orig
-    t_ms = sum(s.elapsed_time(e) for s, e, _ in recs)
-    flops = sum(f for _, _, f in recs)
+    t_ms = sum(r[0].elapsed_time(r[1]) for r in recs)
+    flops = sum(r[2] for r in recs)
+    nbytes = sum(r[3] for r in recs)
     n = len(recs) // steps
-    return flops / steps, t_ms / steps, n
+    return flops / steps, t_ms / steps, n, nbytes / steps
 
 
 def forward_flops(model, size, batch):
@@ -139,6 +154,71 @@ def nms_bench(device, reps=5):
             "bit_exact_img0_vs_oracle": bool(exact)}
 
 
+def train_bench(kind, batch, size, steps, warmup, device, dist, rank):
+    """steps timed training iterations (parallel.train_step) on this rank."""
+    from jabd_amd import parallel, synth
+    from nets.retinaface_training import MultiBoxLoss, weights_init
+    from utils.anchors import Anchors
+    import contextlib
+    import io
+    if kind == "mnv3":
+        from nets.retinaface_r import RetinaFace
+        from utils.config import cfg_mnet as cfg
+    else:
+        from nets.retinaface_eca_nonlocal import RetinaFace
+        from utils.config import cfg_re50 as cfg
+    torch.manual_seed(0)
+    model = RetinaFace(cfg=cfg, mode="train")
+    with contextlib.redirect_stdout(io.StringIO()):
+        weights_init(model)
+    model = model.to(device).train()
+    if dist:
+        parallel.broadcast_buffers(model)
+        for p in model.parameters():
+            dist.broadcast(p.data, src=0)
+    opt = torch.optim.Adam(model.parameters(), 1e-3, weight_decay=5e-4)
+    crit = MultiBoxLoss(2, 0.35, 7, cfg["variance"], True)
+    pri = Anchors(cfg, image_size=(size, size)).get_anchors().to(device)
+    x = synth.images(batch, size, seed=1234 + rank, device=device)
+    tg = [torch.from_numpy(t).to(device) for t in synth.targets(batch, size, seed=4321 + rank)]
+    reducer = parallel.GradAllReduce(model) if dist else None
+    for _ in range(warmup):
+        parallel.train_step(model, crit, opt, x, tg, pri, reducer=reducer)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss, _ = parallel.train_step(model, crit, opt, x, tg, pri, reducer=reducer)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    world = dist.get_world_size() if dist else 1
+    mem = torch.cuda.max_memory_allocated(device) / 2**30
+    del model, opt, x, tg
+    torch.cuda.empty_cache()
+    return {"images_per_sec": batch * steps * world / el, "ms_per_step": el / steps * 1e3,
+            "per_gpu_batch": batch, "global_batch": batch * world, "image_size": size,
+            "steps": steps, "warmup": warmup, "loss_last": float(loss), "max_mem_gib": mem}
+
+
+def pmc_traffic():
+    """Conv-GEMM HBM bytes per step from the committed rocprofv3 PMC passes
+    (tools/pmc_traffic.py -> profiles/<round>/pmc_traffic.json), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        return json.load(f)
+
+
 def cpu_baseline(size, seconds):
     from oracle import model_ref
     from nets.retinaface_r import RetinaFace
@@ -180,6 +260,12 @@ def main():
     from jabd_amd import synth
     model = build_model(device)
     x = synth.images(args.batch, args.size, seed=1234 + rank, device=device)
+    if args.pmc_forward_only:
+        with torch.no_grad():
+            for _ in range(args.steps):
+                model(x)
+        torch.cuda.synchronize()
+        return
 
     with torch.no_grad():
         for _ in range(args.warmup):
@@ -205,13 +291,26 @@ def main():
     value = imgs / el
 
     extra = {}
+    if not args.no_train:
+        tr = {"C4_mnv3": train_bench("mnv3", args.batch, args.size, args.train_steps, 3, device,
+                                     dist, rank)}
+        if world == 1 and args.r50_batch > 0:
+            tr["C3_r50"] = train_bench("r50", args.r50_batch, args.size, max(2, args.train_steps // 2),
+                                       2, device, None, rank)
+        extra["train"] = tr
     if rank == 0:
-        flops_step, t_ms, n_launch = conv_roofline(model, x, max(3, min(args.steps, 10)))
+        flops_step, t_ms, n_launch, alg_bytes = conv_roofline(model, x, max(3, min(args.steps, 10)))
         ach = flops_step / (t_ms * 1e-3) / 1e12
+        pmc = pmc_traffic()
         extra["roofline"] = {
             "bound": "mfma", "kernel": f"conv_gemm_kernel (all {n_launch} launches per step)",
             "achieved": ach, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-            "frac": ach / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
+            "frac": ach / PEAK_FP32_MFMA_TFLOPS,
+            "traffic": pmc["conv_hbm_bytes_per_step"] if pmc else None,
+            "traffic_unit": "HBM bytes per step over all conv_gemm launches (PMC, "
+                            "2*FETCH_SIZE + WRITE_SIZE, see DESIGN.md)",
+            "traffic_source": pmc["source"] if pmc else None,
+            "algorithmic_bytes_per_step": alg_bytes,
             "conv_ms_per_step": t_ms, "conv_gflop_per_step": flops_step / 1e9}
         extra["forward_gflop_per_image"] = forward_flops(model, args.size, 1) / 1e9
         if not args.no_nms:
