@@ -205,6 +205,23 @@ typedef struct jabd_dw_args {
 int64_t jabd_dw_nblk(int64_t B, int64_t OH, int64_t OW, int64_t C);
 int jabd_dwconv_nhwc_f32(const jabd_dw_args* args, jabd_stream_t stream);
 
+/* A1 fused block front half (eval) — nets/mobilenetV3.py:141-142: expand 1x1
+ * conv (+ folded bn1, packed like jabd_conv_args.w, Kc = ceil(Cin/16)) + act
+ * -> depthwise k x k (pad k/2, + folded bn2) + act, and the ECA pool partial
+ * sums part [B][nblk][E] (nblk = jabd_expand_dw_nblk).  The expanded tensor
+ * stays on chip.  act: NONE / RELU / HSWISH (act1 == act2 in Block_eca). */
+typedef struct jabd_expdw_args {
+  const float* x; int64_t x_bs; int32_t x_ps, Cin;
+  int32_t B, H, W, E;
+  const void* we; const float* be; int32_t Ntiles, Kc;
+  const float* wd; const float* bd;
+  int32_t k, stride, act, nblk;
+  float* y; int64_t y_bs; int32_t y_ps, OH, OW, reserved0;
+  float* part;
+} jabd_expdw_args;
+int64_t jabd_expand_dw_nblk(int32_t OH, int32_t OW, int32_t k, int32_t stride);
+int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_t stream);
+
 /* Per-(image, block, channel) sums of an NHWC tensor (ECA pooling of a tensor
  * not produced by the dw kernel: C3/C4/C5 and the FPN outputs). */
 int jabd_channel_sum_f32(const float* x, int64_t x_bs, int32_t x_ps, int64_t B, int64_t HW,

@@ -1,0 +1,339 @@
+// A1 fused MobileNetV3 block front half, eval mode (nets/mobilenetV3.py:
+// 141-142): expand 1x1 conv + folded BN + act  ->  depthwise k x k + folded BN
+// + act  ->  ECA average-pool partial sums.  The expanded tensor never
+// touches HBM: it is the largest activation of the network (e.g. 64 channels
+// at 512x512 for block 2) and the unfused path writes it once and reads it
+// back (plus halo) once.
+//
+// Workgroup = one TH x TW output tile x EC expanded channels of one image.
+//  phase 1: the input tile (plus the k-1 halo, all Cin channels, 16 at a
+//           time) is staged in LDS; the expand GEMM runs on the fp32 MFMA
+//           with swapped operands (A = packed weights, B = pixels) so each
+//           lane ends up holding 4 consecutive expanded channels of one
+//           pixel; bias + act + zero outside the image (the depthwise conv
+//           zero-pads the *activated* map), written to LDS as [pixel][EC].
+//  phase 2: depthwise register strips (4 outputs along W per thread) read
+//           the LDS tile, add bias, activate, store NHWC and accumulate the
+//           ECA sums, reduced per workgroup in a fixed order into
+//           part[b][tile][E] (deterministic, no atomics).
+// The LDS buffer is shared by the two phases (the expand accumulators live
+// in registers across the switch).  Workgroup ids are decoded XCD-aware: the
+// EC-chunks of one tile land on the same XCD (id % 8), so their re-reads of
+// the input tile hit that XCD's L2.
+#include "common.h"
+#include "conv_args.h"
+
+namespace jabd {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float xd_act(float v, int act) {
+  switch (act) {
+    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_HSWISH: {
+      float r = fminf(fmaxf(v + 3.f, 0.f), 6.f);
+      return v * r / 6.f;
+    }
+    default: return v;
+  }
+}
+
+template <int K, int S, int TH, int TW, int EC>
+struct XdCfg {
+  static constexpr int PAD = K / 2;
+  static constexpr int IH = (TH - 1) * S + K, IW = (TW - 1) * S + K;
+  static constexpr int IPX = IH * IW;
+  static constexpr int IPAD = (IPX + 15) / 16 * 16;
+  static constexpr int XP = 20;      // staged-input pitch (16 channels + 4)
+  static constexpr int EP = EC + 4;  // expanded-tile pitch
+  static constexpr int NPB = IPAD / 16, NNT = EC / 16, NBLK = NPB * NNT;
+  static constexpr int BPW = (NBLK + 3) / 4;  // MFMA blocks per wave
+  static constexpr int LDS_X = IPAD * XP, LDS_E = IPAD * EP;
+  static constexpr int LDS = LDS_X > LDS_E ? LDS_X : LDS_E;
+  static constexpr int PW = 4, NSTRIP = TW / PW, NC4 = EC / 4;
+  static constexpr int ITEMS = TH * NSTRIP * NC4;
+  static constexpr int SPAN = (PW - 1) * S + K;
+  static_assert(TW % PW == 0 && 256 % NC4 == 0, "tile shape");
+  static_assert(LDS * 4 <= 160 * 1024, "LDS");
+};
+
+// Persistent: workgroup L walks work items i = L, L + G, ... (G = grid, a
+// multiple of 8, so every item of a WG stays on that WG's XCD).  Item i ->
+// (tile, EC-chunk) with the chunks of one tile on one XCD.  A work item is
+// Kc stages (16 input channels each); the global loads of the next stage
+// (possibly the next item's first) are issued into registers before the
+// current stage's MFMAs / depthwise phase, so HBM latency overlaps compute.
+struct XdItem {
+  int b, t_in, oh0, ow0, ih0, iw0, c0;
+};
+
+template <int K, int S, int TH, int TW, int EC>
+__device__ __forceinline__ bool xd_item(const jabd_expdw_args& p, int64_t i, int tiles_w,
+                                        int tiles_img, int nch, int64_t nitems, XdItem& it) {
+  using C = XdCfg<K, S, TH, TW, EC>;
+  if (i >= nitems) return false;
+  const int xcd = (int)(i & 7);
+  const int64_t q = i >> 3;
+  const int chunk = (int)(q % nch);
+  const int64_t tile = (q / nch) * 8 + xcd;
+  if (tile >= (int64_t)p.B * tiles_img) return false;
+  it.b = (int)(tile / tiles_img);
+  it.t_in = (int)(tile - (int64_t)it.b * tiles_img);
+  const int ty = it.t_in / tiles_w, tx = it.t_in - ty * tiles_w;
+  it.oh0 = ty * TH;
+  it.ow0 = tx * TW;
+  it.ih0 = it.oh0 * S - C::PAD;
+  it.iw0 = it.ow0 * S - C::PAD;
+  it.c0 = chunk * EC;
+  return true;
+}
+
+template <int K, int S, int TH, int TW, int EC>
+__global__ __launch_bounds__(256, 2) void expdw_kernel(const jabd_expdw_args p, int tiles_w,
+                                                    int tiles_img, int nch, int64_t nitems) {
+  using C = XdCfg<K, S, TH, TW, EC>;
+  constexpr int NPF = (C::IPAD * 4 + 255) / 256;  // prefetched float4 per thread per stage
+  __shared__ __attribute__((aligned(16))) float lds[C::LDS];
+  __shared__ float4 wsh[K * K + 1][C::NC4];  // this chunk's dw taps + bias (row K*K)
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, j = lane & 15, g = lane >> 4;
+  const f32x4* wpk = reinterpret_cast<const f32x4*>(p.we);
+  const int G = gridDim.x;
+
+  // tiles that straddle the 8-aligned tile padding are skipped: advance to
+  // the next real item (uniform per workgroup)
+  auto next_item = [&](int64_t i, XdItem& it) -> int64_t {
+    while (i < nitems && !xd_item<K, S, TH, TW, EC>(p, i, tiles_w, tiles_img, nch, nitems, it))
+      i += G;
+    return i;
+  };
+  float4 pf[NPF];
+  auto prefetch = [&](const XdItem& it, int kc) {
+    const float* xb = p.x + (int64_t)it.b * p.x_bs;
+#pragma unroll
+    for (int u = 0; u < NPF; ++u) {
+      const int idx = u * 256 + t;
+      const int px = idx >> 2, c4 = (idx & 3) * 4;
+      const int ci = 16 * kc + c4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (px < C::IPX && ci < p.Cin) {
+        const int r = px / C::IW, cc = px - r * C::IW;
+        const int ih = it.ih0 + r, iw = it.iw0 + cc;
+        if (ih >= 0 && ih < p.H && iw >= 0 && iw < p.W)
+          v = *reinterpret_cast<const float4*>(xb + ((int64_t)ih * p.W + iw) * p.x_ps + ci);
+      }
+      pf[u] = v;
+    }
+  };
+
+  XdItem cur, nxt;
+  int64_t ci_idx = next_item(blockIdx.x, cur);
+  if (ci_idx >= nitems) return;
+  prefetch(cur, 0);
+  const int c4 = t % C::NC4, chl = 4 * c4;
+  // expand-GEMM channel block of this wave (blk = wave + 4u -> nt = blk % NNT)
+  const int ntw = wave % C::NNT;
+
+  while (true) {
+    f32x4 acc[C::BPW];
+#pragma unroll
+    for (int u = 0; u < C::BPW; ++u) acc[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int nt0 = cur.c0 / 16;
+    int64_t nx_idx = -1;
+    for (int kc = 0; kc < p.Kc; ++kc) {
+      // regs -> LDS (this stage's input channels)
+#pragma unroll
+      for (int u = 0; u < NPF; ++u) {
+        const int idx = u * 256 + t;
+        if (idx < C::IPAD * 4)
+          *reinterpret_cast<float4*>(lds + (idx >> 2) * C::XP + (idx & 3) * 4) = pf[u];
+      }
+      __syncthreads();
+      // issue the next stage's loads
+      if (kc + 1 < p.Kc) {
+        prefetch(cur, kc + 1);
+      } else {
+        nx_idx = next_item(ci_idx + G, nxt);
+        if (nx_idx < nitems) prefetch(nxt, 0);
+      }
+      if (nt0 + ntw < p.Ntiles) {
+        const f32x4 a = wpk[((int64_t)kc * p.Ntiles + nt0 + ntw) * 64 + lane];
+#pragma unroll
+        for (int u = 0; u < C::BPW; ++u) {
+          const int blk = wave + 4 * u;
+          if (blk < C::NBLK) {
+            const int pb = blk / C::NNT;
+            const f32x4 bv =
+                *reinterpret_cast<const f32x4*>(lds + (pb * 16 + j) * C::XP + 4 * g);
+            acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bv.x, acc[u], 0, 0, 0);
+            acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bv.y, acc[u], 0, 0, 0);
+            acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bv.z, acc[u], 0, 0, 0);
+            acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bv.w, acc[u], 0, 0, 0);
+          }
+        }
+      }
+      __syncthreads();
+    }
+    // acc[u][r] = expanded channel 16nt + 4g + r of tile pixel 16pb + j
+#pragma unroll
+    for (int u = 0; u < C::BPW; ++u) {
+      const int blk = wave + 4 * u;
+      if (blk < C::NBLK) {
+        const int pb = blk / C::NNT, nt = blk - pb * C::NNT;
+        const int px = pb * 16 + j, ch = 16 * nt + 4 * g;
+        float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (px < C::IPX && cur.c0 + ch < p.E) {
+          const int r = px / C::IW, cc = px - r * C::IW;
+          const int ih = cur.ih0 + r, iw = cur.iw0 + cc;
+          if (ih >= 0 && ih < p.H && iw >= 0 && iw < p.W) {
+            const float4 bi = *reinterpret_cast<const float4*>(p.be + cur.c0 + ch);
+            o.x = xd_act(acc[u][0] + bi.x, p.act);
+            o.y = xd_act(acc[u][1] + bi.y, p.act);
+            o.z = xd_act(acc[u][2] + bi.z, p.act);
+            o.w = xd_act(acc[u][3] + bi.w, p.act);
+          }
+        }
+        *reinterpret_cast<float4*>(lds + px * C::EP + ch) = o;
+      }
+    }
+    for (int idx = t; idx < (K * K + 1) * C::NC4; idx += 256) {
+      const int tp = idx / C::NC4, q4 = idx - tp * C::NC4;
+      const int cc = cur.c0 + 4 * q4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (cc < p.E)
+        v = *reinterpret_cast<const float4*>((tp < K * K ? p.wd + (int64_t)tp * p.E : p.bd) + cc);
+      wsh[tp][q4] = v;
+    }
+    __syncthreads();
+
+    // depthwise phase
+    const bool chv = cur.c0 + chl < p.E;
+    float4 psum = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (chv) {
+      const float4 bias2 = wsh[K * K][c4];
+      float* yb = p.y + (int64_t)cur.b * p.y_bs + cur.c0 + chl;
+#pragma unroll 1
+      for (int itm = t; itm < C::ITEMS; itm += 256) {
+        const int strip = itm / C::NC4;
+        const int orow = strip / C::NSTRIP, st = strip - orow * C::NSTRIP;
+        const int oh = cur.oh0 + orow, owb = cur.ow0 + st * C::PW;
+        if (oh >= p.OH || owb >= p.OW) continue;
+        float4 a2[C::PW];
+#pragma unroll
+        for (int o = 0; o < C::PW; ++o) a2[o] = bias2;
+#pragma unroll 1
+        for (int kh = 0; kh < K; ++kh) {
+          const float* rowp = lds + ((orow * S + kh) * C::IW + st * C::PW * S) * C::EP + chl;
+          float4 row[C::SPAN];
+#pragma unroll
+          for (int c = 0; c < C::SPAN; ++c)
+            row[c] = *reinterpret_cast<const float4*>(rowp + c * C::EP);
+          float4 wk[K];
+#pragma unroll
+          for (int kw = 0; kw < K; ++kw) wk[kw] = wsh[kh * K + kw][c4];
+#pragma unroll
+          for (int o = 0; o < C::PW; ++o)
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw) {
+              const float4 xv = row[o * S + kw], wv = wk[kw];
+              a2[o].x = fmaf(xv.x, wv.x, a2[o].x);
+              a2[o].y = fmaf(xv.y, wv.y, a2[o].y);
+              a2[o].z = fmaf(xv.z, wv.z, a2[o].z);
+              a2[o].w = fmaf(xv.w, wv.w, a2[o].w);
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < C::PW; ++o) {
+          if (owb + o >= p.OW) break;
+          float4 v;
+          v.x = xd_act(a2[o].x, p.act);
+          v.y = xd_act(a2[o].y, p.act);
+          v.z = xd_act(a2[o].z, p.act);
+          v.w = xd_act(a2[o].w, p.act);
+          *reinterpret_cast<float4*>(yb + ((int64_t)oh * p.OW + owb + o) * p.y_ps) = v;
+          psum.x += v.x; psum.y += v.y; psum.z += v.z; psum.w += v.w;
+        }
+      }
+    }
+    if (p.part) {
+      __syncthreads();
+      float4* red = reinterpret_cast<float4*>(lds);
+      red[t] = psum;
+      __syncthreads();
+      if (t < C::NC4 && cur.c0 + 4 * t < p.E) {
+        float4 sm = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int r = 0; r < 256 / C::NC4; ++r) {
+          const float4 v = red[r * C::NC4 + t];
+          sm.x += v.x; sm.y += v.y; sm.z += v.z; sm.w += v.w;
+        }
+        *reinterpret_cast<float4*>(p.part + ((int64_t)cur.b * tiles_img + cur.t_in) * p.E +
+                                   cur.c0 + 4 * t) = sm;
+      }
+    }
+    __syncthreads();  // LDS (Es / red) free for the next item's staging
+    if (nx_idx >= nitems) break;
+    cur = nxt;
+    ci_idx = nx_idx;
+  }
+}
+
+constexpr int kXdWgPerCu = 2;
+
+struct XdTile {
+  int th, tw;
+};
+
+static XdTile xd_tile(int k, int s) {
+  (void)k;
+  return s == 1 ? XdTile{16, 16} : XdTile{8, 8};
+}
+
+}  // namespace jabd
+
+using namespace jabd;
+
+extern "C" int64_t jabd_expand_dw_nblk(int32_t OH, int32_t OW, int32_t k, int32_t stride) {
+  if (OH <= 0 || OW <= 0 || (stride != 1 && stride != 2)) return -1;
+  const XdTile tl = xd_tile(k, stride);
+  return cdiv(OH, tl.th) * cdiv(OW, tl.tw);
+}
+
+extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_t stream) {
+  JABD_REQUIRE(args, "expand_dw: null args");
+  const jabd_expdw_args& a = *args;
+  JABD_REQUIRE(a.x && a.we && a.be && a.wd && a.bd && a.y, "expand_dw: null pointer");
+  JABD_REQUIRE(a.Cin % 4 == 0 && a.x_ps % 4 == 0 && a.E % 4 == 0 && a.y_ps % 4 == 0 &&
+                   a.y_ps >= a.E && a.x_ps >= a.Cin,
+               "expand_dw: channel counts / strides must be multiples of 4");
+  JABD_REQUIRE(a.Kc == (a.Cin + 15) / 16 && a.Ntiles * 16 >= a.E, "expand_dw: packing mismatch");
+  JABD_REQUIRE((a.k == 3 || a.k == 5) && (a.stride == 1 || a.stride == 2) &&
+                   a.OH == (a.H + 2 * (a.k / 2) - a.k) / a.stride + 1 &&
+                   a.OW == (a.W + 2 * (a.k / 2) - a.k) / a.stride + 1,
+               "expand_dw: unsupported geometry");
+  JABD_REQUIRE(a.act == ACT_NONE || a.act == ACT_RELU || a.act == ACT_HSWISH,
+               "expand_dw: act %d", a.act);
+  const XdTile tl = xd_tile(a.k, a.stride);
+  const int tiles_w = (int)cdiv(a.OW, tl.tw);
+  const int tiles_img = (int)cdiv(a.OH, tl.th) * tiles_w;
+  JABD_REQUIRE(!a.part || a.nblk == tiles_img, "expand_dw: nblk %d != %d", a.nblk, tiles_img);
+  const int EC = a.E <= 16 ? 16 : 32;
+  const int nch = (int)cdiv(a.E, EC);
+  const int64_t ntiles = (int64_t)a.B * tiles_img;
+  const int64_t nitems = cdiv(ntiles, 8) * 8 * nch;
+  // persistent grid: a multiple of 8 (XCD-stable item ownership)
+  int64_t grid = kXdWgPerCu * 256;
+  if (grid > nitems) grid = nitems;  // nitems is a multiple of 8
+  hipStream_t st = as_stream(stream);
+#define XD_CASE(K_, S_, TH_, TW_, EC_)                                                       \
+  if (a.k == K_ && a.stride == S_ && EC == EC_) {                                            \
+    expdw_kernel<K_, S_, TH_, TW_, EC_><<<(unsigned)grid, 256, 0, st>>>(a, tiles_w, tiles_img, \
+                                                                       nch, nitems);         \
+    return check_launch("expand_dw");                                                        \
+  }
+  XD_CASE(3, 1, 16, 16, 16) XD_CASE(3, 1, 16, 16, 32)
+  XD_CASE(5, 1, 16, 16, 16) XD_CASE(5, 1, 16, 16, 32)
+  XD_CASE(3, 2, 8, 8, 16) XD_CASE(3, 2, 8, 8, 32)
+  XD_CASE(5, 2, 8, 8, 16) XD_CASE(5, 2, 8, 8, 32)
+#undef XD_CASE
+  set_error("expand_dw: no kernel for k=%d stride=%d", a.k, a.stride);
+  return JABD_EINVAL;
+}

@@ -65,6 +65,20 @@ class DwArgs(ctypes.Structure):
     ]
 
 
+class ExpDwArgs(ctypes.Structure):
+    """Mirror of `jabd_expdw_args` (include/jabd.h)."""
+    _fields_ = [
+        ("x", c_vp), ("x_bs", c_i64), ("x_ps", c_i32), ("Cin", c_i32),
+        ("B", c_i32), ("H", c_i32), ("W", c_i32), ("E", c_i32),
+        ("we", c_vp), ("be", c_vp), ("Ntiles", c_i32), ("Kc", c_i32),
+        ("wd", c_vp), ("bd", c_vp),
+        ("k", c_i32), ("stride", c_i32), ("act", c_i32), ("nblk", c_i32),
+        ("y", c_vp), ("y_bs", c_i64), ("y_ps", c_i32), ("OH", c_i32), ("OW", c_i32),
+        ("reserved0", c_i32),
+        ("part", c_vp),
+    ]
+
+
 # name -> argtypes (every function returns int status unless listed in _RESTYPE)
 SIGNATURES = {
     "jabd_version": [],
@@ -91,6 +105,8 @@ SIGNATURES = {
     "jabd_stem_nchw_f32": [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp],
     "jabd_dw_nblk": [c_i64, c_i64, c_i64, c_i64],
     "jabd_dwconv_nhwc_f32": [ctypes.POINTER(DwArgs), c_vp],
+    "jabd_expand_dw_nblk": [c_i32, c_i32, c_i32, c_i32],
+    "jabd_expand_dw_nhwc_f32": [ctypes.POINTER(ExpDwArgs), c_vp],
     "jabd_channel_sum_f32": [c_vp, c_i64, c_i32, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp],
     "jabd_eca_gate_f32": [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp,
                           c_vp],
@@ -133,6 +149,7 @@ SIGNATURES = {
                              c_vp],
 }
 _RESTYPE = {"jabd_version": ctypes.c_char_p, "jabd_dw_nblk": ctypes.c_int64,
+            "jabd_expand_dw_nblk": ctypes.c_int64,
             "jabd_bn_nblk": ctypes.c_int64, "jabd_conv_wgrad_part_floats": ctypes.c_int64,
             "jabd_dw_wgrad_part_floats": ctypes.c_int64}
 

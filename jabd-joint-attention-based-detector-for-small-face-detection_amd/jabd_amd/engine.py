@@ -18,11 +18,16 @@ forward as a fixed sequence of libjabd kernels on NHWC fp32 activations:
 
 There is no CPU path: inputs must be float32 tensors on the GPU.
 """
+import os
+
 import torch
 
 from . import functional as F
 
 NLM_SIZES_DEFAULT = (1, 4, 8, 12)
+# MNv3 blocks run expand 1x1 + depthwise as one kernel (csrc/expdw.hip);
+# JABD_FUSE_EXPAND_DW=0 selects the two-kernel path (A/B measurement, tests).
+FUSE_EXPAND_DW = os.environ.get("JABD_FUSE_EXPAND_DW", "1") != "0"
 
 
 def _params_signature(module):
@@ -133,9 +138,13 @@ class _MNv3Block:
             self.project = F.pack_conv(blk.conv3, blk.bn3)
 
     def forward(self, x):
-        e = F.conv(x, self.expand, act=self.act)
-        d, part = F.dwconv(e, self.dw_w, self.dw_b, self.k, self.stride, act=self.act,
-                           partials=True)
+        if FUSE_EXPAND_DW:
+            d, part = F.expand_dw(x, self.expand, self.dw_w, self.dw_b, self.k, self.stride,
+                                  act=self.act)
+        else:
+            e = F.conv(x, self.expand, act=self.act)
+            d, part = F.dwconv(e, self.dw_w, self.dw_b, self.k, self.stride, act=self.act,
+                               partials=True)
         sc = F.eca_gate(part, d.shape[1] * d.shape[2], self.eca, "hsigmoid")
         if self.kind == "identity":
             return F.conv(d, self.project, act=self.act, ascale=sc, res=x)

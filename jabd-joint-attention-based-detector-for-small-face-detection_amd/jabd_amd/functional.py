@@ -9,7 +9,7 @@ import ctypes
 
 import torch
 
-from ._lib import ConvArgs, DwArgs, call, lib
+from ._lib import ConvArgs, DwArgs, ExpDwArgs, call, lib
 
 ACT = {"none": 0, "relu": 1, "leaky": 2, "hswish": 3, "hsigmoid": 4, "sigmoid": 5}
 
@@ -182,6 +182,34 @@ def dwconv(x, w, bias, k, stride, act="none", slope=0.0, partials=False):
         part = torch.empty((B, nb, C), dtype=torch.float32, device=x.device)
         a.nblk, a.part = nb, part.data_ptr()
     call("jabd_dwconv_nhwc_f32", ctypes.byref(a), _stream())
+    return y, part
+
+
+def expand_dw(x, pk, w, bias, k, stride, act="none", partials=True):
+    """Fused expand 1x1 (PackedConv pk, folded BN) + act -> depthwise k x k
+    (pad k//2, folded BN) + act; returns (y, ECA partials [B, nblk, E])."""
+    _check("expand_dw.x", x)
+    B, H, W, C = x.shape
+    if pk.KH != 1 or pk.KW != 1 or pk.Cin != C or pk.Cin2:
+        raise ValueError("expand_dw: pk must be a plain 1x1 conv over all input channels")
+    E = pk.Cout
+    pad = k // 2
+    OH = (H + 2 * pad - k) // stride + 1
+    OW = (W + 2 * pad - k) // stride + 1
+    y = torch.empty((B, OH, OW, E), dtype=torch.float32, device=x.device)
+    a = ExpDwArgs()
+    a.x, a.x_bs, a.x_ps, a.Cin = x.data_ptr(), x.stride(0), C, C
+    a.B, a.H, a.W, a.E = B, H, W, E
+    a.we, a.be, a.Ntiles, a.Kc = pk.w.data_ptr(), pk.bias.data_ptr(), pk.Ntiles, pk.Kc
+    a.wd, a.bd = w.data_ptr(), bias.data_ptr()
+    a.k, a.stride, a.act = k, stride, ACT[act]
+    a.y, a.y_bs, a.y_ps, a.OH, a.OW = y.data_ptr(), y.stride(0), E, OH, OW
+    part = None
+    if partials:
+        nb = int(lib().jabd_expand_dw_nblk(OH, OW, k, stride))
+        part = torch.empty((B, nb, E), dtype=torch.float32, device=x.device)
+        a.nblk, a.part = nb, part.data_ptr()
+    call("jabd_expand_dw_nhwc_f32", ctypes.byref(a), _stream())
     return y, part
 
 

@@ -1,0 +1,62 @@
+"""Fused MobileNetV3 expand 1x1 + depthwise kernel (csrc/expdw.hip) against
+a PyTorch fp32 reference of the same folded ops (nets/mobilenetV3.py:141-142)
+and against the two-kernel HIP path, for every Block_eca geometry of
+JABD-MNv3 (k, stride, Cin, E) on ragged map sizes."""
+import pytest
+import torch
+import torch.nn.functional as tF
+
+from _util import rel_err
+
+# (k, Cin, E, stride, act) — the 15 Block_eca specs of nets/mobilenetV3.py:452-522
+BLOCKS = [(3, 16, 16, 1, "relu"), (3, 16, 64, 2, "relu"), (3, 24, 72, 1, "relu"),
+          (5, 24, 72, 2, "relu"), (5, 40, 120, 1, "relu"), (3, 40, 240, 2, "hswish"),
+          (3, 80, 200, 1, "hswish"), (3, 80, 184, 1, "hswish"), (3, 80, 480, 1, "hswish"),
+          (3, 112, 672, 1, "hswish"), (5, 112, 672, 2, "hswish"), (5, 160, 960, 1, "hswish")]
+
+
+def _act(x, act):
+    return tF.relu(x) if act == "relu" else tF.hardswish(x)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", BLOCKS, ids=lambda s: "k%d_c%d_e%d_s%d" % s[:4])
+@pytest.mark.parametrize("hw", [(37, 29), (64, 64)])
+def test_expand_dw_parity(cuda, spec, hw):
+    from jabd_amd import functional as F
+    k, cin, E, s, act = spec
+    H, W = hw
+    g = torch.Generator().manual_seed(k * 1000 + cin + E + s)
+    B = 2
+    x = torch.randn(B, cin, H, W, generator=g)
+    conv1 = torch.nn.Conv2d(cin, E, 1, bias=False)
+    bn1 = torch.nn.BatchNorm2d(E)
+    conv2 = torch.nn.Conv2d(E, E, k, s, k // 2, groups=E, bias=False)
+    bn2 = torch.nn.BatchNorm2d(E)
+    with torch.no_grad():
+        conv1.weight.copy_(torch.randn(conv1.weight.shape, generator=g) / cin ** 0.5)
+        conv2.weight.copy_(torch.randn(conv2.weight.shape, generator=g) / k)
+        for bn in (bn1, bn2):
+            bn.weight.copy_(1 + 0.2 * torch.randn(E, generator=g))
+            bn.bias.copy_(0.3 * torch.randn(E, generator=g))
+            bn.running_mean.copy_(0.1 * torch.randn(E, generator=g))
+            bn.running_var.copy_(0.5 + torch.rand(E, generator=g))
+    for m in (conv1, bn1, conv2, bn2):
+        m.eval()
+    with torch.no_grad():
+        ref = _act(bn2(conv2(_act(bn1(conv1(x)), act))), act)
+    pk = F.pack_conv(conv1.to(cuda), bn1.to(cuda))
+    dw_w, dw_b = F.pack_dw(conv2.to(cuda), bn2.to(cuda))
+    xg = x.permute(0, 2, 3, 1).contiguous().to(cuda)
+    y, part = F.expand_dw(xg, pk, dw_w, dw_b, k, s, act=act)
+    torch.cuda.synchronize()
+    got = y.permute(0, 3, 1, 2).cpu()
+    assert got.shape == ref.shape
+    assert rel_err(got, ref) < 2e-5, rel_err(got, ref)
+    # ECA pool partials: per-image channel sums of the activated output
+    sums = part.sum(1).cpu().double()
+    assert rel_err(sums, ref.double().sum((2, 3))) < 1e-5
+    # the two-kernel path computes the same tensor
+    e = F.conv(xg, pk, act=act)
+    y2, part2 = F.dwconv(e, dw_w, dw_b, k, s, act=act, partials=True)
+    assert rel_err(y, y2) < 2e-5
