@@ -27,15 +27,14 @@ namespace jabd {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ float xd_act(float v, int act) {
-  switch (act) {
-    case ACT_RELU: return v > 0.f ? v : 0.f;
-    case ACT_HSWISH: {
-      float r = fminf(fmaxf(v + 3.f, 0.f), 6.f);
-      return v * r / 6.f;
-    }
-    default: return v;
-  }
+// Activation fixed at compile time (no per-element branch).  Hardswish
+// multiplies by 1/6 instead of dividing (<= 1 ulp from x*relu6(x+3)/6; an
+// IEEE divide is ~10 VALU instructions per element here).
+template <int ACT>
+__device__ __forceinline__ float xd_act(float v) {
+  if (ACT == ACT_RELU) return v > 0.f ? v : 0.f;
+  if (ACT == ACT_HSWISH) return v * fminf(fmaxf(v + 3.f, 0.f), 6.f) * (1.f / 6.f);
+  return v;
 }
 
 template <int K, int S, int TH, int TW, int EC>
@@ -50,7 +49,7 @@ struct XdCfg {
   static constexpr int BPW = (NBLK + 3) / 4;  // MFMA blocks per wave
   static constexpr int LDS_X = IPAD * XP, LDS_E = IPAD * EP;
   static constexpr int LDS = LDS_X > LDS_E ? LDS_X : LDS_E;
-  static constexpr int PW = 4, NSTRIP = TW / PW, NC4 = EC / 4;
+  static constexpr int PW = S == 1 ? 4 : 2, NSTRIP = TW / PW, NC4 = EC / 4;
   static constexpr int ITEMS = TH * NSTRIP * NC4;
   static constexpr int SPAN = (PW - 1) * S + K;
   static_assert(TW % PW == 0 && 256 % NC4 == 0, "tile shape");
@@ -68,17 +67,18 @@ struct XdItem {
 };
 
 template <int K, int S, int TH, int TW, int EC>
-__device__ __forceinline__ bool xd_item(const jabd_expdw_args& p, int64_t i, int tiles_w,
-                                        int tiles_img, int nch, int64_t nitems, XdItem& it) {
+__device__ __forceinline__ bool xd_item(const jabd_expdw_args& p, int i, int tiles_w,
+                                        int tiles_img, int nch, int nitems, XdItem& it) {
   using C = XdCfg<K, S, TH, TW, EC>;
   if (i >= nitems) return false;
-  const int xcd = (int)(i & 7);
-  const int64_t q = i >> 3;
-  const int chunk = (int)(q % nch);
-  const int64_t tile = (q / nch) * 8 + xcd;
-  if (tile >= (int64_t)p.B * tiles_img) return false;
-  it.b = (int)(tile / tiles_img);
-  it.t_in = (int)(tile - (int64_t)it.b * tiles_img);
+  const int xcd = i & 7;
+  const int q = i >> 3;
+  const int qn = q / nch;
+  const int chunk = q - qn * nch;
+  const int tile = qn * 8 + xcd;
+  if (tile >= p.B * tiles_img) return false;
+  it.b = tile / tiles_img;
+  it.t_in = tile - it.b * tiles_img;
   const int ty = it.t_in / tiles_w, tx = it.t_in - ty * tiles_w;
   it.oh0 = ty * TH;
   it.ow0 = tx * TW;
@@ -88,9 +88,9 @@ __device__ __forceinline__ bool xd_item(const jabd_expdw_args& p, int64_t i, int
   return true;
 }
 
-template <int K, int S, int TH, int TW, int EC>
+template <int K, int S, int TH, int TW, int EC, int ACT>
 __global__ __launch_bounds__(256, 2) void expdw_kernel(const jabd_expdw_args p, int tiles_w,
-                                                    int tiles_img, int nch, int64_t nitems) {
+                                                       int tiles_img, int nch, int nitems) {
   using C = XdCfg<K, S, TH, TW, EC>;
   constexpr int NPF = (C::IPAD * 4 + 255) / 256;  // prefetched float4 per thread per stage
   __shared__ __attribute__((aligned(16))) float lds[C::LDS];
@@ -101,32 +101,37 @@ __global__ __launch_bounds__(256, 2) void expdw_kernel(const jabd_expdw_args p, 
 
   // tiles that straddle the 8-aligned tile padding are skipped: advance to
   // the next real item (uniform per workgroup)
-  auto next_item = [&](int64_t i, XdItem& it) -> int64_t {
+  auto next_item = [&](int i, XdItem& it) -> int {
     while (i < nitems && !xd_item<K, S, TH, TW, EC>(p, i, tiles_w, tiles_img, nch, nitems, it))
       i += G;
     return i;
   };
   float4 pf[NPF];
+  // this thread's (tile row, tile col) of each prefetch slot; rr = -1 marks
+  // padding slots.  The channel quad (t & 3) is the same for every slot.
+  int pr[NPF], pc[NPF];
+#pragma unroll
+  for (int u = 0; u < NPF; ++u) {
+    const int px = (u * 256 + t) >> 2;
+    pr[u] = px < C::IPX ? px / C::IW : -1;
+    pc[u] = px < C::IPX ? px - (px / C::IW) * C::IW : 0;
+  }
+  const int cq = (t & 3) * 4;
   auto prefetch = [&](const XdItem& it, int kc) {
-    const float* xb = p.x + (int64_t)it.b * p.x_bs;
+    const float* xb = p.x + (int64_t)it.b * p.x_bs + 16 * kc + cq;
+    const bool cv = 16 * kc + cq < p.Cin;
 #pragma unroll
     for (int u = 0; u < NPF; ++u) {
-      const int idx = u * 256 + t;
-      const int px = idx >> 2, c4 = (idx & 3) * 4;
-      const int ci = 16 * kc + c4;
+      const int ih = it.ih0 + pr[u], iw = it.iw0 + pc[u];
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (px < C::IPX && ci < p.Cin) {
-        const int r = px / C::IW, cc = px - r * C::IW;
-        const int ih = it.ih0 + r, iw = it.iw0 + cc;
-        if (ih >= 0 && ih < p.H && iw >= 0 && iw < p.W)
-          v = *reinterpret_cast<const float4*>(xb + ((int64_t)ih * p.W + iw) * p.x_ps + ci);
-      }
+      if (cv && pr[u] >= 0 && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W)
+        v = *reinterpret_cast<const float4*>(xb + (ih * p.W + iw) * p.x_ps);
       pf[u] = v;
     }
   };
 
   XdItem cur, nxt;
-  int64_t ci_idx = next_item(blockIdx.x, cur);
+  int ci_idx = next_item(blockIdx.x, cur);
   if (ci_idx >= nitems) return;
   prefetch(cur, 0);
   const int c4 = t % C::NC4, chl = 4 * c4;
@@ -138,7 +143,7 @@ __global__ __launch_bounds__(256, 2) void expdw_kernel(const jabd_expdw_args p, 
 #pragma unroll
     for (int u = 0; u < C::BPW; ++u) acc[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
     const int nt0 = cur.c0 / 16;
-    int64_t nx_idx = -1;
+    int nx_idx = -1;
     for (int kc = 0; kc < p.Kc; ++kc) {
       // regs -> LDS (this stage's input channels)
 #pragma unroll
@@ -186,10 +191,10 @@ __global__ __launch_bounds__(256, 2) void expdw_kernel(const jabd_expdw_args p, 
           const int ih = cur.ih0 + r, iw = cur.iw0 + cc;
           if (ih >= 0 && ih < p.H && iw >= 0 && iw < p.W) {
             const float4 bi = *reinterpret_cast<const float4*>(p.be + cur.c0 + ch);
-            o.x = xd_act(acc[u][0] + bi.x, p.act);
-            o.y = xd_act(acc[u][1] + bi.y, p.act);
-            o.z = xd_act(acc[u][2] + bi.z, p.act);
-            o.w = xd_act(acc[u][3] + bi.w, p.act);
+            o.x = xd_act<ACT>(acc[u][0] + bi.x);
+            o.y = xd_act<ACT>(acc[u][1] + bi.y);
+            o.z = xd_act<ACT>(acc[u][2] + bi.z);
+            o.w = xd_act<ACT>(acc[u][3] + bi.w);
           }
         }
         *reinterpret_cast<float4*>(lds + px * C::EP + ch) = o;
@@ -245,10 +250,10 @@ __global__ __launch_bounds__(256, 2) void expdw_kernel(const jabd_expdw_args p, 
         for (int o = 0; o < C::PW; ++o) {
           if (owb + o >= p.OW) break;
           float4 v;
-          v.x = xd_act(a2[o].x, p.act);
-          v.y = xd_act(a2[o].y, p.act);
-          v.z = xd_act(a2[o].z, p.act);
-          v.w = xd_act(a2[o].w, p.act);
+          v.x = xd_act<ACT>(a2[o].x);
+          v.y = xd_act<ACT>(a2[o].y);
+          v.z = xd_act<ACT>(a2[o].z);
+          v.w = xd_act<ACT>(a2[o].w);
           *reinterpret_cast<float4*>(yb + ((int64_t)oh * p.OW + owb + o) * p.y_ps) = v;
           psum.x += v.x; psum.y += v.y; psum.z += v.z; psum.w += v.w;
         }
@@ -319,21 +324,32 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
   const int nch = (int)cdiv(a.E, EC);
   const int64_t ntiles = (int64_t)a.B * tiles_img;
   const int64_t nitems = cdiv(ntiles, 8) * 8 * nch;
+  JABD_REQUIRE(nitems < ((int64_t)1 << 31) && (int64_t)a.H * a.W * a.x_ps < ((int64_t)1 << 31),
+               "expand_dw: problem too large for 32-bit item / pixel indexing");
   // persistent grid: a multiple of 8 (XCD-stable item ownership)
   int64_t grid = kXdWgPerCu * 256;
   if (grid > nitems) grid = nitems;  // nitems is a multiple of 8
   hipStream_t st = as_stream(stream);
-#define XD_CASE(K_, S_, TH_, TW_, EC_)                                                       \
-  if (a.k == K_ && a.stride == S_ && EC == EC_) {                                            \
-    expdw_kernel<K_, S_, TH_, TW_, EC_><<<(unsigned)grid, 256, 0, st>>>(a, tiles_w, tiles_img, \
-                                                                       nch, nitems);         \
-    return check_launch("expand_dw");                                                        \
+#define XD_LAUNCH(K_, S_, TH_, TW_, EC_, ACT_)                                            \
+  expdw_kernel<K_, S_, TH_, TW_, EC_, ACT_><<<(unsigned)grid, 256, 0, st>>>(a, tiles_w,     \
+                                                                           tiles_img, nch, \
+                                                                           (int)nitems)
+#define XD_CASE(K_, S_, TH_, TW_, EC_)                                    \
+  if (a.k == K_ && a.stride == S_ && EC == EC_) {                         \
+    if (a.act == ACT_RELU)                                                \
+      XD_LAUNCH(K_, S_, TH_, TW_, EC_, ACT_RELU);                         \
+    else if (a.act == ACT_HSWISH)                                         \
+      XD_LAUNCH(K_, S_, TH_, TW_, EC_, ACT_HSWISH);                       \
+    else                                                                  \
+      XD_LAUNCH(K_, S_, TH_, TW_, EC_, ACT_NONE);                         \
+    return check_launch("expand_dw");                                     \
   }
   XD_CASE(3, 1, 16, 16, 16) XD_CASE(3, 1, 16, 16, 32)
   XD_CASE(5, 1, 16, 16, 16) XD_CASE(5, 1, 16, 16, 32)
   XD_CASE(3, 2, 8, 8, 16) XD_CASE(3, 2, 8, 8, 32)
   XD_CASE(5, 2, 8, 8, 16) XD_CASE(5, 2, 8, 8, 32)
 #undef XD_CASE
+#undef XD_LAUNCH
   set_error("expand_dw: no kernel for k=%d stride=%d", a.k, a.stride);
   return JABD_EINVAL;
 }
