@@ -19,6 +19,10 @@
 // optional K-concatenated second source (the block's skip branch folded into
 // the same GEMM); residual add; activation; channel-offset / strided output
 // (SSH concat, head layout).
+#include <stdlib.h>
+
+#include <algorithm>
+
 #include "common.h"
 #include "conv_args.h"
 
@@ -32,9 +36,9 @@ __device__ __forceinline__ float act_apply(float v, int act, float slope) {
     case ACT_LEAKY: return v > 0.f ? v : v * slope;
     case ACT_HSWISH: {
       float r = fminf(fmaxf(v + 3.f, 0.f), 6.f);
-      return v * r / 6.f;
+      return v * r * (1.f / 6.f);
     }
-    case ACT_HSIGMOID: return fminf(fmaxf(v + 3.f, 0.f), 6.f) / 6.f;
+    case ACT_HSIGMOID: return fminf(fmaxf(v + 3.f, 0.f), 6.f) * (1.f / 6.f);
     case ACT_SIGMOID: return 1.f / (1.f + expf(-v));
     default: return v;
   }
@@ -187,16 +191,28 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
 #pragma unroll
       for (int u = 0; u < TN; ++u) b_nxt[u] = wbase[(kc + 1) * wstride_k + u * 64];
     }
+    // k-step outermost: consecutive MFMAs update independent accumulators
+    // (16x16x4 f32: 32-cycle issue, 40-cycle dependent latency)
 #pragma unroll
-    for (int t = 0; t < TM; ++t) {
+    for (int t = 0; t < TM; ++t)
 #pragma unroll
-      for (int u = 0; u < TN; ++u) {
+      for (int u = 0; u < TN; ++u)
         acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(b_cur[u].x, a_cur[t].x, acc[t][u], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
         acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(b_cur[u].y, a_cur[t].y, acc[t][u], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
         acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(b_cur[u].z, a_cur[t].z, acc[t][u], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
         acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(b_cur[u].w, a_cur[t].w, acc[t][u], 0, 0, 0);
-      }
-    }
     if (more) {
 #pragma unroll
       for (int t = 0; t < TM; ++t) a_cur[t] = a_nxt[t];
@@ -275,6 +291,172 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// 1x1 / stride-1 fast path.  Same MFMA mapping as conv_gemm_kernel, but the
+// A operand of pixel m is the contiguous row x + m*x_ps (no im2col index
+// math, no generic-path registers), so the kernel holds ~half the VGPRs and
+// runs at twice the occupancy — the layers it serves (MobileNetV3 project
+// convs, FPN laterals, ResNet 1x1s) are memory-bound and latency-limited.
+//   X2: 0 = no second source, 1 = same-resolution K-concat source (MNv3
+//   skip), 2 = strided K-concat source (ResNet downsample).
+// Host guarantees: Cin, x_ps, x_c0, Cin2, x2_ps % 4 == 0; batch-contiguous
+// x / y / res (bs == pixels * ps); M * max(ps) < 2^31; v4 epilogue.
+// ---------------------------------------------------------------------------
+template <int TM, int TN, int X2, bool ASCALE>
+__global__ __launch_bounds__(256) void conv1x1_kernel(const ConvArgs p) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int g = lane >> 4, j = lane & 15;
+  const int nblk_n = p.Ntiles / TN;
+  const int bid = blockIdx.x;
+  const int nb = bid % nblk_n;
+  const int mb = bid / nblk_n;
+  const int m_wave = (mb * 4 + wave) * (16 * TM);
+  const int OHW = p.OH * p.OW;
+  const int M = (int)p.M;
+
+  int pm[TM];  // pixel index (clamped), -1 when out of range
+#pragma unroll
+  for (int t = 0; t < TM; ++t) {
+    const int m = m_wave + t * 16 + j;
+    pm[t] = m < M ? m : -1;
+  }
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int u = 0; u < TN; ++u) acc[t][u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const float4* wbase = reinterpret_cast<const float4*>(p.w) + ((int64_t)nb * TN) * 64 + lane;
+  const int wstride_k = p.Ntiles * 64;
+  const float* xg = p.x + p.x_c0 + 4 * g;
+  const int x2_pix = X2 == 2 ? (int)(p.x2_bs / p.x2_ps) : 0;  // x2 pixels per image
+
+  auto load = [&](int kc, float4 (&a)[TM]) {
+    const int k4 = kc * 16 + 4 * g;
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int m = pm[t];
+      if (m >= 0) {
+        if (k4 < p.Cin) {
+          r = *reinterpret_cast<const float4*>(xg + m * p.x_ps + kc * 16);
+          if (ASCALE) {
+            const int b = m / OHW;
+            const float4 s4 = *reinterpret_cast<const float4*>(p.ascale + b * (int)p.ascale_bs + k4);
+            r.x *= s4.x; r.y *= s4.y; r.z *= s4.z; r.w *= s4.w;
+          }
+        } else if (X2 != 0 && k4 < p.Cin + p.Cin2) {
+          int q;
+          if (X2 == 1) {
+            q = m;
+          } else {
+            const int b = m / OHW, rr = m - b * OHW;
+            const int oh = rr / p.OW, ow = rr - oh * p.OW;
+            q = b * x2_pix + (oh * p.x2_stride) * p.x2_W + ow * p.x2_stride;
+          }
+          r = *reinterpret_cast<const float4*>(p.x2 + q * p.x2_ps + (k4 - p.Cin));
+        }
+      }
+      a[t] = r;
+    }
+  };
+
+  float4 a_cur[TM], b_cur[TN];
+  load(0, a_cur);
+#pragma unroll
+  for (int u = 0; u < TN; ++u) b_cur[u] = wbase[u * 64];
+
+  for (int kc = 0; kc < p.Kc; ++kc) {
+    float4 a_nxt[TM], b_nxt[TN];
+    const bool more = kc + 1 < p.Kc;
+    if (more) {
+      load(kc + 1, a_nxt);
+#pragma unroll
+      for (int u = 0; u < TN; ++u) b_nxt[u] = wbase[(kc + 1) * wstride_k + u * 64];
+    }
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(b_cur[u].x, a_cur[t].x, acc[t][u], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(b_cur[u].y, a_cur[t].y, acc[t][u], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(b_cur[u].z, a_cur[t].z, acc[t][u], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(b_cur[u].w, a_cur[t].w, acc[t][u], 0, 0, 0);
+    if (more) {
+#pragma unroll
+      for (int t = 0; t < TM; ++t) a_cur[t] = a_nxt[t];
+#pragma unroll
+      for (int u = 0; u < TN; ++u) b_cur[u] = b_nxt[u];
+    }
+  }
+
+  // epilogue (LDS-staged whole-row stores), acc[t][u][r] = Y[pixel][16(nb*TN+u) + 4g + r]
+  constexpr int LDW = 16 * TN + 4;
+  __shared__ float s_epi[4 * 16 * LDW];
+  float* sm = s_epi + wave * 16 * LDW;
+#pragma unroll
+  for (int t = 0; t < TM; ++t) {
+#pragma unroll
+    for (int u = 0; u < TN; ++u)
+      *reinterpret_cast<f32x4*>(sm + j * LDW + 16 * u + 4 * g) = acc[t][u];
+    __syncthreads();
+#pragma unroll
+    for (int f0 = 0; f0 < 16 * 4 * TN; f0 += 64) {
+      const int f = f0 + lane;
+      const int q = f / (4 * TN), c4 = f - q * (4 * TN);
+      const int m = __shfl(pm[t], q);  // outside the branch (inactive lanes read 0)
+      const int n0 = nb * TN * 16 + 4 * c4;
+      if (m >= 0 && n0 < p.Cout) {
+        float4 v = *reinterpret_cast<const float4*>(sm + q * LDW + 4 * c4);
+        if (p.bias) {
+          const float4 bb = *reinterpret_cast<const float4*>(p.bias + n0);
+          v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
+        }
+        if (p.res) {
+          const float4 rr = *reinterpret_cast<const float4*>(p.res + m * p.res_ps + p.res_c0 + n0);
+          v.x += rr.x; v.y += rr.y; v.z += rr.z; v.w += rr.w;
+        }
+        v.x = act_apply(v.x, p.act, p.slope);
+        v.y = act_apply(v.y, p.act, p.slope);
+        v.z = act_apply(v.z, p.act, p.slope);
+        v.w = act_apply(v.w, p.act, p.slope);
+        *reinterpret_cast<float4*>(p.y + m * p.y_ps + p.y_c0 + n0) = v;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int TM, int TN>
+static int launch_1x1(const ConvArgs& a, hipStream_t st) {
+  const int64_t grid = cdiv(a.M, (int64_t)4 * 16 * TM) * (a.Ntiles / TN);
+  JABD_REQUIRE(grid < (int64_t)0x7fffffff, "conv: grid too large");
+  const int x2 = !a.x2 ? 0 : (a.x2_stride == 1 ? 1 : 2);
+  const bool as = a.ascale != nullptr;
+#define C1_CASE(X2_, AS_)                                                    \
+  if (x2 == X2_ && as == AS_) {                                              \
+    conv1x1_kernel<TM, TN, X2_, AS_><<<(unsigned)grid, 256, 0, st>>>(a);     \
+    return check_launch("conv1x1");                                          \
+  }
+  C1_CASE(0, false) C1_CASE(0, true) C1_CASE(1, false) C1_CASE(1, true)
+  C1_CASE(2, false) C1_CASE(2, true)
+#undef C1_CASE
+  return JABD_EINVAL;
+}
+
 template <int TM, int TN>
 static int launch_conv(const ConvArgs& a, bool vec4, hipStream_t st) {
   const int64_t rows_per_blk = 4 * 16 * TM;
@@ -304,6 +486,16 @@ extern "C" int jabd_conv_pack_tn(int cout) {
     if (w < waste || (w == waste && tn > best)) { waste = w; best = tn; }
   }
   return best;
+}
+
+// JABD_CONV_GENERIC=1 forces the generic implicit-GEMM kernel (A/B tests).
+static bool conv_generic_only() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("JABD_CONV_GENERIC");
+    v = e && e[0] == '1' ? 1 : 0;
+  }
+  return v == 1;
 }
 
 extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t stream) {
@@ -345,6 +537,29 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
   hipStream_t st = as_stream(stream);
   const int tn = a.tn;
   JABD_REQUIRE(a.Ntiles % tn == 0, "conv: Ntiles %% tn != 0");
+  const int64_t OHW = (int64_t)a.OH * a.OW;
+  const int64_t maxps = std::max<int64_t>(std::max<int64_t>(a.x_ps, a.y_ps),
+                                          std::max<int64_t>(a.res ? a.res_ps : 0,
+                                                            a.x2 ? a.x2_ps : 0));
+  const bool fast1x1 =
+      is1x1 && !a.tconv && vec4 && (a.flags & 1) && a.x_bs == OHW * a.x_ps &&
+      a.y_bs == OHW * a.y_ps && (!a.res || a.res_bs == OHW * a.res_ps) &&
+      (!a.ascale || a.ascale_bs % 4 == 0) &&
+      (!a.x2 || (a.x2_stride == 1 ? (a.x2_W == a.OW && a.x2_bs == OHW * a.x2_ps)
+                                  : (a.x2_stride > 1 && a.x2_bs % a.x2_ps == 0 &&
+                                     a.x2_bs * a.B < ((int64_t)1 << 31)))) &&
+      (a.M + 64) * (maxps + 16) < ((int64_t)1 << 31) && !conv_generic_only();
+  if (fast1x1) {
+    switch (tn) {
+      case 1: return launch_1x1<4, 1>(a, st);
+      case 2: return launch_1x1<4, 2>(a, st);
+      case 3: return launch_1x1<4, 3>(a, st);
+      case 4: return launch_1x1<4, 4>(a, st);
+      case 5: return launch_1x1<4, 5>(a, st);
+      case 8: return launch_1x1<2, 8>(a, st);
+      default: break;
+    }
+  }
   switch (tn) {
     case 1: return launch_conv<4, 1>(a, vec4, st);
     case 2: return launch_conv<4, 2>(a, vec4, st);

@@ -54,6 +54,7 @@ struct XdCfg {
   static constexpr int SPAN = (PW - 1) * S + K;
   static_assert(TW % PW == 0 && 256 % NC4 == 0, "tile shape");
   static_assert(LDS * 4 <= 160 * 1024, "LDS");
+  static_assert((K * K + 1) * NC4 <= 256, "dw taps: one float4 per thread");
 };
 
 // Persistent: workgroup L walks work items i = L, L + G, ... (G = grid, a
@@ -117,6 +118,16 @@ __global__ __launch_bounds__(256, 2) void expdw_kernel(const jabd_expdw_args p, 
     pc[u] = px < C::IPX ? px - (px / C::IW) * C::IW : 0;
   }
   const int cq = (t & 3) * 4;
+  const int c4 = t % C::NC4, chl = 4 * c4;
+  // expand-GEMM channel block of this wave (blk = wave + 4u -> nt = blk % NNT)
+  const int ntw = wave % C::NNT;
+  constexpr int NWD = (K * K + 1) * C::NC4;  // dw taps + bias float4 of one chunk
+  // Register prefetch of everything a stage / item reads from global memory:
+  // input pixels (pf), this wave's packed expand weights (pa), and at an
+  // item's first stage its expand bias (pbi) and dw taps (pwd), so no global
+  // load latency is exposed between the barriers of an item.
+  f32x4 pa_n = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float4 pbi_n = make_float4(0.f, 0.f, 0.f, 0.f), pwd_n = pbi_n;
   auto prefetch = [&](const XdItem& it, int kc) {
     const float* xb = p.x + (int64_t)it.b * p.x_bs + 16 * kc + cq;
     const bool cv = 16 * kc + cq < p.Cin;
@@ -128,15 +139,25 @@ __global__ __launch_bounds__(256, 2) void expdw_kernel(const jabd_expdw_args p, 
         v = *reinterpret_cast<const float4*>(xb + (ih * p.W + iw) * p.x_ps);
       pf[u] = v;
     }
+    const int nt = it.c0 / 16 + ntw;
+    if (nt < p.Ntiles) pa_n = wpk[(kc * p.Ntiles + nt) * 64 + lane];
+    if (kc == 0) {
+      const int ch = it.c0 + 16 * ntw + 4 * g;
+      if (ch < p.E) pbi_n = *reinterpret_cast<const float4*>(p.be + ch);
+      if (t < NWD) {
+        const int tp = t / C::NC4, cc = it.c0 + 4 * (t - tp * C::NC4);
+        pwd_n = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (cc < p.E)
+          pwd_n = *reinterpret_cast<const float4*>((tp < K * K ? p.wd + tp * p.E : p.bd) + cc);
+      }
+    }
   };
 
   XdItem cur, nxt;
   int ci_idx = next_item(blockIdx.x, cur);
   if (ci_idx >= nitems) return;
   prefetch(cur, 0);
-  const int c4 = t % C::NC4, chl = 4 * c4;
-  // expand-GEMM channel block of this wave (blk = wave + 4u -> nt = blk % NNT)
-  const int ntw = wave % C::NNT;
+  float4 pbi = pbi_n, pwd = pwd_n;
 
   while (true) {
     f32x4 acc[C::BPW];
@@ -152,6 +173,7 @@ __global__ __launch_bounds__(256, 2) void expdw_kernel(const jabd_expdw_args p, 
         if (idx < C::IPAD * 4)
           *reinterpret_cast<float4*>(lds + (idx >> 2) * C::XP + (idx & 3) * 4) = pf[u];
       }
+      const f32x4 a = pa_n;
       __syncthreads();
       // issue the next stage's loads
       if (kc + 1 < p.Kc) {
@@ -161,7 +183,6 @@ __global__ __launch_bounds__(256, 2) void expdw_kernel(const jabd_expdw_args p, 
         if (nx_idx < nitems) prefetch(nxt, 0);
       }
       if (nt0 + ntw < p.Ntiles) {
-        const f32x4 a = wpk[((int64_t)kc * p.Ntiles + nt0 + ntw) * 64 + lane];
 #pragma unroll
         for (int u = 0; u < C::BPW; ++u) {
           const int blk = wave + 4 * u;
@@ -190,7 +211,7 @@ __global__ __launch_bounds__(256, 2) void expdw_kernel(const jabd_expdw_args p, 
           const int r = px / C::IW, cc = px - r * C::IW;
           const int ih = cur.ih0 + r, iw = cur.iw0 + cc;
           if (ih >= 0 && ih < p.H && iw >= 0 && iw < p.W) {
-            const float4 bi = *reinterpret_cast<const float4*>(p.be + cur.c0 + ch);
+            const float4 bi = pbi;  // ch = 16*ntw + 4g for every block of this wave
             o.x = xd_act<ACT>(acc[u][0] + bi.x);
             o.y = xd_act<ACT>(acc[u][1] + bi.y);
             o.z = xd_act<ACT>(acc[u][2] + bi.z);
@@ -200,14 +221,7 @@ __global__ __launch_bounds__(256, 2) void expdw_kernel(const jabd_expdw_args p, 
         *reinterpret_cast<float4*>(lds + px * C::EP + ch) = o;
       }
     }
-    for (int idx = t; idx < (K * K + 1) * C::NC4; idx += 256) {
-      const int tp = idx / C::NC4, q4 = idx - tp * C::NC4;
-      const int cc = cur.c0 + 4 * q4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (cc < p.E)
-        v = *reinterpret_cast<const float4*>((tp < K * K ? p.wd + (int64_t)tp * p.E : p.bd) + cc);
-      wsh[tp][q4] = v;
-    }
+    if (t < NWD) wsh[t / C::NC4][t % C::NC4] = pwd;
     __syncthreads();
 
     // depthwise phase
@@ -278,6 +292,8 @@ __global__ __launch_bounds__(256, 2) void expdw_kernel(const jabd_expdw_args p, 
     if (nx_idx >= nitems) break;
     cur = nxt;
     ci_idx = nx_idx;
+    pbi = pbi_n;
+    pwd = pwd_n;
   }
 }
 
