@@ -20,6 +20,8 @@
 // in registers across the switch).  Workgroup ids are decoded XCD-aware: the
 // EC-chunks of one tile land on the same XCD (id % 8), so their re-reads of
 // the input tile hit that XCD's L2.
+#include <stdlib.h>
+
 #include "common.h"
 #include "conv_args.h"
 
@@ -90,7 +92,7 @@ __device__ __forceinline__ bool xd_item(const jabd_expdw_args& p, int i, int til
 }
 
 template <int K, int S, int TH, int TW, int EC, int ACT>
-__global__ __launch_bounds__(256, 2) void expdw_kernel(const jabd_expdw_args p, int tiles_w,
+__global__ __launch_bounds__(256, EC == 16 ? 3 : 2) void expdw_kernel(const jabd_expdw_args p, int tiles_w,
                                                        int tiles_img, int nch, int nitems) {
   using C = XdCfg<K, S, TH, TW, EC>;
   constexpr int NPF = (C::IPAD * 4 + 255) / 256;  // prefetched float4 per thread per stage
@@ -297,7 +299,21 @@ __global__ __launch_bounds__(256, 2) void expdw_kernel(const jabd_expdw_args p, 
   }
 }
 
-constexpr int kXdWgPerCu = 2;
+static int64_t xd_grid(const void* fn, int64_t nitems) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 256, 0) != hipSuccess || per < 1)
+    per = 1;
+  int64_t grid = (int64_t)per * cus / 8 * 8;
+  if (grid < 8) grid = 8;
+  return grid < nitems ? grid : nitems;  // nitems is a multiple of 8
+}
 
 struct XdTile {
   int th, tw;
@@ -336,20 +352,27 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
   const int tiles_w = (int)cdiv(a.OW, tl.tw);
   const int tiles_img = (int)cdiv(a.OH, tl.th) * tiles_w;
   JABD_REQUIRE(!a.part || a.nblk == tiles_img, "expand_dw: nblk %d != %d", a.nblk, tiles_img);
-  const int EC = a.E <= 16 ? 16 : 32;
+  static int ec16 = -1;
+  if (ec16 < 0) {
+    const char* e = getenv("JABD_EXPDW_EC16");
+    ec16 = e && e[0] == '1' ? 1 : 0;
+  }
+  const int EC = (a.E <= 16 || ec16) ? 16 : 32;
   const int nch = (int)cdiv(a.E, EC);
   const int64_t ntiles = (int64_t)a.B * tiles_img;
   const int64_t nitems = cdiv(ntiles, 8) * 8 * nch;
   JABD_REQUIRE(nitems < ((int64_t)1 << 31) && (int64_t)a.H * a.W * a.x_ps < ((int64_t)1 << 31),
                "expand_dw: problem too large for 32-bit item / pixel indexing");
-  // persistent grid: a multiple of 8 (XCD-stable item ownership)
-  int64_t grid = kXdWgPerCu * 256;
-  if (grid > nitems) grid = nitems;  // nitems is a multiple of 8
   hipStream_t st = as_stream(stream);
-#define XD_LAUNCH(K_, S_, TH_, TW_, EC_, ACT_)                                            \
-  expdw_kernel<K_, S_, TH_, TW_, EC_, ACT_><<<(unsigned)grid, 256, 0, st>>>(a, tiles_w,     \
-                                                                           tiles_img, nch, \
-                                                                           (int)nitems)
+  // persistent grid = the workgroups that are resident at once (a multiple of
+  // 8 for XCD-stable item ownership; any more would run as a late tail)
+#define XD_LAUNCH(K_, S_, TH_, TW_, EC_, ACT_)                                                \
+  do {                                                                                        \
+    const int64_t grid = xd_grid((const void*)expdw_kernel<K_, S_, TH_, TW_, EC_, ACT_>, nitems); \
+    expdw_kernel<K_, S_, TH_, TW_, EC_, ACT_><<<(unsigned)grid, 256, 0, st>>>(a, tiles_w,     \
+                                                                             tiles_img, nch,  \
+                                                                             (int)nitems);    \
+  } while (0)
 #define XD_CASE(K_, S_, TH_, TW_, EC_)                                    \
   if (a.k == K_ && a.stride == S_ && EC == EC_) {                         \
     if (a.act == ACT_RELU)                                                \

@@ -53,19 +53,36 @@ __global__ void eca_gate_kernel(const float* __restrict__ part, int64_t nblk, in
                                 const float* __restrict__ w1d, int k, int gate,
                                 float* __restrict__ scale, float* __restrict__ mean_out) {
   extern __shared__ float mean[];
+  __shared__ float red[256];
   const int b = blockIdx.x;
   const float* pb = part + (int64_t)b * nblk * C;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    // 8 independent accumulators keep 8 loads in flight (fixed order -> deterministic)
-    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    int64_t q = 0;
-    for (; q + 8 <= nblk; q += 8) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s[u] += pb[(q + u) * C + c];
+  // channels across `lanes` threads, partial blocks across 256/lanes rows,
+  // then a fixed-order combine (deterministic)
+  const int lanes = C < 64 ? C : 64;
+  const int rows = blockDim.x / lanes;
+  const int t = threadIdx.x, r = t / lanes, cl = t - (t / lanes) * lanes;
+  for (int c0 = 0; c0 < C; c0 += lanes) {  // uniform trip count (barriers inside)
+    const int c = c0 + cl;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    if (r < rows && c < C) {
+      int64_t q = r;
+      for (; q + 3 * rows < nblk; q += 4 * rows) {
+        s0 += pb[q * C + c];
+        s1 += pb[(q + rows) * C + c];
+        s2 += pb[(q + 2 * rows) * C + c];
+        s3 += pb[(q + 3 * rows) * C + c];
+      }
+      for (; q < nblk; q += rows) s0 += pb[q * C + c];
     }
-    for (; q < nblk; ++q) s[0] += pb[q * C + c];
-    mean[c] = (((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]))) * inv_hw;
-    if (mean_out) mean_out[(int64_t)b * C + c] = mean[c];
+    red[t] = (s0 + s1) + (s2 + s3);
+    __syncthreads();
+    if (t < lanes && c < C) {
+      float sm = 0.f;
+      for (int q = 0; q < rows; ++q) sm += red[q * lanes + t];
+      mean[c] = sm * inv_hw;
+      if (mean_out) mean_out[(int64_t)b * C + c] = mean[c];
+    }
+    __syncthreads();
   }
   __syncthreads();
   const int h = (k - 1) / 2;
@@ -75,7 +92,7 @@ __global__ void eca_gate_kernel(const float* __restrict__ part, int64_t nblk, in
       const int cc = c + t - h;
       if (cc >= 0 && cc < C) y = fmaf(w1d[t], mean[cc], y);
     }
-    float g = gate == ACT_SIGMOID ? 1.f / (1.f + expf(-y)) : fminf(fmaxf(y + 3.f, 0.f), 6.f) / 6.f;
+    float g = gate == ACT_SIGMOID ? 1.f / (1.f + expf(-y)) : fminf(fmaxf(y + 3.f, 0.f), 6.f) * (1.f / 6.f);
     scale[(int64_t)b * C + c] = g;
   }
 }

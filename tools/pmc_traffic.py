@@ -1,4 +1,4 @@
-"""Conv-GEMM HBM traffic per step from two rocprofv3 PMC passes.
+"""Conv-stack (conv_gemm / conv1x1 / fused expand_dw) HBM traffic per step from two rocprofv3 PMC passes.
 
 Usage (on the GPU box, one counter per pass as MI355X_MICROARCH.md
 §rocprofv3 PMC slots requires — FETCH_SIZE and WRITE_SIZE do not fit one pass):
@@ -18,7 +18,7 @@ import glob
 import json
 import sys
 
-KERNEL = "conv_gemm_kernel"
+KERNELS = ("conv_gemm_kernel", "conv1x1_kernel", "expdw_kernel")  # the conv stack
 
 
 def _sum(d, counter):
@@ -28,7 +28,7 @@ def _sum(d, counter):
     tot, n = 0.0, 0
     for f in files:
         for r in csv.DictReader(open(f)):
-            if r.get("Counter_Name") == counter and KERNEL in r.get("Kernel_Name", ""):
+            if r.get("Counter_Name") == counter and any(k in r.get("Kernel_Name", "") for k in KERNELS):
                 tot += float(r["Counter_Value"])
                 n += 1
     return tot, n
