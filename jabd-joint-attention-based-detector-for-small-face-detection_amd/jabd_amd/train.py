@@ -127,7 +127,10 @@ def _dgrad(dy, weight, stride, pad, H, W):
     pk = _packed(weight, transposed=True)
     B = dy.shape[0]
     dx = torch.empty((B, H, W, pk.Cout), dtype=torch.float32, device=dy.device)
-    a = _conv_args(dy, pk, dx, stride, pad, tconv=True, OH=H, OW=W)
+    # a 1x1 / stride-1 data gradient is a plain 1x1 conv with the transposed
+    # weights (takes the conv1x1 fast path)
+    plain = pk.KH == 1 and pk.KW == 1 and stride == 1 and pad == 0
+    a = _conv_args(dy, pk, dx, stride, pad, tconv=not plain, OH=H, OW=W)
     call("jabd_conv2d_nhwc_f32", ctypes.byref(a), _st())
     return dx
 
