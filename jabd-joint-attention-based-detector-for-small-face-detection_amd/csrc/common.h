@@ -49,8 +49,9 @@ struct Carve {
 struct Sizer {
   size_t used = 0;
   template <typename T>
-  void take(size_t count) {
+  T* take(size_t count) {
     used = align_up(used) + align_up(count * sizeof(T));
+    return nullptr;
   }
 };
 

@@ -8,9 +8,14 @@
 //                    every image's rows contiguous, in stable descending-score
 //                    order (ties by lower row index, as torch's stable sort).
 //   3. nms_gather    sorted boxes (float4) + areas + original row ids.
-//   4. nms_mask      upper-triangular IoU bitmask, 64x64 tiles, one lane per
-//                    row box, column boxes broadcast from LDS; stored sparse:
-//                    the in-block word per row + a list of non-zero words.
+//   4. mask          which later-ranked boxes each box suppresses, as the
+//                    in-block word per row + a sparse list per row.  Two
+//                    producers, chosen per image on the device:
+//                    grid (candidate-pruned, thr >= 0, finite boxes): only
+//                    pairs of similar area in neighbouring cells are tested
+//                    (grid_* kernels below);  dense (NaN boxes, thr < 0, or
+//                    more candidate pairs than the workspace holds): every
+//                    pair in 64x64 tiles (nms_mask).
 //   5. nms_scan      one workgroup per image walks the row blocks on the
 //                    device (suppressed-set bitset in LDS, next block's lists
 //                    prefetched), writes kept rows + count.
@@ -18,6 +23,10 @@
 // (no FMA in (x2-x1)*(y2-y1) or inter/(a+b-inter)).
 #include <hipcub/hipcub.hpp>
 #include <math.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <cmath>
 
 #include "common.h"
 #include "nms_internal.h"
@@ -28,6 +37,16 @@ static constexpr int kImgBits = 8;
 static constexpr int kRowBits = 24;
 static constexpr int64_t kMaxRows = (int64_t(1) << kRowBits);
 static constexpr int kMaxImg = 254;  // 255 marks a filtered-out row
+
+// JABD_NMS_DENSE=1 disables the grid producer (A/B tests and measurement).
+static bool nms_dense_only() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("JABD_NMS_DENSE");
+    v = e && e[0] == '1' ? 1 : 0;
+  }
+  return v == 1;
+}
 
 // Images per sort pass: <= 254 and the sort size must fit hipcub's int.
 static int64_t images_per_pass(int64_t batch, int64_t n) {
@@ -134,9 +153,10 @@ __device__ __forceinline__ bool iou_gt(float ix1, float iy1, float ix2, float iy
 __global__ __launch_bounds__(256) void nms_mask(
     const float4* __restrict__ sbox, const float* __restrict__ sarea,
     const int* __restrict__ counts, int64_t n, int64_t nb, double thr,
-    const int* __restrict__ nanflag, uint64_t* __restrict__ diag, int* __restrict__ nzcnt,
-    int* __restrict__ ent_cb, uint64_t* __restrict__ ent_bits) {
+    const int* __restrict__ nanflag, const int* __restrict__ dense, uint64_t* __restrict__ diag,
+    int* __restrict__ nzcnt, int* __restrict__ ent_cb, uint64_t* __restrict__ ent_bits) {
   const int b = blockIdx.z;
+  if (!dense[b]) return;  // this image's mask came from the grid path
   const int64_t rb = blockIdx.y;
   const int64_t cbg = (int64_t)blockIdx.x * kColBlocksPerWG;
   const int cnt = counts[b];
@@ -228,6 +248,257 @@ __global__ __launch_bounds__(256) void nms_mask(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Grid (candidate-pruned) mask.  For thr >= 0 a pair can only have IoU > t
+// if each axis has a 1-D IoU > t (IoU <= IoU_x, IoU_y), which needs
+//   * widths within a factor t (IoU_x <= w_min / w_max), heights alike, and
+//   * |dcx| < (w_i + w_j)(1 - t) / (2(1 + t)) <= f * max width, dcy alike
+//     (f = (1 - t)/(1 + t); 1-D overlap <= (w_i + w_j)/2 - |dcx|).
+// Boxes are binned by (log w, log h) classes of width W'/kK, W' >= 1.01 *
+// -ln(t), so such pairs are at most kK classes apart per axis, and per class
+// into cells of s_x = 1.05 f x the largest width of width classes c-kK..c+kK
+// (s_y alike), so their centres are at most one cell apart.  Each box tests
+// its own class (later ranks) and the "forward" half of its neighbour classes
+// in its 3x3 cell neighbourhood — every unordered pair exactly once — with
+// the same exact IoU comparison as the dense path.  Candidate boxes are read
+// from a copy in key order (cell runs are contiguous).  Inactive boxes (x2 <= x1,
+// y2 <= y1 or infinite area) can neither suppress nor be suppressed at
+// t >= 0 and are not binned.  An image falls back to the dense producer
+// (dense[b] != 0) if it has NaN boxes, a cell index beyond +-2^14, or more
+// off-block pairs than the workspace holds.
+// Key: image 8 | width class 10 | height class 10 | cell y 18 | cell x 18.
+// ---------------------------------------------------------------------------
+static constexpr int kNC = 1024;          // log-extent classes per axis
+static constexpr int kClassOff = 512;
+static constexpr int kCellOff = 1 << 17;  // 18-bit biased cell coordinates
+static constexpr int kCellLim = 1 << 14;
+static constexpr int64_t kPairsPerBox = 128;  // off-block pair capacity per box
+static constexpr int kK = 2;                  // class sub-division (neighbour range)
+
+__device__ __forceinline__ bool grid_active(float4 bx, float a) {
+  return bx.z > bx.x && bx.w > bx.y && a < INFINITY;
+}
+
+__device__ __forceinline__ int grid_class(float e, float inv_w) {
+  float c = floorf(logf(e) * inv_w);
+  c = fminf(fmaxf(c, (float)-kClassOff), (float)(kNC - 1 - kClassOff));
+  return (int)c + kClassOff;
+}
+
+// largest extent of classes c-kK..c+kK (ext = one axis' per-class maxima) x f
+__device__ __forceinline__ float grid_cell_size(const unsigned* ext, int c, float f) {
+  float e = 0.f;
+#pragma unroll
+  for (int d = -kK; d <= kK; ++d)
+    if (c + d >= 0 && c + d < kNC) e = fmaxf(e, __uint_as_float(ext[c + d]));
+  return e * f;
+}
+
+__device__ __forceinline__ uint64_t grid_key(int b, int cw, int ch, int y, int x) {
+  return ((uint64_t)b << 56) | ((uint64_t)cw << 46) | ((uint64_t)ch << 36) |
+         ((uint64_t)(y + kCellOff) << 18) | (uint64_t)(x + kCellOff);
+}
+
+// ext[b][0][cw] = largest width of width class cw, ext[b][1][ch] = largest height
+__global__ void grid_ext(const float4* __restrict__ sbox, const float* __restrict__ sarea,
+                         const int* __restrict__ counts, const int* __restrict__ nanflag,
+                         int64_t n, float inv_w, unsigned* __restrict__ ext,
+                         int* __restrict__ dense) {
+  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (r == 0 && nanflag[b]) atomicOr(&dense[b], 1);
+  if (r >= counts[b]) return;
+  const float4 bx = sbox[(int64_t)b * n + r];
+  const float a = sarea[(int64_t)b * n + r];
+  if (!grid_active(bx, a)) return;
+  const float w = bx.z - bx.x, h = bx.w - bx.y;
+  atomicMax(&ext[(int64_t)b * 2 * kNC + grid_class(w, inv_w)], __float_as_uint(w));
+  atomicMax(&ext[(int64_t)b * 2 * kNC + kNC + grid_class(h, inv_w)], __float_as_uint(h));
+}
+
+__global__ void grid_keys(const float4* __restrict__ sbox, const float* __restrict__ sarea,
+                          const int* __restrict__ counts, int64_t n, float inv_w, float fcell,
+                          const unsigned* __restrict__ ext, uint64_t* __restrict__ key,
+                          int* __restrict__ val, int* __restrict__ nact, int* __restrict__ dense) {
+  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (r >= n) return;
+  const int64_t o = (int64_t)b * n + r;
+  uint64_t k = ~0ull;
+  if (r < counts[b] && !(dense[b] & 1)) {
+    const float4 bx = sbox[o];
+    const float a = sarea[o];
+    if (grid_active(bx, a)) {
+      const int cw = grid_class(bx.z - bx.x, inv_w), ch = grid_class(bx.w - bx.y, inv_w);
+      const unsigned* e = ext + (int64_t)b * 2 * kNC;
+      const float sx = grid_cell_size(e, cw, fcell), sy = grid_cell_size(e + kNC, ch, fcell);
+      const float fx = floorf((bx.x + bx.z) * 0.5f / sx), fy = floorf((bx.y + bx.w) * 0.5f / sy);
+      if (fabsf(fx) < (float)kCellLim && fabsf(fy) < (float)kCellLim) {
+        k = grid_key(b, cw, ch, (int)fy, (int)fx);
+        atomicAdd(&nact[b], 1);
+      } else {
+        atomicOr(&dense[b], 2);
+      }
+    }
+  }
+  key[o] = k;
+  val[o] = (int)r;
+}
+
+// candidate data in key order: gbox[q] = sbox[rank sval[q]] (+ area)
+__global__ void grid_gather(const uint64_t* __restrict__ skey, const int* __restrict__ sval,
+                            int64_t total, const float4* __restrict__ sbox,
+                            const float* __restrict__ sarea, int64_t n, float4* __restrict__ gbox,
+                            float* __restrict__ garea) {
+  const int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (q >= total) return;
+  const uint64_t k = skey[q];
+  if (k == ~0ull) return;
+  const int64_t o = (int64_t)(k >> 56) * n + sval[q];
+  gbox[q] = sbox[o];
+  garea[q] = sarea[o];
+}
+
+__device__ __forceinline__ int64_t lower_bound_u64(const uint64_t* a, int64_t lo, int64_t hi,
+                                                   uint64_t v) {
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void grid_pairs(
+    const uint64_t* __restrict__ skey, const int* __restrict__ sval, int64_t total,
+    const float4* __restrict__ gbox, const float* __restrict__ garea, int64_t n, int bc,
+    float inv_w, float fcell, const unsigned* __restrict__ ext, const int* __restrict__ nact,
+    double thr, int64_t cap, int* __restrict__ dense, uint64_t* __restrict__ diag,
+    int* __restrict__ npairs, int* __restrict__ rowcnt, int* __restrict__ prow,
+    int* __restrict__ pcol, int* __restrict__ pslot) {
+  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  if (p >= total) return;
+  const uint64_t k = skey[p];
+  if (k == ~0ull) return;
+  const int b = (int)(k >> 56);
+  if (dense[b] & 3) return;
+  int64_t seg0 = 0;
+  for (int q = 0; q < b; ++q) seg0 += nact[q];
+  const int64_t seg1 = seg0 + nact[b];
+  const int i = sval[p];
+  const float4 bi = gbox[p];
+  const float ai = garea[p];
+  const int cw = (int)((k >> 46) & (kNC - 1)), ch = (int)((k >> 36) & (kNC - 1));
+  const unsigned* ew = ext + (int64_t)b * 2 * kNC;
+  const unsigned* eh = ew + kNC;
+  const float cx = (bi.x + bi.z) * 0.5f, cy = (bi.y + bi.w) * 0.5f;
+  const float thrf = (float)thr;
+  const uint64_t lt = (1ull << lane) - 1;
+
+  // Off-block pairs are buffered per lane and flushed in bursts: one counter
+  // atomic per wave reserves every lane's slots (ballot prefix sum), and the
+  // per-row slot atomics of a burst are issued back to back so their
+  // latencies overlap (a returning atomic per pair serialises the kernel).
+  constexpr int kBuf = 8;
+  int pr[kBuf], pc[kBuf], np = 0;
+  auto flush = [&]() {
+    const int lb = __builtin_amdgcn_readfirstlane(b);
+    const bool mine = b == lb;
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int bit = 0; bit < 4; ++bit) {
+      const uint64_t mb = __ballot(mine && ((np >> bit) & 1));
+      pre += __popcll(mb & lt) << bit;
+      tot += __popcll(mb) << bit;
+    }
+    int base = 0;
+    if (tot) {
+      const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
+      if (lane == leader) base = atomicAdd(&npairs[lb], tot);
+      base = __shfl(base, leader) + pre;
+    }
+    if (!mine && np) base = atomicAdd(&npairs[b], np);  // wave spans two images
+    int ps[kBuf];
+#pragma unroll
+    for (int q = 0; q < kBuf; ++q)
+      if (q < np && base + q < cap) ps[q] = atomicAdd(&rowcnt[(int64_t)b * n + pr[q]], 1);
+#pragma unroll
+    for (int q = 0; q < kBuf; ++q) {
+      if (q < np) {
+        if (base + q < cap) {
+          const int64_t o = (int64_t)b * cap + base + q;
+          prow[o] = pr[q];
+          pcol[o] = pc[q];
+          pslot[o] = ps[q];
+        } else {
+          atomicOr(&dense[b], 4);
+        }
+      }
+    }
+    np = 0;
+  };
+
+  // own class, then the forward half of the neighbour classes:
+  // (0, 1..kK) and (1..kK, -kK..kK)
+  constexpr int NNB = kK + kK * (2 * kK + 1);
+  for (int nbr = 0; nbr <= NNB; ++nbr) {
+    int cw2, ch2;
+    if (nbr <= kK) {
+      cw2 = cw;
+      ch2 = ch + nbr;
+    } else {
+      const int q2 = nbr - kK - 1;
+      cw2 = cw + 1 + q2 / (2 * kK + 1);
+      ch2 = ch - kK + q2 % (2 * kK + 1);
+    }
+    if (cw2 >= kNC || ch2 < 0 || ch2 >= kNC || ew[cw2] == 0u || eh[ch2] == 0u) continue;
+    const float sx = grid_cell_size(ew, cw2, fcell), sy = grid_cell_size(eh, ch2, fcell);
+    const float fx = floorf(cx / sx), fy = floorf(cy / sy);
+    if (fabsf(fx) > (float)(kCellLim + 1) || fabsf(fy) > (float)(kCellLim + 1)) continue;
+    const int X = (int)fx, Y = (int)fy;
+    for (int dy = -1; dy <= 1; ++dy) {
+      const uint64_t lo = grid_key(b, cw2, ch2, Y + dy, X - 1);
+      const uint64_t hi = grid_key(b, cw2, ch2, Y + dy, X + 1);
+      for (int64_t q = lower_bound_u64(skey, seg0, seg1, lo); q < seg1 && skey[q] <= hi; ++q) {
+        const int j = sval[q];
+        // same class: each pair once, from the lower rank
+        bool hit = !(nbr == 0 && j <= i);
+        if (hit) hit = iou_gt(bi.x, bi.y, bi.z, bi.w, ai, gbox[q], garea[q], thr, thrf, true);
+        if (hit) {
+          const int row = i < j ? i : j, col = i < j ? j : i;
+          if ((row >> 6) == (col >> 6)) {
+            atomicOr((unsigned long long*)&diag[(int64_t)b * n + row],
+                     (unsigned long long)1 << (col & 63));
+          } else {
+#pragma unroll
+            for (int t2 = 0; t2 < kBuf; ++t2)
+              if (t2 == np) {
+                pr[t2] = row;
+                pc[t2] = col;
+              }
+            ++np;
+          }
+        }
+        if (__ballot(np == kBuf)) flush();
+      }
+    }
+  }
+  flush();
+}
+
+// CSR of each row's off-block columns: csr[rowoff[row] + slot] = col.
+__global__ void grid_scatter(const int* __restrict__ npairs, const int* __restrict__ dense,
+                             int64_t cap, int64_t n, const int* __restrict__ prow,
+                             const int* __restrict__ pcol, const int* __restrict__ pslot,
+                             const int* __restrict__ rowoff, int* __restrict__ csr) {
+  const int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (dense[b] || s >= cap || s >= npairs[b]) return;
+  const int64_t o = (int64_t)b * cap + s;
+  csr[rowoff[(int64_t)b * n + prow[o]] + pslot[o]] = pcol[o];
+}
+
 // One workgroup per image walks the row blocks in rank order.  Block c's
 // suppressed-set word comes from LDS; wave 0 resolves the block (only rows
 // with in-block suppressions need the ordered pass); then every kept row
@@ -238,6 +509,8 @@ static constexpr int kPrefetchEnt = 4;  // list entries per row prefetched (256 
 __global__ __launch_bounds__(256) void nms_scan(
     const uint64_t* __restrict__ diag, const int* __restrict__ nzcnt,
     const int* __restrict__ ent_cb, const uint64_t* __restrict__ ent_bits,
+    const int* __restrict__ dense, const int* __restrict__ rowcnt, const int* __restrict__ rowoff,
+    const int* __restrict__ csr,
     const int* __restrict__ sidx, const int* __restrict__ counts, int64_t n, int64_t nb, int img0,
     int64_t* __restrict__ keep, int64_t keep_bstride, int64_t* __restrict__ n_keep) {
   extern __shared__ unsigned long long removed[];
@@ -250,7 +523,9 @@ __global__ __launch_bounds__(256) void nms_scan(
   for (int64_t w = tid; w < nbv; w += blockDim.x) removed[w] = 0;
   if (tid == 0) s_nkeep = 0;
   const uint64_t* dimg = diag + (int64_t)b * n;
-  const int* cimg = nzcnt + (int64_t)b * n;
+  const bool dn = dense[b] != 0;  // mask lists: dense (cb, bits) entries or grid CSR columns
+  const int* cimg = (dn ? nzcnt : rowcnt) + (int64_t)b * n;
+  const int* oimg = rowoff + (int64_t)b * n;
   const int64_t ebase = (int64_t)b * ent_base(nb, nb);
   const int* sid = sidx + (int64_t)b * n;
   int64_t* kout = keep + (int64_t)(b + img0) * keep_bstride;
@@ -263,9 +538,15 @@ __global__ __launch_bounds__(256) void nms_scan(
       pcnt = cimg[r];
       if (e == 0) pdiag = dimg[r];
       if (e < pcnt) {
-        const int64_t off = ebase + ent_base(c, nb) + (int64_t)lane * (nb - c - 1) + e;
-        pcb = ent_cb[off];
-        pbits = ent_bits[off];
+        if (dn) {
+          const int64_t off = ebase + ent_base(c, nb) + (int64_t)lane * (nb - c - 1) + e;
+          pcb = ent_cb[off];
+          pbits = ent_bits[off];
+        } else {
+          const int col = csr[oimg[r] + e];
+          pcb = col >> 6;
+          pbits = (uint64_t)1 << (col & 63);
+        }
       }
     }
   };
@@ -306,10 +587,18 @@ __global__ __launch_bounds__(256) void nms_scan(
     const uint64_t kept = s_kept;
     if ((kept >> lane) & 1) {
       if (e < pcnt) atomicOr(&removed[pcb], (unsigned long long)pbits);
-      if (e == 0 && pcnt > kPrefetchEnt) {  // long lists: rare slow path
-        const int64_t off = ebase + ent_base(c, nb) + (int64_t)lane * (nb - c - 1);
-        for (int q = kPrefetchEnt; q < pcnt; ++q)
-          atomicOr(&removed[ent_cb[off + q]], (unsigned long long)ent_bits[off + q]);
+      if (pcnt > kPrefetchEnt) {  // long lists: the row's 4 threads share the rest
+        if (dn) {
+          const int64_t off = ebase + ent_base(c, nb) + (int64_t)lane * (nb - c - 1);
+          for (int q = kPrefetchEnt + e; q < pcnt; q += kPrefetchEnt)
+            atomicOr(&removed[ent_cb[off + q]], (unsigned long long)ent_bits[off + q]);
+        } else {
+          const int* lst = csr + oimg[c * 64 + lane];
+          for (int q = kPrefetchEnt + e; q < pcnt; q += kPrefetchEnt) {
+            const int col = lst[q];
+            atomicOr(&removed[col >> 6], 1ull << (col & 63));
+          }
+        }
       }
     }
     prefetch(c + 1, pdiag, pcnt, pcb, pbits);
@@ -323,30 +612,83 @@ static size_t sort_temp_bytes(int64_t items) {
   size_t bytes = 0;
   (void)hipcub::DeviceRadixSort::SortKeys(nullptr, bytes, (const uint64_t*)nullptr,
                                     (uint64_t*)nullptr, (int)items, 0, 64, (hipStream_t)0);
-  return bytes;
+  size_t b2 = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b2, (const uint64_t*)nullptr,
+                                           (uint64_t*)nullptr, (const int*)nullptr, (int*)nullptr,
+                                           (int)items, 0, 64, (hipStream_t)0);
+  size_t b3 = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b3, (const int*)nullptr, (int*)nullptr,
+                                         (int)items, (hipStream_t)0);
+  return std::max(bytes, std::max(b2, b3));
 }
 
+struct NmsWs {
+  uint64_t *kin, *kout;
+  char* tmp;
+  size_t tmp_bytes;
+  float4* sbox;
+  float* sarea;
+  int *sidx, *counts, *nanflag;
+  uint64_t* diag;
+  int* nzcnt;
+  int* ent_cb;
+  uint64_t* ent_bits;
+  // grid path
+  unsigned* ext;
+  int *dense, *nact, *npairs, *gval_in, *gval_out, *rowcnt, *rowoff, *prow, *pcol, *pslot, *csr;
+  float4* gbox;
+  float* garea;
+  int64_t cap;
+};
+
 template <typename A>
-static void carve_nms(A& a, int64_t batch, int64_t n) {
-  int64_t bc = images_per_pass(batch, n);
-  int64_t nb = cdiv(n, 64);
-  a.template take<uint64_t>(bc * n);       // keys in
-  a.template take<uint64_t>(bc * n);       // keys out
-  a.template take<char>(sort_temp_bytes(bc * n));
-  a.template take<float4>(bc * n);         // sorted boxes
-  a.template take<float>(bc * n);          // sorted areas
-  a.template take<int>(bc * n);            // sorted row ids
-  a.template take<int>(bc);                // counts
-  a.template take<int>(bc);                // NaN-box flags
-  a.template take<uint64_t>(bc * n);       // diag words
-  a.template take<int>(bc * n);            // list lengths
-  a.template take<int>(bc * 64 * (nb * (nb - 1) / 2 + 1));       // list column blocks
-  a.template take<uint64_t>(bc * 64 * (nb * (nb - 1) / 2 + 1));  // list bit words
+static void carve_nms(A& a, int64_t batch, int64_t n, NmsWs* w) {
+  const int64_t bc = images_per_pass(batch, n);
+  const int64_t nb = cdiv(n, 64);
+  const int64_t ents = bc * 64 * (nb * (nb - 1) / 2 + 1);
+  const int64_t cap = kPairsPerBox * (n > 0 ? n : 1);
+  const size_t tb = sort_temp_bytes(bc * n);
+#define T(type, cnt, field)                        \
+  do {                                             \
+    auto* ptr_ = a.template take<type>(cnt);       \
+    if (w) w->field = reinterpret_cast<decltype(w->field)>(ptr_); \
+  } while (0)
+  T(uint64_t, bc * n, kin);     // keys in (also the grid keys)
+  T(uint64_t, bc * n, kout);    // keys out (also the sorted grid keys)
+  T(char, tb, tmp);
+  T(float4, bc * n, sbox);
+  T(float, bc * n, sarea);
+  T(int, bc * n, sidx);
+  T(int, bc, counts);
+  T(int, bc, nanflag);
+  T(uint64_t, bc * n, diag);
+  T(int, bc * n, nzcnt);
+  T(int, ents, ent_cb);
+  T(uint64_t, ents, ent_bits);
+  T(unsigned, bc * 2 * kNC, ext);
+  T(int, bc, dense);
+  T(int, bc, nact);
+  T(int, bc, npairs);
+  T(int, bc * n, gval_in);
+  T(int, bc * n, gval_out);
+  T(int, bc * n, rowcnt);
+  T(int, bc * n, rowoff);
+  T(int, bc * cap, prow);
+  T(int, bc * cap, pcol);
+  T(int, bc * cap, pslot);
+  T(int, bc * cap, csr);
+  T(float4, bc * n, gbox);
+  T(float, bc * n, garea);
+#undef T
+  if (w) {
+    w->tmp_bytes = tb;
+    w->cap = cap;
+  }
 }
 
 size_t nms_ws_bytes(int64_t batch, int64_t n) {
   Sizer s;
-  carve_nms(s, batch, n);
+  carve_nms(s, batch, n, (NmsWs*)nullptr);
   return s.used;
 }
 
@@ -369,49 +711,78 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
                nms_ws_bytes(batch, n));
   const int filter = score_thr > -INFINITY ? 1 : 0;
   const int64_t per_pass = images_per_pass(batch, n);
+  // log-area class width W' >= 1.01 * -ln(thr) (wider is always safe)
+  const bool grid = iou_thr >= 0.0 && !nms_dense_only();
+  double wcls = iou_thr > 0.0 ? 1.01 * -std::log(iou_thr) : INFINITY;
+  if (wcls < 0.2) wcls = 0.2;  // wider classes are always safe; keeps ln-range / W' < kNC
+  wcls /= kK;
+  const float inv_w = std::isinf(wcls) ? 0.f : (float)(1.0 / wcls);
+  // cell scale f = (1 - t) / (1 + t) (>= 0.05), with a 5% rounding margin
+  const double tcl = iou_thr > 0.0 ? std::min(iou_thr, 1.0) : 0.0;
+  const float fcell = (float)(1.05 * std::max((1.0 - tcl) / (1.0 + tcl), 0.05));
   for (int64_t img0 = 0; img0 < batch; img0 += per_pass) {
     const int bc = (int)min(per_pass, batch - img0);
     Carve cv(ws, ws_bytes);
-    uint64_t* kin = cv.take<uint64_t>((size_t)bc * n);
-    uint64_t* kout = cv.take<uint64_t>((size_t)bc * n);
-    size_t tmp_bytes = sort_temp_bytes((int64_t)bc * n);
-    char* tmp = cv.take<char>(tmp_bytes);
-    float4* sbox = cv.take<float4>((size_t)bc * n);
-    float* sarea = cv.take<float>((size_t)bc * n);
-    int* sidx = cv.take<int>((size_t)bc * n);
-    int* counts = cv.take<int>(bc);
-    int* nanflag = cv.take<int>(bc);
-    uint64_t* diag = cv.take<uint64_t>((size_t)bc * n);
-    int* nzcnt = cv.take<int>((size_t)bc * n);
-    int* ent_cb = cv.take<int>((size_t)bc * 64 * (nb * (nb - 1) / 2 + 1));
-    uint64_t* ent_bits = cv.take<uint64_t>((size_t)bc * 64 * (nb * (nb - 1) / 2 + 1));
+    NmsWs w;
+    carve_nms(cv, bc, n, &w);
     if (!cv.ok()) {
       set_error("nms: workspace carve overflow");
       return JABD_EWS;
     }
-    JABD_HIP(hipMemsetAsync(counts, 0, sizeof(int) * bc, st));
-    JABD_HIP(hipMemsetAsync(nanflag, 0, sizeof(int) * bc, st));
-    JABD_HIP(hipMemsetAsync(nzcnt, 0, sizeof(int) * bc * n, st));
+    JABD_HIP(hipMemsetAsync(w.counts, 0, sizeof(int) * bc, st));
+    JABD_HIP(hipMemsetAsync(w.nanflag, 0, sizeof(int) * bc, st));
+    JABD_HIP(hipMemsetAsync(w.nzcnt, 0, sizeof(int) * bc * n, st));
     dim3 g1((unsigned)cdiv(n, 256), bc);
     nms_keys<<<g1, 256, 0, st>>>(scores, score_stride, score_bstride, n_valid, n, bc,
-                                  score_thr, filter, (int)img0, kin, counts);
+                                  score_thr, filter, (int)img0, w.kin, w.counts);
     if (int e = check_launch("nms_keys")) return e;
-    JABD_HIP(hipcub::DeviceRadixSort::SortKeys(tmp, tmp_bytes, kin, kout, (int)(bc * n), 0,
-                                               64, st));
+    JABD_HIP(hipcub::DeviceRadixSort::SortKeys(w.tmp, w.tmp_bytes, w.kin, w.kout, (int)(bc * n),
+                                               0, 64, st));
     nms_gather<<<(unsigned)cdiv((int64_t)bc * n, 256), 256, 0, st>>>(
-        kout, (int64_t)bc * n, boxes, box_stride, box_bstride, counts, bc, n, (int)img0,
-        sbox, sarea, sidx, nanflag);
+        w.kout, (int64_t)bc * n, boxes, box_stride, box_bstride, w.counts, bc, n, (int)img0,
+        w.sbox, w.sarea, w.sidx, w.nanflag);
     if (int e = check_launch("nms_gather")) return e;
+    if (grid) {
+      JABD_HIP(hipMemsetAsync(w.dense, 0, sizeof(int) * bc, st));
+      JABD_HIP(hipMemsetAsync(w.nact, 0, sizeof(int) * bc, st));
+      JABD_HIP(hipMemsetAsync(w.npairs, 0, sizeof(int) * bc, st));
+      JABD_HIP(hipMemsetAsync(w.ext, 0, sizeof(unsigned) * bc * 2 * kNC, st));
+      JABD_HIP(hipMemsetAsync(w.diag, 0, sizeof(uint64_t) * bc * n, st));
+      JABD_HIP(hipMemsetAsync(w.rowcnt, 0, sizeof(int) * bc * n, st));
+      grid_ext<<<g1, 256, 0, st>>>(w.sbox, w.sarea, w.counts, w.nanflag, n, inv_w, w.ext, w.dense);
+      if (int e = check_launch("grid_ext")) return e;
+      grid_keys<<<g1, 256, 0, st>>>(w.sbox, w.sarea, w.counts, n, inv_w, fcell, w.ext, w.kin,
+                                     w.gval_in, w.nact, w.dense);
+      if (int e = check_launch("grid_keys")) return e;
+      JABD_HIP(hipcub::DeviceRadixSort::SortPairs(w.tmp, w.tmp_bytes, w.kin, w.kout, w.gval_in,
+                                                  w.gval_out, (int)(bc * n), 0, 64, st));
+      grid_gather<<<(unsigned)cdiv((int64_t)bc * n, 256), 256, 0, st>>>(
+          w.kout, w.gval_out, (int64_t)bc * n, w.sbox, w.sarea, n, w.gbox, w.garea);
+      if (int e = check_launch("grid_gather")) return e;
+      grid_pairs<<<(unsigned)cdiv((int64_t)bc * n, 256), 256, 0, st>>>(
+          w.kout, w.gval_out, (int64_t)bc * n, w.gbox, w.garea, n, bc, inv_w, fcell, w.ext, w.nact,
+          iou_thr, w.cap, w.dense, w.diag, w.npairs, w.rowcnt, w.prow, w.pcol, w.pslot);
+      if (int e = check_launch("grid_pairs")) return e;
+      JABD_HIP(hipcub::DeviceScan::ExclusiveSum(w.tmp, w.tmp_bytes, w.rowcnt, w.rowoff,
+                                                (int)(bc * n), st));
+      dim3 gs((unsigned)cdiv(w.cap, 256), bc);
+      grid_scatter<<<gs, 256, 0, st>>>(w.npairs, w.dense, w.cap, n, w.prow, w.pcol, w.pslot,
+                                       w.rowoff, w.csr);
+      if (int e = check_launch("grid_scatter")) return e;
+    } else {
+      JABD_HIP(hipMemsetD32Async((hipDeviceptr_t)w.dense, 1, bc, st));
+    }
     dim3 g2((unsigned)cdiv(nb, kColBlocksPerWG), (unsigned)nb, (unsigned)bc);
-    nms_mask<<<g2, 256, 0, st>>>(sbox, sarea, counts, n, nb, iou_thr, nanflag, diag, nzcnt,
-                                 ent_cb, ent_bits);
+    nms_mask<<<g2, 256, 0, st>>>(w.sbox, w.sarea, w.counts, n, nb, iou_thr, w.nanflag, w.dense,
+                                 w.diag, w.nzcnt, w.ent_cb, w.ent_bits);
     if (int e = check_launch("nms_mask")) return e;
     if (nb * sizeof(uint64_t) > 64 * 1024) {
       JABD_HIP(hipFuncSetAttribute((const void*)nms_scan,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     }
-    nms_scan<<<bc, 256, nb * sizeof(uint64_t), st>>>(diag, nzcnt, ent_cb, ent_bits, sidx, counts,
-                                                      n, nb, (int)img0, keep, n, n_keep);
+    nms_scan<<<bc, 256, nb * sizeof(uint64_t), st>>>(
+        w.diag, w.nzcnt, w.ent_cb, w.ent_bits, w.dense, w.rowcnt, w.rowoff, w.csr, w.sidx,
+        w.counts, n, nb, (int)img0, keep, n, n_keep);
     if (int e = check_launch("nms_scan")) return e;
   }
   return JABD_OK;

@@ -76,6 +76,8 @@ def test_golden_decode_hip(cuda):
     pri = box_ref.anchors(CFG, (128, 128)).to(cuda)
     loc = torch.from_numpy(G["loss_loc"][0]).to(cuda)
     landm = torch.from_numpy(G["loss_landm"][0]).to(cuda)
-    np.testing.assert_array_equal(ops.decode(loc, pri, [0.1, 0.2]).cpu().numpy(), G["decode_boxes"])
+    # exp() may differ by an ulp between HIP and the CPU library (as in test_decode_parity)
+    np.testing.assert_allclose(ops.decode(loc, pri, [0.1, 0.2]).cpu().numpy(), G["decode_boxes"],
+                               rtol=1e-6, atol=1e-7)
     np.testing.assert_array_equal(ops.decode_landm(landm, pri, [0.1, 0.2]).cpu().numpy(),
                                   G["decode_landms"])
