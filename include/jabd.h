@@ -177,9 +177,16 @@ typedef struct jabd_conv_args {
                              input ((oh+pad-kh)/stride, (ow+pad-kw)/stride) */
   int32_t flags, reserved1; /* library-internal */
   int64_t M; /* filled in by the library */
+  /* optional second packing for the 32x32x2-MFMA 1x1 kernel (nullable):
+   * float4 [ceil(K/32)*4][ntiles32][64], each float4 holding
+   * W[8*k8 + 4*(lane>>5) + e][32*nt + (lane&31)], e = 0..3; tn32 tiles per
+   * workgroup (jabd_conv_pack_tn32), ntiles32 a multiple of tn32. */
+  const void* w32; int32_t ntiles32, tn32;
 } jabd_conv_args;
 /* N-tiles (16 output channels each) grouped per workgroup for a Cout. */
 int jabd_conv_pack_tn(int cout);
+/* 32-channel N-tiles per workgroup of the 32x32x2 1x1 kernel for a Cout. */
+int jabd_conv_pack_tn32(int cout);
 int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t stream);
 
 /* A1 MobileNetV3 stem — nets/mobilenetV3.py:455-457,511: conv3x3/s2/p1 3->16

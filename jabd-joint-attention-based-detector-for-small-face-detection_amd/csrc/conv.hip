@@ -498,6 +498,24 @@ static bool conv_generic_only() {
   return v == 1;
 }
 
+namespace jabd {
+int conv1x1_m32_dispatch(const ConvArgs& a, hipStream_t st);
+}
+
+// Which 1x1 kernel: the 32x32x2 LDS-weight kernel (conv32.hip) pays off when
+// the GEMM is compute-heavy.  JABD_CONV32=0 / 1 forces it off / on (A/B).
+static bool use_conv32(const ConvArgs& a) {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("JABD_CONV32");
+    v = e && e[0] == '0' ? 0 : (e && e[0] == '1' ? 1 : -1);
+  }
+  if (!a.w32 || a.tn32 <= 0 || a.ntiles32 % a.tn32 || a.ntiles32 * 32 < a.Cout) return false;
+  if (v >= 0) return v == 1;
+  const int K = a.Cin + (a.x2 ? a.Cin2 : 0);
+  return a.Cout >= 96 && K >= 96;
+}
+
 extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t stream) {
   JABD_REQUIRE(args, "conv: null args");
   ConvArgs a = *args;
@@ -549,6 +567,10 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
                                   : (a.x2_stride > 1 && a.x2_bs % a.x2_ps == 0 &&
                                      a.x2_bs * a.B < ((int64_t)1 << 31)))) &&
       (a.M + 64) * (maxps + 16) < ((int64_t)1 << 31) && !conv_generic_only();
+  if (fast1x1 && use_conv32(a)) {
+    const int r = conv1x1_m32_dispatch(a, st);
+    if (r >= 0) return r;
+  }
   if (fast1x1) {
     switch (tn) {
       case 1: return launch_1x1<4, 1>(a, st);

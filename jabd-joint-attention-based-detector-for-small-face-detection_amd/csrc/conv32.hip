@@ -1,0 +1,283 @@
+// 1x1 stride-1 convolutions (A1 project/expand convs, A4 FPN laterals, A5
+// ResNet 1x1s) on the 32x32x2 fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+//   Y[m, n] = act( sum_k X[m, k] * W[k, n] + bias[n] (+ R[m, n]) )
+//
+// Why a second GEMM kernel next to conv.hip's 16x16x4 one: the 32x32 tile
+// does 2x the FLOPs per operand register, so a wave's 64-pixel x 128-channel
+// tile needs 6 float4 operands per 8 k (16x16x4: 12), and the weights of a
+// K stage are staged ONCE per workgroup in LDS (shared by the 4 waves)
+// instead of being re-read from L2 by every wave.  This serves the
+// compute-heavy layers (K >= ~100, Cout >= ~96), where conv.hip sat at
+// 30-45% of the fp32 MFMA peak.
+//
+// Operand mapping (swapped, as conv.hip): MFMA A = weights (row i = output
+// channel), MFMA B = pixels (column j = pixel), so lane l ends up holding, for
+// pixel j = l & 31, the channels 8*(r>>2) + 4*(l>>5) + (r&3): four float4
+// runs of 4 consecutive channels.  The MFMA contracts k over the lane half
+// (l >> 5); each lane loads a float4 of 4 consecutive channels and feeds
+// component e to MFMA e, so within an 8-channel group the logical k order is
+// (4h + e).  Weights are pre-packed in exactly that order (PackedConv.w32):
+//   w32[k8][nt][lane] = float4{ W[8k8 + 4(lane>>5) + e][32nt + (lane&31)] }.
+// One K stage is BK = 32 channels = 4 groups.
+//
+// Fusions: ECA gate (per-(image, input channel) scale) folded into the
+// weights while staging them (a workgroup's pixels lie in one image);
+// K-concatenated second source (MNv3 skip / ResNet downsample); bias;
+// residual; activation; channel-offset / strided output.
+#include <stdlib.h>
+
+#include <algorithm>
+
+#include "common.h"
+#include "conv_args.h"
+
+namespace jabd {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float act32(float v, int act, float slope) {
+  switch (act) {
+    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_LEAKY: return v > 0.f ? v : v * slope;
+    case ACT_HSWISH: return v * fminf(fmaxf(v + 3.f, 0.f), 6.f) * (1.f / 6.f);
+    case ACT_HSIGMOID: return fminf(fmaxf(v + 3.f, 0.f), 6.f) * (1.f / 6.f);
+    case ACT_SIGMOID: return 1.f / (1.f + expf(-v));
+    default: return v;
+  }
+}
+
+constexpr int kBK = 32;          // K channels per stage
+constexpr int kG = kBK / 8;      // 8-channel groups per stage
+
+// Workgroup = 4 waves stacked along M (BM = 128*TM pixels) x BN = 32*TN
+// channels.  Tiles never straddle an image when `per_img` (ECA gate folded
+// into the staged weights), else M is tiled flat.
+template <int TM, int TN>
+__global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, int mtiles_img,
+                                                             int per_img) {
+  constexpr int BM = 4 * 32 * TM;
+  constexpr int NB4 = kG * TN * 64;            // float4 of one weight stage
+  constexpr int NBT = (NB4 + 255) / 256;       // ... per thread
+  __shared__ float4 sB[2][NB4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = lane >> 5, j = lane & 31;
+  const int nblk_n = p.Ntiles / TN;  // Ntiles counts 32-channel tiles here
+  const int bid = blockIdx.x;
+  const int nb = bid % nblk_n, mb = bid / nblk_n;
+  const int OHW = p.OH * p.OW;
+  const int M = (int)p.M;
+  int img = 0, m_lo, m_hi;
+  if (per_img) {
+    img = mb / mtiles_img;
+    m_lo = img * OHW + (mb - img * mtiles_img) * BM;
+    m_hi = min(img * OHW + OHW, M);
+  } else {
+    m_lo = mb * BM;
+    m_hi = M;
+  }
+  int pm[TM];
+#pragma unroll
+  for (int t = 0; t < TM; ++t) {
+    const int m = m_lo + wave * 32 * TM + t * 32 + j;
+    pm[t] = m < m_hi ? m : -1;
+  }
+  const int Kt = p.Cin + (p.x2 ? p.Cin2 : 0);
+  const int S = (Kt + kBK - 1) / kBK;
+  const int x2_pix = (p.x2 && p.x2_stride != 1) ? (int)(p.x2_bs / p.x2_ps) : 0;
+  const float4* wg = reinterpret_cast<const float4*>(p.w);
+  const float* sc = p.ascale ? p.ascale + (int64_t)img * p.ascale_bs : nullptr;
+
+  auto load_a = [&](int s, float4 (&a)[TM][kG]) {
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int q = 0; q < kG; ++q) {
+        const int k4 = s * kBK + 8 * q + 4 * h;
+        const int m = pm[t];
+        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m >= 0) {
+          if (k4 < p.Cin) {
+            r = *reinterpret_cast<const float4*>(p.x + (int64_t)m * p.x_ps + p.x_c0 + k4);
+          } else if (k4 < Kt) {
+            int qq = m;
+            if (p.x2_stride != 1) {
+              const int b = m / OHW, rr = m - b * OHW;
+              const int oh = rr / p.OW, ow = rr - oh * p.OW;
+              qq = b * x2_pix + (oh * p.x2_stride) * p.x2_W + ow * p.x2_stride;
+            }
+            r = *reinterpret_cast<const float4*>(p.x2 + (int64_t)qq * p.x2_ps + (k4 - p.Cin));
+          }
+        }
+        a[t][q] = r;
+      }
+  };
+  // weight stage s -> registers (ECA gate applied to the rows k < Cin)
+  auto load_b = [&](int s, float4 (&b)[NBT]) {
+#pragma unroll
+    for (int i = 0; i < NBT; ++i) {
+      const int f = i * 256 + threadIdx.x;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (f < NB4) {
+        const int g = f / (TN * 64), rem = f - g * (TN * 64);
+        const int u = rem >> 6, l = rem & 63;
+        const int k8 = s * kG + g;
+        v = wg[((int64_t)k8 * p.Ntiles + nb * TN + u) * 64 + l];
+        if (sc) {
+          const int k0 = 8 * k8 + 4 * (l >> 5);
+          if (k0 < p.Cin) {
+            const float4 s4 = *reinterpret_cast<const float4*>(sc + k0);
+            v.x *= s4.x; v.y *= s4.y; v.z *= s4.z; v.w *= s4.w;
+          }
+        }
+      }
+      b[i] = v;
+    }
+  };
+  auto store_b = [&](int buf, const float4 (&b)[NBT]) {
+#pragma unroll
+    for (int i = 0; i < NBT; ++i) {
+      const int f = i * 256 + threadIdx.x;
+      if (f < NB4) sB[buf][f] = b[i];
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int u = 0; u < TN; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
+
+  float4 a_cur[TM][kG], a_nxt[TM][kG], b_nxt[NBT];
+  load_a(0, a_cur);
+  load_b(0, b_nxt);
+  store_b(0, b_nxt);
+  __syncthreads();
+  for (int s = 0; s < S; ++s) {
+    const bool more = s + 1 < S;
+    if (more) {
+      load_a(s + 1, a_nxt);
+      load_b(s + 1, b_nxt);
+    }
+    const float4* bs = sB[s & 1];
+#pragma unroll
+    for (int q = 0; q < kG; ++q) {
+      float4 bw[TN];
+#pragma unroll
+      for (int u = 0; u < TN; ++u) bw[u] = bs[(q * TN + u) * 64 + lane];
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int u = 0; u < TN; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(bw[u].x, a_cur[t][q].x, acc[t][u], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int u = 0; u < TN; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(bw[u].y, a_cur[t][q].y, acc[t][u], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int u = 0; u < TN; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(bw[u].z, a_cur[t][q].z, acc[t][u], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int u = 0; u < TN; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(bw[u].w, a_cur[t][q].w, acc[t][u], 0, 0, 0);
+    }
+    if (more) {
+      store_b((s + 1) & 1, b_nxt);
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int q = 0; q < kG; ++q) a_cur[t][q] = a_nxt[t][q];
+    }
+    __syncthreads();
+  }
+
+  // epilogue: acc[t][u][4c + e] = Y[pixel pm[t]][nb*BN + 32u + 8c + 4h + e]
+#pragma unroll
+  for (int t = 0; t < TM; ++t) {
+    const int m = pm[t];
+    if (m < 0) continue;
+    float* yrow = p.y + (int64_t)m * p.y_ps + p.y_c0;
+    const float* rrow = p.res ? p.res + (int64_t)m * p.res_ps + p.res_c0 : nullptr;
+#pragma unroll
+    for (int u = 0; u < TN; ++u)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int n = (nb * TN + u) * 32 + 8 * c + 4 * h;
+        if (n >= p.Cout) continue;
+        float4 v = make_float4(acc[t][u][4 * c], acc[t][u][4 * c + 1], acc[t][u][4 * c + 2],
+                               acc[t][u][4 * c + 3]);
+        if (p.bias) {
+          const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
+          v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
+        }
+        if (rrow) {
+          const float4 rr = *reinterpret_cast<const float4*>(rrow + n);
+          v.x += rr.x; v.y += rr.y; v.z += rr.z; v.w += rr.w;
+        }
+        v.x = act32(v.x, p.act, p.slope);
+        v.y = act32(v.y, p.act, p.slope);
+        v.z = act32(v.z, p.act, p.slope);
+        v.w = act32(v.w, p.act, p.slope);
+        *reinterpret_cast<float4*>(yrow + n) = v;
+      }
+  }
+}
+
+template <int TM, int TN>
+static int launch_m32(const ConvArgs& a, hipStream_t st) {
+  constexpr int BM = 4 * 32 * TM;
+  const int64_t OHW = (int64_t)a.OH * a.OW;
+  const int per_img = a.ascale != nullptr;
+  const int64_t mt_img = cdiv(OHW, BM);
+  const int64_t mtiles = per_img ? mt_img * a.B : cdiv(a.M, BM);
+  const int64_t grid = mtiles * (a.Ntiles / TN);
+  JABD_REQUIRE(grid < (int64_t)0x7fffffff, "conv32: grid too large");
+  conv1x1_m32_kernel<TM, TN><<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, per_img);
+  return check_launch("conv1x1_m32");
+}
+
+}  // namespace jabd
+
+using namespace jabd;
+
+// N-tiles (32 output channels each) per workgroup for the 32x32 kernel.
+// Prefers a 64x128 wave tile (TM=2, TN<=4), else the exact-fit wide tile.
+extern "C" int jabd_conv_pack_tn32(int cout) {
+  const int nt = (cout + 31) / 32;
+  if (nt <= 4) return nt;
+  if (nt % 4 == 0) return 4;
+  int best = 4, waste = (nt + 3) / 4 * 4 - nt;
+  for (int tn : {5, 6, 7}) {
+    const int w = (nt + tn - 1) / tn * tn - nt;
+    if (w < waste) { waste = w; best = tn; }
+  }
+  return best;
+}
+
+namespace jabd {
+// Called by jabd_conv2d_nhwc_f32 for 1x1 / stride-1 convs when the caller
+// supplied the 32x32 packing (args->w32).  Returns -1 when this kernel does
+// not take the shape (the caller then uses conv.hip).
+int conv1x1_m32_dispatch(const ConvArgs& a0, hipStream_t st) {
+  ConvArgs a = a0;
+  a.w = a0.w32;
+  a.Ntiles = a0.ntiles32;
+  switch (a0.tn32) {
+    case 1: return launch_m32<2, 1>(a, st);
+    case 2: return launch_m32<2, 2>(a, st);
+    case 3: return launch_m32<2, 3>(a, st);
+    case 4: return launch_m32<2, 4>(a, st);
+    case 5: return launch_m32<1, 5>(a, st);
+    case 6: return launch_m32<1, 6>(a, st);
+    case 7: return launch_m32<1, 7>(a, st);
+    default: return -1;
+  }
+}
+}  // namespace jabd

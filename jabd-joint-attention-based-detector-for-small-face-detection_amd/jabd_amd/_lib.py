@@ -48,6 +48,7 @@ class ConvArgs(ctypes.Structure):
         ("nchw_in", c_i32), ("tconv", c_i32),
         ("flags", c_i32), ("reserved1", c_i32),
         ("M", c_i64),
+        ("w32", c_vp), ("ntiles32", c_i32), ("tn32", c_i32),
     ]
 
 
@@ -101,6 +102,7 @@ SIGNATURES = {
                                    c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "jabd_multibox_loss_finalize_f32": [c_vp, c_vp, c_vp, c_vp],
     "jabd_conv_pack_tn": [c_int],
+    "jabd_conv_pack_tn32": [c_int],
     "jabd_conv2d_nhwc_f32": [ctypes.POINTER(ConvArgs), c_vp],
     "jabd_stem_nchw_f32": [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp],
     "jabd_dw_nblk": [c_i64, c_i64, c_i64, c_i64],

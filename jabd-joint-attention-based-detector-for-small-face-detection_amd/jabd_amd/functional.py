@@ -50,6 +50,23 @@ class PackedConv:
         wp = wp.view(self.Kc, 4, 4, self.Ntiles, 16).permute(0, 3, 1, 4, 2).contiguous()
         self.w = wp
         self.bias = bias.contiguous().float() if bias is not None else None
+        self.w32 = None
+        if KH == 1 and KW == 1:
+            self._pack32(w2d)
+
+    def _pack32(self, w2d):
+        """Second packing for the 32x32x2 1x1 kernel (csrc/conv32.hip):
+        float4 [K8][ntiles32][64 lanes], lane = 32h + j holding
+        W[8k8 + 4h + e][32nt + j] for e = 0..3; K padded to 32."""
+        K, cout = w2d.shape
+        self.tn32 = int(lib().jabd_conv_pack_tn32(cout))
+        nt = (cout + 31) // 32
+        self.ntiles32 = (nt + self.tn32 - 1) // self.tn32 * self.tn32
+        k8 = (K + 31) // 32 * 4
+        wp = torch.zeros((k8 * 8, self.ntiles32 * 32), dtype=torch.float32, device=w2d.device)
+        wp[:K, :cout] = w2d
+        # [K8, h, e, NT, j] -> [K8, NT, h, j, e]
+        self.w32 = wp.view(k8, 2, 4, self.ntiles32, 32).permute(0, 3, 1, 4, 2).contiguous()
 
 
 def conv_weight_2d(weight):
@@ -139,6 +156,8 @@ def conv(x, pk, stride=1, pad=0, act="none", slope=0.0, ascale=None, x2=None, x2
         a.res, a.res_bs, a.res_ps, a.res_c0 = res.data_ptr(), res.stride(0), res.shape[3], 0
     a.y, a.y_bs, a.y_ps, a.y_c0 = out.data_ptr(), out.stride(0), out.shape[3], out_c0
     a.OH, a.OW, a.Cout, a.Ntiles, a.tn, a.Kc = OH, OW, pk.Cout, pk.Ntiles, pk.tn, pk.Kc
+    if pk.w32 is not None and stride == 1 and pad == 0 and not nchw_in:
+        a.w32, a.ntiles32, a.tn32 = pk.w32.data_ptr(), pk.ntiles32, pk.tn32
     a.KH, a.KW, a.stride, a.pad = pk.KH, pk.KW, stride, pad
     a.act, a.slope = ACT[act], float(slope)
     a.nchw_in = 1 if nchw_in else 0

@@ -1,0 +1,149 @@
+"""Microbenchmark of single conv launches at the C2 / R50 layer shapes.
+
+Each shape runs with the library's current kernel choice (set JABD_CONV32 /
+JABD_CONV_GENERIC in the environment for A/B), checks the output against a
+torch fp32 reference on the GPU (max-abs error / max-abs ref), and prints
+us / TFLOP/s / algorithmic GB/s (input, skip source, residual, weights,
+output) and the roofline time max(FLOP/157.3T, bytes/8T).
+
+  python3 tools/convbench.py [--set mnv3|r50|all] [--reps 20]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "jabd-joint-attention-based-detector-for-small-face-detection_amd")]
+from jabd_amd import functional as F  # noqa: E402
+
+# (name, B, H, W, Cin, Cout, k, stride, x2 channels (0 = none), ascale, res, act)
+MNV3 = [
+    ("b1.proj", 32, 512, 512, 16, 16, 1, 1, 0, 1, 1, "relu"),
+    ("b2.proj", 32, 256, 256, 64, 24, 1, 1, 16, 1, 0, "relu"),
+    ("b3.proj", 32, 256, 256, 72, 24, 1, 1, 0, 1, 1, "relu"),
+    ("b4.proj", 32, 128, 128, 72, 40, 1, 1, 24, 1, 0, "relu"),
+    ("b5.proj", 32, 128, 128, 120, 40, 1, 1, 0, 1, 1, "relu"),
+    ("b7.proj", 32, 64, 64, 240, 80, 1, 1, 40, 1, 0, "hswish"),
+    ("b8.proj", 32, 64, 64, 200, 80, 1, 1, 0, 1, 1, "hswish"),
+    ("b11.proj", 32, 64, 64, 480, 112, 1, 1, 80, 1, 0, "hswish"),
+    ("b12.proj", 32, 64, 64, 672, 112, 1, 1, 0, 1, 1, "hswish"),
+    ("b13.proj", 32, 32, 32, 672, 160, 1, 1, 112, 1, 0, "hswish"),
+    ("b14.proj", 32, 32, 32, 672, 160, 1, 1, 0, 1, 1, "hswish"),
+    ("b15.proj", 32, 32, 32, 960, 160, 1, 1, 0, 1, 1, "hswish"),
+    ("b12.exp", 32, 64, 64, 112, 672, 1, 1, 0, 0, 0, "hswish"),
+    ("b15.exp", 32, 32, 32, 160, 960, 1, 1, 0, 0, 0, "hswish"),
+    ("fpn.lat1", 32, 128, 128, 40, 40, 1, 1, 0, 1, 0, "leaky"),
+    ("ssh1.c3", 32, 128, 128, 40, 20, 3, 1, 0, 1, 0, "relu"),
+    ("merge1", 32, 128, 128, 40, 40, 3, 1, 0, 0, 0, "leaky"),
+]
+R50 = [
+    ("l1.c1", 16, 256, 256, 64, 64, 1, 1, 0, 0, 0, "relu"),
+    ("l1.c2", 16, 256, 256, 64, 64, 3, 1, 0, 0, 0, "relu"),
+    ("l1.c3", 16, 256, 256, 64, 256, 1, 1, 64, 0, 0, "relu"),
+    ("l2.c1", 16, 128, 128, 512, 128, 1, 1, 0, 0, 0, "relu"),
+    ("l2.c2", 16, 128, 128, 128, 128, 3, 1, 0, 0, 0, "relu"),
+    ("l2.c3", 16, 128, 128, 128, 512, 1, 1, 0, 0, 1, "relu"),
+    ("l3.c1", 16, 64, 64, 1024, 256, 1, 1, 0, 0, 0, "relu"),
+    ("l3.c2", 16, 64, 64, 256, 256, 3, 1, 0, 0, 0, "relu"),
+    ("l3.c3", 16, 64, 64, 256, 1024, 1, 1, 0, 0, 1, "relu"),
+    ("l4.c1", 16, 32, 32, 2048, 512, 1, 1, 0, 0, 0, "relu"),
+    ("l4.c2", 16, 32, 32, 512, 512, 3, 1, 0, 0, 0, "relu"),
+    ("l4.c3", 16, 32, 32, 512, 2048, 1, 1, 0, 0, 1, "relu"),
+]
+
+
+def ref(x, w2d, bias, k, stride, x2, sc, res, act):
+    xs = x * sc[:, None, None, :] if sc is not None else x
+    xn = xs.permute(0, 3, 1, 2)
+    cout = w2d.shape[1]
+    cin = x.shape[3]
+    wt = w2d[:k * k * cin].reshape(k, k, cin, cout).permute(3, 2, 0, 1)
+    y = torch.nn.functional.conv2d(xn, wt, None, stride, k // 2)
+    if x2 is not None:
+        y = y + torch.nn.functional.conv2d(x2.permute(0, 3, 1, 2),
+                                           w2d[k * k * cin:].t()[:, :, None, None])
+    y = y.permute(0, 2, 3, 1) + bias
+    if res is not None:
+        y = y + res
+    if act == "relu":
+        y = torch.relu(y)
+    elif act == "leaky":
+        y = torch.nn.functional.leaky_relu(y, 0.1)
+    elif act == "hswish":
+        y = torch.nn.functional.hardswish(y)
+    return y
+
+
+def run(shape, reps):
+    name, B, H, W, cin, cout, k, stride, c2, asc, hasres, act = shape
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(B, H, W, cin, device=dev, generator=g)
+    x2 = torch.randn(B, H, W, c2, device=dev, generator=g) if c2 else None
+    K = k * k * cin + c2
+    w2d = torch.randn(K, cout, device=dev, generator=g) / K ** 0.5
+    bias = torch.randn(cout, device=dev, generator=g)
+    sc = torch.rand(B, cin, device=dev, generator=g) if asc else None
+    OH, OW = (H - 1) // stride + 1, (W - 1) // stride + 1
+    res = torch.randn(B, OH, OW, cout, device=dev, generator=g) if hasres else None
+    pk = F.PackedConv(w2d, bias, k, k, cin, c2)
+    kw = dict(stride=stride, pad=k // 2, act=act, slope=0.1, ascale=sc, x2=x2, res=res)
+    y = F.conv(x, pk, **kw)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    r = ref(x, w2d, bias, k, stride, x2, sc, res, act)
+    err = float((y - r).abs().max() / r.abs().max())
+    for _ in range(3):
+        F.conv(x, pk, **kw)
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        F.conv(x, pk, **kw)
+    e.record()
+    torch.cuda.synchronize()
+    t = s.elapsed_time(e) / reps * 1e3
+    M = B * OH * OW
+    fl = 2.0 * M * K * cout
+    nb = 4.0 * (x.numel() + (x2.numel() if c2 else 0) + (res.numel() if hasres else 0)
+                + K * cout + M * cout)
+    roof = max(fl / 157.3e12, nb / 8e12) * 1e6
+    tl = ""
+    if k == 1 and not c2 and not asc and os.environ.get("CB_TORCH"):
+        a2, w2 = x.reshape(-1, cin), w2d.contiguous()
+        torch.mm(a2, w2)
+        s.record()
+        for _ in range(reps):
+            torch.mm(a2, w2)
+        e.record()
+        torch.cuda.synchronize()
+        tl = "  torch.mm %7.1f us" % (s.elapsed_time(e) / reps * 1e3)
+    print("%-9s M%8d K%5d N%5d k%d  %8.1f us  %6.1f TF  %6.0f GB/s  roof %7.1f (%3.0f%%)  err %.1e"
+          % (name, M, K, cout, k, t, fl / t / 1e6, nb / t / 1e3, roof, 100 * roof / t, err)
+          + tl, flush=True)
+    return t, roof, err
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--set", default="mnv3")
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    shapes = {"mnv3": MNV3, "r50": R50, "all": MNV3 + R50}[args.set]
+    if args.only:
+        shapes = [s for s in shapes if s[0] in args.only.split(",")]
+    print("# JABD_CONV32=%s JABD_CONV_GENERIC=%s" % (os.environ.get("JABD_CONV32"),
+                                                    os.environ.get("JABD_CONV_GENERIC")))
+    bad = 0
+    for sh in shapes:
+        _, _, err = run(sh, args.reps)
+        bad += err > 1e-4
+    print("# errors > 1e-4:", bad)
+
+
+if __name__ == "__main__":
+    main()
