@@ -233,6 +233,12 @@ int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_t stream);
  * not produced by the dw kernel: C3/C4/C5 and the FPN outputs). */
 int jabd_channel_sum_f32(const float* x, int64_t x_bs, int32_t x_ps, int64_t B, int64_t HW,
                          int64_t C, int64_t nblk, float* part, jabd_stream_t stream);
+/* First level of a two-level, fixed-order sum of per-block partials:
+ * out[b][s][c] = sum of part[b][r][c] over rows r in [s*R, (s+1)*R),
+ * R = ceil(nblk / nsplit).  Feeds jabd_eca_gate_f32 (with nblk = nsplit) when
+ * a producer wrote many partial rows (one per depthwise tile). */
+int jabd_partial_reduce_f32(const float* part, int64_t nblk, int64_t B, int64_t C, int64_t nsplit,
+                            float* out, jabd_stream_t stream);
 /* A2 ECA gate — nets/mobilenetV3.py:343-348 (gate=HSIGMOID) and
  * nets/retinaface_r.py:219-224 (gate=SIGMOID): mean = sum(part)/HW,
  * Conv1d(1,1,k,pad=(k-1)/2,no bias) over channels, gate -> scale [B][C]. */

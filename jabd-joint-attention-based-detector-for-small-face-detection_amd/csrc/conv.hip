@@ -475,6 +475,20 @@ static int launch_conv(const ConvArgs& a, bool vec4, hipStream_t st) {
 
 using namespace jabd;
 
+namespace jabd {
+// (tn, tm) -> kernel instance; -1 when not instantiated.
+template <bool FAST>
+static int dispatch_conv(const ConvArgs& a, int tn, int tm, bool vec4, hipStream_t st) {
+#define DC(TM_, TN_)                                                         \
+  if (tm == TM_ && tn == TN_)                                                \
+    return FAST ? launch_1x1<TM_, TN_>(a, st) : launch_conv<TM_, TN_>(a, vec4, st);
+  DC(4, 1) DC(2, 1) DC(1, 1) DC(4, 2) DC(2, 2) DC(1, 2) DC(4, 3) DC(2, 3) DC(1, 3)
+  DC(4, 4) DC(2, 4) DC(1, 4) DC(4, 5) DC(2, 5) DC(1, 5) DC(2, 8) DC(1, 8)
+#undef DC
+  return -1;
+}
+}  // namespace jabd
+
 extern "C" int jabd_conv_pack_tn(int cout) {
   // N-tile group per launch: minimise padded columns, cap accumulators.
   int tiles = (cout + 15) / 16;
@@ -571,28 +585,20 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
     const int r = conv1x1_m32_dispatch(a, st);
     if (r >= 0) return r;
   }
-  if (fast1x1) {
-    switch (tn) {
-      case 1: return launch_1x1<4, 1>(a, st);
-      case 2: return launch_1x1<4, 2>(a, st);
-      case 3: return launch_1x1<4, 3>(a, st);
-      case 4: return launch_1x1<4, 4>(a, st);
-      case 5: return launch_1x1<4, 5>(a, st);
-      case 8: return launch_1x1<2, 8>(a, st);
-      default: break;
-    }
-  }
-  switch (tn) {
-    case 1: return launch_conv<4, 1>(a, vec4, st);
-    case 2: return launch_conv<4, 2>(a, vec4, st);
-    case 3: return launch_conv<4, 3>(a, vec4, st);
-    case 4: return launch_conv<4, 4>(a, vec4, st);
-    case 5: return launch_conv<4, 5>(a, vec4, st);
-    case 8: return launch_conv<2, 8>(a, vec4, st);
-    default:
-      set_error("conv: unsupported tn=%d", tn);
-      return JABD_EINVAL;
-  }
+  // Pixel tiles per wave: 4 x 16 by default; small-M layers (the SSH / FPN
+  // convs at 32x32 and 64x64) drop to 2 or 1 so the grid still fills the
+  // 256 CUs several times over.
+  const int64_t nblk_n = a.Ntiles / tn;
+  auto grid_for = [&](int tm) { return cdiv(a.M, (int64_t)64 * tm) * nblk_n; };
+  const int tm_max = tn == 8 ? 2 : 4;
+  int tm = tm_max;
+  while (tm > 1 && grid_for(tm) < 1024) tm >>= 1;
+  const int r = fast1x1 ? dispatch_conv<true>(a, tn, tm, vec4, st) : -1;
+  if (r >= 0) return r;
+  const int r2 = dispatch_conv<false>(a, tn, tm, vec4, st);
+  if (r2 >= 0) return r2;
+  set_error("conv: unsupported tn=%d", tn);
+  return JABD_EINVAL;
 }
 
 // ---------------------------------------------------------------------------

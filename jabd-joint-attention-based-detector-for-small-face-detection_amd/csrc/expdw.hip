@@ -57,6 +57,7 @@ struct XdCfg {
   static_assert(TW % PW == 0 && 256 % NC4 == 0, "tile shape");
   static_assert(LDS * 4 <= 160 * 1024, "LDS");
   static_assert((K * K + 1) * NC4 <= 256, "dw taps: one float4 per thread");
+  static_assert(64 % NC4 == 0, "channel quads must tile a wave");
 };
 
 // Persistent: workgroup L walks work items i = L, L + G, ... (G = grid, a
@@ -69,20 +70,39 @@ struct XdItem {
   int b, t_in, oh0, ow0, ih0, iw0, c0;
 };
 
+// n / d for 0 <= n < 2^31 by multiply-high and shift (host-built divisor):
+// the per-item decode would otherwise run three ~40-instruction integer
+// divisions on the scalar unit.
+struct FastDiv {
+  uint32_t m, l, d;
+};
+static FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint64_t m = ((((uint64_t)1 << l) - d) << 32) / d + 1;
+  return FastDiv{(uint32_t)m, l, d};
+}
+__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
+  return (int)((__umulhi((uint32_t)n, f.m) + (uint32_t)n) >> f.l);
+}
+struct XdDivs {
+  FastDiv nch, tiles_img, tiles_w;
+};
+
 template <int K, int S, int TH, int TW, int EC>
-__device__ __forceinline__ bool xd_item(const jabd_expdw_args& p, int i, int tiles_w,
-                                        int tiles_img, int nch, int nitems, XdItem& it) {
+__device__ __forceinline__ bool xd_item(const jabd_expdw_args& p, int i, const XdDivs& dv,
+                                        int nitems, XdItem& it) {
   using C = XdCfg<K, S, TH, TW, EC>;
   if (i >= nitems) return false;
   const int xcd = i & 7;
   const int q = i >> 3;
-  const int qn = q / nch;
-  const int chunk = q - qn * nch;
+  const int qn = fdiv(q, dv.nch);
+  const int chunk = q - qn * (int)dv.nch.d;
   const int tile = qn * 8 + xcd;
-  if (tile >= p.B * tiles_img) return false;
-  it.b = tile / tiles_img;
-  it.t_in = tile - it.b * tiles_img;
-  const int ty = it.t_in / tiles_w, tx = it.t_in - ty * tiles_w;
+  if (tile >= p.B * (int)dv.tiles_img.d) return false;
+  it.b = fdiv(tile, dv.tiles_img);
+  it.t_in = tile - it.b * (int)dv.tiles_img.d;
+  const int ty = fdiv(it.t_in, dv.tiles_w), tx = it.t_in - ty * (int)dv.tiles_w.d;
   it.oh0 = ty * TH;
   it.ow0 = tx * TW;
   it.ih0 = it.oh0 * S - C::PAD;
@@ -92,8 +112,8 @@ __device__ __forceinline__ bool xd_item(const jabd_expdw_args& p, int i, int til
 }
 
 template <int K, int S, int TH, int TW, int EC, int ACT>
-__global__ __launch_bounds__(256, EC == 16 ? 3 : 2) void expdw_kernel(const jabd_expdw_args p, int tiles_w,
-                                                       int tiles_img, int nch, int nitems) {
+__global__ __launch_bounds__(256, EC == 16 ? 3 : 2) void expdw_kernel(const jabd_expdw_args p, const XdDivs dv,
+                                                       int nitems) {
   using C = XdCfg<K, S, TH, TW, EC>;
   constexpr int NPF = (C::IPAD * 4 + 255) / 256;  // prefetched float4 per thread per stage
   __shared__ __attribute__((aligned(16))) float lds[C::LDS];
@@ -105,7 +125,7 @@ __global__ __launch_bounds__(256, EC == 16 ? 3 : 2) void expdw_kernel(const jabd
   // tiles that straddle the 8-aligned tile padding are skipped: advance to
   // the next real item (uniform per workgroup)
   auto next_item = [&](int i, XdItem& it) -> int {
-    while (i < nitems && !xd_item<K, S, TH, TW, EC>(p, i, tiles_w, tiles_img, nch, nitems, it))
+    while (i < nitems && !xd_item<K, S, TH, TW, EC>(p, i, dv, nitems, it))
       i += G;
     return i;
   };
@@ -276,17 +296,29 @@ __global__ __launch_bounds__(256, EC == 16 ? 3 : 2) void expdw_kernel(const jabd
       }
     }
     if (p.part) {
+      // threads with the same channel quad sit at lanes c4, c4 + NC4, ...:
+      // butterfly over the lane bits above log2(NC4) (fixed order), then
+      // combine the 4 waves' results in LDS
+#pragma unroll
+      for (int off = C::NC4; off < 64; off <<= 1) {
+        psum.x += __shfl_xor(psum.x, off);
+        psum.y += __shfl_xor(psum.y, off);
+        psum.z += __shfl_xor(psum.z, off);
+        psum.w += __shfl_xor(psum.w, off);
+      }
       __syncthreads();
       float4* red = reinterpret_cast<float4*>(lds);
-      red[t] = psum;
+      if (lane < C::NC4) red[wave * C::NC4 + lane] = psum;
       __syncthreads();
       if (t < C::NC4 && cur.c0 + 4 * t < p.E) {
-        float4 sm = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int r = 0; r < 256 / C::NC4; ++r) {
-          const float4 v = red[r * C::NC4 + t];
-          sm.x += v.x; sm.y += v.y; sm.z += v.z; sm.w += v.w;
-        }
-        *reinterpret_cast<float4*>(p.part + ((int64_t)cur.b * tiles_img + cur.t_in) * p.E +
+        const float4 a0 = red[t], a1 = red[C::NC4 + t], a2 = red[2 * C::NC4 + t],
+                     a3 = red[3 * C::NC4 + t];
+        float4 sm;
+        sm.x = (a0.x + a1.x) + (a2.x + a3.x);
+        sm.y = (a0.y + a1.y) + (a2.y + a3.y);
+        sm.z = (a0.z + a1.z) + (a2.z + a3.z);
+        sm.w = (a0.w + a1.w) + (a2.w + a3.w);
+        *reinterpret_cast<float4*>(p.part + ((int64_t)cur.b * (int)dv.tiles_img.d + cur.t_in) * p.E +
                                    cur.c0 + 4 * t) = sm;
       }
     }
@@ -364,13 +396,14 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
   JABD_REQUIRE(nitems < ((int64_t)1 << 31) && (int64_t)a.H * a.W * a.x_ps < ((int64_t)1 << 31),
                "expand_dw: problem too large for 32-bit item / pixel indexing");
   hipStream_t st = as_stream(stream);
+  const XdDivs dv{make_fastdiv((uint32_t)nch), make_fastdiv((uint32_t)tiles_img),
+                  make_fastdiv((uint32_t)tiles_w)};
   // persistent grid = the workgroups that are resident at once (a multiple of
   // 8 for XCD-stable item ownership; any more would run as a late tail)
 #define XD_LAUNCH(K_, S_, TH_, TW_, EC_, ACT_)                                                \
   do {                                                                                        \
     const int64_t grid = xd_grid((const void*)expdw_kernel<K_, S_, TH_, TW_, EC_, ACT_>, nitems); \
-    expdw_kernel<K_, S_, TH_, TW_, EC_, ACT_><<<(unsigned)grid, 256, 0, st>>>(a, tiles_w,     \
-                                                                             tiles_img, nch,  \
+    expdw_kernel<K_, S_, TH_, TW_, EC_, ACT_><<<(unsigned)grid, 256, 0, st>>>(a, dv,         \
                                                                              (int)nitems);    \
   } while (0)
 #define XD_CASE(K_, S_, TH_, TW_, EC_)                                    \

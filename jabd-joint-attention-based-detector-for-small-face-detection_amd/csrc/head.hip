@@ -3,6 +3,8 @@
 // fused with the FPN's nearest up-sample and lateral add, and the three
 // detection heads written straight into the anchor-major output layout.
 // All HBM/latency-bound: one pass over each activation, fixed-order sums.
+#include <algorithm>
+
 #include "common.h"
 #include "conv_args.h"
 
@@ -94,6 +96,36 @@ __global__ void eca_gate_kernel(const float* __restrict__ part, int64_t nblk, in
     }
     float g = gate == ACT_SIGMOID ? 1.f / (1.f + expf(-y)) : fminf(fmaxf(y + 3.f, 0.f), 6.f) * (1.f / 6.f);
     scale[(int64_t)b * C + c] = g;
+  }
+}
+
+// First level of the ECA pool for many partial rows: block (s, b) sums rows
+// [s*R, min(nblk, (s+1)*R)) of part[b] in row order into out[b][s] — a
+// deterministic two-level sum that spreads the read of nblk x C partials over
+// nsplit x B workgroups instead of B.
+__global__ __launch_bounds__(256) void partial_reduce_kernel(const float* __restrict__ part,
+                                                             int nblk, int C, int R,
+                                                             float* __restrict__ out) {
+  const int s = blockIdx.x, b = blockIdx.y, nsplit = gridDim.x;
+  const int r0 = s * R, r1 = min(nblk, r0 + R);
+  const float* pb = part + (int64_t)b * nblk * C;
+  float* ob = out + ((int64_t)b * nsplit + s) * C;
+  if ((C & 3) == 0) {
+    const int C4 = C >> 2;
+    for (int c4 = threadIdx.x; c4 < C4; c4 += blockDim.x) {
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int r = r0; r < r1; ++r) {
+        const float4 v = reinterpret_cast<const float4*>(pb + (int64_t)r * C)[c4];
+        a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+      }
+      reinterpret_cast<float4*>(ob)[c4] = a;
+    }
+  } else {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      float a = 0.f;
+      for (int r = r0; r < r1; ++r) a += pb[(int64_t)r * C + c];
+      ob[c] = a;
+    }
   }
 }
 
@@ -352,6 +384,19 @@ extern "C" int jabd_channel_sum_f32(const float* x, int64_t x_bs, int32_t x_ps, 
   channel_sum_kernel<<<g, kSumThreads, rows * cw * sizeof(float), as_stream(stream)>>>(
       x, x_bs, x_ps, HW, (int)C, per, nblk, part);
   return check_launch("channel_sum");
+}
+
+extern "C" int jabd_partial_reduce_f32(const float* part, int64_t nblk, int64_t B, int64_t C,
+                                       int64_t nsplit, float* out, jabd_stream_t stream) {
+  JABD_REQUIRE(part && out && B > 0 && C > 0 && nblk > 0 && nsplit > 0 && nsplit <= nblk &&
+                   nblk * C < ((int64_t)1 << 31) && B <= 65535,
+               "partial_reduce: bad args");
+  const int64_t R = cdiv(nblk, nsplit);
+  dim3 g((unsigned)nsplit, (unsigned)B);
+  const int threads = C >= 1024 ? 256 : (int)std::max<int64_t>(64, cdiv(cdiv(C, 4), 64) * 64);
+  partial_reduce_kernel<<<g, threads, 0, as_stream(stream)>>>(part, (int)nblk, (int)C, (int)R,
+                                                             out);
+  return check_launch("partial_reduce");
 }
 
 extern "C" int jabd_eca_gate_f32(const float* part, int64_t nblk, int64_t B, int64_t C,

@@ -245,6 +245,12 @@ def channel_sums(x, nblk=None):
 
 def eca_gate(part, hw, w1d, gate, return_mean=False):
     B, nblk, C = part.shape
+    if nblk > 64:  # many tile partials: reduce them over many workgroups first
+        nsplit = min(64, (nblk + 7) // 8)
+        red = torch.empty((B, nsplit, C), dtype=torch.float32, device=part.device)
+        call("jabd_partial_reduce_f32", part.data_ptr(), nblk, B, C, nsplit, red.data_ptr(),
+             _stream())
+        part, nblk = red, nsplit
     scale = torch.empty((B, C), dtype=torch.float32, device=part.device)
     mean = torch.empty((B, C), dtype=torch.float32, device=part.device) if return_mean else None
     call("jabd_eca_gate_f32", part.data_ptr(), nblk, B, C, hw, w1d.data_ptr(), w1d.numel(),

@@ -127,20 +127,74 @@ def run(shape, reps):
     return t, roof, err
 
 
+# expand 1x1 + depthwise (fused kernel): (name, B, H, W, Cin, E, k, stride, act)
+XD = [
+    ("b1.xd", 32, 512, 512, 16, 16, 3, 1, "relu"),
+    ("b2.xd", 32, 512, 512, 16, 64, 3, 2, "relu"),
+    ("b3.xd", 32, 256, 256, 24, 72, 3, 1, "relu"),
+    ("b4.xd", 32, 256, 256, 24, 72, 5, 2, "relu"),
+    ("b5.xd", 32, 128, 128, 40, 120, 5, 1, "relu"),
+    ("b7.xd", 32, 128, 128, 40, 240, 3, 2, "hswish"),
+    ("b8.xd", 32, 64, 64, 80, 200, 3, 1, "hswish"),
+    ("b11.xd", 32, 64, 64, 80, 480, 3, 1, "hswish"),
+    ("b12.xd", 32, 64, 64, 112, 672, 3, 1, "hswish"),
+    ("b13.xd", 32, 64, 64, 112, 672, 5, 2, "hswish"),
+    ("b14.xd", 32, 32, 32, 160, 672, 5, 1, "hswish"),
+    ("b15.xd", 32, 32, 32, 160, 960, 5, 1, "hswish"),
+]
+
+
+def run_xd(shape, reps):
+    name, B, H, W, cin, E, k, stride, act = shape
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(B, H, W, cin, device=dev, generator=g)
+    we = torch.randn(cin, E, device=dev, generator=g) / cin ** 0.5
+    be = torch.randn(E, device=dev, generator=g) * 0.1
+    wd = torch.randn(k * k, E, device=dev, generator=g) / k
+    bd = torch.randn(E, device=dev, generator=g) * 0.1
+    pk = F.PackedConv(we, be, 1, 1, cin)
+    y, part = F.expand_dw(x, pk, wd, bd, k, stride, act=act)
+    fa = torch.relu if act == "relu" else torch.nn.functional.hardswish
+    e1 = fa(x.reshape(-1, cin) @ we + be).reshape(B, H, W, E).permute(0, 3, 1, 2)
+    r = torch.nn.functional.conv2d(e1, wd.t().reshape(E, 1, k, k), bd, stride, k // 2, 1, E)
+    r = fa(r).permute(0, 2, 3, 1)
+    err = float((y - r).abs().max() / r.abs().max())
+    perr = float((part.sum(1) - r.sum((1, 2))).abs().max() / r.sum((1, 2)).abs().max())
+    for _ in range(3):
+        F.expand_dw(x, pk, wd, bd, k, stride, act=act)
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        F.expand_dw(x, pk, wd, bd, k, stride, act=act)
+    e.record()
+    torch.cuda.synchronize()
+    t = s.elapsed_time(e) / reps * 1e3
+    fl = 2.0 * B * H * W * cin * E + 2.0 * y.numel() * k * k
+    nb = 4.0 * (x.numel() + y.numel())
+    roof = max(fl / 157.3e12, nb / 8e12) * 1e6
+    print("%-9s %4dx%-4d %4d->%-4d k%d s%d  %8.1f us  %6.1f TF  %6.0f GB/s  roof %7.1f (%3.0f%%)  "
+          "err %.1e part %.1e" % (name, H, W, cin, E, k, stride, t, fl / t / 1e6, nb / t / 1e3,
+                                  roof, 100 * roof / t, err, perr), flush=True)
+    return t, roof, max(err, perr)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--set", default="mnv3")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="")
     args = ap.parse_args()
-    shapes = {"mnv3": MNV3, "r50": R50, "all": MNV3 + R50}[args.set]
+    shapes = {"mnv3": MNV3, "r50": R50, "all": MNV3 + R50, "xd": XD}[args.set]
     if args.only:
         shapes = [s for s in shapes if s[0] in args.only.split(",")]
     print("# JABD_CONV32=%s JABD_CONV_GENERIC=%s" % (os.environ.get("JABD_CONV32"),
                                                     os.environ.get("JABD_CONV_GENERIC")))
     bad = 0
     for sh in shapes:
-        _, _, err = run(sh, args.reps)
+        _, _, err = (run_xd if args.set == "xd" else run)(sh, args.reps)
         bad += err > 1e-4
     print("# errors > 1e-4:", bad)
 
