@@ -66,6 +66,17 @@ struct XdCfg {
 // Kc stages (16 input channels each); the global loads of the next stage
 // (possibly the next item's first) are issued into registers before the
 // current stage's MFMAs / depthwise phase, so HBM latency overlaps compute.
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is also a
+// workgroup-scope fence on global memory, so the compiler drains every
+// outstanding global load (s_waitcnt vmcnt(0)) before it — which would
+// retire the next item's register prefetch at the first barrier after it is
+// issued.  The LDS ordering this kernel needs is just lgkmcnt(0) + s_barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 struct XdItem {
   int b, t_in, oh0, ow0, ih0, iw0, c0;
 };
@@ -196,7 +207,7 @@ __global__ __launch_bounds__(256, EC == 16 ? 3 : 2) void expdw_kernel(const jabd
           *reinterpret_cast<float4*>(lds + (idx >> 2) * C::XP + (idx & 3) * 4) = pf[u];
       }
       const f32x4 a = pa_n;
-      __syncthreads();
+      lds_barrier();
       // issue the next stage's loads
       if (kc + 1 < p.Kc) {
         prefetch(cur, kc + 1);
@@ -219,7 +230,7 @@ __global__ __launch_bounds__(256, EC == 16 ? 3 : 2) void expdw_kernel(const jabd
           }
         }
       }
-      __syncthreads();
+      lds_barrier();
     }
     // acc[u][r] = expanded channel 16nt + 4g + r of tile pixel 16pb + j
 #pragma unroll
@@ -244,7 +255,7 @@ __global__ __launch_bounds__(256, EC == 16 ? 3 : 2) void expdw_kernel(const jabd
       }
     }
     if (t < NWD) wsh[t / C::NC4][t % C::NC4] = pwd;
-    __syncthreads();
+    lds_barrier();
 
     // depthwise phase
     const bool chv = cur.c0 + chl < p.E;
@@ -306,10 +317,10 @@ __global__ __launch_bounds__(256, EC == 16 ? 3 : 2) void expdw_kernel(const jabd
         psum.z += __shfl_xor(psum.z, off);
         psum.w += __shfl_xor(psum.w, off);
       }
-      __syncthreads();
+      lds_barrier();
       float4* red = reinterpret_cast<float4*>(lds);
       if (lane < C::NC4) red[wave * C::NC4 + lane] = psum;
-      __syncthreads();
+      lds_barrier();
       if (t < C::NC4 && cur.c0 + 4 * t < p.E) {
         const float4 a0 = red[t], a1 = red[C::NC4 + t], a2 = red[2 * C::NC4 + t],
                      a3 = red[3 * C::NC4 + t];
@@ -322,7 +333,7 @@ __global__ __launch_bounds__(256, EC == 16 ? 3 : 2) void expdw_kernel(const jabd
                                    cur.c0 + 4 * t) = sm;
       }
     }
-    __syncthreads();  // LDS (Es / red) free for the next item's staging
+    lds_barrier();  // LDS (Es / red) free for the next item's staging
     if (nx_idx >= nitems) break;
     cur = nxt;
     ci_idx = nx_idx;

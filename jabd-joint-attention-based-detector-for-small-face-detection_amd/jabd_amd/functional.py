@@ -204,6 +204,9 @@ def dwconv(x, w, bias, k, stride, act="none", slope=0.0, partials=False):
     return y, part
 
 
+_XD_DBG = 0  # kernel-phase skip mask for tools/convbench.py timing experiments only
+
+
 def expand_dw(x, pk, w, bias, k, stride, act="none", partials=True):
     """Fused expand 1x1 (PackedConv pk, folded BN) + act -> depthwise k x k
     (pad k//2, folded BN) + act; returns (y, ECA partials [B, nblk, E])."""
@@ -223,6 +226,7 @@ def expand_dw(x, pk, w, bias, k, stride, act="none", partials=True):
     a.wd, a.bd = w.data_ptr(), bias.data_ptr()
     a.k, a.stride, a.act = k, stride, ACT[act]
     a.y, a.y_bs, a.y_ps, a.OH, a.OW = y.data_ptr(), y.stride(0), E, OH, OW
+    a.reserved0 = _XD_DBG
     part = None
     if partials:
         nb = int(lib().jabd_expand_dw_nblk(OH, OW, k, stride))

@@ -155,6 +155,9 @@ def run_xd(shape, reps):
     bd = torch.randn(E, device=dev, generator=g) * 0.1
     pk = F.PackedConv(we, be, 1, 1, cin)
     y, part = F.expand_dw(x, pk, wd, bd, k, stride, act=act)
+    dbg = int(os.environ.get("XD_DBG", "0"))
+    if dbg:
+        F._XD_DBG = dbg
     fa = torch.relu if act == "relu" else torch.nn.functional.hardswish
     e1 = fa(x.reshape(-1, cin) @ we + be).reshape(B, H, W, E).permute(0, 3, 1, 2)
     r = torch.nn.functional.conv2d(e1, wd.t().reshape(E, 1, k, k), bd, stride, k // 2, 1, E)
