@@ -513,7 +513,7 @@ static bool conv_generic_only() {
 }
 
 namespace jabd {
-int conv1x1_m32_dispatch(const ConvArgs& a, hipStream_t st);
+int conv1x1_m32_dispatch(const ConvArgs& a, hipStream_t st, bool kxk);
 }
 
 // Which 1x1 kernel: the 32x32x2 LDS-weight kernel (conv32.hip) pays off when
@@ -526,7 +526,8 @@ static bool use_conv32(const ConvArgs& a) {
   }
   if (!a.w32 || a.tn32 <= 0 || a.ntiles32 % a.tn32 || a.ntiles32 * 32 < a.Cout) return false;
   if (v >= 0) return v == 1;
-  const int K = a.Cin + (a.x2 ? a.Cin2 : 0);
+  const int K = a.KH * a.KW * a.Cin + (a.x2 ? a.Cin2 : 0);
+  if (a.KH * a.KW > 1) return a.Cout >= 64 && K >= 288;
   return a.Cout >= 96 && K >= 96;
 }
 
@@ -582,7 +583,13 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
                                      a.x2_bs * a.B < ((int64_t)1 << 31)))) &&
       (a.M + 64) * (maxps + 16) < ((int64_t)1 << 31) && !conv_generic_only();
   if (fast1x1 && use_conv32(a)) {
-    const int r = conv1x1_m32_dispatch(a, st);
+    const int r = conv1x1_m32_dispatch(a, st, false);
+    if (r >= 0) return r;
+  }
+  // k x k implicit GEMM on the 32x32 kernel: 32-channel stages inside one tap
+  if (!is1x1 && vec4 && (a.flags & 1) && !a.x2 && a.Cin % 32 == 0 && (!a.tconv || a.stride == 1) &&
+      a.x_bs % 4 == 0 && use_conv32(a)) {
+    const int r = conv1x1_m32_dispatch(a, st, true);
     if (r >= 0) return r;
   }
   // Pixel tiles per wave: 4 x 16 by default; small-M layers (the SSH / FPN

@@ -53,7 +53,10 @@ constexpr int kG = kBK / 8;      // 8-channel groups per stage
 // Workgroup = 4 waves stacked along M (BM = 128*TM pixels) x BN = 32*TN
 // channels.  Tiles never straddle an image when `per_img` (ECA gate folded
 // into the staged weights), else M is tiled flat.
-template <int TM, int TN>
+// KXK: k x k implicit GEMM (tap-major K; every 32-channel stage lies inside
+// one tap, host guarantees Cin % 32 == 0, no K-concat source); stride-1
+// transposed form (tconv) for the data gradient.
+template <int TM, int TN, bool KXK>
 __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, int mtiles_img,
                                                              int per_img) {
   constexpr int BM = 4 * 32 * TM;
@@ -82,13 +85,43 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
     const int m = m_lo + wave * 32 * TM + t * 32 + j;
     pm[t] = m < m_hi ? m : -1;
   }
-  const int Kt = p.Cin + (p.x2 ? p.Cin2 : 0);
+  const int Kt = KXK ? p.KH * p.KW * p.Cin : p.Cin + (p.x2 ? p.Cin2 : 0);
   const int S = (Kt + kBK - 1) / kBK;
+  // KXK: per-lane output coordinates (oh, ow) and image base of each pixel tile
+  int poh[TM], pow_[TM];
+  int64_t pbase[TM];
+  if constexpr (KXK) {
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      const int m = pm[t] >= 0 ? pm[t] : 0;
+      const int b = m / OHW, r = m - b * OHW;
+      poh[t] = r / p.OW;
+      pow_[t] = r - poh[t] * p.OW;
+      pbase[t] = (int64_t)b * p.x_bs + p.x_c0;
+    }
+  }
+  const int cps = p.Cin / kBK;  // KXK: stages per tap
   const int x2_pix = (p.x2 && p.x2_stride != 1) ? (int)(p.x2_bs / p.x2_ps) : 0;
   const float4* wg = reinterpret_cast<const float4*>(p.w);
   const float* sc = p.ascale ? p.ascale + (int64_t)img * p.ascale_bs : nullptr;
 
   auto load_a = [&](int s, float4 (&a)[TM][kG]) {
+    if constexpr (KXK) {
+      const int tap = s / cps, ci0 = (s - tap * cps) * kBK;
+      const int kh = tap / p.KW, kw = tap - kh * p.KW;
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        const int ih = p.tconv ? poh[t] + p.pad - kh : poh[t] * p.stride - p.pad + kh;
+        const int iw = p.tconv ? pow_[t] + p.pad - kw : pow_[t] * p.stride - p.pad + kw;
+        const bool ok = pm[t] >= 0 && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+        const float* src = p.x + pbase[t] + ((int64_t)ih * p.W + iw) * p.x_ps + ci0 + 4 * h;
+#pragma unroll
+        for (int q = 0; q < kG; ++q)
+          a[t][q] = ok ? *reinterpret_cast<const float4*>(src + 8 * q)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      return;
+    }
 #pragma unroll
     for (int t = 0; t < TM; ++t)
 #pragma unroll
@@ -124,7 +157,8 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
         const int k8 = s * kG + g;
         v = wg[((int64_t)k8 * p.Ntiles + nb * TN + u) * 64 + l];
         if (sc) {
-          const int k0 = 8 * k8 + 4 * (l >> 5);
+          int k0 = 8 * k8 + 4 * (l >> 5);
+          if (KXK) k0 -= (s / cps) * p.Cin;  // channel within the stage's tap
           if (k0 < p.Cin) {
             const float4 s4 = *reinterpret_cast<const float4*>(sc + k0);
             v.x *= s4.x; v.y *= s4.y; v.z *= s4.z; v.w *= s4.w;
@@ -230,7 +264,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
   }
 }
 
-template <int TM, int TN>
+template <int TM, int TN, bool KXK>
 static int launch_m32(const ConvArgs& a, hipStream_t st) {
   constexpr int BM = 4 * 32 * TM;
   const int64_t OHW = (int64_t)a.OH * a.OW;
@@ -239,7 +273,7 @@ static int launch_m32(const ConvArgs& a, hipStream_t st) {
   const int64_t mtiles = per_img ? mt_img * a.B : cdiv(a.M, BM);
   const int64_t grid = mtiles * (a.Ntiles / TN);
   JABD_REQUIRE(grid < (int64_t)0x7fffffff, "conv32: grid too large");
-  conv1x1_m32_kernel<TM, TN><<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, per_img);
+  conv1x1_m32_kernel<TM, TN, KXK><<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, per_img);
   return check_launch("conv1x1_m32");
 }
 
@@ -265,19 +299,22 @@ namespace jabd {
 // Called by jabd_conv2d_nhwc_f32 for 1x1 / stride-1 convs when the caller
 // supplied the 32x32 packing (args->w32).  Returns -1 when this kernel does
 // not take the shape (the caller then uses conv.hip).
-int conv1x1_m32_dispatch(const ConvArgs& a0, hipStream_t st) {
+int conv1x1_m32_dispatch(const ConvArgs& a0, hipStream_t st, bool kxk) {
   ConvArgs a = a0;
   a.w = a0.w32;
   a.Ntiles = a0.ntiles32;
+#define M32(TM_, TN_) \
+  return kxk ? launch_m32<TM_, TN_, true>(a, st) : launch_m32<TM_, TN_, false>(a, st);
   switch (a0.tn32) {
-    case 1: return launch_m32<2, 1>(a, st);
-    case 2: return launch_m32<2, 2>(a, st);
-    case 3: return launch_m32<2, 3>(a, st);
-    case 4: return launch_m32<2, 4>(a, st);
-    case 5: return launch_m32<1, 5>(a, st);
-    case 6: return launch_m32<1, 6>(a, st);
-    case 7: return launch_m32<1, 7>(a, st);
+    case 1: M32(2, 1)
+    case 2: M32(2, 2)
+    case 3: M32(2, 3)
+    case 4: M32(2, 4)
+    case 5: M32(1, 5)
+    case 6: M32(1, 6)
+    case 7: M32(1, 7)
     default: return -1;
   }
+#undef M32
 }
 }  // namespace jabd

@@ -51,7 +51,7 @@ class PackedConv:
         self.w = wp
         self.bias = bias.contiguous().float() if bias is not None else None
         self.w32 = None
-        if KH == 1 and KW == 1:
+        if (KH == 1 and KW == 1) or (Cin % 32 == 0 and not Cin2):
             self._pack32(w2d)
 
     def _pack32(self, w2d):
@@ -156,7 +156,7 @@ def conv(x, pk, stride=1, pad=0, act="none", slope=0.0, ascale=None, x2=None, x2
         a.res, a.res_bs, a.res_ps, a.res_c0 = res.data_ptr(), res.stride(0), res.shape[3], 0
     a.y, a.y_bs, a.y_ps, a.y_c0 = out.data_ptr(), out.stride(0), out.shape[3], out_c0
     a.OH, a.OW, a.Cout, a.Ntiles, a.tn, a.Kc = OH, OW, pk.Cout, pk.Ntiles, pk.tn, pk.Kc
-    if pk.w32 is not None and stride == 1 and pad == 0 and not nchw_in:
+    if pk.w32 is not None and not nchw_in:
         a.w32, a.ntiles32, a.tn32 = pk.w32.data_ptr(), pk.ntiles32, pk.tn32
     a.KH, a.KW, a.stride, a.pad = pk.KH, pk.KW, stride, pad
     a.act, a.slope = ACT[act], float(slope)

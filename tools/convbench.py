@@ -51,6 +51,9 @@ R50 = [
     ("l4.c1", 16, 32, 32, 2048, 512, 1, 1, 0, 0, 0, "relu"),
     ("l4.c2", 16, 32, 32, 512, 512, 3, 1, 0, 0, 0, "relu"),
     ("l4.c3", 16, 32, 32, 512, 2048, 1, 1, 0, 0, 1, "relu"),
+    ("l2.c2s2", 16, 256, 256, 128, 128, 3, 2, 0, 0, 0, "relu"),
+    ("l4.c2s2", 16, 64, 64, 512, 512, 3, 2, 0, 0, 0, "relu"),
+    ("l3.c2as", 16, 64, 64, 256, 256, 3, 1, 0, 1, 0, "relu"),
 ]
 
 
