@@ -101,6 +101,7 @@ def conv_roofline(model, x, steps):
         K = pk.KH * pk.KW * pk.Cin + pk.Cin2
         # algorithmic bytes: input read once, weights once, output written once
         nbytes = 4.0 * (xx.numel() + (kw["x2"].numel() if kw.get("x2") is not None else 0)
+                        + (kw["res"].numel() if kw.get("res") is not None else 0)
                         + K * pk.Cout + M * pk.Cout)
         recs.append((s, e, 2.0 * M * K * pk.Cout, nbytes))
         return out
@@ -127,6 +128,35 @@ def conv_roofline(model, x, steps):
     nbytes = sum(r[3] for r in recs)
     n = len(recs) // steps
     return flops / steps, t_ms / steps, n, nbytes / steps
+
+
+def r50_roofline(device, size, batch=16, steps=3):
+    """Conv-stack roofline of the R50 RetinaFace (configs[2] model) eval forward:
+    the compute-bound backbone of BASELINE.json's north-star conv target."""
+    from nets.retinaface_eca_nonlocal import RetinaFace
+    from nets.retinaface_training import weights_init
+    from utils.config import cfg_re50
+    from jabd_amd import synth
+    import contextlib
+    import io
+    torch.manual_seed(0)
+    m = RetinaFace(cfg=cfg_re50, mode="eval")
+    with contextlib.redirect_stdout(io.StringIO()):
+        weights_init(m)
+    m = m.eval().to(device)
+    x = synth.images(batch, size, seed=99, device=device)
+    with torch.no_grad():
+        for _ in range(2):
+            m(x)
+    torch.cuda.synchronize()
+    flops, t_ms, n, nbytes = conv_roofline(m, x, steps)
+    ach = flops / (t_ms * 1e-3) / 1e12
+    del m, x
+    torch.cuda.empty_cache()
+    return {"bound": "mfma", "kernel": f"R50 RetinaFace eval forward conv stack ({n} launches)",
+            "workload": f"bs{batch} {size}x{size}", "achieved": ach,
+            "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_FP32_MFMA_TFLOPS,
+            "conv_ms_per_step": t_ms, "conv_gflop_per_step": flops / 1e9}
 
 
 def forward_flops(model, size, batch):
@@ -321,14 +351,9 @@ def main():
     value = imgs / el
 
     extra = {}
-    if not args.no_train:
-        tr = {"C4_mnv3": train_bench("mnv3", args.batch, args.size, args.train_steps, 3, device,
-                                     dist, rank)}
-        if world == 1 and args.r50_batch > 0:
-            tr["C3_r50"] = train_bench("r50", args.r50_batch, args.size, max(2, args.train_steps // 2),
-                                       2, device, None, rank)
-        extra["train"] = tr
     if rank == 0:
+        # conv-stack roofline on the C2 model right after its timed loop (before
+        # the training legs reshuffle the allocator)
         flops_step, t_ms, n_launch, alg_bytes = conv_roofline(model, x, max(3, min(args.steps, 10)))
         ach = flops_step / (t_ms * 1e-3) / 1e12
         pmc = pmc_traffic()
@@ -345,6 +370,16 @@ def main():
             "achieved_hbm_gbs": alg_bytes / (t_ms * 1e-3) / 1e9,
             "hbm_frac": alg_bytes / (t_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
             "conv_ms_per_step": t_ms, "conv_gflop_per_step": flops_step / 1e9}
+        if world == 1 and args.r50_batch > 0:
+            extra["roofline_r50"] = r50_roofline(device, args.size)
+    if not args.no_train:
+        tr = {"C4_mnv3": train_bench("mnv3", args.batch, args.size, args.train_steps, 3, device,
+                                     dist, rank)}
+        if world == 1 and args.r50_batch > 0:
+            tr["C3_r50"] = train_bench("r50", args.r50_batch, args.size, max(2, args.train_steps // 2),
+                                       2, device, None, rank)
+        extra["train"] = tr
+    if rank == 0:
         extra["forward_gflop_per_image"] = forward_flops(model, args.size, 1) / 1e9
         if not args.no_nms:
             extra["nms"] = nms_bench(device)

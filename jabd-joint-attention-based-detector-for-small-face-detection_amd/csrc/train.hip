@@ -921,6 +921,60 @@ __global__ void heads_gather_kernel(const float* __restrict__ gl, const float* _
 // Max-pool backward (gather form): each input pixel sums dy of the windows
 // whose (first, NaN-propagating) argmax it is — F.max_pool2d semantics.
 // ---------------------------------------------------------------------------
+// Channel-vectorised form (C % 4 == 0): one thread per (input pixel, 4
+// channels), 32-bit index math, only the windows that contain the pixel, the
+// argmax of each recomputed with the same first-max / last-NaN rule per
+// channel.  Deterministic gather (no atomics).
+__global__ __launch_bounds__(256) void maxpool_bwd4_kernel(const float* __restrict__ x,
+                                                          const float* __restrict__ dy, int H,
+                                                          int W, int C4, int OH, int OW, int k,
+                                                          int s, int pad, int total,
+                                                          float* __restrict__ dx) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c4 = i % C4;
+  int r = i / C4;
+  const int iw = r % W;
+  r /= W;
+  const int ih = r % H;
+  const int b = r / H;
+  const float4* xb = reinterpret_cast<const float4*>(x) + (int64_t)b * H * W * C4 + c4;
+  const float4* dyb = reinterpret_cast<const float4*>(dy) + (int64_t)b * OH * OW * C4 + c4;
+  // windows (oh, ow) with oh*s - pad <= ih <= oh*s - pad + k - 1
+  const int oh0 = max(0, (ih + pad - k + s) / s), oh1 = min(OH - 1, (ih + pad) / s);
+  const int ow0 = max(0, (iw + pad - k + s) / s), ow1 = min(OW - 1, (iw + pad) / s);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const int me = ih * W + iw;
+  for (int oh = oh0; oh <= oh1; ++oh)
+    for (int ow = ow0; ow <= ow1; ++ow) {
+      float best[4];
+      int arg[4] = {-1, -1, -1, -1};
+      for (int a = 0; a < k; ++a) {
+        const int yh = oh * s - pad + a;
+        if (yh < 0 || yh >= H) continue;
+        for (int q = 0; q < k; ++q) {
+          const int yw = ow * s - pad + q;
+          if (yw < 0 || yw >= W) continue;
+          const int pos = yh * W + yw;
+          const float4 v4 = xb[(int64_t)pos * C4];
+          const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (arg[e] < 0 || v[e] > best[e] || v[e] != v[e]) {
+              best[e] = v[e];
+              arg[e] = pos;
+            }
+        }
+      }
+      const float4 g = dyb[(int64_t)(oh * OW + ow) * C4];
+      if (arg[0] == me) acc[0] += g.x;
+      if (arg[1] == me) acc[1] += g.y;
+      if (arg[2] == me) acc[2] += g.z;
+      if (arg[3] == me) acc[3] += g.w;
+    }
+  reinterpret_cast<float4*>(dx)[i] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+}
+
 __global__ void maxpool_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy, int H,
                                    int W, int C, int OH, int OW, int k, int s, int pad,
                                    int64_t total, float* __restrict__ dx) {
@@ -1178,6 +1232,14 @@ extern "C" int jabd_maxpool_bwd_f32(const float* x, const float* dy, int32_t B, 
   JABD_REQUIRE(x && dy && dx, "maxpool_bwd: null");
   const int OH = (H + 2 * pad - k) / stride + 1, OW = (W + 2 * pad - k) / stride + 1;
   const int64_t total = (int64_t)B * H * W * C;
+  if (C % 4 == 0 && total / 4 < ((int64_t)1 << 31) &&
+      (reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) |
+       reinterpret_cast<uintptr_t>(dx)) % 16 == 0) {
+    const int t4 = (int)(total / 4);
+    maxpool_bwd4_kernel<<<(unsigned)cdiv(t4, 256), 256, 0, as_stream(stream)>>>(
+        x, dy, H, W, C / 4, OH, OW, k, stride, pad, t4, dx);
+    return check_launch("maxpool_bwd4");
+  }
   maxpool_bwd_kernel<<<(unsigned)cdiv(total, 256), 256, 0, as_stream(stream)>>>(
       x, dy, H, W, C, OH, OW, k, stride, pad, total, dx);
   return check_launch("maxpool_bwd");
