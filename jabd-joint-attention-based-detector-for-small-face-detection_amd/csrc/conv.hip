@@ -587,8 +587,9 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
     if (r >= 0) return r;
   }
   // k x k implicit GEMM on the 32x32 kernel: 32-channel stages inside one tap
-  if (!is1x1 && vec4 && (a.flags & 1) && !a.x2 && a.Cin % 32 == 0 && (!a.tconv || a.stride == 1) &&
-      a.x_bs % 4 == 0 && use_conv32(a)) {
+  if (!is1x1 && vec4 && (a.flags & 1) && !a.x2 && a.Cin % 32 == 0 &&
+      (!a.tconv || a.stride == 1 || (a.stride == 2 && !a.ascale)) && a.x_bs % 4 == 0 &&
+      a.y_bs == OHW * a.y_ps && (!a.res || a.res_bs == OHW * a.res_ps) && use_conv32(a)) {
     const int r = conv1x1_m32_dispatch(a, st, true);
     if (r >= 0) return r;
   }

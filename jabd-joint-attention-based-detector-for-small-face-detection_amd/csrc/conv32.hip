@@ -57,8 +57,12 @@ constexpr int kG = kBK / 8;      // 8-channel groups per stage
 // one tap, host guarantees Cin % 32 == 0, no K-concat source); stride-1
 // transposed form (tconv) for the data gradient.
 template <int TM, int TN, bool KXK>
+// phase >= 0 (KXK, stride-2 tconv): this launch covers only the output
+// pixels (2i + ph, 2j + pw), phase = 2 ph + pw, and only the taps that reach
+// them — the sub-pixel decomposition of a strided data gradient (the other
+// 3/4 of a naive transposed conv's taps read structural zeros).
 __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, int mtiles_img,
-                                                             int per_img) {
+                                                             int per_img, int phase) {
   constexpr int BM = 4 * 32 * TM;
   constexpr int NB4 = kG * TN * 64;            // float4 of one weight stage
   constexpr int NBT = (NB4 + 255) / 256;       // ... per thread
@@ -69,7 +73,14 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
   const int bid = blockIdx.x;
   const int nb = bid % nblk_n, mb = bid / nblk_n;
   const int OHW = p.OH * p.OW;
-  const int M = (int)p.M;
+  // phase geometry: sub-grid SH x SW of output pixels, taps kh0 + 2i, kw0 + 2j
+  const int ph = phase >> 1, pw = phase & 1;
+  const int SH = phase >= 0 ? (p.OH - ph + 1) >> 1 : p.OH;
+  const int SW = phase >= 0 ? (p.OW - pw + 1) >> 1 : p.OW;
+  const int kh0 = phase >= 0 ? (ph + p.pad) & 1 : 0, kw0 = phase >= 0 ? (pw + p.pad) & 1 : 0;
+  const int nkh = phase >= 0 ? (p.KH - kh0 + 1) >> 1 : p.KH;
+  const int nkw = phase >= 0 ? (p.KW - kw0 + 1) >> 1 : p.KW;
+  const int M = phase >= 0 ? p.B * SH * SW : (int)p.M;
   int img = 0, m_lo, m_hi;
   if (per_img) {
     img = mb / mtiles_img;
@@ -85,19 +96,25 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
     const int m = m_lo + wave * 32 * TM + t * 32 + j;
     pm[t] = m < m_hi ? m : -1;
   }
-  const int Kt = KXK ? p.KH * p.KW * p.Cin : p.Cin + (p.x2 ? p.Cin2 : 0);
+  const int Kt = KXK ? nkh * nkw * p.Cin : p.Cin + (p.x2 ? p.Cin2 : 0);
   const int S = (Kt + kBK - 1) / kBK;
-  // KXK: per-lane output coordinates (oh, ow) and image base of each pixel tile
-  int poh[TM], pow_[TM];
+  // KXK: per-lane output coordinates (oh, ow), image base of each pixel tile,
+  // and the flat output pixel om (differs from m in phase mode)
+  int poh[TM], pow_[TM], om[TM];
   int64_t pbase[TM];
+#pragma unroll
+  for (int t = 0; t < TM; ++t) om[t] = pm[t];
   if constexpr (KXK) {
 #pragma unroll
     for (int t = 0; t < TM; ++t) {
       const int m = pm[t] >= 0 ? pm[t] : 0;
-      const int b = m / OHW, r = m - b * OHW;
-      poh[t] = r / p.OW;
-      pow_[t] = r - poh[t] * p.OW;
+      const int SHW = SH * SW;
+      const int b = m / SHW, r = m - b * SHW;
+      const int i = r / SW, jj = r - i * SW;
+      poh[t] = phase >= 0 ? 2 * i + ph : i;
+      pow_[t] = phase >= 0 ? 2 * jj + pw : jj;
       pbase[t] = (int64_t)b * p.x_bs + p.x_c0;
+      if (pm[t] >= 0) om[t] = (b * p.OH + poh[t]) * p.OW + pow_[t];
     }
   }
   const int cps = p.Cin / kBK;  // KXK: stages per tap
@@ -107,12 +124,17 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
 
   auto load_a = [&](int s, float4 (&a)[TM][kG]) {
     if constexpr (KXK) {
-      const int tap = s / cps, ci0 = (s - tap * cps) * kBK;
-      const int kh = tap / p.KW, kw = tap - kh * p.KW;
+      const int tl = s / cps, ci0 = (s - tl * cps) * kBK;
+      const int khi = tl / nkw;
+      const int kh = kh0 + (phase >= 0 ? 2 : 1) * khi;
+      const int kw = kw0 + (phase >= 0 ? 2 : 1) * (tl - khi * nkw);
 #pragma unroll
       for (int t = 0; t < TM; ++t) {
-        const int ih = p.tconv ? poh[t] + p.pad - kh : poh[t] * p.stride - p.pad + kh;
-        const int iw = p.tconv ? pow_[t] + p.pad - kw : pow_[t] * p.stride - p.pad + kw;
+        // tconv: stride 1, or stride 2 in phase mode (the division is exact)
+        const int ih = p.tconv ? (poh[t] + p.pad - kh) >> (phase >= 0 ? 1 : 0)
+                               : poh[t] * p.stride - p.pad + kh;
+        const int iw = p.tconv ? (pow_[t] + p.pad - kw) >> (phase >= 0 ? 1 : 0)
+                               : pow_[t] * p.stride - p.pad + kw;
         const bool ok = pm[t] >= 0 && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
         const float* src = p.x + pbase[t] + ((int64_t)ih * p.W + iw) * p.x_ps + ci0 + 4 * h;
 #pragma unroll
@@ -147,6 +169,12 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
   };
   // weight stage s -> registers (ECA gate applied to the rows k < Cin)
   auto load_b = [&](int s, float4 (&b)[NBT]) {
+    // phase mode: local stage -> the global tap's weight stage
+    if (KXK && phase >= 0) {
+      const int tl = s / cps, khi = tl / nkw;
+      const int tap = (kh0 + 2 * khi) * p.KW + kw0 + 2 * (tl - khi * nkw);
+      s = tap * cps + (s - tl * cps);
+    }
 #pragma unroll
     for (int i = 0; i < NBT; ++i) {
       const int f = i * 256 + threadIdx.x;
@@ -185,9 +213,11 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
       for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
 
   float4 a_cur[TM][kG], a_nxt[TM][kG], b_nxt[NBT];
-  load_a(0, a_cur);
-  load_b(0, b_nxt);
-  store_b(0, b_nxt);
+  if (S > 0) {  // (a phase of a 1x1 stride-2 data gradient has no taps: zeros)
+    load_a(0, a_cur);
+    load_b(0, b_nxt);
+    store_b(0, b_nxt);
+  }
   __syncthreads();
   for (int s = 0; s < S; ++s) {
     const bool more = s + 1 < S;
@@ -235,8 +265,8 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
   // epilogue: acc[t][u][4c + e] = Y[pixel pm[t]][nb*BN + 32u + 8c + 4h + e]
 #pragma unroll
   for (int t = 0; t < TM; ++t) {
-    const int m = pm[t];
-    if (m < 0) continue;
+    const int m = om[t];
+    if (pm[t] < 0) continue;
     float* yrow = p.y + (int64_t)m * p.y_ps + p.y_c0;
     const float* rrow = p.res ? p.res + (int64_t)m * p.res_ps + p.res_c0 : nullptr;
 #pragma unroll
@@ -270,10 +300,24 @@ static int launch_m32(const ConvArgs& a, hipStream_t st) {
   const int64_t OHW = (int64_t)a.OH * a.OW;
   const int per_img = a.ascale != nullptr;
   const int64_t mt_img = cdiv(OHW, BM);
+  if (KXK && a.tconv && a.stride == 2) {  // sub-pixel phases, one launch each
+    JABD_REQUIRE(!per_img, "conv32: phase mode without ascale");
+    for (int ph = 0; ph < 2; ++ph)
+      for (int pw = 0; pw < 2; ++pw) {
+        const int64_t Mp = (int64_t)a.B * ((a.OH - ph + 1) / 2) * ((a.OW - pw + 1) / 2);
+        if (Mp <= 0) continue;
+        const int64_t grid = cdiv(Mp, BM) * (a.Ntiles / TN);
+        JABD_REQUIRE(grid < (int64_t)0x7fffffff, "conv32: grid too large");
+        conv1x1_m32_kernel<TM, TN, KXK><<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, 0,
+                                                                        2 * ph + pw);
+        if (int e = check_launch("conv1x1_m32")) return e;
+      }
+    return JABD_OK;
+  }
   const int64_t mtiles = per_img ? mt_img * a.B : cdiv(a.M, BM);
   const int64_t grid = mtiles * (a.Ntiles / TN);
   JABD_REQUIRE(grid < (int64_t)0x7fffffff, "conv32: grid too large");
-  conv1x1_m32_kernel<TM, TN, KXK><<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, per_img);
+  conv1x1_m32_kernel<TM, TN, KXK><<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, per_img, -1);
   return check_launch("conv1x1_m32");
 }
 

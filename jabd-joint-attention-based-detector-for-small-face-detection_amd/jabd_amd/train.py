@@ -91,7 +91,7 @@ def _conv_args(x, pk, y, stride, pad, nchw_in=False, ascale=None, tconv=False, O
     a.KH, a.KW, a.stride, a.pad = pk.KH, pk.KW, stride, pad
     a.nchw_in = 1 if nchw_in else 0
     a.tconv = 1 if tconv else 0
-    if pk.w32 is not None and not nchw_in and (not tconv or stride == 1):
+    if pk.w32 is not None and not nchw_in and (not tconv or stride <= 2):
         a.w32, a.ntiles32, a.tn32 = pk.w32.data_ptr(), pk.ntiles32, pk.tn32
     return a
 

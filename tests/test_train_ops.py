@@ -28,7 +28,9 @@ def _check(got_list, ref_list, names):
 @pytest.mark.gpu
 @pytest.mark.parametrize("cin,cout,k,s,h", [(16, 64, 1, 1, 12), (40, 40, 3, 1, 9), (256, 128, 3, 1, 4),
                                             (64, 64, 3, 2, 11), (256, 512, 1, 2, 8),
-                                            (12, 10, 3, 1, 7), (1024, 256, 1, 1, 4)])
+                                            (12, 10, 3, 1, 7), (1024, 256, 1, 1, 4),
+                                            (128, 128, 3, 2, 10), (64, 96, 3, 2, 9),
+                                            (96, 64, 1, 2, 7)])
 def test_convfn_grads(cuda, cin, cout, k, s, h):
     from jabd_amd.train import ConvFn
     g = torch.Generator().manual_seed(cin + k)
