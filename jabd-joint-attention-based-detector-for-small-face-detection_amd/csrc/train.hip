@@ -10,6 +10,7 @@
 #include "conv_args.h"
 
 namespace jabd {
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -630,6 +631,150 @@ __global__ __launch_bounds__(256) void wgrad_reduce2_kernel(const float* __restr
 
 static int wv_tile(int64_t n) { return n <= 16 ? 16 : (n <= 32 ? 32 : 64); }
 
+// ---------------------------------------------------------------------------
+// Weight gradient on the 32x32x2 fp32 MFMA: dW[k][n] = sum_m A[m][k] dY[m][n]
+// (A = im2col(x) on the fly, k = tap * Cin + ci).  Workgroup tile KT x NT
+// (4 waves as 2 x 2, wave tile KT/2 x NT/2 of 32x32 blocks) over a chunk of
+// pixels; each stage stages kWg32Px pixels of A and dY in LDS in their
+// natural [pixel][channel] layout (float4 global loads and LDS stores); the
+// MFMA contracts the 2 pixels of a lane half (lane l: pixel 2pp + (l >> 5),
+// row/col l & 31), so every operand read is a conflict-free ds_read_b32 of 32
+// consecutive floats.  2x the FLOPs per LDS operand of the 16x16x4 kernel.
+// Global loads of stage s+1 are in registers while stage s computes.
+// ---------------------------------------------------------------------------
+constexpr int kWg32Px = 32;  // pixels per stage
+
+template <int KT, int NT>
+__global__ __launch_bounds__(256, 2) void conv_wgrad32_kernel(const ConvArgs p, int px_per_wg,
+                                                              int fast1x1,
+                                                              float* __restrict__ part) {
+  constexpr int TK = KT / 64, TNn = NT / 64;          // 32x32 blocks per wave (k, n)
+  constexpr int QA = kWg32Px * KT / 4 / 256, QD = kWg32Px * NT / 4 / 256;
+  __shared__ float Xs[kWg32Px * KT];
+  __shared__ float Ds[kWg32Px * NT];
+  const int K = p.KH * p.KW * p.Cin;
+  const int k0 = blockIdx.x * KT, n0 = blockIdx.y * NT;
+  const int chunk = blockIdx.z;
+  const int mbeg = chunk * px_per_wg;
+  const int mend = min(mbeg + px_per_wg, (int)p.M);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int h = lane >> 5, j = lane & 31;
+  const int wk = (wave >> 1) * (KT / 2), wn = (wave & 1) * (NT / 2);
+  const int OHW = p.OH * p.OW;
+
+  float4 ra[QA], rd[QD];
+  auto load_stage = [&](int px0) {
+#pragma unroll
+    for (int q = 0; q < QA; ++q) {
+      const int idx = q * 256 + t;
+      const int px = idx / (KT / 4), c4 = (idx % (KT / 4)) * 4;
+      const int m = px0 + px, k = k0 + c4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (m < mend && k < K) {
+        const int b = m / OHW;
+        int ci = k;
+        int64_t off;
+        bool ok = true;
+        if (fast1x1) {
+          off = (int64_t)m * p.x_ps + p.x_c0 + k;
+        } else {
+          const int rr = m - b * OHW;
+          const int oh = rr / p.OW, ow = rr - oh * p.OW;
+          const int tap = k / p.Cin;
+          ci = k - tap * p.Cin;
+          const int kh = tap / p.KW, kw = tap - kh * p.KW;
+          const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
+          ok = ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+          off = (int64_t)b * p.x_bs + ((int64_t)ih * p.W + iw) * p.x_ps + p.x_c0 + ci;
+        }
+        if (ok) {
+          v = *reinterpret_cast<const float4*>(p.x + off);
+          if (p.ascale) {
+            const float4 s4 =
+                *reinterpret_cast<const float4*>(p.ascale + (int64_t)b * p.ascale_bs + ci);
+            v.x *= s4.x; v.y *= s4.y; v.z *= s4.z; v.w *= s4.w;
+          }
+        }
+      }
+      ra[q] = v;
+    }
+#pragma unroll
+    for (int q = 0; q < QD; ++q) {
+      const int idx = q * 256 + t;
+      const int px = idx / (NT / 4), c4 = (idx % (NT / 4)) * 4;
+      const int m = px0 + px, n = n0 + c4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (m < mend && n < p.Cout)
+        v = *reinterpret_cast<const float4*>(p.y + (int64_t)m * p.y_ps + p.y_c0 + n);
+      rd[q] = v;
+    }
+  };
+
+  f32x16 acc[TK][TNn];
+#pragma unroll
+  for (int u = 0; u < TK; ++u)
+#pragma unroll
+    for (int v = 0; v < TNn; ++v)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[u][v][r] = 0.f;
+
+  load_stage(mbeg);
+  for (int px0 = mbeg; px0 < mend; px0 += kWg32Px) {
+#pragma unroll
+    for (int q = 0; q < QA; ++q)
+      reinterpret_cast<float4*>(Xs)[q * 256 + t] = ra[q];
+#pragma unroll
+    for (int q = 0; q < QD; ++q)
+      reinterpret_cast<float4*>(Ds)[q * 256 + t] = rd[q];
+    __syncthreads();
+    if (px0 + kWg32Px < mend) load_stage(px0 + kWg32Px);
+#pragma unroll 4
+    for (int pp = 0; pp < kWg32Px / 2; ++pp) {
+      const int row = 2 * pp + h;
+      float a[TK], b[TNn];
+#pragma unroll
+      for (int u = 0; u < TK; ++u) a[u] = Xs[row * KT + wk + 32 * u + j];
+#pragma unroll
+      for (int v = 0; v < TNn; ++v) b[v] = Ds[row * NT + wn + 32 * v + j];
+#pragma unroll
+      for (int u = 0; u < TK; ++u)
+#pragma unroll
+        for (int v = 0; v < TNn; ++v)
+          acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[v], acc[u][v], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // acc[u][v][r]: k = k0 + wk + 32u + 8(r>>2) + 4h + (r&3), n = n0 + wn + 32v + j
+  float* pc = part + (int64_t)chunk * K * p.Cout;
+#pragma unroll
+  for (int u = 0; u < TK; ++u)
+#pragma unroll
+    for (int v = 0; v < TNn; ++v) {
+      const int n = n0 + wn + 32 * v + j;
+      if (n >= p.Cout) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int k = k0 + wk + 32 * u + 8 * (r >> 2) + 4 * h + (r & 3);
+        if (k < K) pc[(int64_t)k * p.Cout + n] = acc[u][v][r];
+      }
+    }
+}
+
+// The 32x32 wgrad kernel takes NHWC/vector shapes with K, Cout >= 64;
+// JABD_WGRAD32=0 forces the 16x16x4 kernels (A/B).
+static bool wgrad32_ok(const ConvArgs& a) {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("JABD_WGRAD32");
+    v = e && e[0] == '0' ? 0 : 1;
+  }
+  const int64_t K = (int64_t)a.KH * a.KW * a.Cin;
+  return v == 1 && K >= 64 && a.Cout >= 64;
+}
+// 128-wide tiles unless they pad more than 1/8 beyond what 64-wide ones do
+static int wg32_tile(int64_t n) { return cdiv(n, 128) * 128 - n <= n / 8 ? 128 : 64; }
+
+
 static bool wgrad_vec_ok(const ConvArgs& a) {
   return !a.nchw_in && a.Cin % 4 == 0 && a.x_ps % 4 == 0 && a.x_c0 % 4 == 0 && a.Cout % 4 == 0 &&
          a.y_ps % 4 == 0 && a.y_c0 % 4 == 0 && a.y_bs == (int64_t)a.OH * a.OW * a.y_ps &&
@@ -639,7 +784,9 @@ static bool wgrad_vec_ok(const ConvArgs& a) {
 static int64_t wgrad_chunks(const ConvArgs& a) {
   const int64_t K = (int64_t)a.KH * a.KW * a.Cin;
   const bool vec = wgrad_vec_ok(a);
-  const int64_t tk = vec ? wv_tile(K) : kWgT, tn = vec ? wv_tile(a.Cout) : kWgT;
+  const bool w32 = vec && wgrad32_ok(a);
+  const int64_t tk = w32 ? wg32_tile(K) : (vec ? wv_tile(K) : kWgT);
+  const int64_t tn = w32 ? wg32_tile(a.Cout) : (vec ? wv_tile(a.Cout) : kWgT);
   const int64_t tiles = cdiv(K, tk) * cdiv(a.Cout, tn);
   int64_t nchunk = cdiv(2048, tiles);
   const int64_t maxchunk = cdiv(a.M, kWgPx);
@@ -1103,7 +1250,17 @@ extern "C" int jabd_conv_wgrad_f32(const jabd_conv_args* args, float* part, floa
   const int64_t per = cdiv(cdiv(a.M, nchunk), kWgPx) * kWgPx;
   const int64_t nch = cdiv(a.M, per);
   hipStream_t st = as_stream(stream);
-  if (wgrad_vec_ok(a)) {
+  if (wgrad_vec_ok(a) && wgrad32_ok(a)) {
+    const int tk = wg32_tile(K), tn = wg32_tile(a.Cout);
+    const int fast = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.H == a.OH &&
+                     a.W == a.OW;
+    dim3 g((unsigned)cdiv(K, tk), (unsigned)cdiv(a.Cout, tn), (unsigned)nch);
+#define W32_CASE(KT_, NT_)                                                        \
+  if (tk == KT_ && tn == NT_)                                                     \
+    conv_wgrad32_kernel<KT_, NT_><<<g, 256, 0, st>>>(a, (int)per, fast, part);
+    W32_CASE(64, 64) W32_CASE(64, 128) W32_CASE(128, 64) W32_CASE(128, 128)
+#undef W32_CASE
+  } else if (wgrad_vec_ok(a)) {
     const int tk = wv_tile(K), tn = wv_tile(a.Cout);
     const int fast = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.H == a.OH &&
                      a.W == a.OW;
