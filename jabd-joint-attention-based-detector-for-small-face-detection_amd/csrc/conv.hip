@@ -338,7 +338,7 @@ __global__ __launch_bounds__(256) void conv1x1_kernel(const ConvArgs p) {
     for (int t = 0; t < TM; ++t) {
       float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
       const int m = pm[t];
-      if (m >= 0) {
+      if (m >= 0 && !(p.reserved1 & 1)) {
         if (k4 < p.Cin) {
           r = *reinterpret_cast<const float4*>(xg + m * p.x_ps + kc * 16);
           if (ASCALE) {
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(256) void conv1x1_kernel(const ConvArgs p) {
         v.y = act_apply(v.y, p.act, p.slope);
         v.z = act_apply(v.z, p.act, p.slope);
         v.w = act_apply(v.w, p.act, p.slope);
-        *reinterpret_cast<float4*>(p.y + m * p.y_ps + p.y_c0 + n0) = v;
+        if (!(p.reserved1 & 2)) *reinterpret_cast<float4*>(p.y + m * p.y_ps + p.y_c0 + n0) = v;
       }
     }
     __syncthreads();
@@ -598,9 +598,21 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
   // 256 CUs several times over.
   const int64_t nblk_n = a.Ntiles / tn;
   auto grid_for = [&](int tm) { return cdiv(a.M, (int64_t)64 * tm) * nblk_n; };
-  const int tm_max = tn == 8 ? 2 : 4;
+  // Short-K GEMMs are load-latency bound with few k-steps per wave: fewer
+  // pixel tiles per wave (fewer VGPRs, more resident waves) overlap more
+  // loads with MFMAs (measured on the C2 layers: tools/convbench.py).
+  const int Kall = a.KH * a.KW * a.Cin + (a.x2 ? a.Cin2 : 0);
+  const int tm_max = tn == 8 ? 2 : (Kall <= 32 ? 2 : (Kall <= 160 ? 1 : (Kall <= 400 ? 2 : 4)));
   int tm = tm_max;
   while (tm > 1 && grid_for(tm) < 1024) tm >>= 1;
+  {  // JABD_CONV_TM=1|2|4 forces the pixel tiles per wave (A/B experiments)
+    static int ftm = -1;
+    if (ftm < 0) {
+      const char* e = getenv("JABD_CONV_TM");
+      ftm = e ? atoi(e) : 0;
+    }
+    if (ftm == 1 || ftm == 2 || (ftm == 4 && tn != 8)) tm = ftm;
+  }
   const int r = fast1x1 ? dispatch_conv<true>(a, tn, tm, vec4, st) : -1;
   if (r >= 0) return r;
   const int r2 = dispatch_conv<false>(a, tn, tm, vec4, st);

@@ -127,6 +127,9 @@ def pack_dw(conv, bn):
 
 
 # ----------------------------------------------------------------------------- kernels
+_CONV_DBG = 0  # load/store skip mask for tools/convbench.py timing experiments only
+
+
 def conv(x, pk, stride=1, pad=0, act="none", slope=0.0, ascale=None, x2=None, x2_stride=1,
          res=None, out=None, out_c0=0, nchw_in=False, x_c0=0):
     """Implicit-GEMM conv.  x [B,H,W,C*] NHWC (or NCHW input if nchw_in)."""
@@ -161,6 +164,7 @@ def conv(x, pk, stride=1, pad=0, act="none", slope=0.0, ascale=None, x2=None, x2
     a.KH, a.KW, a.stride, a.pad = pk.KH, pk.KW, stride, pad
     a.act, a.slope = ACT[act], float(slope)
     a.nchw_in = 1 if nchw_in else 0
+    a.reserved1 = _CONV_DBG
     call("jabd_conv2d_nhwc_f32", ctypes.byref(a), _stream())
     return out
 

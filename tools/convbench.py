@@ -94,6 +94,7 @@ def run(shape, reps):
     pk = F.PackedConv(w2d, bias, k, k, cin, c2)
     kw = dict(stride=stride, pad=k // 2, act=act, slope=0.1, ascale=sc, x2=x2, res=res)
     y = F.conv(x, pk, **kw)
+    F._CONV_DBG = int(os.environ.get("CONV_DBG", "0"))
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.backends.cudnn.allow_tf32 = False
     r = ref(x, w2d, bias, k, stride, x2, sc, res, act)
