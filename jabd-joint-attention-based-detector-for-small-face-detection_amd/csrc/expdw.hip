@@ -342,6 +342,191 @@ __global__ __launch_bounds__(256, EC == 16 ? 3 : 2) void expdw_kernel(const jabd
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Non-persistent form: one workgroup per work item (tile x EC-chunk), no
+// state carried across items.  The persistent kernel above spends ~1100
+// instructions per item-wave (SGPR spills to VGPR lanes, loop-carried copies
+// of the prefetched operands, a branch per epilogue block); this one decodes
+// its item once, loads through a buffer descriptor whose range check zeroes
+// out-of-image pixels (no branch per load), and builds the expanded tile with
+// selects.  Latency hiding comes from the resident workgroups instead of a
+// cross-item register prefetch.
+// ---------------------------------------------------------------------------
+template <int K, int S, int TH, int TW, int EC, int ACT>
+__global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p, const XdDivs dv,
+                                                       int nitems) {
+  using C = XdCfg<K, S, TH, TW, EC>;
+  constexpr int NPF = (C::IPAD * 4 + 255) / 256;
+  constexpr int NWD = (K * K + 1) * C::NC4;
+  __shared__ __attribute__((aligned(16))) float lds[C::LDS];
+  __shared__ float4 wsh[K * K + 1][C::NC4];
+  XdItem it;
+  if (!xd_item<K, S, TH, TW, EC>(p, blockIdx.x, dv, nitems, it)) return;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, j = lane & 15, g = lane >> 4;
+  const int ntw = wave % C::NNT;
+  const int nt = it.c0 / 16 + ntw;
+  const bool ntv = nt < p.Ntiles;
+  const int ntc = ntv ? nt : 0;
+  const f32x4* wpk = reinterpret_cast<const f32x4*>(p.we);
+  // small operands first (consumed after the expand phase)
+  const int chb = it.c0 + 16 * ntw + 4 * g;
+  const bool chok = chb < p.E;
+  const float4 pbi = *reinterpret_cast<const float4*>(p.be + (chok ? chb : 0));
+  float4 pwd = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (t < NWD) {
+    const int tp = t / C::NC4, cc = it.c0 + 4 * (t - tp * C::NC4);
+    const float4 w = *reinterpret_cast<const float4*>((tp < K * K ? p.wd + tp * p.E : p.bd) +
+                                                      (cc < p.E ? cc : 0));
+    pwd = cc < p.E ? w : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // input stage loads through a buffer descriptor: an out-of-range slot gets
+  // voffset 0xFFFFFFF0 and reads zeros (host: x < 4 GiB)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.x), (short)0, (int)(uint32_t)((int64_t)p.B * p.x_bs * 4), 0x00020000);
+  const int cq = (t & 3) * 4;
+  float4 pf[NPF];
+  auto load_stage = [&](int kc) {
+    const int cofs = 16 * kc + cq;
+    const uint32_t base = (uint32_t)(it.b * p.x_bs + cofs);
+#pragma unroll
+    for (int u = 0; u < NPF; ++u) {
+      const int px = (u * 256 + t) >> 2;
+      const int r = px / C::IW, c = px - r * C::IW;
+      const int ih = it.ih0 + r, iw = it.iw0 + c;
+      const bool ok = px < C::IPX && cofs < p.Cin && (unsigned)ih < (unsigned)p.H &&
+                      (unsigned)iw < (unsigned)p.W;
+      const uint32_t off = ok ? (base + (uint32_t)((ih * p.W + iw) * p.x_ps)) * 4u : 0xFFFFFFF0u;
+      pf[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+    }
+  };
+  f32x4 acc[C::BPW];
+#pragma unroll
+  for (int u = 0; u < C::BPW; ++u) acc[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  load_stage(0);
+  for (int kc = 0; kc < p.Kc; ++kc) {
+    f32x4 a = wpk[(kc * p.Ntiles + ntc) * 64 + lane];
+#pragma unroll
+    for (int u = 0; u < NPF; ++u) {
+      const int idx = u * 256 + t;
+      if (idx < C::IPAD * 4)
+        *reinterpret_cast<float4*>(lds + (idx >> 2) * C::XP + (idx & 3) * 4) = pf[u];
+    }
+    __syncthreads();
+    if (kc + 1 < p.Kc) load_stage(kc + 1);
+    if (!ntv) a = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < C::BPW; ++u) {
+      const int blk = wave + 4 * u;
+      if (blk < C::NBLK) {
+        const int pb = blk / C::NNT;
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(lds + (pb * 16 + j) * C::XP + 4 * g);
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bv.x, acc[u], 0, 0, 0);
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bv.y, acc[u], 0, 0, 0);
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bv.z, acc[u], 0, 0, 0);
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bv.w, acc[u], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // expanded tile: bias + act, zero outside the image / on padded channels
+#pragma unroll
+  for (int u = 0; u < C::BPW; ++u) {
+    const int blk = wave + 4 * u;
+    if (blk < C::NBLK) {
+      const int pb = blk / C::NNT;
+      const int px = pb * 16 + j, ch = 16 * ntw + 4 * g;
+      const int r = px / C::IW, c = px - r * C::IW;
+      const int ih = it.ih0 + r, iw = it.iw0 + c;
+      const bool ok = chok && px < C::IPX && (unsigned)ih < (unsigned)p.H &&
+                      (unsigned)iw < (unsigned)p.W;
+      float4 o;
+      o.x = ok ? xd_act<ACT>(acc[u][0] + pbi.x) : 0.f;
+      o.y = ok ? xd_act<ACT>(acc[u][1] + pbi.y) : 0.f;
+      o.z = ok ? xd_act<ACT>(acc[u][2] + pbi.z) : 0.f;
+      o.w = ok ? xd_act<ACT>(acc[u][3] + pbi.w) : 0.f;
+      *reinterpret_cast<float4*>(lds + px * C::EP + ch) = o;
+    }
+  }
+  if (t < NWD) wsh[t / C::NC4][t % C::NC4] = pwd;
+  __syncthreads();
+
+  // depthwise phase
+  const int c4 = t % C::NC4, chl = 4 * c4;
+  const bool chv = it.c0 + chl < p.E;
+  float4 psum = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (chv) {
+    const float4 bias2 = wsh[K * K][c4];
+    float* yb = p.y + (int64_t)it.b * p.y_bs + it.c0 + chl;
+#pragma unroll 1
+    for (int itm = t; itm < C::ITEMS; itm += 256) {
+      const int strip = itm / C::NC4;
+      const int orow = strip / C::NSTRIP, st = strip - orow * C::NSTRIP;
+      const int oh = it.oh0 + orow, owb = it.ow0 + st * C::PW;
+      if (oh >= p.OH || owb >= p.OW) continue;
+      float4 a2[C::PW];
+#pragma unroll
+      for (int o = 0; o < C::PW; ++o) a2[o] = bias2;
+#pragma unroll 1
+      for (int kh = 0; kh < K; ++kh) {
+        const float* rowp = lds + ((orow * S + kh) * C::IW + st * C::PW * S) * C::EP + chl;
+        float4 row[C::SPAN];
+#pragma unroll
+        for (int c = 0; c < C::SPAN; ++c)
+          row[c] = *reinterpret_cast<const float4*>(rowp + c * C::EP);
+        float4 wk[K];
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw) wk[kw] = wsh[kh * K + kw][c4];
+#pragma unroll
+        for (int o = 0; o < C::PW; ++o)
+#pragma unroll
+          for (int kw = 0; kw < K; ++kw) {
+            const float4 xv = row[o * S + kw], wv = wk[kw];
+            a2[o].x = fmaf(xv.x, wv.x, a2[o].x);
+            a2[o].y = fmaf(xv.y, wv.y, a2[o].y);
+            a2[o].z = fmaf(xv.z, wv.z, a2[o].z);
+            a2[o].w = fmaf(xv.w, wv.w, a2[o].w);
+          }
+      }
+#pragma unroll
+      for (int o = 0; o < C::PW; ++o) {
+        if (owb + o >= p.OW) break;
+        float4 v;
+        v.x = xd_act<ACT>(a2[o].x);
+        v.y = xd_act<ACT>(a2[o].y);
+        v.z = xd_act<ACT>(a2[o].z);
+        v.w = xd_act<ACT>(a2[o].w);
+        *reinterpret_cast<float4*>(yb + ((int64_t)oh * p.OW + owb + o) * p.y_ps) = v;
+        psum.x += v.x; psum.y += v.y; psum.z += v.z; psum.w += v.w;
+      }
+    }
+  }
+  if (p.part) {
+#pragma unroll
+    for (int off = C::NC4; off < 64; off <<= 1) {
+      psum.x += __shfl_xor(psum.x, off);
+      psum.y += __shfl_xor(psum.y, off);
+      psum.z += __shfl_xor(psum.z, off);
+      psum.w += __shfl_xor(psum.w, off);
+    }
+    __syncthreads();
+    float4* red = reinterpret_cast<float4*>(lds);
+    if (lane < C::NC4) red[wave * C::NC4 + lane] = psum;
+    __syncthreads();
+    if (t < C::NC4 && it.c0 + 4 * t < p.E) {
+      const float4 a0 = red[t], a1 = red[C::NC4 + t], a2 = red[2 * C::NC4 + t],
+                   a3 = red[3 * C::NC4 + t];
+      float4 sm;
+      sm.x = (a0.x + a1.x) + (a2.x + a3.x);
+      sm.y = (a0.y + a1.y) + (a2.y + a3.y);
+      sm.z = (a0.z + a1.z) + (a2.z + a3.z);
+      sm.w = (a0.w + a1.w) + (a2.w + a3.w);
+      *reinterpret_cast<float4*>(p.part + ((int64_t)it.b * (int)dv.tiles_img.d + it.t_in) * p.E +
+                                 it.c0 + 4 * t) = sm;
+    }
+  }
+}
+
 static int64_t xd_grid(const void* fn, int64_t nitems) {
   static int cus = 0;
   if (!cus) {
@@ -411,8 +596,19 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
                   make_fastdiv((uint32_t)tiles_w)};
   // persistent grid = the workgroups that are resident at once (a multiple of
   // 8 for XCD-stable item ownership; any more would run as a late tail)
+  static int xdv = -1;  // JABD_EXPDW_V=1: the persistent kernel (A/B)
+  if (xdv < 0) {
+    const char* e = getenv("JABD_EXPDW_V");
+    xdv = e && e[0] == '1' ? 1 : 2;
+  }
+  const bool v2 = xdv == 2 && (int64_t)a.B * a.x_bs * 4 < ((int64_t)1 << 32) - 16;
 #define XD_LAUNCH(K_, S_, TH_, TW_, EC_, ACT_)                                                \
   do {                                                                                        \
+    if (v2) {                                                                                 \
+      expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_><<<(unsigned)nitems, 256, 0, st>>>(a, dv,    \
+                                                                              (int)nitems);   \
+      break;                                                                                  \
+    }                                                                                         \
     const int64_t grid = xd_grid((const void*)expdw_kernel<K_, S_, TH_, TW_, EC_, ACT_>, nitems); \
     expdw_kernel<K_, S_, TH_, TW_, EC_, ACT_><<<(unsigned)grid, 256, 0, st>>>(a, dv,         \
                                                                              (int)nitems);    \
