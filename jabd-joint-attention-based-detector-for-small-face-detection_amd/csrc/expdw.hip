@@ -363,6 +363,10 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
   __shared__ float4 wsh[K * K + 1][C::NC4];
   XdItem it;
   if (!xd_item<K, S, TH, TW, EC>(p, blockIdx.x, dv, nitems, it)) return;
+  // the whole input tile (halo included) inside the image: no per-pixel
+  // bounds in the loads or the expanded-tile epilogue (most tiles)
+  const bool interior =
+      it.ih0 >= 0 && it.iw0 >= 0 && it.ih0 + C::IH <= p.H && it.iw0 + C::IW <= p.W;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, j = lane & 15, g = lane >> 4;
   const int ntw = wave % C::NNT;
   const int nt = it.c0 / 16 + ntw;
@@ -389,20 +393,23 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
   auto load_stage = [&](int kc) {
     const int cofs = 16 * kc + cq;
     const uint32_t base = (uint32_t)(it.b * p.x_bs + cofs);
+    const bool cok = cofs < p.Cin;
 #pragma unroll
     for (int u = 0; u < NPF; ++u) {
       const int px = (u * 256 + t) >> 2;
       const int r = px / C::IW, c = px - r * C::IW;
       const int ih = it.ih0 + r, iw = it.iw0 + c;
-      const bool ok = px < C::IPX && cofs < p.Cin && (unsigned)ih < (unsigned)p.H &&
-                      (unsigned)iw < (unsigned)p.W;
+      const bool ok = px < C::IPX && cok &&
+                      (interior || ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W));
       const uint32_t off = ok ? (base + (uint32_t)((ih * p.W + iw) * p.x_ps)) * 4u : 0xFFFFFFF0u;
       pf[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
     }
   };
+  // accumulators start at the expand bias (no epilogue add)
   f32x4 acc[C::BPW];
+  const f32x4 bias4 = (f32x4){pbi.x, pbi.y, pbi.z, pbi.w};
 #pragma unroll
-  for (int u = 0; u < C::BPW; ++u) acc[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int u = 0; u < C::BPW; ++u) acc[u] = bias4;
   load_stage(0);
   for (int kc = 0; kc < p.Kc; ++kc) {
     f32x4 a = wpk[(kc * p.Ntiles + ntc) * 64 + lane];
@@ -429,23 +436,41 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
     }
     __syncthreads();
   }
-  // expanded tile: bias + act, zero outside the image / on padded channels
+  // expanded tile: act, zero outside the image / on padded channels
+  if (interior) {
 #pragma unroll
-  for (int u = 0; u < C::BPW; ++u) {
-    const int blk = wave + 4 * u;
-    if (blk < C::NBLK) {
-      const int pb = blk / C::NNT;
-      const int px = pb * 16 + j, ch = 16 * ntw + 4 * g;
-      const int r = px / C::IW, c = px - r * C::IW;
-      const int ih = it.ih0 + r, iw = it.iw0 + c;
-      const bool ok = chok && px < C::IPX && (unsigned)ih < (unsigned)p.H &&
-                      (unsigned)iw < (unsigned)p.W;
-      float4 o;
-      o.x = ok ? xd_act<ACT>(acc[u][0] + pbi.x) : 0.f;
-      o.y = ok ? xd_act<ACT>(acc[u][1] + pbi.y) : 0.f;
-      o.z = ok ? xd_act<ACT>(acc[u][2] + pbi.z) : 0.f;
-      o.w = ok ? xd_act<ACT>(acc[u][3] + pbi.w) : 0.f;
-      *reinterpret_cast<float4*>(lds + px * C::EP + ch) = o;
+    for (int u = 0; u < C::BPW; ++u) {
+      const int blk = wave + 4 * u;
+      if (blk < C::NBLK) {
+        const int pb = blk / C::NNT;
+        const int px = pb * 16 + j, ch = 16 * ntw + 4 * g;
+        const bool ok = chok && (pb * 16 + 16 <= C::IPX || px < C::IPX);
+        float4 o;
+        o.x = ok ? xd_act<ACT>(acc[u][0]) : 0.f;
+        o.y = ok ? xd_act<ACT>(acc[u][1]) : 0.f;
+        o.z = ok ? xd_act<ACT>(acc[u][2]) : 0.f;
+        o.w = ok ? xd_act<ACT>(acc[u][3]) : 0.f;
+        *reinterpret_cast<float4*>(lds + px * C::EP + ch) = o;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < C::BPW; ++u) {
+      const int blk = wave + 4 * u;
+      if (blk < C::NBLK) {
+        const int pb = blk / C::NNT;
+        const int px = pb * 16 + j, ch = 16 * ntw + 4 * g;
+        const int r = px / C::IW, c = px - r * C::IW;
+        const int ih = it.ih0 + r, iw = it.iw0 + c;
+        const bool ok = chok && px < C::IPX && (unsigned)ih < (unsigned)p.H &&
+                        (unsigned)iw < (unsigned)p.W;
+        float4 o;
+        o.x = ok ? xd_act<ACT>(acc[u][0]) : 0.f;
+        o.y = ok ? xd_act<ACT>(acc[u][1]) : 0.f;
+        o.z = ok ? xd_act<ACT>(acc[u][2]) : 0.f;
+        o.w = ok ? xd_act<ACT>(acc[u][3]) : 0.f;
+        *reinterpret_cast<float4*>(lds + px * C::EP + ch) = o;
+      }
     }
   }
   if (t < NWD) wsh[t / C::NC4][t % C::NC4] = pwd;
@@ -527,6 +552,7 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
   }
 }
 
+
 static int64_t xd_grid(const void* fn, int64_t nitems) {
   static int cus = 0;
   if (!cus) {
@@ -555,6 +581,15 @@ static XdTile xd_tile(int k, int s) {
 }  // namespace jabd
 
 using namespace jabd;
+
+static int xd_version() {
+  static int xdv = -1;  // JABD_EXPDW_V=1: the persistent kernel (A/B), else workgroup-per-item
+  if (xdv < 0) {
+    const char* e = getenv("JABD_EXPDW_V");
+    xdv = e && e[0] == '1' ? 1 : 2;
+  }
+  return xdv;
+}
 
 extern "C" int64_t jabd_expand_dw_nblk(int32_t OH, int32_t OW, int32_t k, int32_t stride) {
   if (OH <= 0 || OW <= 0 || (stride != 1 && stride != 2)) return -1;
@@ -585,7 +620,9 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
     const char* e = getenv("JABD_EXPDW_EC16");
     ec16 = e && e[0] == '1' ? 1 : 0;
   }
-  const int EC = (a.E <= 16 || ec16) ? 16 : 32;
+  // 16-channel chunks for small E, and for the 5x5 stride-2 tile (19x19 input
+  // pixels: the 32-channel tile's LDS allows only 2 resident workgroups)
+  const int EC = (a.E <= 16 || ec16 || (a.k == 5 && a.stride == 2 && a.Cin <= 32)) ? 16 : 32;
   const int nch = (int)cdiv(a.E, EC);
   const int64_t ntiles = (int64_t)a.B * tiles_img;
   const int64_t nitems = cdiv(ntiles, 8) * 8 * nch;
@@ -596,12 +633,7 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
                   make_fastdiv((uint32_t)tiles_w)};
   // persistent grid = the workgroups that are resident at once (a multiple of
   // 8 for XCD-stable item ownership; any more would run as a late tail)
-  static int xdv = -1;  // JABD_EXPDW_V=1: the persistent kernel (A/B)
-  if (xdv < 0) {
-    const char* e = getenv("JABD_EXPDW_V");
-    xdv = e && e[0] == '1' ? 1 : 2;
-  }
-  const bool v2 = xdv == 2 && (int64_t)a.B * a.x_bs * 4 < ((int64_t)1 << 32) - 16;
+  const bool v2 = xd_version() != 1 && (int64_t)a.B * a.x_bs * 4 < ((int64_t)1 << 32) - 16;
 #define XD_LAUNCH(K_, S_, TH_, TW_, EC_, ACT_)                                                \
   do {                                                                                        \
     if (v2) {                                                                                 \
