@@ -51,51 +51,43 @@ __global__ __launch_bounds__(kSumThreads) void channel_sum_kernel(
 }
 
 // scale[b][c] = gate( sum_t w[t] * mean[b][c + t - (k-1)/2] )   (zero padded)
-__global__ void eca_gate_kernel(const float* __restrict__ part, int64_t nblk, int C, float inv_hw,
-                                const float* __restrict__ w1d, int k, int gate,
-                                float* __restrict__ scale, float* __restrict__ mean_out) {
-  extern __shared__ float mean[];
-  __shared__ float red[256];
-  const int b = blockIdx.x;
-  const float* pb = part + (int64_t)b * nblk * C;
-  // channels across `lanes` threads, partial blocks across 256/lanes rows,
-  // then a fixed-order combine (deterministic)
-  const int lanes = C < 64 ? C : 64;
-  const int rows = blockDim.x / lanes;
-  const int t = threadIdx.x, r = t / lanes, cl = t - (t / lanes) * lanes;
-  for (int c0 = 0; c0 < C; c0 += lanes) {  // uniform trip count (barriers inside)
-    const int c = c0 + cl;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    if (r < rows && c < C) {
-      int64_t q = r;
-      for (; q + 3 * rows < nblk; q += 4 * rows) {
-        s0 += pb[q * C + c];
-        s1 += pb[(q + rows) * C + c];
-        s2 += pb[(q + 2 * rows) * C + c];
-        s3 += pb[(q + 3 * rows) * C + c];
-      }
-      for (; q < nblk; q += rows) s0 += pb[q * C + c];
-    }
-    red[t] = (s0 + s1) + (s2 + s3);
-    __syncthreads();
-    if (t < lanes && c < C) {
-      float sm = 0.f;
-      for (int q = 0; q < rows; ++q) sm += red[q * lanes + t];
-      mean[c] = sm * inv_hw;
-      if (mean_out) mean_out[(int64_t)b * C + c] = mean[c];
-    }
-    __syncthreads();
-  }
-  __syncthreads();
+// One thread per channel of a block's window [c0 - h, c0 - h + blockDim):
+// mean over the partial rows in row order, then the Conv1d over the window
+// and the gate for the blockDim - 2h channels whose taps are all inside it.
+// Grid (channel windows, B); one barrier.
+__global__ __launch_bounds__(256) void eca_gate_kernel(const float* __restrict__ part,
+                                                       int64_t nblk, int C, float inv_hw,
+                                                       const float* __restrict__ w1d, int k,
+                                                       int gate, float* __restrict__ scale,
+                                                       float* __restrict__ mean_out) {
+  __shared__ float mean[256];
   const int h = (k - 1) / 2;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float y = 0.f;
-    for (int t = 0; t < k; ++t) {
-      const int cc = c + t - h;
-      if (cc >= 0 && cc < C) y = fmaf(w1d[t], mean[cc], y);
+  const int oc = blockDim.x - 2 * h;  // output channels per block
+  const int b = blockIdx.y, t = threadIdx.x;
+  const int c = blockIdx.x * oc - h + t;
+  float m = 0.f;
+  if (c >= 0 && c < C) {
+    const float* pb = part + (int64_t)b * nblk * C + c;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // 4 loads in flight, fixed order
+    int64_t r = 0;
+    for (; r + 3 < nblk; r += 4) {
+      s0 += pb[r * C];
+      s1 += pb[(r + 1) * C];
+      s2 += pb[(r + 2) * C];
+      s3 += pb[(r + 3) * C];
     }
-    float g = gate == ACT_SIGMOID ? 1.f / (1.f + expf(-y)) : fminf(fmaxf(y + 3.f, 0.f), 6.f) * (1.f / 6.f);
+    for (; r < nblk; ++r) s0 += pb[r * C];
+    m = ((s0 + s1) + (s2 + s3)) * inv_hw;
+  }
+  mean[t] = m;  // zero outside [0, C): the Conv1d's zero padding
+  __syncthreads();
+  if (t >= h && t < h + oc && c < C) {
+    float y = 0.f;
+    for (int q = 0; q < k; ++q) y = fmaf(w1d[q], mean[t - h + q], y);
+    const float g = gate == ACT_SIGMOID ? 1.f / (1.f + expf(-y))
+                                        : fminf(fmaxf(y + 3.f, 0.f), 6.f) * (1.f / 6.f);
     scale[(int64_t)b * C + c] = g;
+    if (mean_out) mean_out[(int64_t)b * C + c] = m;
   }
 }
 
@@ -406,8 +398,11 @@ extern "C" int jabd_eca_gate_f32(const float* part, int64_t nblk, int64_t B, int
                "eca_gate: bad args");
   JABD_REQUIRE(gate == ACT_SIGMOID || gate == ACT_HSIGMOID, "eca_gate: gate must be (h)sigmoid");
   JABD_REQUIRE(C * sizeof(float) <= 64 * 1024, "eca_gate: C too large");
-  eca_gate_kernel<<<(unsigned)B, 256, C * sizeof(float), as_stream(stream)>>>(
-      part, nblk, (int)C, 1.f / (float)hw, w1d, k, gate, scale, mean_out);
+  JABD_REQUIRE(k <= 31, "eca_gate: k too large");
+  const int oc = 256 - 2 * ((k - 1) / 2);
+  dim3 g((unsigned)cdiv(C, oc), (unsigned)B);
+  eca_gate_kernel<<<g, 256, 0, as_stream(stream)>>>(part, nblk, (int)C, 1.f / (float)hw, w1d, k,
+                                                    gate, scale, mean_out);
   return check_launch("eca_gate");
 }
 
