@@ -175,9 +175,39 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
   const float4* wbase = reinterpret_cast<const float4*>(p.w) + ((int64_t)nb * TN) * 64 + lane;
   const int64_t wstride_k = (int64_t)p.Ntiles * 64;
 
+  // k x k taps walked incrementally (no per-load integer division): the
+  // lane's next float4 is channel tci of tap (tkh, tkw); each K chunk
+  // advances it by 16 channels.  Used for plain forward k x k convs.
+  const bool taps = VEC4 && !p.tconv && !p.x2 && p.KH * p.KW > 1;
+  int tci = 4 * g, tkh = 0, tkw = 0;
+  auto tap_advance = [&](int by) {
+    tci += by;
+    while (tci >= p.Cin) {
+      tci -= p.Cin;
+      if (++tkw == p.KW) { tkw = 0; ++tkh; }
+    }
+  };
+  auto load_tap = [&](int t) -> float4 {
+    float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int ih = poh[t] * p.stride - p.pad + tkh, iw = pow_[t] * p.stride - p.pad + tkw;
+    if (pv[t] && tkh < p.KH && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W) {
+      r = *reinterpret_cast<const float4*>(p.x + (int64_t)pb[t] * p.x_bs +
+                                           ((int64_t)ih * p.W + iw) * p.x_ps + p.x_c0 + tci);
+      if (p.ascale) {
+        const float4 s4 =
+            *reinterpret_cast<const float4*>(p.ascale + (int64_t)pb[t] * p.ascale_bs + tci);
+        r.x *= s4.x; r.y *= s4.y; r.z *= s4.z; r.w *= s4.w;
+      }
+    }
+    return r;
+  };
+  if (taps) tap_advance(0);
+
   float4 a_cur[TM], b_cur[TN];
 #pragma unroll
-  for (int t = 0; t < TM; ++t) a_cur[t] = load_a<VEC4>(p, pb[t], poh[t], pow_[t], pv[t], 4 * g);
+  for (int t = 0; t < TM; ++t)
+    a_cur[t] = taps ? load_tap(t) : load_a<VEC4>(p, pb[t], poh[t], pow_[t], pv[t], 4 * g);
+  if (taps) tap_advance(16);
 #pragma unroll
   for (int u = 0; u < TN; ++u) b_cur[u] = wbase[u * 64];
 
@@ -186,8 +216,14 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
     const bool more = kc + 1 < p.Kc;
     if (more) {
       const int k4 = (kc + 1) * 16 + 4 * g;
+      if (taps) {
 #pragma unroll
-      for (int t = 0; t < TM; ++t) a_nxt[t] = load_a<VEC4>(p, pb[t], poh[t], pow_[t], pv[t], k4);
+        for (int t = 0; t < TM; ++t) a_nxt[t] = load_tap(t);
+        tap_advance(16);
+      } else {
+#pragma unroll
+        for (int t = 0; t < TM; ++t) a_nxt[t] = load_a<VEC4>(p, pb[t], poh[t], pow_[t], pv[t], k4);
+      }
 #pragma unroll
       for (int u = 0; u < TN; ++u) b_nxt[u] = wbase[(kc + 1) * wstride_k + u * 64];
     }
