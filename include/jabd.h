@@ -182,6 +182,11 @@ typedef struct jabd_conv_args {
    * W[8*k8 + 4*(lane>>5) + e][32*nt + (lane&31)], e = 0..3; tn32 tiles per
    * workgroup (jabd_conv_pack_tn32), ntiles32 a multiple of tn32. */
   const void* w32; int32_t ntiles32, tn32;
+  /* optional split output (nullable y2): output channels n >= nsplit go to
+   * y2 at channel y2_c0 + n - nsplit with activation act2/slope2 (two
+   * convolutions of one input fused along N, e.g. the SSH branches that read
+   * the same tensor).  nsplit % 4 == 0; served by the generic kernel. */
+  float* y2; int64_t y2_bs; int32_t y2_ps, y2_c0, nsplit, act2; float slope2; int32_t reserved2;
 } jabd_conv_args;
 /* N-tiles (16 output channels each) grouped per workgroup for a Cout. */
 int jabd_conv_pack_tn(int cout);

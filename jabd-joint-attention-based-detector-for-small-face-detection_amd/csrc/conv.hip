@@ -275,6 +275,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
       const long long yoff = pv[t] ? (long long)((int64_t)pb[t] * p.y_bs + pix * p.y_ps + p.y_c0) : -1;
       const long long roff =
           p.res ? (long long)((int64_t)pb[t] * p.res_bs + pix * p.res_ps + p.res_c0) : 0;
+      const long long y2off =
+          p.y2 ? (long long)((int64_t)pb[t] * p.y2_bs + pix * p.y2_ps + p.y2_c0) : 0;
       __syncthreads();
 #pragma unroll
       for (int f0 = 0; f0 < 16 * 4 * TN; f0 += 64) {
@@ -283,6 +285,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
         // shuffles stay outside the divergent branch (an inactive source lane reads as 0)
         const long long yo = __shfl(yoff, q);
         const long long ro = __shfl(roff, q);
+        const long long y2o = __shfl(y2off, q);
         const int n0 = nb * TN * 16 + 4 * c4;
         if (yo >= 0 && n0 < p.Cout) {
           float4 v = *reinterpret_cast<const float4*>(sm + q * LDW + 4 * c4);
@@ -294,11 +297,19 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
             const float4 rr = *reinterpret_cast<const float4*>(p.res + ro + n0);
             v.x += rr.x; v.y += rr.y; v.z += rr.z; v.w += rr.w;
           }
-          v.x = act_apply(v.x, p.act, p.slope);
-          v.y = act_apply(v.y, p.act, p.slope);
-          v.z = act_apply(v.z, p.act, p.slope);
-          v.w = act_apply(v.w, p.act, p.slope);
-          *reinterpret_cast<float4*>(p.y + yo + n0) = v;
+          if (p.y2 && n0 >= p.nsplit) {  // second fused convolution's channels
+            v.x = act_apply(v.x, p.act2, p.slope2);
+            v.y = act_apply(v.y, p.act2, p.slope2);
+            v.z = act_apply(v.z, p.act2, p.slope2);
+            v.w = act_apply(v.w, p.act2, p.slope2);
+            *reinterpret_cast<float4*>(p.y2 + y2o + (n0 - p.nsplit)) = v;
+          } else {
+            v.x = act_apply(v.x, p.act, p.slope);
+            v.y = act_apply(v.y, p.act, p.slope);
+            v.z = act_apply(v.z, p.act, p.slope);
+            v.w = act_apply(v.w, p.act, p.slope);
+            *reinterpret_cast<float4*>(p.y + yo + n0) = v;
+          }
         }
       }
       __syncthreads();
@@ -583,6 +594,10 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
                  "conv: output size mismatch");
   }
   const bool is1x1 = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
+  JABD_REQUIRE(!a.y2 || (a.nsplit > 0 && a.nsplit % 4 == 0 && a.nsplit < a.Cout &&
+                         a.y2_ps % 4 == 0 && a.y2_c0 % 4 == 0 && a.y2_bs % 4 == 0 &&
+                         (reinterpret_cast<uintptr_t>(a.y2) & 15) == 0 && !a.res && !a.tconv),
+               "conv: split output needs nsplit %% 4 == 0, 16-byte aligned y2, no residual");
   JABD_REQUIRE(!a.x2 || ((a.KH * a.KW * a.Cin) % 4 == 0 && a.Cin2 % 4 == 0 && a.x2_ps % 4 == 0 &&
                          a.x2_stride > 0 && !a.nchw_in),
                "conv: K-concat needs K and Cin2 multiples of 4");
@@ -600,6 +615,7 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
                     (!a.res || (a.res_ps % 4 == 0 && a.res_c0 % 4 == 0 && a.res_bs % 4 == 0)) &&
                     (al & 15) == 0;
     a.flags = v4 ? 1 : 0;
+    JABD_REQUIRE(!a.y2 || v4, "conv: split output needs the vector epilogue layout");
   }
   const bool vec4 = !a.nchw_in && a.Cin % 4 == 0 && a.x_ps % 4 == 0 && a.x_c0 % 4 == 0 &&
                     (reinterpret_cast<uintptr_t>(a.x) & 15) == 0;
@@ -611,7 +627,7 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
                                           std::max<int64_t>(a.res ? a.res_ps : 0,
                                                             a.x2 ? a.x2_ps : 0));
   const bool fast1x1 =
-      is1x1 && !a.tconv && vec4 && (a.flags & 1) && a.x_bs == OHW * a.x_ps &&
+      is1x1 && !a.tconv && vec4 && (a.flags & 1) && !a.y2 && a.x_bs == OHW * a.x_ps &&
       a.y_bs == OHW * a.y_ps && (!a.res || a.res_bs == OHW * a.res_ps) &&
       (!a.ascale || a.ascale_bs % 4 == 0) &&
       (!a.x2 || (a.x2_stride == 1 ? (a.x2_W == a.OW && a.x2_bs == OHW * a.x2_ps)
@@ -623,7 +639,7 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
     if (r >= 0) return r;
   }
   // k x k implicit GEMM on the 32x32 kernel: 32-channel stages inside one tap
-  if (!is1x1 && vec4 && (a.flags & 1) && !a.x2 && a.Cin % 32 == 0 &&
+  if (!is1x1 && vec4 && (a.flags & 1) && !a.x2 && !a.y2 && a.Cin % 32 == 0 &&
       (!a.tconv || a.stride == 1 || (a.stride == 2 && !a.ascale)) && a.x_bs % 4 == 0 &&
       a.y_bs == OHW * a.y_ps && (!a.res || a.res_bs == OHW * a.res_ps) && use_conv32(a)) {
     const int r = conv1x1_m32_dispatch(a, st, true);

@@ -49,6 +49,8 @@ class ConvArgs(ctypes.Structure):
         ("flags", c_i32), ("reserved1", c_i32),
         ("M", c_i64),
         ("w32", c_vp), ("ntiles32", c_i32), ("tn32", c_i32),
+        ("y2", c_vp), ("y2_bs", c_i64), ("y2_ps", c_i32), ("y2_c0", c_i32), ("nsplit", c_i32),
+        ("act2", c_i32), ("slope2", c_f32), ("reserved2", c_i32),
     ]
 
 

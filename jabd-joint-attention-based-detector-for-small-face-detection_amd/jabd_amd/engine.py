@@ -61,7 +61,24 @@ class _Head:
         self.ssh = []
         q = m.ssh1.conv5X5_1[0].out_channels
         qp = (q + 3) // 4 * 4 if q % 4 else None  # 10-channel branches stored as 12
+        # SSH (nets/layers.py:37-68): the two branches that read `o` (conv3X3,
+        # conv5X5_1) and the two that read t (conv5X5_2, conv7X7_2) run as one
+        # GEMM each with a split output (fused along N); every part's output
+        # channels are padded to a multiple of 4 for the vector epilogue.
+        q4 = (q + 3) // 4 * 4
+        h2 = m.ssh1.conv3X3[0].out_channels
+        # (R50's 256-channel SSH keeps five GEMMs: each takes the 32x32 k x k
+        # kernel, which the split output does not)
+        self.ssh_split = h2 % 4 == 0 and m.ssh1.conv3X3[0].in_channels % 32 != 0
         for s in (m.ssh1, m.ssh2, m.ssh3):
+            if self.ssh_split:
+                self.ssh.append((
+                    F.pack_conv_cat([(s.conv3X3[0], s.conv3X3[1], None),
+                                     (s.conv5X5_1[0], s.conv5X5_1[1], qp)]),
+                    F.pack_conv_cat([(s.conv5X5_2[0], s.conv5X5_2[1], q4),
+                                     (s.conv7X7_2[0], s.conv7X7_2[1], qp)], cin_pad=qp),
+                    F.pack_conv(s.conv7x7_3[0], s.conv7x7_3[1], cin_pad=qp)))
+                continue
             self.ssh.append((F.pack_conv(s.conv3X3[0], s.conv3X3[1]),
                              F.pack_conv(s.conv5X5_1[0], s.conv5X5_1[1], cout_pad=qp),
                              F.pack_conv(s.conv5X5_2[0], s.conv5X5_2[1], cin_pad=qp),
@@ -97,13 +114,27 @@ class _Head:
         for i, o in enumerate(levels):
             _, h, w, C = o.shape
             sc = F.eca_gate(F.channel_sums(o), h * w, self.eca_fpn, "sigmoid")
-            c3, c51, c52, c72, c73 = self.ssh[i]
             feat = torch.empty((B, h, w, C), dtype=torch.float32, device=dev)
-            F.conv(o, c3, pad=1, act="relu", ascale=sc, out=feat, out_c0=0)
-            t = F.conv(o, c51, pad=1, act="leaky", slope=self.leaky, ascale=sc)
-            F.conv(t, c52, pad=1, act="relu", out=feat, out_c0=C // 2)
-            t2 = F.conv(t, c72, pad=1, act="leaky", slope=self.leaky)
-            F.conv(t2, c73, pad=1, act="relu", out=feat, out_c0=3 * C // 4)
+            if self.ssh_split:
+                # feat = [conv3X3 (C/2) | conv5X5_2 (C/4) | conv7x7_3 (C/4)]; the
+                # fused middle GEMM writes conv5X5_2 padded to a multiple of 4,
+                # whose zero pad channels conv7x7_3 overwrites right after
+                ca, cb, c73 = self.ssh[i]
+                qp_ = cb.Cin
+                t = torch.empty((B, h, w, qp_), dtype=torch.float32, device=dev)
+                t2 = torch.empty((B, h, w, qp_), dtype=torch.float32, device=dev)
+                F.conv(o, ca, pad=1, act="relu", ascale=sc, out=feat, out_c0=0, y2=t,
+                       nsplit=C // 2, act2="leaky", slope2=self.leaky)
+                F.conv(t, cb, pad=1, act="relu", out=feat, out_c0=C // 2, y2=t2,
+                       nsplit=cb.Cout - qp_, act2="leaky", slope2=self.leaky)
+                F.conv(t2, c73, pad=1, act="relu", out=feat, out_c0=3 * C // 4)
+            else:
+                c3, c51, c52, c72, c73 = self.ssh[i]
+                F.conv(o, c3, pad=1, act="relu", ascale=sc, out=feat, out_c0=0)
+                t = F.conv(o, c51, pad=1, act="leaky", slope=self.leaky, ascale=sc)
+                F.conv(t, c52, pad=1, act="relu", out=feat, out_c0=C // 2)
+                t2 = F.conv(t, c72, pad=1, act="leaky", slope=self.leaky)
+                F.conv(t2, c73, pad=1, act="relu", out=feat, out_c0=3 * C // 4)
             wt, bs = self.heads[i]
             F.heads(feat, wt, bs, loc, conf, landm, a_off, softmax)
             a_off += 2 * h * w

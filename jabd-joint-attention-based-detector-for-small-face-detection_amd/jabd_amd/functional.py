@@ -90,6 +90,23 @@ def pack_conv(conv, bn=None, extra=None, cin_pad=None, cout_pad=None):
     cin_pad / cout_pad zero-extend the input / output channels (a 10-channel
     SSH tensor stored as 12 channels takes the 16-byte vector path; the extra
     output channels compute exactly 0)."""
+    w2d, bias, kh, kw, cin, cin2 = _fold_conv(conv, bn, extra, cin_pad, cout_pad)
+    return PackedConv(w2d, bias, kh, kw, cin, cin2)
+
+
+def pack_conv_cat(parts, cin_pad=None):
+    """Two or more convolutions of the same input fused along N (output
+    channels concatenated in order): parts = [(conv, bn, cout_pad), ...].
+    Used with conv(..., y2=, nsplit=) to write the parts to separate tensors."""
+    ws, bs = [], []
+    for conv, bn, cout_pad in parts:
+        w2d, bias, kh, kw, cin, _ = _fold_conv(conv, bn, None, cin_pad, cout_pad)
+        ws.append(w2d)
+        bs.append(bias if bias is not None else w2d.new_zeros(w2d.shape[1]))
+    return PackedConv(torch.cat(ws, 1).contiguous(), torch.cat(bs).contiguous(), kh, kw, cin)
+
+
+def _fold_conv(conv, bn, extra, cin_pad, cout_pad):
     wt = conv.weight.detach().float()
     cb = conv.bias.detach().float() if conv.bias is not None else None
     if bn is not None:
@@ -114,8 +131,7 @@ def pack_conv(conv, bn=None, extra=None, cin_pad=None, cout_pad=None):
         w2d = torch.cat([w2d, w2], 0)
         bias = t2 if bias is None else bias + t2
     kh, kw = conv.weight.shape[2], conv.weight.shape[3]
-    return PackedConv(w2d.detach(), bias.detach() if bias is not None else None, kh, kw, cin,
-                      cin2)
+    return (w2d.detach(), bias.detach() if bias is not None else None, kh, kw, cin, cin2)
 
 
 def pack_dw(conv, bn):
@@ -131,8 +147,12 @@ _CONV_DBG = 0  # load/store skip mask for tools/convbench.py timing experiments 
 
 
 def conv(x, pk, stride=1, pad=0, act="none", slope=0.0, ascale=None, x2=None, x2_stride=1,
-         res=None, out=None, out_c0=0, nchw_in=False, x_c0=0):
-    """Implicit-GEMM conv.  x [B,H,W,C*] NHWC (or NCHW input if nchw_in)."""
+         res=None, out=None, out_c0=0, nchw_in=False, x_c0=0, y2=None, y2_c0=0, nsplit=0,
+         act2="none", slope2=0.0):
+    """Implicit-GEMM conv.  x [B,H,W,C*] NHWC (or NCHW input if nchw_in).
+
+    Split output: with y2 [B,OH,OW,C2], output channels >= nsplit go to y2 at
+    channel y2_c0 + (n - nsplit) with act2 / slope2."""
     _check("conv.x", x)
     if nchw_in:
         B, cin, H, W = x.shape
@@ -165,6 +185,10 @@ def conv(x, pk, stride=1, pad=0, act="none", slope=0.0, ascale=None, x2=None, x2
     a.act, a.slope = ACT[act], float(slope)
     a.nchw_in = 1 if nchw_in else 0
     a.reserved1 = _CONV_DBG
+    if y2 is not None:
+        _check("conv.y2", y2)
+        a.y2, a.y2_bs, a.y2_ps, a.y2_c0 = y2.data_ptr(), y2.stride(0), y2.shape[3], y2_c0
+        a.nsplit, a.act2, a.slope2 = nsplit, ACT[act2], float(slope2)
     call("jabd_conv2d_nhwc_f32", ctypes.byref(a), _stream())
     return out
 
