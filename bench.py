@@ -70,14 +70,19 @@ def build_model(device):
     return m.eval().to(device)
 
 
-def _expdw_work(xx, pk, k, stride, y):
+def _expdw_work(xx, pk, k, stride, y, skip=False):
     """(FLOPs, algorithmic bytes) of one fused expand+depthwise launch: the
     expand GEMM over every input pixel plus the k x k depthwise MACs; bytes =
-    input read once + output written once + weights."""
+    input read once + output written once + weights (+ the fused stride-2
+    skip branch's dw3x3 MACs and output)."""
     B, H, W, C = xx.shape
     E = pk.Cout
     flops = 2.0 * B * H * W * C * E + 2.0 * y.numel() * k * k
     nbytes = 4.0 * (xx.numel() + y.numel() + C * E + k * k * E)
+    if skip:
+        npx = y.shape[0] * y.shape[1] * y.shape[2]
+        flops += 2.0 * npx * C * 9
+        nbytes += 4.0 * npx * C
     return flops, nbytes
 
 
@@ -110,10 +115,10 @@ def conv_roofline(model, x, steps):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
-        y, part = orig_xd(xx, pk, w, b, k, stride, **kw)
+        out = orig_xd(xx, pk, w, b, k, stride, **kw)
         e.record()
-        recs.append((s, e) + _expdw_work(xx, pk, k, stride, y))
-        return y, part
+        recs.append((s, e) + _expdw_work(xx, pk, k, stride, out[0], kw.get("skip") is not None))
+        return out
 
     F.conv, F.expand_dw = timed_conv, timed_xd
     try:
@@ -177,11 +182,14 @@ def forward_flops(model, size, batch):
         return y, p
 
     def xd(xx, pk, w, b, k, stride, **kw):
-        y, p = orig_xd(xx, pk, w, b, k, stride, **kw)
+        out = orig_xd(xx, pk, w, b, k, stride, **kw)
+        y = out[0]
         # the reference's expand conv runs over the input pixels only once
         B, H, W, C = xx.shape
         tot[0] += 2.0 * B * H * W * C * pk.Cout + 2.0 * y.numel() * k * k
-        return y, p
+        if kw.get("skip") is not None:  # the fused skip branch's dw3x3/s2
+            tot[0] += 2.0 * y.shape[0] * y.shape[1] * y.shape[2] * C * 9
+        return out
 
     F.conv, F.dwconv, F.expand_dw = c, d, xd
     try:
