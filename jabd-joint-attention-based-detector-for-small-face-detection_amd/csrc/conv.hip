@@ -44,6 +44,14 @@ __device__ __forceinline__ float act_apply(float v, int act, float slope) {
   }
 }
 
+// The epilogue staging regions are wave-private: ordering a wave's own LDS
+// writes before its reads needs lgkmcnt(0), not a workgroup barrier (which
+// would also align the four waves and drain their outstanding loads).
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
 __device__ __forceinline__ float4 load_x2(const ConvArgs& p, int b, int oh, int ow, int c) {
   const float* src = p.x2 + (int64_t)b * p.x2_bs +
                      ((int64_t)oh * p.x2_stride * p.x2_W + (int64_t)ow * p.x2_stride) * p.x2_ps;
@@ -277,7 +285,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
           p.res ? (long long)((int64_t)pb[t] * p.res_bs + pix * p.res_ps + p.res_c0) : 0;
       const long long y2off =
           p.y2 ? (long long)((int64_t)pb[t] * p.y2_bs + pix * p.y2_ps + p.y2_c0) : 0;
-      __syncthreads();
+      wave_lds_sync();  // wave-private LDS region
 #pragma unroll
       for (int f0 = 0; f0 < 16 * 4 * TN; f0 += 64) {
         const int f = f0 + lane;
@@ -312,7 +320,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
           }
         }
       }
-      __syncthreads();
+      wave_lds_sync();  // wave-private LDS region
     }
     return;
   }
@@ -459,7 +467,7 @@ __global__ __launch_bounds__(256) void conv1x1_kernel(const ConvArgs p) {
 #pragma unroll
     for (int u = 0; u < TN; ++u)
       *reinterpret_cast<f32x4*>(sm + j * LDW + 16 * u + 4 * g) = acc[t][u];
-    __syncthreads();
+    wave_lds_sync();  // wave-private LDS region
 #pragma unroll
     for (int f0 = 0; f0 < 16 * 4 * TN; f0 += 64) {
       const int f = f0 + lane;
@@ -483,7 +491,7 @@ __global__ __launch_bounds__(256) void conv1x1_kernel(const ConvArgs p) {
         if (!(p.reserved1 & 2)) *reinterpret_cast<float4*>(p.y + m * p.y_ps + p.y_c0 + n0) = v;
       }
     }
-    __syncthreads();
+    wave_lds_sync();  // wave-private LDS region
   }
 }
 
