@@ -349,6 +349,23 @@ int conv1x1_m32_dispatch(const ConvArgs& a0, hipStream_t st, bool kxk) {
   a.Ntiles = a0.ntiles32;
 #define M32(TM_, TN_) \
   return kxk ? launch_m32<TM_, TN_, true>(a, st) : launch_m32<TM_, TN_, false>(a, st);
+  static int ftm = -1;  // JABD_M32_TM=1: 32-pixel wave tiles for TN <= 4 (A/B)
+  if (ftm < 0) {
+    const char* e = getenv("JABD_M32_TM");
+    ftm = e ? atoi(e) : 0;
+  }
+  // 32-pixel wave tiles (more, shorter workgroups) measured faster on large
+  // GEMMs without a folded ECA gate (R50: 5-10%); the gate's per-workgroup
+  // weight scaling makes them slower there
+  if (ftm == 1 || (ftm == 0 && !a0.ascale && a0.M >= 262144)) {
+    switch (a0.tn32) {
+      case 1: M32(1, 1)
+      case 2: M32(1, 2)
+      case 3: M32(1, 3)
+      case 4: M32(1, 4)
+      default: break;
+    }
+  }
   switch (a0.tn32) {
     case 1: M32(2, 1)
     case 2: M32(2, 2)
