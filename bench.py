@@ -14,8 +14,8 @@ Extra fields on the one JSON line:
                boxes/sec, bit-exact NMS kernel pipeline (sort+mask+scan).
   train        C4 (configs[3]): JABD-MobileNetV3 training step, 32 images/GPU
                at 1024x1024 (forward, MultiBoxLoss with on-device matching,
-               backward, SUM gradient all-reduce over RCCL when N>1, Adam
-               wd 5e-4 as train_mobilenetV3_ecagai.py:564) on every rank ->
+               backward, SUM gradient all-reduce over RCCL when N>1, fused Adam
+               (csrc/adam.hip) wd 5e-4 as train_mobilenetV3_ecagai.py:564) on every rank ->
                whole-job images/sec, data-parallel weak scaling; at N=1 also
                C3 (configs[2]): R50 RetinaFace training step at bs64 1024x1024.
   cpu_baseline the oracle's PyTorch-CPU restatement of the same forward at
@@ -224,7 +224,7 @@ def nms_bench(device, reps=5):
 
 def train_bench(kind, batch, size, steps, warmup, device, dist, rank):
     """steps timed training iterations (parallel.train_step) on this rank."""
-    from jabd_amd import parallel, synth
+    from jabd_amd import optim, parallel, synth
     from nets.retinaface_training import MultiBoxLoss, weights_init
     from utils.anchors import Anchors
     import contextlib
@@ -244,7 +244,7 @@ def train_bench(kind, batch, size, steps, warmup, device, dist, rank):
         parallel.broadcast_buffers(model)
         for p in model.parameters():
             dist.broadcast(p.data, src=0)
-    opt = torch.optim.Adam(model.parameters(), 1e-3, weight_decay=5e-4)
+    opt = optim.Adam(model.parameters(), 1e-3, weight_decay=5e-4)  # fused HIP step
     crit = MultiBoxLoss(2, 0.35, 7, cfg["variance"], True)
     pri = Anchors(cfg, image_size=(size, size)).get_anchors().to(device)
     x = synth.images(batch, size, seed=1234 + rank, device=device)

@@ -340,6 +340,20 @@ int jabd_scale_bwd_f32(const float* da, const float* x, int64_t B, int64_t HW, i
 int jabd_heads_gather_f32(const float* gloc, const float* gconf, const float* glandm, int32_t B,
                           int64_t A, int64_t a_off, int32_t HW, float* dout,
                           jabd_stream_t stream);
+/* Fused Adam step over many fp32 tensors in one launch (replaces the
+ * torch.optim.Adam(lr, weight_decay=5e-4) step of
+ * train_mobilenetV3_ecagai.py:564 / :588 optimizer.step(); same math and
+ * order as torch's single-tensor Adam, amsgrad off, maximize off).
+ * rows: DEVICE array of {float* param; const float* grad; float* exp_avg;
+ * float* exp_avg_sq; int64_t numel} (40 bytes each).  chunks: DEVICE array
+ * filled (on the host) by jabd_adam_fill_chunks from the HOST numel array;
+ * jabd_adam_num_chunks gives its length.  bias_correction1/2 = 1 - beta^step.
+ * Scalars are doubles, rounded to fp32 where torch rounds its Python floats. */
+int64_t jabd_adam_num_chunks(const int64_t* numel, int64_t ntensors);
+int jabd_adam_fill_chunks(const int64_t* numel, int64_t ntensors, int64_t* chunks);
+int jabd_adam_step_f32(const void* rows, const int64_t* chunks, int64_t nchunks, double lr,
+                       double beta1, double beta2, double eps, double weight_decay,
+                       double bias_correction1, double bias_correction2, jabd_stream_t stream);
 /* Max-pool backward (F.max_pool2d first-max / NaN semantics), NHWC. */
 int jabd_maxpool_bwd_f32(const float* x, const float* dy, int32_t B, int32_t H, int32_t W,
                          int32_t C, int32_t k, int32_t stride, int32_t pad, float* dx,

@@ -152,11 +152,16 @@ SIGNATURES = {
     "jabd_upsample_nearest_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp],
     "jabd_maxpool_bwd_f32": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp,
                              c_vp],
+    "jabd_adam_num_chunks": [c_vp, c_i64],
+    "jabd_adam_fill_chunks": [c_vp, c_i64, c_vp],
+    "jabd_adam_step_f32": [c_vp, c_vp, c_i64, c_f64, c_f64, c_f64, c_f64, c_f64, c_f64, c_f64,
+                           c_vp],
 }
 _RESTYPE = {"jabd_version": ctypes.c_char_p, "jabd_dw_nblk": ctypes.c_int64,
             "jabd_expand_dw_nblk": ctypes.c_int64,
             "jabd_bn_nblk": ctypes.c_int64, "jabd_conv_wgrad_part_floats": ctypes.c_int64,
-            "jabd_dw_wgrad_part_floats": ctypes.c_int64}
+            "jabd_dw_wgrad_part_floats": ctypes.c_int64,
+            "jabd_adam_num_chunks": ctypes.c_int64}
 
 _lock = threading.Lock()
 _lib = None
