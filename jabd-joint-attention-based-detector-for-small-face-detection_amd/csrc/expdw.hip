@@ -34,7 +34,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // IEEE divide is ~10 VALU instructions per element here).
 template <int ACT>
 __device__ __forceinline__ float xd_act(float v) {
-  if (ACT == ACT_RELU) return v > 0.f ? v : 0.f;
+  if (ACT == ACT_RELU) return fmaxf(v, 0.f);  // one v_max (a select is cmp + cndmask)
   if (ACT == ACT_HSWISH) return v * fminf(fmaxf(v + 3.f, 0.f), 6.f) * (1.f / 6.f);
   return v;
 }
@@ -353,7 +353,7 @@ __global__ __launch_bounds__(256, EC == 16 ? 3 : 2) void expdw_kernel(const jabd
 // selects.  Latency hiding comes from the resident workgroups instead of a
 // cross-item register prefetch.
 // ---------------------------------------------------------------------------
-template <int K, int S, int TH, int TW, int EC, int ACT>
+template <int K, int S, int TH, int TW, int EC, int ACT, int KP>
 __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p, const XdDivs dv,
                                                        int nitems) {
   using C = XdCfg<K, S, TH, TW, EC>;
@@ -389,8 +389,11 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(p.x), (short)0, (int)(uint32_t)((int64_t)p.B * p.x_bs * 4), 0x00020000);
   const int cq = (t & 3) * 4;
-  float4 pf[NPF];
-  auto load_stage = [&](int kc) {
+  // KP-deep register ring of input stages: stage kc + KP is issued as soon
+  // as stage kc has been written to LDS, and the raw LDS barriers below keep
+  // it in flight across the MFMA phase (a __syncthreads() would drain it).
+  float4 pf[KP][NPF];
+  auto load_stage = [&](int kc, float4 (&dst)[NPF]) {
     const int cofs = 16 * kc + cq;
     const uint32_t base = (uint32_t)(it.b * p.x_bs + cofs);
     const bool cok = cofs < p.Cin;
@@ -402,7 +405,7 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
       const bool ok = px < C::IPX && cok &&
                       (interior || ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W));
       const uint32_t off = ok ? (base + (uint32_t)((ih * p.W + iw) * p.x_ps)) * 4u : 0xFFFFFFF0u;
-      pf[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+      dst[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
     }
   };
   // accumulators start at the expand bias (no epilogue add)
@@ -410,31 +413,43 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
   const f32x4 bias4 = (f32x4){pbi.x, pbi.y, pbi.z, pbi.w};
 #pragma unroll
   for (int u = 0; u < C::BPW; ++u) acc[u] = bias4;
-  load_stage(0);
-  for (int kc = 0; kc < p.Kc; ++kc) {
-    f32x4 a = wpk[(kc * p.Ntiles + ntc) * 64 + lane];
 #pragma unroll
-    for (int u = 0; u < NPF; ++u) {
-      const int idx = u * 256 + t;
-      if (idx < C::IPAD * 4)
-        *reinterpret_cast<float4*>(lds + (idx >> 2) * C::XP + (idx & 3) * 4) = pf[u];
-    }
-    __syncthreads();
-    if (kc + 1 < p.Kc) load_stage(kc + 1);
-    if (!ntv) a = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < KP; ++s)
+    if (s < p.Kc) load_stage(s, pf[s]);
+  for (int kc0 = 0; kc0 < p.Kc; kc0 += KP) {
 #pragma unroll
-    for (int u = 0; u < C::BPW; ++u) {
-      const int blk = wave + 4 * u;
-      if (blk < C::NBLK) {
-        const int pb = blk / C::NNT;
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(lds + (pb * 16 + j) * C::XP + 4 * g);
-        acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bv.x, acc[u], 0, 0, 0);
-        acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bv.y, acc[u], 0, 0, 0);
-        acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bv.z, acc[u], 0, 0, 0);
-        acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bv.w, acc[u], 0, 0, 0);
+    for (int s = 0; s < KP; ++s) {
+      const int kc = kc0 + s;
+      if (kc >= p.Kc) break;
+      f32x4 a = wpk[(kc * p.Ntiles + ntc) * 64 + lane];
+#pragma unroll
+      for (int u = 0; u < NPF; ++u) {
+        const int idx = u * 256 + t;
+        if (idx < C::IPAD * 4)
+          *reinterpret_cast<float4*>(lds + (idx >> 2) * C::XP + (idx & 3) * 4) = pf[s][u];
       }
+      // retire the weight load here, before the next stage's loads are in
+      // flight: the compiler's vmcnt tracking cannot count through the
+      // predicated prefetch and would otherwise wait vmcnt(0) (draining the
+      // prefetch) at the first MFMA
+      if (!ntv) a = (f32x4){0.f, 0.f, 0.f, 0.f};
+      asm volatile("" : "+v"(a));
+      lds_barrier();
+      if (kc + KP < p.Kc) load_stage(kc + KP, pf[s]);
+#pragma unroll
+      for (int u = 0; u < C::BPW; ++u) {
+        const int blk = wave + 4 * u;
+        if (blk < C::NBLK) {
+          const int pb = blk / C::NNT;
+          const f32x4 bv = *reinterpret_cast<const f32x4*>(lds + (pb * 16 + j) * C::XP + 4 * g);
+          acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bv.x, acc[u], 0, 0, 0);
+          acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bv.y, acc[u], 0, 0, 0);
+          acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bv.z, acc[u], 0, 0, 0);
+          acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bv.w, acc[u], 0, 0, 0);
+        }
+      }
+      lds_barrier();
     }
-    __syncthreads();
   }
   // expanded tile: act, zero outside the image / on padded channels
   if (interior) {
@@ -591,6 +606,18 @@ static int xd_version() {
   return xdv;
 }
 
+// JABD_EXPDW_KP=2|3: input register ring depth (A/B).  Default 1: deeper
+// rings measured 0-7% slower (b3/b4/b11/b12 in tools/convbench.py --set xd),
+// the VGPRs they take cost occupancy and the stage latency is not the bound.
+static int xd_kp() {
+  static int kp = -1;
+  if (kp < 0) {
+    const char* e = getenv("JABD_EXPDW_KP");
+    kp = e && (e[0] == '2' || e[0] == '3') ? e[0] - '0' : 1;
+  }
+  return kp;
+}
+
 extern "C" int64_t jabd_expand_dw_nblk(int32_t OH, int32_t OW, int32_t k, int32_t stride) {
   if (OH <= 0 || OW <= 0 || (stride != 1 && stride != 2)) return -1;
   const XdTile tl = xd_tile(k, stride);
@@ -637,8 +664,15 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
 #define XD_LAUNCH(K_, S_, TH_, TW_, EC_, ACT_)                                                \
   do {                                                                                        \
     if (v2) {                                                                                 \
-      expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_><<<(unsigned)nitems, 256, 0, st>>>(a, dv,    \
-                                                                              (int)nitems);   \
+      if (a.Kc == 1 || xd_kp() == 1)                                                          \
+        expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1><<<(unsigned)nitems, 256, 0, st>>>(     \
+            a, dv, (int)nitems);                                                              \
+      else if (a.Kc == 2 || xd_kp() == 2)                                                     \
+        expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 2><<<(unsigned)nitems, 256, 0, st>>>(     \
+            a, dv, (int)nitems);                                                              \
+      else                                                                                    \
+        expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 3><<<(unsigned)nitems, 256, 0, st>>>(     \
+            a, dv, (int)nitems);                                                              \
       break;                                                                                  \
     }                                                                                         \
     const int64_t grid = xd_grid((const void*)expdw_kernel<K_, S_, TH_, TW_, EC_, ACT_>, nitems); \
