@@ -26,6 +26,14 @@ inline int check_launch(const char* what) {
   return JABD_OK;
 }
 
+// nn.Hardsigmoid / nn.Hardswish (relu6(x + 3) / 6 and x * that) as
+// clamp(x/6 + 1/2, 0, 1): one fma + one med3 (+ one mul) instead of add, max,
+// min, mul (, mul).  Within 2 ulp of the reference formula.
+__device__ __forceinline__ float hsigmoid_f(float v) {
+  return __builtin_amdgcn_fmed3f(fmaf(v, 1.f / 6.f, 0.5f), 0.f, 1.f);
+}
+__device__ __forceinline__ float hswish_f(float v) { return v * hsigmoid_f(v); }
+
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 

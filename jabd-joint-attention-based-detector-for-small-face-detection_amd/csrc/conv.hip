@@ -34,11 +34,8 @@ __device__ __forceinline__ float act_apply(float v, int act, float slope) {
   switch (act) {
     case ACT_RELU: return v > 0.f ? v : 0.f;
     case ACT_LEAKY: return v > 0.f ? v : v * slope;
-    case ACT_HSWISH: {
-      float r = fminf(fmaxf(v + 3.f, 0.f), 6.f);
-      return v * r * (1.f / 6.f);
-    }
-    case ACT_HSIGMOID: return fminf(fmaxf(v + 3.f, 0.f), 6.f) * (1.f / 6.f);
+    case ACT_HSWISH: return hswish_f(v);
+    case ACT_HSIGMOID: return hsigmoid_f(v);
     case ACT_SIGMOID: return 1.f / (1.f + expf(-v));
     default: return v;
   }
@@ -684,50 +681,80 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
 // ---------------------------------------------------------------------------
 // MobileNetV3 stem: conv3x3/s2/p1, 3 -> 16 channels, read straight from the
 // NCHW network input (layout conversion fused), folded BN + activation,
-// NHWC output.  One thread per output pixel; weights broadcast from LDS.
+// NHWC output.  One thread per output pixel.
+//  - all 27 input values are loaded up front (27 loads in flight per lane);
+//  - the 27x16 weights and the bias are read at wave-uniform addresses, so
+//    they arrive through scalar loads and feed the FMAs as SGPR operands; an
+//    empty asm with a memory clobber between taps keeps the compiler from
+//    hoisting all 432 of them at once (that spills the scalar file);
+//  - the 64 B per pixel go out through a wave-private LDS transpose, so each
+//    store instruction writes one contiguous 1 KiB run of the wave's 4 KiB
+//    NHWC block instead of 64 lanes at a 64 B stride.
 // Reference: nets/mobilenetV3.py:455-457,511 (conv1 + bn1 + hs1).
 // ---------------------------------------------------------------------------
 namespace jabd {
 constexpr int kStemOut = 16;
+constexpr int kStemThreads = 128;
 
-__global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ x, int H, int W,
-                                                   int OH, int OW, const float* __restrict__ w,
-                                                   const float* __restrict__ bias, int act,
-                                                   float* __restrict__ y) {
-  __shared__ float sw[27 * kStemOut];
-  __shared__ float sb[kStemOut];
-  for (int t = threadIdx.x; t < 27 * kStemOut; t += blockDim.x) sw[t] = w[t];
-  if (threadIdx.x < kStemOut) sb[threadIdx.x] = bias[threadIdx.x];
-  __syncthreads();
+template <int ACT>
+__global__ __launch_bounds__(kStemThreads) void stem_kernel(const float* __restrict__ x, int H,
+                                                            int W, int OH, int OW,
+                                                            const float* __restrict__ w,
+                                                            const float* __restrict__ bias,
+                                                            float* __restrict__ y) {
+  __shared__ float4 st[kStemThreads / 64][64 * kStemOut / 4 + 64 / 8];  // +1 float4 per 8 px
   const int b = blockIdx.z, oh = blockIdx.y;
-  const int ow = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ow >= OW) return;
-  float o[kStemOut];
-#pragma unroll
-  for (int n = 0; n < kStemOut; ++n) o[n] = sb[n];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ow0 = blockIdx.x * kStemThreads + wave * 64;  // this wave's first pixel
+  const int ow = ow0 + lane;
+  const bool pv = ow < OW;
   const float* xb = x + (int64_t)b * 3 * H * W;
+  const int64_t HW = (int64_t)H * W;
+  float v[27];
 #pragma unroll
   for (int kh = 0; kh < 3; ++kh) {
     const int ih = 2 * oh - 1 + kh;
-    if (ih < 0 || ih >= H) continue;
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
       const int iw = 2 * ow - 1 + kw;
-      if (iw < 0 || iw >= W) continue;
+      const bool ok = pv && ih >= 0 && ih < H && iw >= 0 && iw < W;
+      const float* xp = xb + (ok ? (int64_t)ih * W + iw : 0);
 #pragma unroll
       for (int ci = 0; ci < 3; ++ci) {
-        const float v = xb[((int64_t)ci * H + ih) * W + iw];
-        const float* wr = sw + ((kh * 3 + kw) * 3 + ci) * kStemOut;
-#pragma unroll
-        for (int n = 0; n < kStemOut; ++n) o[n] = fmaf(wr[n], v, o[n]);
+        const float t = xp[ci * HW];
+        v[(kh * 3 + kw) * 3 + ci] = ok ? t : 0.f;
       }
     }
   }
-  float4* yp = reinterpret_cast<float4*>(y + (((int64_t)b * OH + oh) * OW + ow) * kStemOut);
+  float o[kStemOut];
+#pragma unroll
+  for (int n = 0; n < kStemOut; ++n) o[n] = bias[n];
+#pragma unroll
+  for (int tp = 0; tp < 27; ++tp) {
+    asm volatile("" ::: "memory");
+    const float* wr = w + tp * kStemOut;
+#pragma unroll
+    for (int n = 0; n < kStemOut; ++n) o[n] = fmaf(wr[n], v[tp], o[n]);
+  }
+  auto f = [](float u) {
+    return ACT == ACT_HSWISH ? hswish_f(u) : ACT == ACT_RELU ? fmaxf(u, 0.f) : u;
+  };
+  // pixel p's 4 float4 at st[4p + p/8 + q]: the pad keeps the 16 B writes of
+  // 8 consecutive lanes on distinct banks
+  float4* sw = st[wave];
 #pragma unroll
   for (int q = 0; q < kStemOut / 4; ++q)
-    yp[q] = make_float4(act_apply(o[4 * q], act, 0.f), act_apply(o[4 * q + 1], act, 0.f),
-                        act_apply(o[4 * q + 2], act, 0.f), act_apply(o[4 * q + 3], act, 0.f));
+    sw[4 * lane + (lane >> 3) + q] =
+        make_float4(f(o[4 * q]), f(o[4 * q + 1]), f(o[4 * q + 2]), f(o[4 * q + 3]));
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private region
+  float4* yw = reinterpret_cast<float4*>(y + (((int64_t)b * OH + oh) * OW + ow0) * kStemOut);
+  const int npx = min(64, OW - ow0);
+#pragma unroll
+  for (int q = 0; q < kStemOut / 4; ++q) {
+    const int i = q * 64 + lane;  // float4 index in the wave's block
+    const int p = i >> 2;
+    if (p < npx) yw[i] = sw[i + (p >> 3)];
+  }
 }
 }  // namespace jabd
 
@@ -736,7 +763,14 @@ extern "C" int jabd_stem_nchw_f32(const float* x, int32_t B, int32_t H, int32_t 
                                   jabd_stream_t stream) {
   JABD_REQUIRE(x && w && bias && y && B > 0 && H > 0 && W > 0, "stem: bad args");
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
-  dim3 g((unsigned)cdiv(OW, 128), (unsigned)OH, (unsigned)B);
-  stem_kernel<<<g, 128, 0, as_stream(stream)>>>(x, H, W, OH, OW, w, bias, act, y);
+  dim3 g((unsigned)cdiv(OW, kStemThreads), (unsigned)OH, (unsigned)B);
+  JABD_REQUIRE(act == ACT_HSWISH || act == ACT_RELU || act == ACT_NONE, "stem: act %d", act);
+  hipStream_t st = as_stream(stream);
+  if (act == ACT_HSWISH)
+    stem_kernel<ACT_HSWISH><<<g, kStemThreads, 0, st>>>(x, H, W, OH, OW, w, bias, y);
+  else if (act == ACT_RELU)
+    stem_kernel<ACT_RELU><<<g, kStemThreads, 0, st>>>(x, H, W, OH, OW, w, bias, y);
+  else
+    stem_kernel<ACT_NONE><<<g, kStemThreads, 0, st>>>(x, H, W, OH, OW, w, bias, y);
   return check_launch("stem");
 }

@@ -40,8 +40,8 @@ __device__ __forceinline__ float act32(float v, int act, float slope) {
   switch (act) {
     case ACT_RELU: return v > 0.f ? v : 0.f;
     case ACT_LEAKY: return v > 0.f ? v : v * slope;
-    case ACT_HSWISH: return v * fminf(fmaxf(v + 3.f, 0.f), 6.f) * (1.f / 6.f);
-    case ACT_HSIGMOID: return fminf(fmaxf(v + 3.f, 0.f), 6.f) * (1.f / 6.f);
+    case ACT_HSWISH: return hswish_f(v);
+    case ACT_HSIGMOID: return hsigmoid_f(v);
     case ACT_SIGMOID: return 1.f / (1.f + expf(-v));
     default: return v;
   }

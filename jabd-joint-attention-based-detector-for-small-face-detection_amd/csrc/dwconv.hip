@@ -16,10 +16,7 @@ __device__ __forceinline__ float dw_act(float v, int act, float slope) {
   switch (act) {
     case ACT_RELU: return v > 0.f ? v : 0.f;
     case ACT_LEAKY: return v > 0.f ? v : v * slope;
-    case ACT_HSWISH: {
-      float r = fminf(fmaxf(v + 3.f, 0.f), 6.f);
-      return v * r * (1.f / 6.f);
-    }
+    case ACT_HSWISH: return hswish_f(v);
     default: return v;
   }
 }

@@ -35,7 +35,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 template <int ACT>
 __device__ __forceinline__ float xd_act(float v) {
   if (ACT == ACT_RELU) return fmaxf(v, 0.f);  // one v_max (a select is cmp + cndmask)
-  if (ACT == ACT_HSWISH) return v * fminf(fmaxf(v + 3.f, 0.f), 6.f) * (1.f / 6.f);
+  if (ACT == ACT_HSWISH) return hswish_f(v);
   return v;
 }
 
@@ -436,16 +436,20 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
       asm volatile("" : "+v"(a));
       lds_barrier();
       if (kc + KP < p.Kc) load_stage(kc + KP, pf[s]);
+      // a wave whose 16-channel tile lies past E skips its MFMAs (wave-uniform;
+      // its accumulators are masked in the epilogue)
+      if (ntv) {
 #pragma unroll
-      for (int u = 0; u < C::BPW; ++u) {
-        const int blk = wave + 4 * u;
-        if (blk < C::NBLK) {
-          const int pb = blk / C::NNT;
-          const f32x4 bv = *reinterpret_cast<const f32x4*>(lds + (pb * 16 + j) * C::XP + 4 * g);
-          acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bv.x, acc[u], 0, 0, 0);
-          acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bv.y, acc[u], 0, 0, 0);
-          acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bv.z, acc[u], 0, 0, 0);
-          acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bv.w, acc[u], 0, 0, 0);
+        for (int u = 0; u < C::BPW; ++u) {
+          const int blk = wave + 4 * u;
+          if (blk < C::NBLK) {
+            const int pb = blk / C::NNT;
+            const f32x4 bv = *reinterpret_cast<const f32x4*>(lds + (pb * 16 + j) * C::XP + 4 * g);
+            acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bv.x, acc[u], 0, 0, 0);
+            acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bv.y, acc[u], 0, 0, 0);
+            acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bv.z, acc[u], 0, 0, 0);
+            acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bv.w, acc[u], 0, 0, 0);
+          }
         }
       }
       lds_barrier();

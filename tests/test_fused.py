@@ -60,3 +60,25 @@ def test_expand_dw_parity(cuda, spec, hw):
     e = F.conv(xg, pk, act=act)
     y2, part2 = F.dwconv(e, dw_w, dw_b, k, s, act=act, partials=True)
     assert rel_err(y, y2) < 2e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("act", ["hswish", "relu", "none"])
+@pytest.mark.parametrize("hw", [(37, 29), (128, 96), (1, 2)])
+def test_stem_parity(cuda, act, hw):
+    """MNv3 stem (nets/mobilenetV3.py:455-457,511): conv3x3/s2/p1 3->16 on the
+    NCHW input + folded bias + act, NHWC out, vs torch fp32 conv2d."""
+    from jabd_amd import functional as F
+    H, W = hw
+    g = torch.Generator().manual_seed(H * 131 + W)
+    x = torch.randn(3, 3, H, W, generator=g) * 50
+    w = torch.randn(16, 3, 3, 3, generator=g) / 27 ** 0.5
+    b = torch.randn(16, generator=g)
+    ref = tF.conv2d(x, w, b, stride=2, padding=1)
+    ref = {"hswish": tF.hardswish, "relu": tF.relu, "none": lambda t: t}[act](ref)
+    wp = w.permute(2, 3, 1, 0).reshape(27, 16).contiguous()  # [(kh,kw,ci)][co]
+    y = F.stem(x.to(cuda), wp.to(cuda), b.to(cuda), act)
+    torch.cuda.synchronize()
+    got = y.permute(0, 3, 1, 2).cpu()
+    assert got.shape == ref.shape
+    assert rel_err(got, ref) < 2e-6, rel_err(got, ref)
