@@ -94,19 +94,35 @@ __global__ __launch_bounds__(kRedThreads) void bn_stats_part_kernel(
 }
 
 // Deterministic fp64 sum over the nblk partial blocks of part[b][0|1][c] for
-// the `lanes` channels of this workgroup (rows of threads stride the blocks,
-// then a fixed-order LDS combine); valid in threads t < lanes.
+// the kFinLanes channels of this workgroup: kFinThreads / kFinLanes rows of
+// threads stride the blocks (8 independent loads in flight per thread, so
+// ~1024 partials take two L2 round trips instead of a 256-deep chain), then a
+// fixed-shape LDS tree over the rows.  Valid in threads t < kFinLanes.
+constexpr int kFinThreads = 1024, kFinLanes = 16, kFinRows = kFinThreads / kFinLanes;
+
 __device__ __forceinline__ void bn_final_sums(const float* __restrict__ part, int64_t nblk, int C,
-                                              int lanes, double& S, double& Q) {
-  __shared__ double ls[kRedThreads], lq[kRedThreads];
+                                              double& S, double& Q) {
+  __shared__ double ls[kFinThreads], lq[kFinThreads];
   const int t = threadIdx.x;
-  const int rows = kRedThreads / lanes;
-  const int r = t / lanes;
-  const int c = blockIdx.x * lanes + t % lanes;
+  const int r = t / kFinLanes;
+  const int c = blockIdx.x * kFinLanes + t % kFinLanes;
   double s = 0.0, q = 0.0;
-  if (r < rows && c < C) {
-#pragma unroll 4
-    for (int64_t b = r; b < nblk; b += rows) {
+  if (c < C) {
+    int64_t b = r;
+    for (; b + 7 * kFinRows < nblk; b += 8 * kFinRows) {
+      float vs[8], vq[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        vs[u] = part[(b + u * kFinRows) * 2 * C + c];
+        vq[u] = part[(b + u * kFinRows) * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s += vs[u];
+        q += vq[u];
+      }
+    }
+    for (; b < nblk; b += kFinRows) {
       s += part[b * 2 * C + c];
       q += part[b * 2 * C + C + c];
     }
@@ -114,29 +130,26 @@ __device__ __forceinline__ void bn_final_sums(const float* __restrict__ part, in
   ls[t] = s;
   lq[t] = q;
   __syncthreads();
-  S = 0.0;
-  Q = 0.0;
-  if (t < lanes)
-    for (int k = 0; k < rows; ++k) {
-      S += ls[k * lanes + t];
-      Q += lq[k * lanes + t];
+#pragma unroll
+  for (int h = kFinThreads / 2; h >= kFinLanes; h >>= 1) {
+    if (t < h) {
+      ls[t] += ls[t + h];
+      lq[t] += lq[t + h];
     }
+    __syncthreads();
+  }
+  S = ls[t % kFinLanes];
+  Q = lq[t % kFinLanes];
 }
 
-static int bn_fin_lanes(int C) {
-  int l = 1;
-  while (l < C && l < 64) l <<= 1;
-  return l;
-}
-
-__global__ __launch_bounds__(kRedThreads) void bn_stats_final_kernel(
+__global__ __launch_bounds__(kFinThreads) void bn_stats_final_kernel(
     const float* __restrict__ x, const float* __restrict__ part, int64_t nblk, int64_t M, int C,
-    int lanes, float momentum, float eps, float* __restrict__ mean, float* __restrict__ invstd,
+    float momentum, float eps, float* __restrict__ mean, float* __restrict__ invstd,
     float* __restrict__ rmean, float* __restrict__ rvar) {
   double S, Q;
-  bn_final_sums(part, nblk, C, lanes, S, Q);
-  const int c = blockIdx.x * lanes + threadIdx.x;
-  if (threadIdx.x >= lanes || c >= C) return;
+  bn_final_sums(part, nblk, C, S, Q);
+  const int c = blockIdx.x * kFinLanes + threadIdx.x;
+  if (threadIdx.x >= kFinLanes || c >= C) return;
   const double ms = S / (double)M;
   double var = Q / (double)M - ms * ms;
   if (var < 0.0) var = 0.0;
@@ -268,13 +281,13 @@ __global__ __launch_bounds__(kRedThreads) void bn_bwd_part_kernel(
   }
 }
 
-__global__ __launch_bounds__(kRedThreads) void bn_bwd_final_kernel(
-    const float* __restrict__ part, int64_t nblk, int C, int lanes, float* __restrict__ dbeta,
+__global__ __launch_bounds__(kFinThreads) void bn_bwd_final_kernel(
+    const float* __restrict__ part, int64_t nblk, int C, float* __restrict__ dbeta,
     float* __restrict__ dgamma) {
   double S, Q;
-  bn_final_sums(part, nblk, C, lanes, S, Q);
-  const int c = blockIdx.x * lanes + threadIdx.x;
-  if (threadIdx.x >= lanes || c >= C) return;
+  bn_final_sums(part, nblk, C, S, Q);
+  const int c = blockIdx.x * kFinLanes + threadIdx.x;
+  if (threadIdx.x >= kFinLanes || c >= C) return;
   dbeta[c] = (float)S;
   dgamma[c] = (float)Q;
 }
@@ -1182,9 +1195,8 @@ extern "C" int jabd_bn_stats_f32(const float* x, int32_t ldx, int64_t M, int32_t
   const int64_t per = bn_rows_per_blk(M, C), nblk = cdiv(M, per);
   bn_stats_part_kernel<<<(unsigned)nblk, kRedThreads, 0, st>>>(x, ldx, M, C, per, part);
   if (int e = check_launch("bn_stats_part")) return e;
-  const int fl = bn_fin_lanes(C);
-  bn_stats_final_kernel<<<(unsigned)cdiv(C, fl), kRedThreads, 0, st>>>(
-      x, part, nblk, M, C, fl, momentum, eps, mean, invstd, running_mean, running_var);
+  bn_stats_final_kernel<<<(unsigned)cdiv(C, kFinLanes), kFinThreads, 0, st>>>(
+      x, part, nblk, M, C, momentum, eps, mean, invstd, running_mean, running_var);
   return check_launch("bn_stats_final");
 }
 
@@ -1219,9 +1231,8 @@ extern "C" int jabd_bn_act_bwd_f32(const float* dy, int32_t lddy, int32_t dyc0, 
                                                             C, mean, invstd, gamma, beta, act,
                                                             slope, per, part);
   if (int e = check_launch("bn_bwd_part")) return e;
-  const int fl = bn_fin_lanes(C);
-  bn_bwd_final_kernel<<<(unsigned)cdiv(C, fl), kRedThreads, 0, st>>>(part, nblk, C, fl, dbeta,
-                                                                     dgamma);
+  bn_bwd_final_kernel<<<(unsigned)cdiv(C, kFinLanes), kFinThreads, 0, st>>>(part, nblk, C,
+                                                                            dbeta, dgamma);
   if (int e = check_launch("bn_bwd_final")) return e;
   int lanes;
   const dim3 grid = ew_grid(M, C, lanes);
