@@ -1,17 +1,20 @@
-# Round profile: bench line, kernel-trace stats of the C2 forward / training
-# steps, and the conv-stack HBM traffic PMC passes (MI355X_MICROARCH.md: one
-# counter family per pass).  Usage on the GPU box: bash tools/gpu_profile.sh r01
+# Round profile: conv-stack HBM traffic PMC passes (MI355X_MICROARCH.md: one
+# counter family per pass), then the bench line (which reads that traffic from
+# profiles/<round>/pmc_traffic.json), then kernel-trace stats of the C2
+# forward / training steps.  Usage on the GPU box: bash tools/gpu_profile.sh r01
 set -o pipefail
 R=${1:-r01}
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/$R
-mkdir -p $O
+mkdir -p $O profiles/$R
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 bench.py --steps 3 --pmc-forward-only > $O/pmc_fetch.log 2>&1 &&
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 bench.py --steps 3 --pmc-forward-only > $O/pmc_write.log 2>&1 &&
+python3 tools/pmc_traffic.py $O/pmc_fetch $O/pmc_write 3 $O/pmc_traffic.json &&
+cp $O/pmc_traffic.json profiles/$R/pmc_traffic.json &&
 timeout -k 10 500 python -u bench.py > $O/bench.log 2>&1 && tail -1 $O/bench.log > $O/bench_line.json &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_fwd -o run -- python3 bench.py --steps 10 --pmc-forward-only > $O/prof_fwd.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_tr_mnv3 -o run -- python3 tools/train_steps.py --kind mnv3 > $O/tr_mnv3.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_tr_r50 -o run -- python3 tools/train_steps.py --kind r50 --batch 64 --steps 2 > $O/tr_r50.log 2>&1 &&
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 bench.py --steps 3 --pmc-forward-only > $O/pmc_fetch.log 2>&1 &&
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 bench.py --steps 3 --pmc-forward-only > $O/pmc_write.log 2>&1 &&
-python3 tools/pmc_traffic.py $O/pmc_fetch $O/pmc_write 3 $O/pmc_traffic.json
+timeout -k 10 200 python3 tools/fwd_ops.py > $O/fwd_ops_c2.txt 2>&1
 echo rc=$?
