@@ -220,7 +220,13 @@ __global__ __launch_bounds__(256) void nlm_pool_kernel(const float* __restrict__
   }
 }
 
-// Per pixel: out = lateral + (W · softmax_S(q·K) V + bW + x)
+// Per pixel: out = lateral + (W · softmax_S(q·K) V + bW + x).
+// A quad of lanes per pixel: lane r of the quad computes q[r] (then the quad
+// exchanges them), scores and softmax partials for every 4th bin s = r, r+4,
+// ... (max, then exp-sum and the V-weighted sum, rescaled to the quad's max
+// and combined by butterfly), and writes every 4th float4 channel group of
+// the output.  One lane per pixel ran the 225-bin chain serially at two waves
+// per SIMD (latency-bound, ~10% of its HBM floor).
 template <int CH>
 __global__ __launch_bounds__(256) void nlm_apply_kernel(
     const float* __restrict__ src, int64_t src_bs, int src_ps, int hs, int ws, int C, int h,
@@ -228,6 +234,7 @@ __global__ __launch_bounds__(256) void nlm_apply_kernel(
     const float* __restrict__ kpool, const float* __restrict__ vpool, int S,
     const float* __restrict__ wW, const float* __restrict__ bW, const float* __restrict__ lateral,
     float* __restrict__ out, float* __restrict__ q_out, float* __restrict__ ctx_out) {
+  static_assert(CH == 4, "one q channel per quad lane");
   extern __shared__ float sm[];  // K [S][CH], V [S][CH], wq [CH][C], wW [C][CH], bW [C]
   const int b = blockIdx.y;
   float* sK = sm;
@@ -245,70 +252,82 @@ __global__ __launch_bounds__(256) void nlm_apply_kernel(
   }
   for (int t = threadIdx.x; t < C; t += blockDim.x) sbW[t] = bW[t];
   __syncthreads();
-  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
-  if (pix >= h * w) return;
-  const int i = pix / w, jx = pix - (pix / w) * w;
+  const int r = threadIdx.x & 3;
+  const int pix = blockIdx.x * (blockDim.x >> 2) + (threadIdx.x >> 2);
+  const bool pv = pix < h * w;
+  const int pc = pv ? pix : 0;  // the quad stays whole for the shuffles
+  const int i = pc / w, jx = pc - (pc / w) * w;
   const float* xp = src + (int64_t)b * src_bs +
                     ((int64_t)nearest_src(i, hs, h) * ws + nearest_src(jx, ws, w)) * src_ps;
-  float q[CH];
-#pragma unroll
-  for (int o = 0; o < CH; ++o) q[o] = bq[o];
+  float qr = bq[r];
   for (int c = 0; c < C; c += 4) {
     const float4 x = *reinterpret_cast<const float4*>(xp + c);
-#pragma unroll
-    for (int o = 0; o < CH; ++o) {
-      const float* wr = sWq + o * C + c;
-      q[o] = fmaf(wr[0], x.x, q[o]);
-      q[o] = fmaf(wr[1], x.y, q[o]);
-      q[o] = fmaf(wr[2], x.z, q[o]);
-      q[o] = fmaf(wr[3], x.w, q[o]);
-    }
+    const float* wr = sWq + r * C + c;
+    qr = fmaf(wr[0], x.x, qr);
+    qr = fmaf(wr[1], x.y, qr);
+    qr = fmaf(wr[2], x.z, qr);
+    qr = fmaf(wr[3], x.w, qr);
   }
+  const int qb = threadIdx.x & ~3;  // quad base lane
+  float q[CH];
+#pragma unroll
+  for (int o = 0; o < CH; ++o) q[o] = __shfl(qr, (qb + o) & 63);
+  const float4* K4 = reinterpret_cast<const float4*>(sK);
+  const float4* V4 = reinterpret_cast<const float4*>(sV);
   float mx = -INFINITY;
-  for (int s = 0; s < S; ++s) {
-    float l = 0.f;
-#pragma unroll
-    for (int o = 0; o < CH; ++o) l = fmaf(q[o], sK[s * CH + o], l);
-    mx = fmaxf(mx, l);
+#pragma unroll 4
+  for (int s = r; s < S; s += 4) {
+    const float4 k = K4[s];
+    mx = fmaxf(mx, fmaf(q[0], k.x, fmaf(q[1], k.y, fmaf(q[2], k.z, q[3] * k.w))));
   }
-  float den = 0.f, cx[CH];
-#pragma unroll
-  for (int o = 0; o < CH; ++o) cx[o] = 0.f;
-  for (int s = 0; s < S; ++s) {
-    float l = 0.f;
-#pragma unroll
-    for (int o = 0; o < CH; ++o) l = fmaf(q[o], sK[s * CH + o], l);
-    const float e = __expf(l - mx);
+  float den = 0.f, cx[CH] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int s = r; s < S; s += 4) {
+    const float4 k = K4[s], v = V4[s];
+    const float e = __expf(fmaf(q[0], k.x, fmaf(q[1], k.y, fmaf(q[2], k.z, q[3] * k.w))) - mx);
     den += e;
-#pragma unroll
-    for (int o = 0; o < CH; ++o) cx[o] = fmaf(e, sV[s * CH + o], cx[o]);
+    cx[0] = fmaf(e, v.x, cx[0]);
+    cx[1] = fmaf(e, v.y, cx[1]);
+    cx[2] = fmaf(e, v.z, cx[2]);
+    cx[3] = fmaf(e, v.w, cx[3]);
   }
+  // combine the quad's partials at the quad max (fixed butterfly order)
+  float M = fmaxf(mx, __shfl_xor(mx, 1));
+  M = fmaxf(M, __shfl_xor(M, 2));
+  const float sc = mx == -INFINITY ? 0.f : __expf(mx - M);  // lane with no bins (S < 4)
+  den *= sc;
+#pragma unroll
+  for (int o = 0; o < CH; ++o) cx[o] *= sc;
+#pragma unroll
+  for (int m = 1; m <= 2; m <<= 1) {
+    den += __shfl_xor(den, m);
+#pragma unroll
+    for (int o = 0; o < CH; ++o) cx[o] += __shfl_xor(cx[o], m);
+  }
+  if (!pv) return;
   const float inv = 1.f / den;
 #pragma unroll
   for (int o = 0; o < CH; ++o) cx[o] *= inv;
-  if (q_out) {  // training: saved for the backward
+  if (q_out && r == 0) {  // training: saved for the backward
     const int64_t mq = ((int64_t)b * h * w + pix) * CH;
-#pragma unroll
-    for (int o = 0; o < CH; ++o) {
-      q_out[mq + o] = q[o];
-      ctx_out[mq + o] = cx[o];
-    }
+    *reinterpret_cast<float4*>(q_out + mq) = make_float4(q[0], q[1], q[2], q[3]);
+    *reinterpret_cast<float4*>(ctx_out + mq) = make_float4(cx[0], cx[1], cx[2], cx[3]);
   }
   const int64_t opix = ((int64_t)b * h * w + pix) * C;
-  for (int c = 0; c < C; c += 4) {
+  for (int c = 4 * r; c < C; c += 16) {
     const float4 x = *reinterpret_cast<const float4*>(xp + c);
     const float4 lt = *reinterpret_cast<const float4*>(lateral + opix + c);
     float v[4] = {x.x, x.y, x.z, x.w};
     float lv[4] = {lt.x, lt.y, lt.z, lt.w};
-    float r[4];
+    float rr[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float a = sbW[c + e];
 #pragma unroll
       for (int o = 0; o < CH; ++o) a = fmaf(sWW[(c + e) * CH + o], cx[o], a);
-      r[e] = lv[e] + (a + v[e]);
+      rr[e] = lv[e] + (a + v[e]);
     }
-    *reinterpret_cast<float4*>(out + opix + c) = make_float4(r[0], r[1], r[2], r[3]);
+    *reinterpret_cast<float4*>(out + opix + c) = make_float4(rr[0], rr[1], rr[2], rr[3]);
   }
 }
 
@@ -323,31 +342,35 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ x,
                                                     float* __restrict__ loc,
                                                     float* __restrict__ conf,
                                                     float* __restrict__ landm) {
-  extern __shared__ float sw[];  // [32][C]
-  for (int t = threadIdx.x; t < kHeadOut * C; t += blockDim.x) sw[t] = wt[t];
-  __syncthreads();
+  // Weights [32][C] are read at wave-uniform addresses (scalar loads, SGPR
+  // FMA operands), 16 outputs x 4 channels at a time; the empty asm with a
+  // memory clobber keeps the compiler from hoisting all 32*C of them into the
+  // scalar file.  An LDS copy costs a broadcast ds_read per 4 FMAs, and the
+  // LDS port was this kernel's bound.
   const int b = blockIdx.y;
-  const int64_t pix = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (pix >= HW) return;
+  const int64_t pix0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const bool pv = pix0 < HW;
+  const int64_t pix = pv ? pix0 : 0;
   const float* xp = x + (int64_t)b * x_bs + pix * x_ps;
   float o[kHeadOut];
 #pragma unroll
   for (int n = 0; n < kHeadOut; ++n) o[n] = bias[n];
+#pragma unroll 1
   for (int c = 0; c < C; c += 4) {
     const float4 v = *reinterpret_cast<const float4*>(xp + c);
 #pragma unroll
-    for (int n = 0; n < kHeadOut; ++n) {
-      const float* wr = sw + n * C + c;
-      o[n] = fmaf(wr[0], v.x, o[n]);
-      o[n] = fmaf(wr[1], v.y, o[n]);
-      o[n] = fmaf(wr[2], v.z, o[n]);
-      o[n] = fmaf(wr[3], v.w, o[n]);
+    for (int h = 0; h < 2; ++h) {
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int n = 16 * h; n < 16 * h + 16; ++n) {
+        const float4 wr = *reinterpret_cast<const float4*>(wt + n * C + c);
+        o[n] = fmaf(wr.x, v.x, o[n]);
+        o[n] = fmaf(wr.y, v.y, o[n]);
+        o[n] = fmaf(wr.z, v.z, o[n]);
+        o[n] = fmaf(wr.w, v.w, o[n]);
+      }
     }
   }
-  const int64_t row = (int64_t)b * A + a_off + pix * 2;  // 2 anchors per position
-  float4* lp = reinterpret_cast<float4*>(loc + row * 4);
-  lp[0] = make_float4(o[0], o[1], o[2], o[3]);
-  lp[1] = make_float4(o[4], o[5], o[6], o[7]);
   float c0 = o[8], c1 = o[9], c2 = o[10], c3 = o[11];
   if (softmax) {  // F.softmax over each anchor's 2 logits
     float m = fmaxf(c0, c1), e0 = expf(c0 - m), e1 = expf(c1 - m), s = e0 + e1;
@@ -355,10 +378,38 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ x,
     m = fmaxf(c2, c3); e0 = expf(c2 - m); e1 = expf(c3 - m); s = e0 + e1;
     c2 = e0 / s; c3 = e1 / s;
   }
-  reinterpret_cast<float4*>(conf + row * 2)[0] = make_float4(c0, c1, c2, c3);
-  float* lm = landm + row * 10;
+  o[8] = c0; o[9] = c1; o[10] = c2; o[11] = c3;
+  // The wave's 64 positions own contiguous runs of loc (8 floats each), conf
+  // (4) and landm (20): transpose through wave-private LDS so every store
+  // instruction writes consecutive 16 B per lane (a per-position store of 20
+  // landmark floats is 20 instructions at an 80 B lane stride).
+  constexpr int P = kHeadOut + 4;  // row pitch (float4-aligned)
+  __shared__ float4 st4[4][64 * P / 4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float4* sw = st4[wave];
 #pragma unroll
-  for (int n = 0; n < 20; ++n) lm[n] = o[12 + n];
+  for (int q = 0; q < kHeadOut / 4; ++q)
+    sw[lane * (P / 4) + q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private region
+  const int64_t p0 = pix0 - lane;
+  const int npx = (int)min<int64_t>(64, HW - p0);
+  if (npx <= 0) return;
+  const int64_t row0 = (int64_t)b * A + a_off + p0 * 2;  // 2 anchors per position
+  float4* lp = reinterpret_cast<float4*>(loc + row0 * 4);
+  float4* cp = reinterpret_cast<float4*>(conf + row0 * 2);
+  float4* mp = reinterpret_cast<float4*>(landm + row0 * 10);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = k * 64 + lane;
+    if (i < 2 * npx) lp[i] = sw[(i >> 1) * (P / 4) + (i & 1)];
+  }
+  if (lane < npx) cp[lane] = sw[lane * (P / 4) + 2];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int i = k * 64 + lane;
+    const int px = i / 5;
+    if (i < 5 * npx) mp[i] = sw[px * (P / 4) + 3 + (i - 5 * px)];
+  }
 }
 
 }  // namespace jabd
@@ -450,7 +501,7 @@ extern "C" int jabd_nlm_apply_f32(const float* src, int64_t src_bs, int32_t src_
   JABD_REQUIRE(C > 0 && C % 4 == 0 && src_ps % 4 == 0 && S > 0, "nlm_apply: bad sizes");
   const size_t smem = (2 * (size_t)S * ch + 2 * (size_t)ch * C + C) * sizeof(float);
   JABD_REQUIRE(smem <= 64 * 1024, "nlm_apply: LDS %zu > 64KiB", smem);
-  dim3 g((unsigned)cdiv((int64_t)h * w, 256), (unsigned)B);
+  dim3 g((unsigned)cdiv((int64_t)h * w, 64), (unsigned)B);  // a quad of lanes per pixel
   nlm_apply_kernel<4><<<g, 256, smem, as_stream(stream)>>>(src, src_bs, src_ps, hs, ws, C, h, w,
                                                            wq, bq, kpool, vpool, S, wW, bW,
                                                            lateral, out, q_out, ctx_out);
@@ -465,7 +516,7 @@ extern "C" int jabd_heads_f32(const float* x, int64_t x_bs, int32_t x_ps, int32_
   JABD_REQUIRE(C % 4 == 0 && x_ps % 4 == 0, "heads: C and pixel stride must be multiples of 4");
   JABD_REQUIRE(a_off + 2 * (int64_t)HW <= A, "heads: anchor range out of bounds");
   dim3 g((unsigned)cdiv(HW, 256), (unsigned)B);
-  heads_kernel<<<g, 256, kHeadOut * C * sizeof(float), as_stream(stream)>>>(
+  heads_kernel<<<g, 256, 0, as_stream(stream)>>>(
       x, x_bs, x_ps, HW, C, wt, bias, A, a_off, softmax, loc, conf, landm);
   return check_launch("heads");
 }
