@@ -360,7 +360,7 @@ int jabd_maxpool_bwd_f32(const float* x, const float* dy, int32_t B, int32_t H, 
                          jabd_stream_t stream);
 /* CSAF/NLM backward (nets/retinaface_r.py:124-152).  attn: from dOut (grad
  * of lateral + NLM(x)) -> dq [M][4], dx_up [M][C] (= dOut + Wq^T dq), and
- * dK/dV [B][S][4] (part: [B][ceil(h*w/256)][S][8] scratch).  proj: PSP
+ * dK/dV [B][S][4] (part: [B][ceil(h*w/64)][S][8] scratch).  proj: PSP
  * backward -> dkv [M][8] and dx_up += Wk^T dk + Wv^T dv.  Up-sample backward
  * gathers dx_up onto the source grid (accumulate=1 adds to dsrc). */
 int jabd_nlm_bwd_attn_f32(const float* dout, int32_t B, int32_t h, int32_t w, int32_t C,

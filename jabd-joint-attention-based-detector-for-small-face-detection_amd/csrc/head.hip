@@ -206,14 +206,24 @@ __global__ __launch_bounds__(256) void nlm_pool_kernel(const float* __restrict__
 #pragma unroll
     for (int q = 0; q < 2 * CH; ++q) a[q] += v[q];
   }
-  __shared__ float red[2 * CH][257];
+  // fixed-shape reduction: wave butterflies, then the 4 wave sums in order
+  // (a 256-long serial LDS sum per channel was most of this kernel's time)
 #pragma unroll
-  for (int q = 0; q < 2 * CH; ++q) red[q][threadIdx.x] = a[q];
+  for (int q = 0; q < 2 * CH; ++q)
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) a[q] += __shfl_xor(a[q], m);
+  __shared__ float red[4][2 * CH];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane < 2 * CH) {
+    float v = a[0];
+#pragma unroll
+    for (int q = 1; q < 2 * CH; ++q) v = lane == q ? a[q] : v;
+    red[wave][lane] = v;
+  }
   __syncthreads();
   if (threadIdx.x < 2 * CH) {
     const int q = threadIdx.x;
-    float t = 0.f;
-    for (int u = 0; u < 256; ++u) t += red[q][u];
+    const float t = (red[0][q] + red[1][q]) + (red[2][q] + red[3][q]);
     const float avg = t / (float)npix;
     if (q < CH) kpool[((int64_t)b * S + s) * CH + q] = avg;
     else vpool[((int64_t)b * S + s) * CH + (q - CH)] = avg;

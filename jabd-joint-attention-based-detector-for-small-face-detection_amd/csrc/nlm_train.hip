@@ -23,7 +23,12 @@ __device__ __forceinline__ int nsrc(int dst, int in, int out) {
 
 constexpr int CH = 4;
 
-// One thread per up-sampled pixel; block partials of dK/dV: part[b][blk][S][8].
+// A quad of lanes per up-sampled pixel (64 pixels per workgroup); lane r of
+// a quad takes the PSP bins s = r, r+4, ...  Softmax max / sums combine over
+// the quad; the per-bin dK/dV sums over the wave's 16 pixels reduce across
+// the 16 lanes that share r (4 butterfly steps for 4 bins at once, where one
+// lane per pixel needed 6 steps per bin).  Block partials of dK/dV:
+// part[b][blk][S][8].
 __global__ __launch_bounds__(256) void nlm_bwd_attn_kernel(
     const float* __restrict__ dout, int h, int w, int C, const float* __restrict__ q,
     const float* __restrict__ kpool, const float* __restrict__ vpool, int S,
@@ -45,72 +50,92 @@ __global__ __launch_bounds__(256) void nlm_bwd_attn_kernel(
     sWq[t] = wq[t];
   }
   __syncthreads();
-  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+  const int r = threadIdx.x & 3;
+  const int pix = blockIdx.x * (blockDim.x >> 2) + (threadIdx.x >> 2);
   const bool ok = pix < h * w;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t m = (int64_t)b * h * w + (ok ? pix : 0);
-  float qv[CH], dctx[CH];
-  for (int o = 0; o < CH; ++o) { qv[o] = ok ? q[m * CH + o] : 0.f; dctx[o] = 0.f; }
+  float qv[CH];
+  {
+    const float4 q4 = *reinterpret_cast<const float4*>(q + m * CH);
+    qv[0] = ok ? q4.x : 0.f; qv[1] = ok ? q4.y : 0.f;
+    qv[2] = ok ? q4.z : 0.f; qv[3] = ok ? q4.w : 0.f;
+  }
+  // dctx[r] by lane r, then exchanged within the quad
   const float* dop = dout + m * C;
-  if (ok) {
+  float dr = 0.f;
+  if (ok)
     for (int c = 0; c < C; c += 4) {
       const float4 g = *reinterpret_cast<const float4*>(dop + c);
-      const float gg[4] = {g.x, g.y, g.z, g.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int o = 0; o < CH; ++o) dctx[o] = fmaf(gg[e], sWW[(c + e) * CH + o], dctx[o]);
+      dr = fmaf(g.x, sWW[(c + 0) * CH + r], dr);
+      dr = fmaf(g.y, sWW[(c + 1) * CH + r], dr);
+      dr = fmaf(g.z, sWW[(c + 2) * CH + r], dr);
+      dr = fmaf(g.w, sWW[(c + 3) * CH + r], dr);
     }
-  }
-  // recompute the softmax row
+  const int qb = lane & ~3;
+  float dctx[CH];
+#pragma unroll
+  for (int o = 0; o < CH; ++o) dctx[o] = __shfl(dr, qb + o);
+  const float4* K4 = reinterpret_cast<const float4*>(sK);
+  const float4* V4 = reinterpret_cast<const float4*>(sV);
+  auto logit = [&](const float4 k) {
+    return fmaf(qv[0], k.x, fmaf(qv[1], k.y, fmaf(qv[2], k.z, qv[3] * k.w)));
+  };
+  auto dprod = [&](const float4 v) {
+    return fmaf(dctx[0], v.x, fmaf(dctx[1], v.y, fmaf(dctx[2], v.z, dctx[3] * v.w)));
+  };
+  // recompute the softmax row (max, then sums, each combined over the quad)
   float mx = -INFINITY;
-  for (int s = 0; s < S; ++s) {
-    float l = 0.f;
-#pragma unroll
-    for (int o = 0; o < CH; ++o) l = fmaf(qv[o], sK[s * CH + o], l);
-    mx = fmaxf(mx, l);
-  }
+  for (int s = r; s < S; s += 4) mx = fmaxf(mx, logit(K4[s]));
+  mx = fmaxf(mx, __shfl_xor(mx, 1));
+  mx = fmaxf(mx, __shfl_xor(mx, 2));
   float den = 0.f, sdp = 0.f;
-  for (int s = 0; s < S; ++s) {
-    float l = 0.f, dp = 0.f;
-#pragma unroll
-    for (int o = 0; o < CH; ++o) {
-      l = fmaf(qv[o], sK[s * CH + o], l);
-      dp = fmaf(dctx[o], sV[s * CH + o], dp);
-    }
-    const float e = __expf(l - mx);
+  for (int s = r; s < S; s += 4) {
+    const float e = __expf(logit(K4[s]) - mx);
     den += e;
-    sdp = fmaf(e, dp, sdp);
+    sdp = fmaf(e, dprod(V4[s]), sdp);
   }
+  den += __shfl_xor(den, 1);
+  den += __shfl_xor(den, 2);
+  sdp += __shfl_xor(sdp, 1);
+  sdp += __shfl_xor(sdp, 2);
   const float inv = 1.f / den;
   sdp *= inv;
   float dq[CH] = {0.f, 0.f, 0.f, 0.f};
-  for (int s = 0; s < S; ++s) {
-    float l = 0.f, dp = 0.f;
-#pragma unroll
-    for (int o = 0; o < CH; ++o) {
-      l = fmaf(qv[o], sK[s * CH + o], l);
-      dp = fmaf(dctx[o], sV[s * CH + o], dp);
-    }
-    const float P = ok ? __expf(l - mx) * inv : 0.f;
-    const float dL = P * (dp - sdp);
+  const int nk = (S + 3) >> 2;  // uniform trip count (shuffles inside)
+  for (int k = 0; k < nk; ++k) {
+    const int s = 4 * k + r;
+    const bool sv = s < S;
+    const float4 kk = K4[sv ? s : 0], vv = V4[sv ? s : 0];
+    const float P = (ok && sv) ? __expf(logit(kk) - mx) * inv : 0.f;
+    const float dL = P * (dprod(vv) - sdp);
+    dq[0] = fmaf(dL, kk.x, dq[0]);
+    dq[1] = fmaf(dL, kk.y, dq[1]);
+    dq[2] = fmaf(dL, kk.z, dq[2]);
+    dq[3] = fmaf(dL, kk.w, dq[3]);
     float v[2 * CH];
 #pragma unroll
     for (int o = 0; o < CH; ++o) {
-      dq[o] = fmaf(dL, sK[s * CH + o], dq[o]);
       v[o] = dL * qv[o];
       v[CH + o] = P * dctx[o];
     }
 #pragma unroll
     for (int o = 0; o < 2 * CH; ++o) {
       float a = v[o];
-      for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off);
+#pragma unroll
+      for (int off = 4; off < 64; off <<= 1) a += __shfl_xor(a, off);
       v[o] = a;
     }
-    if (lane == 0) {
-#pragma unroll
-      for (int o = 0; o < 2 * CH; ++o) red[(wave * S + s) * 2 * CH + o] = v[o];
+    if (lane < 4 && sv) {
+      float4* rd = reinterpret_cast<float4*>(red + (wave * S + s) * 2 * CH);
+      rd[0] = make_float4(v[0], v[1], v[2], v[3]);
+      rd[1] = make_float4(v[4], v[5], v[6], v[7]);
     }
+  }
+#pragma unroll
+  for (int o = 0; o < CH; ++o) {
+    dq[o] += __shfl_xor(dq[o], 1);
+    dq[o] += __shfl_xor(dq[o], 2);
   }
   __syncthreads();
   for (int t = threadIdx.x; t < S * 2 * CH; t += blockDim.x) {
@@ -119,16 +144,16 @@ __global__ __launch_bounds__(256) void nlm_bwd_attn_kernel(
     part[((int64_t)b * nblk + blockIdx.x) * S * 2 * CH + t] = a;
   }
   if (!ok) return;
-  for (int o = 0; o < CH; ++o) dq_out[m * CH + o] = dq[o];
+  if (r == 0) *reinterpret_cast<float4*>(dq_out + m * CH) = make_float4(dq[0], dq[1], dq[2], dq[3]);
   float* dx = dxup + m * C;
-  for (int c = 0; c < C; c += 4) {
+  for (int c = 4 * r; c < C; c += 16) {
     const float4 g = *reinterpret_cast<const float4*>(dop + c);
-    float r[4] = {g.x, g.y, g.z, g.w};  // the "+ x" path
+    float rr[4] = {g.x, g.y, g.z, g.w};  // the "+ x" path
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
-      for (int o = 0; o < CH; ++o) r[e] = fmaf(sWq[o * C + c + e], dq[o], r[e]);
-    *reinterpret_cast<float4*>(dx + c) = make_float4(r[0], r[1], r[2], r[3]);
+      for (int o = 0; o < CH; ++o) rr[e] = fmaf(sWq[o * C + c + e], dq[o], rr[e]);
+    *reinterpret_cast<float4*>(dx + c) = make_float4(rr[0], rr[1], rr[2], rr[3]);
   }
 }
 
@@ -282,7 +307,7 @@ extern "C" int jabd_nlm_bwd_attn_f32(const float* dout, int32_t B, int32_t h, in
   JABD_REQUIRE(dout && q && kpool && vpool && wW && wq && dq && dxup && part && dk && dv &&
                    C % 4 == 0,
                "nlm_bwd_attn: bad args");
-  const int nblk = (int)cdiv((int64_t)h * w, 256);
+  const int nblk = (int)cdiv((int64_t)h * w, 64);  // a lane quad per pixel
   const size_t smem = (2 * (size_t)S * CH + 2 * (size_t)C * CH + 4 * (size_t)S * 2 * CH) * 4;
   JABD_REQUIRE(smem <= 64 * 1024, "nlm_bwd_attn: LDS %zu > 64KiB", smem);
   hipStream_t st = as_stream(stream);

@@ -325,7 +325,7 @@ class NlmFn(torch.autograd.Function):
         ch = wq.shape[0]
         S = kp.shape[1]
         dev = dout.device
-        nblk = (h * w + 255) // 256
+        nblk = (h * w + 63) // 64  # jabd.h: one partial block per 64 pixels
         dq = torch.empty((B, h, w, ch), dtype=torch.float32, device=dev)
         dxup = torch.empty((B, h, w, C), dtype=torch.float32, device=dev)
         part = torch.empty((B, nblk, S, 2 * ch), dtype=torch.float32, device=dev)
