@@ -967,8 +967,9 @@ __global__ void scale_bwd_kernel(const float* __restrict__ da, const float* __re
         const int64_t off = ((int64_t)b * HW + q) * C;
         const float4 g = reinterpret_cast<const float4*>(da + off)[cg];
         const float4 v = reinterpret_cast<const float4*>(x + off)[cg];
-        reinterpret_cast<float4*>(dx + off)[cg] =
-            make_float4(g.x * sc.x, g.y * sc.y, g.z * sc.z, g.w * sc.w);
+        if (dx)  // (jabd_eca_bwd_f32 writes dx in its final pass instead)
+          reinterpret_cast<float4*>(dx + off)[cg] =
+              make_float4(g.x * sc.x, g.y * sc.y, g.z * sc.z, g.w * sc.w);
         acc.x = fmaf(g.x, v.x, acc.x); acc.y = fmaf(g.y, v.y, acc.y);
         acc.z = fmaf(g.z, v.z, acc.z); acc.w = fmaf(g.w, v.w, acc.w);
       }
@@ -1036,18 +1037,24 @@ __global__ void eca_gate_bwd_kernel(const float* __restrict__ part, int nblk, in
   }
 }
 
-__global__ void add_bc_kernel(float* __restrict__ dx, const float* __restrict__ v, int64_t HW, int C,
-                              int64_t total4) {
+// dx = da * s[b][c] + v[b][c]: the gate-scaled gradient plus the ECA mean
+// term in one pass (replaces writing da*s in scale_bwd and a read-modify-write
+// add_bc pass: 4 tensor passes instead of 5).
+__global__ void scale_add_kernel(const float* __restrict__ da, const float* __restrict__ s,
+                                 const float* __restrict__ v, int64_t HW, int C, int64_t total4,
+                                 float* __restrict__ dx) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= total4) return;
   const int C4 = C >> 2;
   const int64_t m = i / C4;
   const int c4 = (int)(i - m * C4);
-  const int b = (int)(m / HW);
-  const float4 a = reinterpret_cast<const float4*>(v + (int64_t)b * C)[c4];
-  float4 d = reinterpret_cast<float4*>(dx)[i];
-  d.x += a.x; d.y += a.y; d.z += a.z; d.w += a.w;
-  reinterpret_cast<float4*>(dx)[i] = d;
+  const int64_t bc = (m / HW) * C4 + c4;
+  const float4 sc = reinterpret_cast<const float4*>(s)[bc];
+  const float4 a = reinterpret_cast<const float4*>(v)[bc];
+  const float4 g = reinterpret_cast<const float4*>(da)[i];
+  reinterpret_cast<float4*>(dx)[i] =
+      make_float4(fmaf(g.x, sc.x, a.x), fmaf(g.y, sc.y, a.y), fmaf(g.z, sc.z, a.z),
+                  fmaf(g.w, sc.w, a.w));
 }
 
 __global__ void eca_w_reduce_kernel(const float* __restrict__ dw1d_img, int B, int k,
@@ -1363,14 +1370,15 @@ extern "C" int jabd_eca_bwd_f32(const float* da, const float* x, int64_t B, int6
   hipStream_t st = as_stream(stream);
   const int64_t per = cdiv(HW, nblk);
   dim3 g((unsigned)nblk, (unsigned)B);
-  scale_bwd_kernel<<<g, 256, 0, st>>>(da, x, scale, HW, C, per, nblk, dx, part);
+  scale_bwd_kernel<<<g, 256, 0, st>>>(da, x, scale, HW, C, per, nblk, nullptr, part);
   if (int e = check_launch("scale_bwd")) return e;
   eca_gate_bwd_kernel<<<(unsigned)B, 256, 2 * C * sizeof(float), st>>>(
       part, nblk, C, mean, scale, w1d, k, gate, 1.f / (float)HW, dmean_ws, dw1d_ws);
   if (int e = check_launch("eca_gate_bwd")) return e;
   const int64_t total4 = B * HW * (C / 4);
-  add_bc_kernel<<<(unsigned)cdiv(total4, 256), 256, 0, st>>>(dx, dmean_ws, HW, C, total4);
-  if (int e = check_launch("eca_add")) return e;
+  scale_add_kernel<<<(unsigned)cdiv(total4, 256), 256, 0, st>>>(da, scale, dmean_ws, HW, C, total4,
+                                                                dx);
+  if (int e = check_launch("eca_scale_add")) return e;
   eca_w_reduce_kernel<<<1, 64, 0, st>>>(dw1d_ws, (int)B, k, dw1d);
   return check_launch("eca_w_reduce");
 }
