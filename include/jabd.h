@@ -103,6 +103,17 @@ int jabd_match_encode_f32(const float* targets, const int64_t* offsets,
                           float* landm_t, void* ws, size_t ws_bytes,
                           jabd_stream_t stream);
 
+/* match_iou() — nets/retinaface_training_DIOU.py:176-246 (the DIoU variant's
+ * matcher): same assignment and landmark encoding as jabd_match_encode_f32,
+ * but loc_t[B,A,4] holds the matched truth corners (x1,y1,x2,y2) unencoded
+ * (:230 `loc = matches`).  Same arguments and workspace. */
+int jabd_match_iou_f32(const float* targets, const int64_t* offsets,
+                       int64_t batch, int64_t max_gt, const float* priors,
+                       int64_t num_priors, float threshold, float var0,
+                       float var1, float* loc_t, int64_t* conf_t,
+                       float* landm_t, void* ws, size_t ws_bytes,
+                       jabd_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * A9 MultiBoxLoss — nets/retinaface_training.py:183-303.
  * Forward writes un-normalised sums and counts so data-parallel callers can
@@ -131,6 +142,27 @@ int jabd_multibox_loss_bwd_f32(const float* loc, const float* conf,
                                const int64_t* counts,
                                float* grad_loc, float* grad_conf,
                                float* grad_landm, jabd_stream_t stream);
+/* The DIoU MultiBoxLoss — nets/retinaface_training_DIOU.py:524-665: sums[0]
+ * is Σ over positives of 1 - clamp(DIoU(decode(loc, prior), loc_t), -1, 1)
+ * (IouLoss 'Diou', :491-522, bbox_overlaps_diou :402-442) with loc_t from
+ * jabd_match_iou_f32; the CE and landmark terms, counts, sel and workspace
+ * are those of jabd_multibox_loss_fwd_f32.  priors [A,4] (cx,cy,w,h). */
+int jabd_multibox_diou_loss_fwd_f32(const float* loc, const float* conf,
+                                    const float* landm, const float* loc_t,
+                                    const int64_t* conf_t, const float* landm_t,
+                                    const float* priors, float var0, float var1,
+                                    int64_t batch, int64_t num_priors, int neg_pos,
+                                    float* sums, int64_t* counts, uint8_t* sel,
+                                    void* ws, size_t ws_bytes, jabd_stream_t stream);
+int jabd_multibox_diou_loss_bwd_f32(const float* loc, const float* conf,
+                                    const float* landm, const float* loc_t,
+                                    const int64_t* conf_t, const float* landm_t,
+                                    const float* priors, float var0, float var1,
+                                    const uint8_t* sel, int64_t batch,
+                                    int64_t num_priors, const float* gout,
+                                    const int64_t* counts, float* grad_loc,
+                                    float* grad_conf, float* grad_landm,
+                                    jabd_stream_t stream);
 /* loss[i] = sums[i] / max(counts[i==2 ? 1 : 0], 1)  (device, 1 thread). */
 int jabd_multibox_loss_finalize_f32(const float* sums, const int64_t* counts,
                                     float* loss, jabd_stream_t stream);

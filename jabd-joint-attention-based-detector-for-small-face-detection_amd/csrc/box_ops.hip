@@ -171,7 +171,10 @@ __global__ __launch_bounds__(256) void match_best_prior_kernel(
 }
 
 // best_truth per prior (:121-123), forced override (:127-130), threshold
-// (:145), encode (:62-73) and encode_landm (:75-86).
+// (:145), encode (:62-73) and encode_landm (:75-86).  kRaw is match_iou()
+// (nets/retinaface_training_DIOU.py:176-246): the same assignment, but loc_t
+// holds the matched truth box corners (:230-231 `loc = matches`).
+template <bool kRaw>
 __global__ __launch_bounds__(256) void match_assign_kernel(
     const float* __restrict__ targets, const int64_t* __restrict__ offsets,
     const float4* __restrict__ pri, int64_t A, const int* __restrict__ forced,
@@ -209,6 +212,9 @@ __global__ __launch_bounds__(256) void match_assign_kernel(
   conf_t[ba] = (int64_t)label;
   // encode: ((m_lo+m_hi)/2 - p_c) / (v0*p_wh); log((m_hi-m_lo)/p_wh) / v1
   const float sw = v0 * p.z, sh = v0 * p.w;
+  if (kRaw) {
+    reinterpret_cast<float4*>(loc_t)[ba] = make_float4(tr[0], tr[1], tr[2], tr[3]);
+  } else {
   float gx = (tr[0] + tr[2]) / 2.f - p.x;
   float gy = (tr[1] + tr[3]) / 2.f - p.y;
   gx /= sw;
@@ -216,6 +222,7 @@ __global__ __launch_bounds__(256) void match_assign_kernel(
   float gw = logf((tr[2] - tr[0]) / p.z) / v1;
   float gh = logf((tr[3] - tr[1]) / p.w) / v1;
   reinterpret_cast<float4*>(loc_t)[ba] = make_float4(gx, gy, gw, gh);
+  }
   float* lm = landm_t + ba * 10;
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
@@ -246,6 +253,100 @@ __device__ __forceinline__ float smooth_l1(float d) {
   return z < 1.f ? 0.5f * z * z : z - 0.5f;
 }
 
+// ---------------------------------------------------------------------------
+// DIoU box term — nets/retinaface_training_DIOU.py: IouLoss 'Diou' (:491-522)
+// over decode() (:319-337) and bbox_overlaps_diou (:402-442), paired rows:
+//   1 - clamp(I/U - |c2-c1|^2 / |outer|^2, -1, 1)
+// ---------------------------------------------------------------------------
+struct DiouTerms {
+  Box4 b;                                  // decoded prediction (bboxes1)
+  float w1, h1, iwr, ihr, iw, ih, inter;   // iwr/ihr before clamp(min=0)
+  float dcx, dcy, diag, owr, ohr, ow, oh, odiag, uni, d;
+};
+
+__device__ __forceinline__ DiouTerms diou_terms(const float4 l, const float4 p, const float4 t,
+                                                float v0, float v1) {
+  const float la[4] = {l.x, l.y, l.z, l.w};
+  DiouTerms r;
+  r.b = decode_one(la, p, v0, v1);
+  const Box4 b = r.b;
+  r.w1 = b.x2 - b.x1;
+  r.h1 = b.y2 - b.y1;
+  const float w2 = t.z - t.x, h2 = t.w - t.y;
+  const float area1 = r.w1 * r.h1, area2 = w2 * h2;
+  const float cx1 = (b.x2 + b.x1) / 2.f, cy1 = (b.y2 + b.y1) / 2.f;
+  const float cx2 = (t.z + t.x) / 2.f, cy2 = (t.w + t.y) / 2.f;
+  r.iwr = nan_min(b.x2, t.z) - nan_max(b.x1, t.x);
+  r.ihr = nan_min(b.y2, t.w) - nan_max(b.y1, t.y);
+  r.iw = nan_max(r.iwr, 0.f);
+  r.ih = nan_max(r.ihr, 0.f);
+  r.inter = r.iw * r.ih;
+  r.dcx = cx2 - cx1;
+  r.dcy = cy2 - cy1;
+  r.diag = r.dcx * r.dcx + r.dcy * r.dcy;
+  r.owr = nan_max(b.x2, t.z) - nan_min(b.x1, t.x);
+  r.ohr = nan_max(b.y2, t.w) - nan_min(b.y1, t.y);
+  r.ow = nan_max(r.owr, 0.f);
+  r.oh = nan_max(r.ohr, 0.f);
+  r.odiag = r.ow * r.ow + r.oh * r.oh;
+  r.uni = area1 + area2 - r.inter;
+  r.d = r.inter / r.uni - r.diag / r.odiag;
+  return r;
+}
+
+__device__ __forceinline__ float diou_loss(const float4 l, const float4 p, const float4 t,
+                                           float v0, float v1) {
+  const float d = diou_terms(l, p, t, v0, v1).d;
+  return 1.f - fminf(fmaxf(d, -1.f), 1.f);
+}
+
+// torch.minimum/maximum backward: the whole gradient to the winner, half each on a tie.
+__device__ __forceinline__ float pick_lo(float a, float b) { return a < b ? 1.f : (a == b ? .5f : 0.f); }
+__device__ __forceinline__ float pick_hi(float a, float b) { return a > b ? 1.f : (a == b ? .5f : 0.f); }
+
+// d(loss)/d(loc) for one positive, scaled by s (= dL/dloss_l / N).
+__device__ __forceinline__ float4 diou_grad(const float4 l, const float4 p, const float4 t,
+                                            float v0, float v1, float s) {
+  const DiouTerms r = diou_terms(l, p, t, v0, v1);
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (!(r.d >= -1.f && r.d <= 1.f)) return g;  // clamp() passes the gradient on [-1, 1]
+  const float gd = -s;
+  const float U2 = r.uni * r.uni;
+  const float gI = gd * (1.f / r.uni + r.inter / U2);
+  const float gA1 = gd * (-r.inter / U2);
+  const float gD = gd * (-1.f / r.odiag);
+  const float gO = gd * (r.diag / (r.odiag * r.odiag));
+  const Box4 b = r.b;
+  float gx1 = 0.f, gy1 = 0.f, gx2 = 0.f, gy2 = 0.f;
+  // area1 = w1*h1
+  gx2 += gA1 * r.h1; gx1 -= gA1 * r.h1;
+  gy2 += gA1 * r.w1; gy1 -= gA1 * r.w1;
+  // inter = clamp(iw)*clamp(ih); iw = min(x2,tx2) - max(x1,tx1)
+  const float giw = r.iwr >= 0.f ? gI * r.ih : 0.f;
+  const float gih = r.ihr >= 0.f ? gI * r.iw : 0.f;
+  gx2 += giw * pick_lo(b.x2, t.z); gx1 -= giw * pick_hi(b.x1, t.x);
+  gy2 += gih * pick_lo(b.y2, t.w); gy1 -= gih * pick_hi(b.y1, t.y);
+  // diag = (c2 - c1)^2, c1 = (x2 + x1)/2
+  const float gcx1 = gD * -2.f * r.dcx, gcy1 = gD * -2.f * r.dcy;
+  gx1 += gcx1 * .5f; gx2 += gcx1 * .5f;
+  gy1 += gcy1 * .5f; gy2 += gcy1 * .5f;
+  // odiag = clamp(ow)^2 + clamp(oh)^2; ow = max(x2,tx2) - min(x1,tx1)
+  const float gow = r.owr >= 0.f ? gO * 2.f * r.ow : 0.f;
+  const float goh = r.ohr >= 0.f ? gO * 2.f * r.oh : 0.f;
+  gx2 += gow * pick_hi(b.x2, t.z); gx1 -= gow * pick_lo(b.x1, t.x);
+  gy2 += goh * pick_hi(b.y2, t.w); gy1 -= goh * pick_lo(b.y1, t.y);
+  // decode: x1 = cx - W/2, x2 = x1 + W; cx = px + l0*v0*pw, W = pw*exp(l2*v1)
+  const float gcx = gx1 + gx2, gcy = gy1 + gy2;
+  const float gW = (gx2 - gx1) * .5f, gH = (gy2 - gy1) * .5f;
+  const float W = p.z * expf(l.z * v1);
+  const float H = p.w * expf(l.w * v1);
+  g.x = gcx * v0 * p.z;
+  g.y = gcy * v0 * p.w;
+  g.z = gW * W * v1;
+  g.w = gH * H * v1;
+  return g;
+}
+
 // Global max of conf (log_sum_exp uses x.data.max(), :86-88): block partials.
 __global__ __launch_bounds__(kLossBlock) void conf_max_partial(const float* __restrict__ conf,
                                                                int64_t total,
@@ -268,10 +369,14 @@ __global__ __launch_bounds__(kLossBlock) void conf_max_partial(const float* __re
 
 // Per prior: box/landmark smooth-L1 partials, positive counts, and the
 // hard-negative mining loss (lse(x) - x[t], positives zeroed, :256-262).
+// kDiou: the box term is the DIoU loss of the decoded prediction against the
+// raw matched truth (retinaface_training_DIOU.py:600-602); pri/v0/v1 unused otherwise.
+template <bool kDiou>
 __global__ __launch_bounds__(kLossBlock) void loss_elem_kernel(
     const float* __restrict__ loc, const float* __restrict__ conf,
     const float* __restrict__ landm, const float* __restrict__ loc_t,
     const int64_t* __restrict__ conf_t, const float* __restrict__ landm_t, int64_t A,
+    const float4* __restrict__ pri, float v0, float v1,
     const float* __restrict__ gmax_part, int n_gmax_part, float* __restrict__ mining,
     uint8_t* __restrict__ sel, float* __restrict__ part_l, float* __restrict__ part_lm,
     int* __restrict__ npos_img, int* __restrict__ npos1_img) {
@@ -297,8 +402,11 @@ __global__ __launch_bounds__(kLossBlock) void loss_elem_kernel(
     if (pos) {
       float4 x = reinterpret_cast<const float4*>(loc)[i];
       float4 y = reinterpret_cast<const float4*>(loc_t)[i];
-      sl = smooth_l1(x.x - y.x) + smooth_l1(x.y - y.y) + smooth_l1(x.z - y.z) +
-           smooth_l1(x.w - y.w);
+      if (kDiou)
+        sl = diou_loss(x, pri[a], y, v0, v1);
+      else
+        sl = smooth_l1(x.x - y.x) + smooth_l1(x.y - y.y) + smooth_l1(x.z - y.z) +
+             smooth_l1(x.w - y.w);
     }
     if (pos1) {
       const float* x = landm + i * 10;
@@ -476,10 +584,12 @@ __global__ void loss_normalize_kernel(const float* __restrict__ sums,
 
 __device__ __forceinline__ float sl1_grad(float d) { return d < -1.f ? -1.f : (d > 1.f ? 1.f : d); }
 
+template <bool kDiou>
 __global__ void loss_bwd_kernel(const float* __restrict__ loc, const float* __restrict__ conf,
                                 const float* __restrict__ landm, const float* __restrict__ loc_t,
                                 const int64_t* __restrict__ conf_t,
                                 const float* __restrict__ landm_t,
+                                const float4* __restrict__ pri, int64_t A, float v0, float v1,
                                 const uint8_t* __restrict__ sel, int64_t total,
                                 const float* __restrict__ gout,
                                 const int64_t* __restrict__ counts, float* __restrict__ gl,
@@ -496,8 +606,11 @@ __global__ void loss_bwd_kernel(const float* __restrict__ loc, const float* __re
     if (pos) {
       float4 x = reinterpret_cast<const float4*>(loc)[i];
       float4 y = reinterpret_cast<const float4*>(loc_t)[i];
-      g = make_float4(sl1_grad(x.x - y.x) * sl, sl1_grad(x.y - y.y) * sl,
-                      sl1_grad(x.z - y.z) * sl, sl1_grad(x.w - y.w) * sl);
+      if (kDiou)
+        g = diou_grad(x, pri[i % A], y, v0, v1, sl);
+      else
+        g = make_float4(sl1_grad(x.x - y.x) * sl, sl1_grad(x.y - y.y) * sl,
+                        sl1_grad(x.z - y.z) * sl, sl1_grad(x.w - y.w) * sl);
     }
     reinterpret_cast<float4*>(gl)[i] = g;
   }
@@ -625,12 +738,10 @@ extern "C" int jabd_match_workspace_size(int64_t batch, int64_t num_priors, size
   return JABD_OK;
 }
 
-extern "C" int jabd_match_encode_f32(const float* targets, const int64_t* offsets,
-                                     int64_t batch, int64_t max_gt, const float* priors,
-                                     int64_t num_priors, float threshold, float var0,
-                                     float var1, float* loc_t, int64_t* conf_t,
-                                     float* landm_t, void* ws, size_t ws_bytes,
-                                     jabd_stream_t stream) {
+static int match_impl(bool raw, const float* targets, const int64_t* offsets, int64_t batch,
+                      int64_t max_gt, const float* priors, int64_t num_priors, float threshold,
+                      float var0, float var1, float* loc_t, int64_t* conf_t, float* landm_t,
+                      void* ws, size_t ws_bytes, jabd_stream_t stream) {
   JABD_REQUIRE(batch >= 0 && num_priors >= 0 && max_gt >= 0, "match: negative size");
   if (batch == 0 || num_priors == 0) return JABD_OK;
   JABD_REQUIRE(max_gt > 0, "match: an image has no targets (reference match() fails too)");
@@ -647,9 +758,32 @@ extern "C" int jabd_match_encode_f32(const float* targets, const int64_t* offset
   match_best_prior_kernel<<<g1, 256, 0, st>>>(targets, offsets, pri, num_priors, forced);
   if (int e = check_launch("match_best_prior")) return e;
   dim3 g2((unsigned)cdiv(num_priors, 256), (unsigned)batch);
-  match_assign_kernel<<<g2, 256, max_gt * 5 * sizeof(float), st>>>(
-      targets, offsets, pri, num_priors, forced, threshold, var0, var1, loc_t, conf_t, landm_t);
+  if (raw)
+    match_assign_kernel<true><<<g2, 256, max_gt * 5 * sizeof(float), st>>>(
+        targets, offsets, pri, num_priors, forced, threshold, var0, var1, loc_t, conf_t, landm_t);
+  else
+    match_assign_kernel<false><<<g2, 256, max_gt * 5 * sizeof(float), st>>>(
+        targets, offsets, pri, num_priors, forced, threshold, var0, var1, loc_t, conf_t, landm_t);
   return check_launch("match_assign");
+}
+
+extern "C" int jabd_match_encode_f32(const float* targets, const int64_t* offsets,
+                                     int64_t batch, int64_t max_gt, const float* priors,
+                                     int64_t num_priors, float threshold, float var0,
+                                     float var1, float* loc_t, int64_t* conf_t,
+                                     float* landm_t, void* ws, size_t ws_bytes,
+                                     jabd_stream_t stream) {
+  return match_impl(false, targets, offsets, batch, max_gt, priors, num_priors, threshold, var0,
+                    var1, loc_t, conf_t, landm_t, ws, ws_bytes, stream);
+}
+
+extern "C" int jabd_match_iou_f32(const float* targets, const int64_t* offsets, int64_t batch,
+                                  int64_t max_gt, const float* priors, int64_t num_priors,
+                                  float threshold, float var0, float var1, float* loc_t,
+                                  int64_t* conf_t, float* landm_t, void* ws, size_t ws_bytes,
+                                  jabd_stream_t stream) {
+  return match_impl(true, targets, offsets, batch, max_gt, priors, num_priors, threshold, var0,
+                    var1, loc_t, conf_t, landm_t, ws, ws_bytes, stream);
 }
 
 extern "C" int jabd_multibox_workspace_size(int64_t batch, int64_t num_priors, size_t* bytes) {
@@ -660,12 +794,11 @@ extern "C" int jabd_multibox_workspace_size(int64_t batch, int64_t num_priors, s
   return JABD_OK;
 }
 
-extern "C" int jabd_multibox_loss_fwd_f32(const float* loc, const float* conf,
-                                          const float* landm, const float* loc_t,
-                                          const int64_t* conf_t, const float* landm_t,
-                                          int64_t batch, int64_t num_priors, int neg_pos,
-                                          float* sums, int64_t* counts, uint8_t* sel, void* ws,
-                                          size_t ws_bytes, jabd_stream_t stream) {
+static int loss_fwd_impl(const float* loc, const float* conf, const float* landm,
+                         const float* loc_t, const int64_t* conf_t, const float* landm_t,
+                         const float* priors, float v0, float v1, int64_t batch,
+                         int64_t num_priors, int neg_pos, float* sums, int64_t* counts,
+                         uint8_t* sel, void* ws, size_t ws_bytes, jabd_stream_t stream) {
   JABD_REQUIRE(batch > 0 && num_priors > 0, "multibox: empty batch");
   JABD_REQUIRE(num_priors < 0x7fffffff, "multibox: too many priors");
   JABD_REQUIRE(loc && conf && landm && loc_t && conf_t && landm_t && sums && counts && sel,
@@ -690,15 +823,44 @@ extern "C" int jabd_multibox_loss_fwd_f32(const float* loc, const float* conf,
   conf_max_partial<<<(unsigned)ng, kLossBlock, 0, st>>>(conf, B * A * 2, gpart);
   if (int e = check_launch("conf_max")) return e;
   dim3 g((unsigned)nblk, (unsigned)B);
-  loss_elem_kernel<<<g, kLossBlock, 0, st>>>(loc, conf, landm, loc_t, conf_t, landm_t, A, gpart,
-                                             (int)ng, mining, sel, part_l, part_lm, npos,
-                                             npos1);
+  const float4* pri = reinterpret_cast<const float4*>(priors);
+  if (pri)
+    loss_elem_kernel<true><<<g, kLossBlock, 0, st>>>(loc, conf, landm, loc_t, conf_t, landm_t, A,
+                                                     pri, v0, v1, gpart, (int)ng, mining, sel,
+                                                     part_l, part_lm, npos, npos1);
+  else
+    loss_elem_kernel<false><<<g, kLossBlock, 0, st>>>(loc, conf, landm, loc_t, conf_t, landm_t,
+                                                      A, pri, v0, v1, gpart, (int)ng, mining,
+                                                      sel, part_l, part_lm, npos, npos1);
   if (int e = check_launch("loss_elem")) return e;
   ohem_select_kernel<<<(unsigned)B, kSelBlock, 0, st>>>(mining, conf, A, neg_pos, npos, sel, ce);
   if (int e = check_launch("ohem_select")) return e;
   loss_final_kernel<<<1, 64, 0, st>>>(part_l, part_lm, B * nblk, ce, npos, npos1, (int)B, sums,
                                       counts);
   return check_launch("loss_final");
+}
+
+extern "C" int jabd_multibox_loss_fwd_f32(const float* loc, const float* conf,
+                                          const float* landm, const float* loc_t,
+                                          const int64_t* conf_t, const float* landm_t,
+                                          int64_t batch, int64_t num_priors, int neg_pos,
+                                          float* sums, int64_t* counts, uint8_t* sel, void* ws,
+                                          size_t ws_bytes, jabd_stream_t stream) {
+  return loss_fwd_impl(loc, conf, landm, loc_t, conf_t, landm_t, nullptr, 0.f, 0.f, batch,
+                       num_priors, neg_pos, sums, counts, sel, ws, ws_bytes, stream);
+}
+
+extern "C" int jabd_multibox_diou_loss_fwd_f32(const float* loc, const float* conf,
+                                               const float* landm, const float* loc_t,
+                                               const int64_t* conf_t, const float* landm_t,
+                                               const float* priors, float var0, float var1,
+                                               int64_t batch, int64_t num_priors, int neg_pos,
+                                               float* sums, int64_t* counts, uint8_t* sel,
+                                               void* ws, size_t ws_bytes,
+                                               jabd_stream_t stream) {
+  JABD_REQUIRE(priors, "multibox_diou: null priors");
+  return loss_fwd_impl(loc, conf, landm, loc_t, conf_t, landm_t, priors, var0, var1, batch,
+                       num_priors, neg_pos, sums, counts, sel, ws, ws_bytes, stream);
 }
 
 extern "C" int jabd_multibox_loss_finalize_f32(const float* sums, const int64_t* counts,
@@ -719,8 +881,26 @@ extern "C" int jabd_multibox_loss_bwd_f32(const float* loc, const float* conf,
   const int64_t total = batch * num_priors;
   if (total <= 0) return JABD_OK;
   JABD_REQUIRE(sel && gout && counts, "multibox_bwd: null pointer");
-  loss_bwd_kernel<<<(unsigned)cdiv(total, 256), 256, 0, as_stream(stream)>>>(
-      loc, conf, landm, loc_t, conf_t, landm_t, sel, total, gout, counts, grad_loc, grad_conf,
-      grad_landm);
+  loss_bwd_kernel<false><<<(unsigned)cdiv(total, 256), 256, 0, as_stream(stream)>>>(
+      loc, conf, landm, loc_t, conf_t, landm_t, nullptr, num_priors, 0.f, 0.f, sel, total, gout,
+      counts, grad_loc, grad_conf, grad_landm);
   return check_launch("multibox_bwd");
+}
+
+extern "C" int jabd_multibox_diou_loss_bwd_f32(const float* loc, const float* conf,
+                                               const float* landm, const float* loc_t,
+                                               const int64_t* conf_t, const float* landm_t,
+                                               const float* priors, float var0, float var1,
+                                               const uint8_t* sel, int64_t batch,
+                                               int64_t num_priors, const float* gout,
+                                               const int64_t* counts, float* grad_loc,
+                                               float* grad_conf, float* grad_landm,
+                                               jabd_stream_t stream) {
+  const int64_t total = batch * num_priors;
+  if (total <= 0) return JABD_OK;
+  JABD_REQUIRE(sel && gout && counts && priors, "multibox_diou_bwd: null pointer");
+  loss_bwd_kernel<true><<<(unsigned)cdiv(total, 256), 256, 0, as_stream(stream)>>>(
+      loc, conf, landm, loc_t, conf_t, landm_t, reinterpret_cast<const float4*>(priors),
+      num_priors, var0, var1, sel, total, gout, counts, grad_loc, grad_conf, grad_landm);
+  return check_launch("multibox_diou_bwd");
 }

@@ -135,11 +135,13 @@ def detect(loc, conf, landm, priors, variances, conf_threshold=0.5, nms_threshol
 
 
 # --------------------------------------------------------------------------- match
-def match_encode(targets, priors, threshold, variances):
+def match_encode(targets, priors, threshold, variances, raw_loc=False):
     """Batched match()+encode() — nets/retinaface_training.py:93-162.
 
     targets: list of B device tensors [n_i,15]; priors [A,4].
     Returns loc_t [B,A,4], conf_t [B,A] int64, landm_t [B,A,10].
+    raw_loc=True is match_iou() (nets/retinaface_training_DIOU.py:176-246):
+    loc_t holds the matched truth corners instead of the encoded offsets.
     """
     priors = _dev("match.priors", priors)
     dev = priors.device
@@ -156,15 +158,19 @@ def match_encode(targets, priors, threshold, variances):
     conf_t = torch.empty((B, A), dtype=torch.int64, device=dev)
     landm_t = torch.empty((B, A, 10), dtype=torch.float32, device=dev)
     ws = _ws(_size_query("jabd_match_workspace_size", B, A), dev)
-    call("jabd_match_encode_f32", _p(flat), _p(offsets), B, max(counts) if counts else 0,
+    call("jabd_match_iou_f32" if raw_loc else "jabd_match_encode_f32", _p(flat), _p(offsets), B, max(counts) if counts else 0,
          _p(priors), A, float(threshold), float(variances[0]), float(variances[1]), _p(loc_t),
          _p(conf_t), _p(landm_t), _p(ws), ws.numel(), _stream())
     return loc_t, conf_t, landm_t
 
 
 # --------------------------------------------------------------------------- loss
-def multibox_sums(loc, conf, landm, loc_t, conf_t, landm_t, neg_pos):
-    """Un-normalised MultiBoxLoss sums [3], counts [2] and the selection mask."""
+def multibox_sums(loc, conf, landm, loc_t, conf_t, landm_t, neg_pos, diou=None):
+    """Un-normalised MultiBoxLoss sums [3], counts [2] and the selection mask.
+
+    diou=(priors [A,4], variances): the box term is the DIoU loss of
+    nets/retinaface_training_DIOU.py:491-522 (loc_t from match_encode(raw_loc=True)).
+    """
     loc, conf, landm = (_dev("loss.loc", loc), _dev("loss.conf", conf),
                         _dev("loss.landm", landm))
     loc_t, landm_t = _dev("loss.loc_t", loc_t), _dev("loss.landm_t", landm_t)
@@ -175,10 +181,24 @@ def multibox_sums(loc, conf, landm, loc_t, conf_t, landm_t, neg_pos):
     counts = torch.empty(2, dtype=torch.int64, device=dev)
     sel = torch.empty((B, A), dtype=torch.uint8, device=dev)
     ws = _ws(_size_query("jabd_multibox_workspace_size", B, A), dev)
-    call("jabd_multibox_loss_fwd_f32", _p(loc), _p(conf), _p(landm), _p(loc_t), _p(conf_t),
-         _p(landm_t), B, A, int(neg_pos), _p(sums), _p(counts), _p(sel), _p(ws), ws.numel(),
-         _stream())
+    if diou is None:
+        call("jabd_multibox_loss_fwd_f32", _p(loc), _p(conf), _p(landm), _p(loc_t), _p(conf_t),
+             _p(landm_t), B, A, int(neg_pos), _p(sums), _p(counts), _p(sel), _p(ws),
+             ws.numel(), _stream())
+    else:
+        pri, var = _diou_priors(diou, A)
+        call("jabd_multibox_diou_loss_fwd_f32", _p(loc), _p(conf), _p(landm), _p(loc_t),
+             _p(conf_t), _p(landm_t), _p(pri), float(var[0]), float(var[1]), B, A,
+             int(neg_pos), _p(sums), _p(counts), _p(sel), _p(ws), ws.numel(), _stream())
     return sums, counts, sel
+
+
+def _diou_priors(diou, A):
+    pri, var = diou
+    pri = _dev("loss.priors", pri)
+    if tuple(pri.shape) != (A, 4):
+        raise ValueError(f"DIoU loss: priors {tuple(pri.shape)} != ({A}, 4)")
+    return pri, var
 
 
 def multibox_normalize(sums, counts):
@@ -187,14 +207,21 @@ def multibox_normalize(sums, counts):
     return loss
 
 
-def multibox_backward(loc, conf, landm, loc_t, conf_t, landm_t, sel, gout, counts):
+def multibox_backward(loc, conf, landm, loc_t, conf_t, landm_t, sel, gout, counts, diou=None):
     B, A = loc.shape[0], loc.shape[1]
     gl = torch.empty_like(loc)
     gc = torch.empty_like(conf)
     glm = torch.empty_like(landm)
     gout = _dev("loss.gout", gout)
-    call("jabd_multibox_loss_bwd_f32", _p(loc), _p(conf), _p(landm), _p(loc_t), _p(conf_t),
-         _p(landm_t), _p(sel), B, A, _p(gout), _p(counts), _p(gl), _p(gc), _p(glm), _stream())
+    if diou is None:
+        call("jabd_multibox_loss_bwd_f32", _p(loc), _p(conf), _p(landm), _p(loc_t), _p(conf_t),
+             _p(landm_t), _p(sel), B, A, _p(gout), _p(counts), _p(gl), _p(gc), _p(glm),
+             _stream())
+    else:
+        pri, var = _diou_priors(diou, A)
+        call("jabd_multibox_diou_loss_bwd_f32", _p(loc), _p(conf), _p(landm), _p(loc_t),
+             _p(conf_t), _p(landm_t), _p(pri), float(var[0]), float(var[1]), _p(sel), B, A,
+             _p(gout), _p(counts), _p(gl), _p(gc), _p(glm), _stream())
     return gl, gc, glm
 
 

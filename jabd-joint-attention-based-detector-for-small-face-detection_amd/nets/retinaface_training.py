@@ -17,13 +17,15 @@ from jabd_amd import ops
 
 class _MultiBoxLossFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, loc, conf, landm, loc_t, conf_t, landm_t, neg_pos, group):
-        sums, counts, sel = ops.multibox_sums(loc, conf, landm, loc_t, conf_t, landm_t, neg_pos)
+    def forward(ctx, loc, conf, landm, loc_t, conf_t, landm_t, neg_pos, group, diou=None):
+        sums, counts, sel = ops.multibox_sums(loc, conf, landm, loc_t, conf_t, landm_t, neg_pos,
+                                              diou)
         if group is not None:
             import torch.distributed as dist
             dist.all_reduce(counts, group=group)
         loss = ops.multibox_normalize(sums, counts)
         ctx.save_for_backward(loc, conf, landm, loc_t, conf_t, landm_t, sel, counts)
+        ctx.diou = diou
         return loss[0], loss[1], loss[2]
 
     @staticmethod
@@ -33,8 +35,8 @@ class _MultiBoxLossFn(torch.autograd.Function):
         z = torch.zeros((), device=dev)
         gout = torch.stack([g if g is not None else z for g in (g_l, g_c, g_lm)]).float()
         gl, gc, glm = ops.multibox_backward(loc, conf, landm, loc_t, conf_t, landm_t, sel,
-                                            gout.contiguous(), counts)
-        return gl, gc, glm, None, None, None, None, None
+                                            gout.contiguous(), counts, ctx.diou)
+        return gl, gc, glm, None, None, None, None, None, None
 
 
 def match(threshold, truths, priors, variances, labels, landms, loc_t, conf_t, landm_t, idx):

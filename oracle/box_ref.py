@@ -111,13 +111,67 @@ def match_batch(targets, priors, threshold=0.35, var=(0.1, 0.2)):
     return torch.stack(locs), torch.stack(confs), torch.stack(landms)
 
 
+def match_iou_batch(targets, priors, threshold=0.35, var=(0.1, 0.2)):
+    """nets/retinaface_training_DIOU.py:176-246 (match_iou) over the per-image loop
+    (:566-580): match()'s assignment, but loc_t = the matched truth corners
+    (:230 `loc = matches`)."""
+    locs, confs, landms = [], [], []
+    for t in targets:
+        _, conf, landm, bti, _ = match(threshold, t[:, :4], priors, var, t[:, -1], t[:, 4:14])
+        locs.append(t[:, :4][bti])
+        confs.append(conf)
+        landms.append(landm)
+    return torch.stack(locs), torch.stack(confs), torch.stack(landms)
+
+
+def bbox_overlaps_diou(b1, b2):
+    """nets/retinaface_training_DIOU.py:402-442 for paired rows (rows == cols, so
+    the exchange branch never runs)."""
+    w1 = b1[:, 2] - b1[:, 0]
+    h1 = b1[:, 3] - b1[:, 1]
+    w2 = b2[:, 2] - b2[:, 0]
+    h2 = b2[:, 3] - b2[:, 1]
+    area1 = w1 * h1
+    area2 = w2 * h2
+    cx1 = (b1[:, 2] + b1[:, 0]) / 2
+    cy1 = (b1[:, 3] + b1[:, 1]) / 2
+    cx2 = (b2[:, 2] + b2[:, 0]) / 2
+    cy2 = (b2[:, 3] + b2[:, 1]) / 2
+    inter_max = torch.min(b1[:, 2:], b2[:, 2:])
+    inter_min = torch.max(b1[:, :2], b2[:, :2])
+    out_max = torch.max(b1[:, 2:], b2[:, 2:])
+    out_min = torch.min(b1[:, :2], b2[:, :2])
+    inter = torch.clamp(inter_max - inter_min, min=0)
+    inter_area = inter[:, 0] * inter[:, 1]
+    inter_diag = (cx2 - cx1) ** 2 + (cy2 - cy1) ** 2
+    outer = torch.clamp(out_max - out_min, min=0)
+    outer_diag = outer[:, 0] ** 2 + outer[:, 1] ** 2
+    union = area1 + area2 - inter_area
+    d = inter_area / union - inter_diag / outer_diag
+    return torch.clamp(d, min=-1.0, max=1.0)
+
+
+def diou_loss_sum(loc_p, loc_t, priors_p, var):
+    """IouLoss(pred_mode='Center', size_sum=True, losstype='Diou').forward
+    (nets/retinaface_training_DIOU.py:500-522) with its decode (:319-337)."""
+    b = torch.cat((priors_p[:, :2] + loc_p[:, :2] * var[0] * priors_p[:, 2:],
+                   priors_p[:, 2:] * torch.exp(loc_p[:, 2:] * var[1])), 1)
+    b = torch.cat((b[:, :2] - b[:, 2:] / 2, b[:, 2:]), 1)     # boxes[:, :2] -= boxes[:, 2:]/2
+    b = torch.cat((b[:, :2], b[:, 2:] + b[:, :2]), 1)         # boxes[:, 2:] += boxes[:, :2]
+    return torch.sum(1.0 - bbox_overlaps_diou(b, loc_t))
+
+
 # ----------------------------------------------------------------------------- loss
 def smooth_l1_sum(x, y):
     return torch.nn.functional.smooth_l1_loss(x, y, reduction="sum")
 
 
-def multibox_loss(loc, conf, landm, loc_t, conf_t, landm_t, neg_pos=7, num_classes=2):
+def multibox_loss(loc, conf, landm, loc_t, conf_t, landm_t, neg_pos=7, num_classes=2,
+                  diou=None):
     """nets/retinaface_training.py:219-303 given matched targets.
+
+    diou=(priors, var): the DIoU variant's box term instead
+    (nets/retinaface_training_DIOU.py:596-602), loc_t from match_iou_batch.
 
     Returns (loss_l, loss_c, loss_landm, info) with info carrying the raw sums,
     counts and the hard-negative selection so tests can check each stage.
@@ -126,7 +180,12 @@ def multibox_loss(loc, conf, landm, loc_t, conf_t, landm_t, neg_pos=7, num_class
     pos1 = conf_t > 0
     s_landm = smooth_l1_sum(landm[pos1].view(-1, 10), landm_t[pos1].view(-1, 10))
     pos = conf_t != 0
-    s_loc = smooth_l1_sum(loc[pos].view(-1, 4), loc_t[pos].view(-1, 4))
+    if diou is None:
+        s_loc = smooth_l1_sum(loc[pos].view(-1, 4), loc_t[pos].view(-1, 4))
+    else:
+        pri_b = diou[0].to(loc.dtype).unsqueeze(0).expand_as(loc)
+        s_loc = diou_loss_sum(loc[pos].view(-1, 4), loc_t[pos].view(-1, 4).to(loc.dtype),
+                              pri_b[pos].view(-1, 4), diou[1])
     conf_t[pos] = 1
     bc = conf.reshape(-1, num_classes)
     gmax = bc.max()

@@ -188,3 +188,44 @@ def test_nms_parity_nan_boxes(cuda):
     ref = box_ref.nms(b, s, 0.3)
     got = ops.nms(torch.from_numpy(b).to(cuda), torch.from_numpy(s).to(cuda), 0.3)
     assert got.cpu().numpy().tolist() == ref.tolist()
+
+
+def test_diou_oracle_kat():
+    """Hand-derived DIoU values for the oracle restatement of
+    nets/retinaface_training_DIOU.py:402-442 and IouLoss (:500-522)."""
+    pri = torch.tensor([[0.5, 0.5, 1.0, 1.0]] * 3)
+    loc = torch.zeros(3, 4)  # decodes to [0, 0, 1, 1]
+    tr = torch.tensor([[0.0, 0.0, 1.0, 1.0],    # identical: DIoU 1, loss 0
+                       [2.0, 0.0, 3.0, 1.0],    # disjoint: 0 - 4/10 -> loss 1.4
+                       [0.5, 0.0, 1.5, 1.0]])   # I/U = .5/1.5, diag .25/(2.25+1)
+    d = box_ref.bbox_overlaps_diou(box_ref.decode(loc, pri, [0.1, 0.2]), tr)
+    ref = torch.tensor([1.0, -0.4, 0.5 / 1.5 - 0.25 / 3.25])
+    torch.testing.assert_close(d, ref, rtol=0, atol=1e-6)
+    s = box_ref.diou_loss_sum(loc, tr, pri, [0.1, 0.2])
+    assert abs(float(s) - float((1 - ref).sum())) < 1e-6
+
+
+def test_match_iou_oracle_keeps_truth_corners():
+    pri = box_ref.anchors(CFG_MNET, (128, 128))
+    from jabd_amd import synth
+    tg = [torch.from_numpy(t) for t in synth.targets(2, 128, seed=4)]
+    rl, rc, rlm = box_ref.match_batch(tg, pri)
+    il, ic, ilm = box_ref.match_iou_batch(tg, pri)
+    assert torch.equal(rc, ic) and torch.equal(rlm, ilm)
+    for b, t in enumerate(tg):   # every loc_t row is one of the image's truth boxes
+        hits = (il[b][:, None, :] == t[None, :, :4]).all(-1).any(-1)
+        assert bool(hits.all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("size,batch", [(256, 4), (640, 2)])
+def test_match_iou_parity(cuda, size, batch):
+    from jabd_amd import ops, synth
+    pri = box_ref.anchors(CFG_MNET, (size, size))
+    tg = [torch.from_numpy(t) for t in synth.targets(batch, size, seed=size + 1)]
+    rl, rc, rlm = box_ref.match_iou_batch(tg, pri)
+    gl, gc, glm = ops.match_encode([t.to(cuda) for t in tg], pri.to(cuda), 0.35, [0.1, 0.2],
+                                   raw_loc=True)
+    assert torch.equal(gc.cpu(), rc)
+    assert torch.equal(gl.cpu(), rl)   # a copy of the truth corners: bit-exact
+    assert torch.equal(glm.cpu(), rlm)
