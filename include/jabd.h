@@ -114,6 +114,27 @@ int jabd_match_iou_f32(const float* targets, const int64_t* offsets,
                        float* landm_t, void* ws, size_t ws_bytes,
                        jabd_stream_t stream);
 
+/* letterbox_image + preprocess_input — utils/utils.py:8-19,27-29 as
+ * predict.py:122,143-152 chains them (§8f rank 3).  src: device float32
+ * [batch, ih, iw, 3] (the np.float32 image); the image is resized to
+ * nw = int(iw*s), nh = int(ih*s), s = min(w/iw, h/ih) (cv2 INTER_LINEAR float
+ * path, restated) and pasted centred on an h x w canvas of `fill` (84 in the
+ * reference).  nchw = 0: dst float32 [batch, h, w, 3] (letterbox_image's
+ * output); nchw = 1: dst float32 [batch, 3, h, w] = canvas - mean3[c] (host
+ * float[3], (104,117,123) in the reference), i.e. the network input. */
+int jabd_letterbox_f32(const float* src, int64_t batch, int ih, int iw,
+                       float* dst, int h, int w, float fill,
+                       const float* mean3, int nchw, jabd_stream_t stream);
+
+/* retinaface_correct_boxes (utils/utils_bbox.py:9-24, only when letterbox
+ * != 0) followed (to_pixels != 0) by predict.py:195-196's rescale of the
+ * normalised box and landmark columns to image pixels, in place on device rows
+ * float32 [n, 15] (jabd_detect_f32's output).  Column 4 (score) untouched.
+ * Every step rounds as numpy's float64 math assigned back to float32. */
+int jabd_correct_boxes_f32(float* rows, int64_t n, int input_h, int input_w,
+                           int image_h, int image_w, int letterbox,
+                           int to_pixels, jabd_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * A9 MultiBoxLoss — nets/retinaface_training.py:183-303.
  * Forward writes un-normalised sums and counts so data-parallel callers can

@@ -652,9 +652,143 @@ static int64_t gmax_blocks(int64_t total) {
   return g < 1 ? 1 : (g > 1024 ? 1024 : g);
 }
 
+// ---------------------------------------------------------------------------
+// letterbox_image + preprocess_input — utils/utils.py:8-19,27-29 as predict.py
+// calls them (:122,143-152): a float32 HWC image is cv2.resize'd (INTER_LINEAR,
+// float path) to nw x nh, pasted at ((h-nh)//2, (w-nw)//2) on a canvas filled
+// with `fill`, then (NCHW mode) the channel means are subtracted and the result
+// transposed to [3, h, w].  cv2's float INTER_LINEAR restated (cv2 is absent
+// here, parity unpinned against it): per axis f = (float)((d + .5) * scale - .5),
+// s = floor(f), f -= s; s < 0 -> (s, f) = (0, 0); s >= n-1 -> (n-1, 0); taps
+// combined as S0*(1-f) + S1*f in fp32 (separate products, -ffp-contract=off),
+// horizontal pass first.  An exact 2x downscale is cv2's INTER_AREA fast path:
+// (S00 + S01 + S10 + S11) * 0.25f.  One thread per canvas pixel, three channels.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void lin_tap(int d, double scale, int n, int& s0, int& s1, float& f) {
+  float fx = (float)((d + 0.5) * scale - 0.5);
+  int s = (int)floorf(fx);
+  fx -= (float)s;
+  if (s < 0) { s = 0; fx = 0.f; }
+  if (s >= n - 1) { s = n - 1; fx = 0.f; }
+  s0 = s;
+  s1 = s + 1 < n ? s + 1 : n - 1;
+  f = fx;
+}
+
+__global__ __launch_bounds__(256) void letterbox_kernel(
+    const float* __restrict__ src, int ih, int iw, float* __restrict__ dst, int h, int w,
+    int nw, int nh, int top, int left, double sx, double sy, int area2x, float fill, float m0,
+    float m1, float m2, int nchw) {
+  const int b = blockIdx.y;
+  const int64_t pix = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (pix >= (int64_t)h * w) return;
+  const int y = (int)(pix / w), x = (int)(pix - (int64_t)y * w);
+  const float* S = src + (int64_t)b * ih * iw * 3;
+  float v[3] = {fill, fill, fill};
+  const int ry = y - top, rx = x - left;
+  if (ry >= 0 && ry < nh && rx >= 0 && rx < nw) {
+    if (area2x) {
+      const float* r0 = S + ((int64_t)(2 * ry) * iw + 2 * rx) * 3;
+      const float* r1 = r0 + (int64_t)iw * 3;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[c] = (r0[c] + r0[c + 3] + r1[c] + r1[c + 3]) * 0.25f;
+    } else {
+      int x0, x1, y0, y1;
+      float fx, fy;
+      lin_tap(rx, sx, iw, x0, x1, fx);
+      lin_tap(ry, sy, ih, y0, y1, fy);
+      const float ax0 = 1.f - fx, ay0 = 1.f - fy;
+      const float* p00 = S + ((int64_t)y0 * iw + x0) * 3;
+      const float* p01 = S + ((int64_t)y0 * iw + x1) * 3;
+      const float* p10 = S + ((int64_t)y1 * iw + x0) * 3;
+      const float* p11 = S + ((int64_t)y1 * iw + x1) * 3;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float h0 = p00[c] * ax0 + p01[c] * fx;
+        const float h1 = p10[c] * ax0 + p11[c] * fx;
+        v[c] = h0 * ay0 + h1 * fy;
+      }
+    }
+  }
+  if (nchw) {
+    float* D = dst + (int64_t)b * 3 * h * w + pix;
+    const int64_t plane = (int64_t)h * w;
+    D[0] = v[0] - m0;
+    D[plane] = v[1] - m1;
+    D[2 * plane] = v[2] - m2;
+  } else {
+    float* D = dst + ((int64_t)b * h * w + pix) * 3;
+    D[0] = v[0]; D[1] = v[1]; D[2] = v[2];
+  }
+}
+
+// retinaface_correct_boxes (utils/utils_bbox.py:9-24) then predict.py's
+// rescale to image pixels (:195-196) on detection rows [n, 15]: numpy does
+// both in float64 and assigns back into the float32 rows, so each step is
+// (float)((double)v - off) * sc) and (float)((double)v * dim).
+__global__ void correct_rows_kernel(float* __restrict__ rows, int64_t n, int letterbox,
+                                    double offx, double offy, double scx, double scy,
+                                    double dimx, double dimy) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n * 15) return;
+  const int c = (int)(i % 15);
+  if (c == 4) return;  // the score column is untouched
+  const bool isx = ((c < 4 ? c : c - 5) & 1) == 0;
+  float v = rows[i];
+  if (letterbox) v = (float)(((double)v - (isx ? offx : offy)) * (isx ? scx : scy));
+  rows[i] = (float)((double)v * (isx ? dimx : dimy));  // x * 1.0 is exact when !to_pixels
+}
+
 }  // namespace jabd
 
 using namespace jabd;
+
+extern "C" int jabd_correct_boxes_f32(float* rows, int64_t n, int input_h, int input_w,
+                                      int image_h, int image_w, int letterbox,
+                                      int to_pixels, jabd_stream_t stream) {
+  JABD_REQUIRE(n >= 0 && image_h > 0 && image_w > 0, "correct_boxes: bad size");
+  JABD_REQUIRE(!letterbox || (input_h > 0 && input_w > 0), "correct_boxes: bad input shape");
+  if (n == 0) return JABD_OK;
+  JABD_REQUIRE(rows, "correct_boxes: null pointer");
+  // utils_bbox.py:10-12, numpy float64 over [h, w] pairs
+  double offx = 0, offy = 0, scx = 1, scy = 1;
+  if (letterbox) {
+    const double r = fmin((double)input_h / image_h, (double)input_w / image_w);
+    const double nh = image_h * r, nw = image_w * r;
+    offy = (input_h - nh) / 2. / input_h;
+    offx = (input_w - nw) / 2. / input_w;
+    scy = input_h / nh;
+    scx = input_w / nw;
+  }
+  correct_rows_kernel<<<(unsigned)cdiv(n * 15, 256), 256, 0, as_stream(stream)>>>(
+      rows, n, letterbox, offx, offy, scx, scy, to_pixels ? (double)image_w : 1.0,
+      to_pixels ? (double)image_h : 1.0);
+  return check_launch("correct_boxes");
+}
+
+extern "C" int jabd_letterbox_f32(const float* src, int64_t batch, int ih, int iw, float* dst,
+                                  int h, int w, float fill, const float* mean3, int nchw,
+                                  jabd_stream_t stream) {
+  JABD_REQUIRE(batch >= 0 && ih > 0 && iw > 0 && h > 0 && w > 0, "letterbox: bad size");
+  JABD_REQUIRE(!nchw || mean3, "letterbox: NCHW output needs the channel means");
+  if (batch == 0) return JABD_OK;
+  JABD_REQUIRE(src && dst, "letterbox: null pointer");
+  // utils/utils.py:10-13: scale = min(w/iw, h/ih); nw = int(iw*scale); nh = int(ih*scale)
+  const double sc = fmin((double)w / iw, (double)h / ih);
+  const int nw = (int)(iw * sc), nh = (int)(ih * sc);
+  JABD_REQUIRE(nw > 0 && nh > 0, "letterbox: image %dx%d collapses to %dx%d", iw, ih, nw, nh);
+  const int top = (h - nh) / 2, left = (w - nw) / 2;
+  // cv2.resize: inv_scale = dsize/ssize, scale = 1/inv_scale; exact 2x -> INTER_AREA
+  const double sx = 1.0 / ((double)nw / iw), sy = 1.0 / ((double)nh / ih);
+  const int area2x = (iw == 2 * nw && ih == 2 * nh) ? 1 : 0;
+  const float m[3] = {nchw ? mean3[0] : 0.f, nchw ? mean3[1] : 0.f, nchw ? mean3[2] : 0.f};
+  const int64_t npix = (int64_t)h * w;
+  dim3 g((unsigned)cdiv(npix, 256), (unsigned)batch);
+  letterbox_kernel<<<g, 256, 0, as_stream(stream)>>>(src, ih, iw, dst, h, w, nw, nh, top, left,
+                                                      sx, sy, area2x, fill, m[0], m[1], m[2],
+                                                      nchw);
+  return check_launch("letterbox");
+}
 
 extern "C" int jabd_decode_f32(const float* loc, const float* priors, int64_t batch,
                                int64_t num_priors, float var0, float var1, float* boxes,

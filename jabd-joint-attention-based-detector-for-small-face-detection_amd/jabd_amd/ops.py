@@ -225,5 +225,48 @@ def multibox_backward(loc, conf, landm, loc_t, conf_t, landm_t, sel, gout, count
     return gl, gc, glm
 
 
+# --------------------------------------------------------------------------- letterbox
+def letterbox(image, size, fill=84.0, mean=None):
+    """utils/utils.py:8-19 letterbox_image (+ :27-29 preprocess_input when `mean`
+    is given) on the device — see jabd_letterbox_f32.
+
+    image: device float32 [ih, iw, 3] or [B, ih, iw, 3]; size = (w, h) as the
+    reference passes it.  mean=None -> [.., h, w, 3] canvas; mean=(m0, m1, m2)
+    -> [B, 3, h, w] network input (canvas - mean, NCHW).
+    """
+    image = _dev("letterbox.image", image)
+    squeeze = image.dim() == 3
+    if squeeze:
+        image = image.unsqueeze(0)
+    if image.dim() != 4 or image.shape[-1] != 3:
+        raise ValueError(f"letterbox: expected [B, H, W, 3], got {tuple(image.shape)}")
+    B, ih, iw = image.shape[0], image.shape[1], image.shape[2]
+    w, h = int(size[0]), int(size[1])
+    if mean is None:
+        out = torch.empty((B, h, w, 3), dtype=torch.float32, device=image.device)
+        m = None
+    else:
+        out = torch.empty((B, 3, h, w), dtype=torch.float32, device=image.device)
+        m = (ctypes.c_float * 3)(*[float(v) for v in mean])
+    call("jabd_letterbox_f32", _p(image), B, ih, iw, _p(out), h, w, float(fill),
+         ctypes.cast(m, ctypes.c_void_p) if m is not None else ctypes.c_void_p(0),
+         0 if mean is None else 1, _stream())
+    return out[0] if (squeeze and mean is None) else out
+
+
+def correct_boxes(rows, input_shape, image_shape, letterbox=True, to_pixels=True):
+    """In place on device rows [n, 15]: retinaface_correct_boxes
+    (utils/utils_bbox.py:9-24, if letterbox) then predict.py:195-196's scale to
+    image pixels.  input_shape = (H, W) of the network input, image_shape =
+    (im_height, im_width)."""
+    rows = _dev("correct_boxes.rows", rows)
+    if rows.dim() != 2 or rows.shape[1] != 15:
+        raise ValueError(f"correct_boxes: expected [n, 15], got {tuple(rows.shape)}")
+    call("jabd_correct_boxes_f32", _p(rows), rows.shape[0], int(input_shape[0]),
+         int(input_shape[1]), int(image_shape[0]), int(image_shape[1]), 1 if letterbox else 0,
+         1 if to_pixels else 0, _stream())
+    return rows
+
+
 def version():
     return lib().jabd_version().decode()

@@ -14,7 +14,13 @@ from jabd_amd import ops
 
 
 def retinaface_correct_boxes(result, input_shape, image_shape):
-    """Undo the letterbox on host numpy rows (pure bookkeeping, reference :9-24)."""
+    """Undo the letterbox (reference :9-24).  A device tensor [n, 15] is corrected
+    in place by jabd_correct_boxes_f32; host numpy rows (the reference's own
+    contract) keep the numpy bookkeeping."""
+    if isinstance(result, torch.Tensor):
+        return ops.correct_boxes(result, [int(v) for v in input_shape],
+                                 [int(v) for v in image_shape], letterbox=True,
+                                 to_pixels=False)
     new_shape = image_shape * np.min(input_shape / image_shape)
     offset = (input_shape - new_shape) / 2. / input_shape
     scale = input_shape / new_shape

@@ -1,0 +1,91 @@
+"""§8f rank 3: predict.py's letterbox + preprocess_input on the device
+(jabd_letterbox_f32) against the numpy restatement in oracle/prep_ref.py.
+The oracle is pinned by hand-derived known answers (cv2 is absent here and the
+reference holds no resized fixture: parity unpinned against cv2 itself).
+GPU parity is bit-exact: the kernel issues the same fp32 ops in the same order."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import prep_ref
+
+
+def test_resize_kat_identity():
+    img = np.random.default_rng(0).uniform(0, 255, (7, 5, 3)).astype(np.float32)
+    assert np.array_equal(prep_ref.resize_linear(img, 5, 7), img)
+
+
+def test_resize_kat_upscale_half_pixel_taps():
+    img = np.zeros((1, 2, 3), np.float32)
+    img[0, 1] = 10
+    out = prep_ref.resize_linear(img, 4, 1)
+    assert np.array_equal(out[0, :, 0], np.array([0, 2.5, 7.5, 10], np.float32))
+
+
+def test_resize_kat_area_2x():
+    img = np.arange(4 * 4 * 3, dtype=np.float32).reshape(4, 4, 3)
+    out = prep_ref.resize_linear(img, 2, 2)
+    assert out[0, 0, 0] == (img[0, 0, 0] + img[0, 1, 0] + img[1, 0, 0] + img[1, 1, 0]) / 4
+
+
+def test_letterbox_kat_padding():
+    img = np.full((10, 20, 3), 7, np.float32)     # 20 wide -> 8x4 inside 8x8
+    lb = prep_ref.letterbox_image(img, (8, 8))
+    assert np.all(lb[:2] == 84) and np.all(lb[6:] == 84) and np.all(lb[2:6] == 7)
+    x = prep_ref.preprocess(img, (8, 8))
+    assert x.shape == (3, 8, 8) and x[0, 0, 0] == 84 - 104 and x[2, 4, 4] == 7 - 123
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ih,iw,w,h", [(480, 640, 320, 320), (300, 200, 640, 640),
+                                       (128, 256, 64, 64), (97, 131, 160, 96),
+                                       (1, 1, 8, 8), (1024, 768, 1024, 1024)])
+def test_letterbox_parity(cuda, ih, iw, w, h):
+    from jabd_amd import ops
+    g = np.random.default_rng(ih * 7 + iw)
+    imgs = g.integers(0, 256, (2, ih, iw, 3)).astype(np.float32)
+    dev = torch.from_numpy(imgs).to(cuda)
+    got = ops.letterbox(dev, (w, h)).cpu().numpy()
+    gotn = ops.letterbox(dev, (w, h), mean=(104, 117, 123)).cpu().numpy()
+    for b in range(2):
+        assert np.array_equal(got[b], prep_ref.letterbox_image(imgs[b], (w, h)))
+        assert np.array_equal(gotn[b], prep_ref.preprocess(imgs[b], (w, h)))
+
+
+@pytest.mark.gpu
+def test_letterbox_image_reference_contract(cuda):
+    from utils.utils import letterbox_image
+    img = np.random.default_rng(1).integers(0, 256, (50, 80, 3)).astype(np.float32)
+    out = letterbox_image(img, [64, 64])
+    assert out.dtype == np.float64 and out.shape == (64, 64, 3)
+    assert np.array_equal(out.astype(np.float32), prep_ref.letterbox_image(img, (64, 64)))
+
+
+def test_correct_rows_kat():
+    """A 200x100 (w x h) image letterboxed into 100x100: scale 0.5, 25-px bars
+    top and bottom.  Normalised (0.5, 0.25..0.75) maps back to the full height."""
+    rows = np.zeros((1, 15), np.float32)
+    rows[0, :4] = [0.0, 0.25, 1.0, 0.75]
+    rows[0, 4] = 0.9
+    out = prep_ref.correct_rows(rows, (100, 100), (100, 200))
+    np.testing.assert_allclose(out[0, :4], [0, 0, 200, 100], atol=1e-4)
+    assert out[0, 4] == np.float32(0.9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lb,px", [(1, 1), (1, 0), (0, 1)])
+@pytest.mark.parametrize("inp,img", [((640, 640), (480, 640)), ((1024, 1024), (1080, 1920)),
+                                     ((320, 480), (333, 211))])
+def test_correct_boxes_parity(cuda, lb, px, inp, img):
+    from jabd_amd import ops
+    rows = np.random.default_rng(sum(img)).uniform(-0.1, 1.1, (257, 15)).astype(np.float32)
+    dev = torch.from_numpy(rows).to(cuda)
+    ops.correct_boxes(dev, inp, img, letterbox=bool(lb), to_pixels=bool(px))
+    ref = prep_ref.correct_rows(rows, inp, img, letterbox=bool(lb), to_pixels=bool(px))
+    assert np.array_equal(dev.cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
+def test_correct_boxes_empty(cuda):
+    from jabd_amd import ops
+    ops.correct_boxes(torch.empty((0, 15), device=cuda), (640, 640), (480, 640))
