@@ -135,6 +135,19 @@ int jabd_correct_boxes_f32(float* rows, int64_t n, int input_h, int input_w,
                            int image_h, int image_w, int letterbox,
                            int to_pixels, jabd_stream_t stream);
 
+/* GPU augmentation — utils/dataloader.py:71-115 (get_random_data, image part)
+ * + :62-64 (preprocess_input, CHW), §8f rank 2.  src: device uint8 RGB
+ * [ih, iw, 3] (the PIL image as an array).  The host draws the reference's
+ * random values (nw, nh, dx, dy, flip, hue, sat, val) in its np.random order;
+ * the device resizes (PIL BICUBIC, restated), pastes at (dx, dy) on grey 128
+ * of h x w, flips, applies the HSV jitter (cv2 float HSV, restated) and writes
+ * dst float32 [3, h, w] = rgb*255 - (104, 117, 123).  Workspace: u8 [ih, nw, 3]. */
+int jabd_augment_workspace_size(int ih, int nw, size_t* bytes);
+int jabd_augment_u8(const uint8_t* src, int ih, int iw, int nw, int nh, int h,
+                    int w, int dx, int dy, int flip, double hue, float sat,
+                    float val, float* dst, void* ws, size_t ws_bytes,
+                    jabd_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * A9 MultiBoxLoss — nets/retinaface_training.py:183-303.
  * Forward writes un-normalised sums and counts so data-parallel callers can

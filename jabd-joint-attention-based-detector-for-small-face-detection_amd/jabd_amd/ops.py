@@ -268,5 +268,23 @@ def correct_boxes(rows, input_shape, image_shape, letterbox=True, to_pixels=True
     return rows
 
 
+# --------------------------------------------------------------------------- augment
+def augment(image_u8, input_shape, nw, nh, dx, dy, flip, hue, sat, val):
+    """utils/dataloader.py:71-115 + :62-64 image part on the device, given the
+    random draws (see utils.dataloader.draw_params).  image_u8: device uint8
+    RGB [ih, iw, 3]; input_shape = (h, w).  Returns float32 [3, h, w]."""
+    img = _dev("augment.image", image_u8, torch.uint8)
+    if img.dim() != 3 or img.shape[2] != 3:
+        raise ValueError(f"augment: expected [H, W, 3] uint8, got {tuple(img.shape)}")
+    ih, iw = int(img.shape[0]), int(img.shape[1])
+    h, w = int(input_shape[0]), int(input_shape[1])
+    out = torch.empty((3, h, w), dtype=torch.float32, device=img.device)
+    ws = _ws(_size_query("jabd_augment_workspace_size", ih, int(nw)), img.device)
+    call("jabd_augment_u8", _p(img), ih, iw, int(nw), int(nh), h, w, int(dx), int(dy),
+         1 if flip else 0, float(hue), float(sat), float(val), _p(out), _p(ws), ws.numel(),
+         _stream())
+    return out
+
+
 def version():
     return lib().jabd_version().decode()
