@@ -222,6 +222,31 @@ def nms_bench(device, reps=5):
             "bit_exact_img0_vs_oracle": bool(exact)}
 
 
+def augment_bench(device, reps=20):
+    """§8f rank 2: get_random_data's image path (jabd_augment_u8) for one
+    768x1024 RGB source onto a 1024x1024 canvas, timed with HIP events on the
+    current stream.  Algorithmic bytes: source u8 read + the u8 horizontal
+    intermediate written and read + fp32 CHW output written."""
+    from jabd_amd import ops
+    ih, iw, h, w = 768, 1024, 1024, 1024
+    nw, nh = 900, 700
+    img = torch.randint(0, 256, (ih, iw, 3), dtype=torch.uint8, device=device)
+    args = ((h, w), nw, nh, 50, 100, True, 0.05, 1.2, 0.9)
+    ops.augment(img, *args)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        ops.augment(img, *args)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    nbytes = ih * iw * 3 + 2 * ih * nw * 3 + 3 * h * w * 4
+    return {"config": "768x1024 u8 RGB -> 1024x1024 (resize 900x700, flip, HSV jitter)",
+            "images_per_sec": 1e3 / ms, "ms_per_call": ms,
+            "algorithmic_bytes": nbytes, "achieved_gbs": nbytes / (ms * 1e-3) / 1e9}
+
+
 def train_bench(kind, batch, size, steps, warmup, device, dist, rank):
     """steps timed training iterations (parallel.train_step) on this rank."""
     from jabd_amd import optim, parallel, synth
@@ -391,6 +416,7 @@ def main():
         extra["forward_gflop_per_image"] = forward_flops(model, args.size, 1) / 1e9
         if not args.no_nms:
             extra["nms"] = nms_bench(device)
+            extra["augment"] = augment_bench(device)
         if world == 1 and not args.no_cpu_baseline:
             extra["cpu_baseline"] = cpu_baseline(args.size, args.cpu_seconds)
         line = {
