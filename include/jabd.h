@@ -148,6 +148,22 @@ int jabd_augment_u8(const uint8_t* src, int ih, int iw, int nw, int nh, int h,
                     float val, float* dst, void* ws, size_t ws_bytes,
                     jabd_stream_t stream);
 
+/* WIDER FACE evaluation core — utils/evaluation.py:255-305 (image_eval +
+ * img_pr_info) summed over images (:347-375), §8f rank 3.  Device float64:
+ * pred [total_preds, 5] (x, y, w, h, normalised score) and gt [total_gts, 4]
+ * (x, y, w, h) rows per image by offsets [num_images + 1]; ignore uint8 per gt
+ * (1 = in the setting's keep list).  Images with no preds or no gts are
+ * skipped (:364-365).  pr_curve [thresh_num, 2] (device, caller-zeroed) is
+ * ACCUMULATED: += (proposals, recalled) per threshold, exact (integer sums). */
+int jabd_wider_eval_workspace_size(int64_t total_preds, int64_t total_gts,
+                                   size_t* bytes);
+int jabd_wider_eval_f64(const double* pred, const int64_t* pred_offsets,
+                        const double* gt, const uint8_t* ignore,
+                        const int64_t* gt_offsets, int64_t num_images,
+                        int64_t total_preds, int64_t total_gts,
+                        double iou_thresh, int thresh_num, double* pr_curve,
+                        void* ws, size_t ws_bytes, jabd_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * A9 MultiBoxLoss — nets/retinaface_training.py:183-303.
  * Forward writes un-normalised sums and counts so data-parallel callers can

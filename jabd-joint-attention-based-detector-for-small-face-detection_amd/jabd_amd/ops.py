@@ -7,6 +7,7 @@ path (the CPU restatement lives in oracle/ and is test-only).
 """
 import math
 
+import numpy as np
 import torch
 
 from ._lib import call, c_size, lib
@@ -284,6 +285,31 @@ def augment(image_u8, input_shape, nw, nh, dx, dy, flip, hue, sat, val):
          1 if flip else 0, float(hue), float(sat), float(val), _p(out), _p(ws), ws.numel(),
          _stream())
     return out
+
+
+# --------------------------------------------------------------------------- WIDER eval
+def wider_pr_curve(preds, gts, ignores, iou_thresh=0.5, thresh_num=1000, device="cuda"):
+    """Σ over images of img_pr_info(image_eval(...)) — utils/evaluation.py:255-305,
+    347-375 — on the device.  preds: list of [n_i, 5] (x, y, w, h, score) arrays,
+    gts: list of [m_i, 4] (x, y, w, h), ignores: list of [m_i] (1 = kept).
+    Returns the float64 pr_curve [thresh_num, 2] (device tensor)."""
+    def cat(xs, k, dt):
+        a = [np.asarray(x, dt).reshape(-1, k) if k else np.asarray(x, dt).reshape(-1) for x in xs]
+        offs = np.zeros(len(a) + 1, np.int64)
+        offs[1:] = np.cumsum([len(x) for x in a])
+        flat = np.concatenate(a) if a else np.zeros((0,) + ((k,) if k else ()), dt)
+        return (torch.from_numpy(np.ascontiguousarray(flat)).to(device),
+                torch.from_numpy(offs).to(device), int(offs[-1]))
+    if not (len(preds) == len(gts) == len(ignores)):
+        raise ValueError("wider_pr_curve: preds, gts and ignores differ in length")
+    p, poff, npred = cat(preds, 5, np.float64)
+    g, goff, ngt = cat(gts, 4, np.float64)
+    ig, _, _ = cat(ignores, 0, np.uint8)
+    pr = torch.zeros((thresh_num, 2), dtype=torch.float64, device=device)
+    ws = _ws(_size_query("jabd_wider_eval_workspace_size", npred, ngt), device)
+    call("jabd_wider_eval_f64", _p(p), _p(poff), _p(g), _p(ig), _p(goff), len(preds), npred, ngt,
+         float(iou_thresh), int(thresh_num), _p(pr), _p(ws), ws.numel(), _stream())
+    return pr
 
 
 def version():
