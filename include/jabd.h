@@ -164,6 +164,17 @@ int jabd_wider_eval_f64(const double* pred, const int64_t* pred_offsets,
                         double iou_thresh, int thresh_num, double* pr_curve,
                         void* ws, size_t ws_bytes, jabd_stream_t stream);
 
+/* Bicubic align_corners=True resize of NHWC fp32 [batch, H, W, C] to
+ * [batch, OH, OW, C] — the CSAF fusion of the bicubic FPN variant
+ * (train_mobilenetV3_ecagai.py:270,279, F.interpolate(..., mode="bicubic",
+ * align_corners=True)), §8f rank 4.  The backward zeroes grad_x and scatters. */
+int jabd_upsample_bicubic_ac_f32(const float* x, int64_t batch, int H, int W,
+                                 int C, float* y, int OH, int OW,
+                                 jabd_stream_t stream);
+int jabd_upsample_bicubic_ac_bwd_f32(const float* grad_y, int64_t batch, int H,
+                                     int W, int C, float* grad_x, int OH, int OW,
+                                     jabd_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * A9 MultiBoxLoss — nets/retinaface_training.py:183-303.
  * Forward writes un-normalised sums and counts so data-parallel callers can

@@ -312,5 +312,41 @@ def wider_pr_curve(preds, gts, ignores, iou_thresh=0.5, thresh_num=1000, device=
     return pr
 
 
+# --------------------------------------------------------------------------- bicubic
+def _bicubic_call(fn, src, size_in, size_out):
+    B, H, W, C = size_in
+    OH, OW = size_out
+    dst = torch.empty((B, OH, OW, C) if fn.endswith("ac_f32") else (B, H, W, C),
+                      dtype=torch.float32, device=src.device)
+    call(fn, _p(src), B, H, W, C, _p(dst), OH, OW, _stream())
+    return dst
+
+
+class UpsampleBicubicFn(torch.autograd.Function):
+    """F.interpolate(x, size, mode="bicubic", align_corners=True) on NHWC
+    (train_mobilenetV3_ecagai.py:270,279), HIP forward and backward."""
+
+    @staticmethod
+    def forward(ctx, x, oh, ow):
+        x = _dev("bicubic.x", x)
+        if x.dim() != 4:
+            raise ValueError(f"bicubic: expected NHWC, got {tuple(x.shape)}")
+        ctx.shape = tuple(x.shape)
+        return _bicubic_call("jabd_upsample_bicubic_ac_f32", x, ctx.shape, (oh, ow))
+
+    @staticmethod
+    def backward(ctx, gy):
+        B, H, W, C = ctx.shape
+        gy = gy.contiguous()
+        gx = _bicubic_call("jabd_upsample_bicubic_ac_bwd_f32", gy, ctx.shape,
+                           (gy.shape[1], gy.shape[2]))
+        return gx, None, None
+
+
+def upsample_bicubic(x_nhwc, size):
+    """NHWC bicubic align_corners resize to size = (OH, OW)."""
+    return UpsampleBicubicFn.apply(x_nhwc, int(size[0]), int(size[1]))
+
+
 def version():
     return lib().jabd_version().decode()
