@@ -175,6 +175,19 @@ int jabd_upsample_bicubic_ac_bwd_f32(const float* grad_y, int64_t batch, int H,
                                      int W, int C, float* grad_x, int OH, int OW,
                                      jabd_stream_t stream);
 
+/* BECA gate — the contrast-ECA block of the bicubic variant
+ * (train_mobilenetV3_ecagai.py:286-316): y = x * Hardsigmoid(conv1d_k(std_hw(x)))
+ * on NHWC fp32 [batch, pixels, C]; w float[k] (k odd, no bias).  stats
+ * float[4, batch*C] (mean, std, pre-activation, gate) is written by the forward
+ * and read by the backward; the backward's ws is float[2, batch*C]. */
+int jabd_beca_fwd_f32(const float* x, int64_t batch, int64_t pixels, int C,
+                      const float* w, int k, float* y, float* stats,
+                      jabd_stream_t stream);
+int jabd_beca_bwd_f32(const float* x, const float* grad_y, int64_t batch,
+                      int64_t pixels, int C, const float* w, int k,
+                      const float* stats, float* grad_x, float* grad_w, float* ws,
+                      jabd_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * A9 MultiBoxLoss — nets/retinaface_training.py:183-303.
  * Forward writes un-normalised sums and counts so data-parallel callers can

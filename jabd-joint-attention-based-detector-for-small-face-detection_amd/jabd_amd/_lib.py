@@ -115,6 +115,9 @@ SIGNATURES = {
     "jabd_upsample_bicubic_ac_f32": [c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp],
     "jabd_upsample_bicubic_ac_bwd_f32": [c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_int,
                                          c_vp],
+    "jabd_beca_fwd_f32": [c_vp, c_i64, c_i64, c_int, c_vp, c_int, c_vp, c_vp, c_vp],
+    "jabd_beca_bwd_f32": [c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp,
+                          c_vp],
     "jabd_match_iou_f32": [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_f32, c_f32, c_f32,
                            c_vp, c_vp, c_vp, c_vp, c_size, c_vp],
     "jabd_multibox_diou_loss_fwd_f32": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32,

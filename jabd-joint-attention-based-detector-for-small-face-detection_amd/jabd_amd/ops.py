@@ -348,5 +348,40 @@ def upsample_bicubic(x_nhwc, size):
     return UpsampleBicubicFn.apply(x_nhwc, int(size[0]), int(size[1]))
 
 
+# --------------------------------------------------------------------------- BECA
+class BecaFn(torch.autograd.Function):
+    """eca_block of the bicubic variant (train_mobilenetV3_ecagai.py:286-316) on
+    NHWC x [B, H, W, C] with the conv1d weight w [k]: x * Hardsigmoid(conv1d(std))."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        x = _dev("beca.x", x)
+        w = _dev("beca.w", w.reshape(-1))
+        B, H, W, C = x.shape
+        y = torch.empty_like(x)
+        stats = torch.empty((4, B * C), dtype=torch.float32, device=x.device)
+        call("jabd_beca_fwd_f32", _p(x), B, H * W, C, _p(w), w.numel(), _p(y), _p(stats),
+             _stream())
+        ctx.save_for_backward(x, w, stats)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, stats = ctx.saved_tensors
+        B, H, W, C = x.shape
+        gy = gy.contiguous()
+        gx = torch.empty_like(x)
+        gw = torch.empty_like(w)
+        ws = torch.empty((2, B * C), dtype=torch.float32, device=x.device)
+        call("jabd_beca_bwd_f32", _p(x), _p(gy), B, H * W, C, _p(w), w.numel(), _p(stats),
+             _p(gx), _p(gw), _p(ws), _stream())
+        return gx, gw
+
+
+def beca(x_nhwc, weight):
+    """weight: the block's Conv1d(1, 1, k) weight (any shape with k elements)."""
+    return BecaFn.apply(x_nhwc, weight.reshape(-1))
+
+
 def version():
     return lib().jabd_version().decode()
