@@ -89,3 +89,30 @@ def test_correct_boxes_parity(cuda, lb, px, inp, img):
 def test_correct_boxes_empty(cuda):
     from jabd_amd import ops
     ops.correct_boxes(torch.empty((0, 15), device=cuda), (640, 640), (480, 640))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lb", [True, False])
+def test_detect_image_pipeline(cuda, lb):
+    """The device detect_image equals its stages composed by hand with the host
+    oracle for the pre/post steps."""
+    from jabd_amd import ops
+    from jabd_amd.predict import detect_image
+    from nets.retinaface_r import RetinaFace
+    from utils.anchors import Anchors
+    from utils.config import cfg_mnet
+    torch.manual_seed(0)
+    net = RetinaFace(cfg=cfg_mnet, mode="eval").eval().to(cuda)
+    img = np.random.default_rng(5).integers(0, 256, (96, 160, 3)).astype(np.float32)
+    got = detect_image(net, img, (128, 128), cfg_mnet, confidence=0.3, letterbox_image=lb)
+    H, W = (128, 128) if lb else (96, 160)
+    x = torch.from_numpy(prep_ref.preprocess(img, (W, H))).unsqueeze(0).to(cuda)
+    pri = Anchors(cfg_mnet, image_size=(H, W)).get_anchors().to(cuda).float()
+    with torch.no_grad():
+        rows, nk = ops.detect(*net(x), pri, cfg_mnet["variance"], 0.3, 0.3)
+    k = int(nk[0])
+    if k == 0:
+        assert len(got) == 0
+        return
+    ref = prep_ref.correct_rows(rows[0, :k].cpu().numpy(), (H, W), (96, 160), letterbox=lb)
+    assert np.array_equal(got, ref)
