@@ -30,3 +30,11 @@ def rel_err(got, ref):
     """max |got - ref| / max |ref|  (scale-aware fp32 error)."""
     got, ref = got.double().cpu(), ref.double().cpu()
     return float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+
+
+def elem_rel_err(got, ref, floor=1e-2):
+    """max_i |got_i - ref_i| / max(|ref_i|, floor * max|ref|): an elementwise
+    relative error whose denominator is floored so exact zeros do not blow it up."""
+    got, ref = got.double().cpu(), ref.double().cpu()
+    den = ref.abs().clamp_min(floor * float(ref.abs().max().clamp_min(1e-30)))
+    return float(((got - ref).abs() / den).max())

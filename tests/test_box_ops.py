@@ -229,3 +229,50 @@ def test_match_iou_parity(cuda, size, batch):
     assert torch.equal(gc.cpu(), rc)
     assert torch.equal(gl.cpu(), rl)   # a copy of the truth corners: bit-exact
     assert torch.equal(glm.cpu(), rlm)
+
+
+def _oracle_nms_many(bx, sc, thr):
+    """oracle/nms_ref.c over several images in parallel threads (ctypes drops
+    the GIL), so the full C5 check stays within seconds."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=len(bx)) as ex:
+        return list(ex.map(lambda b: box_ref.nms(bx[b], sc[b], thr), range(len(bx))))
+
+
+@pytest.mark.gpu
+def test_nms_c5_full_config(cuda):
+    """C5 (BASELINE configs[4]) at full size: 8 images x 100k clustered boxes
+    (seed 99, the bench's input), every image bit-exact vs oracle/nms_ref.c."""
+    from jabd_amd import ops, synth
+    bx, sc = synth.nms_boxes(8, 100_000, seed=99)
+    keep, nk = ops.batched_nms(torch.from_numpy(bx).to(cuda), torch.from_numpy(sc).to(cuda), 0.3)
+    keep, nk = keep.cpu().numpy(), nk.cpu().numpy()
+    refs = _oracle_nms_many(bx, sc, 0.3)
+    for b in range(8):
+        assert nk[b] == len(refs[b]), b
+        assert np.array_equal(keep[b, : nk[b]], refs[b]), b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("thr", [0.3, 0.9])
+def test_nms_pair_capacity_dense_fallback(cuda, thr):
+    """Image 0 is one tight cluster of 12k near-identical boxes: every pair is a
+    grid candidate (n^2/2 = 7.2e7 pairs vs the workspace's 128 per box =
+    1.5e6, csrc/nms.hip kPairsPerBox), so its mask must come from the dense
+    fallback producer; image 1 (ordinary clustered boxes) stays on the grid
+    producer in the same call.  Both bit-exact vs the oracle."""
+    from jabd_amd import ops, synth
+    n = 12_000
+    rng = np.random.default_rng(17)
+    ctr = 0.5 + rng.normal(0, 0.002, (n, 2))
+    wh = 0.1 * (1 + rng.uniform(0, 0.05, (n, 2)))
+    b0 = np.concatenate([ctr - wh / 2, ctr + wh / 2], 1).astype(np.float32)
+    s0 = rng.uniform(0.5, 1.0, n).astype(np.float32)
+    b1, s1 = synth.nms_boxes(1, n, seed=23)
+    bx = np.stack([b0, b1[0]])
+    sc = np.stack([s0, s1[0]])
+    keep, nk = ops.batched_nms(torch.from_numpy(bx).to(cuda), torch.from_numpy(sc).to(cuda), thr)
+    keep, nk = keep.cpu().numpy(), nk.cpu().numpy()
+    refs = _oracle_nms_many(bx, sc, thr)
+    for b in range(2):
+        assert np.array_equal(keep[b, : nk[b]], refs[b]), b

@@ -116,3 +116,47 @@ def test_detect_image_pipeline(cuda, lb):
         return
     ref = prep_ref.correct_rows(rows[0, :k].cpu().numpy(), (H, W), (96, 160), letterbox=lb)
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.gpu
+def test_detect_image_c1_640(cuda):
+    """C1 (BASELINE configs[0]): one 480x640 image through detect_image at
+    640x640, every stage against the host oracle on its own terms:
+    letterbox + preprocess (bit-exact), the forward (<= 1e-3), decode + the
+    >= 0.5 score filter + torchvision-CPU NMS at nms_thres 0.3 (oracle/box_ref +
+    nms_ref.c on the device forward's output) and retinaface_correct_boxes with
+    the pixel rescale (oracle/prep_ref)."""
+    from _util import init_for_parity, rel_err
+    from jabd_amd import ops
+    from jabd_amd.predict import detect_image
+    from nets.retinaface_r import RetinaFace
+    from oracle import box_ref, model_ref
+    from utils.config import cfg_mnet
+    net = init_for_parity(RetinaFace(cfg=cfg_mnet, mode="eval"), seed=3).eval()
+    sd = {k: v.clone() for k, v in net.state_dict().items()}
+    net = net.to(cuda)
+    img = np.random.default_rng(640).integers(0, 256, (480, 640, 3)).astype(np.float32)
+    got = detect_image(net, img, (640, 640), cfg_mnet, confidence=0.5, nms_iou=0.3)
+    # stage 1: letterbox + preprocess_input
+    x_ref = prep_ref.preprocess(img, (640, 640))
+    x_dev = ops.letterbox(torch.from_numpy(img).to(cuda), (640, 640), mean=(104, 117, 123))
+    assert np.array_equal(x_dev[0].cpu().numpy(), x_ref)
+    # stage 2: forward
+    with torch.no_grad():
+        out = net(x_dev)
+        ref = model_ref.retinaface_mnv3(sd, torch.from_numpy(x_ref)[None], "eval")
+    for g, r in zip(out, ref):
+        assert rel_err(g, r) < 1e-3
+    # stage 3: decode + filter + NMS (host oracle on the device forward's output)
+    pri = box_ref.anchors(cfg_mnet, (640, 640))
+    loc, conf, landm = (t[0].cpu() for t in out)
+    var = cfg_mnet["variance"]
+    det = torch.cat([box_ref.decode(loc, pri, var), conf[:, 1:2],
+                     box_ref.decode_landm(landm, pri, var)], -1)
+    rows = box_ref.non_max_suppression(det, 0.5, 0.3)
+    assert len(rows) > 10, "the test image must produce detections"
+    # stage 4: retinaface_correct_boxes + pixel rescale
+    ref_final = prep_ref.correct_rows(np.asarray(rows, np.float32), (640, 640), (480, 640))
+    assert got.shape == ref_final.shape
+    # decode's exp() may differ by an ulp between HIP and the CPU library
+    np.testing.assert_allclose(got, ref_final, rtol=1e-5, atol=1e-3)
