@@ -179,7 +179,8 @@ int jabd_upsample_bicubic_ac_bwd_f32(const float* grad_y, int64_t batch, int H,
  * (train_mobilenetV3_ecagai.py:286-316): y = x * Hardsigmoid(conv1d_k(std_hw(x)))
  * on NHWC fp32 [batch, pixels, C]; w float[k] (k odd, no bias).  stats
  * float[4, batch*C] (mean, std, pre-activation, gate) is written by the forward
- * and read by the backward; the backward's ws is float[2, batch*C]. */
+ * and read by the backward; the backward's ws is float[2, batch*C].  y may be
+ * NULL: the gate alone (stats row 3) for a consumer that scales on load. */
 int jabd_beca_fwd_f32(const float* x, int64_t batch, int64_t pixels, int C,
                       const float* w, int k, float* y, float* stats,
                       jabd_stream_t stream);
@@ -363,7 +364,8 @@ int jabd_eca_gate_f32(const float* part, int64_t nblk, int64_t B, int64_t C, int
  *   array) of f_key(x) / f_value(x)  (wk/wv [ch][C], bk/bv [ch]); kv_ws is
  *   scratch [B][hs*ws][2*ch].  Built for ch == 4 (the JABD NLM).
  * nlm_apply: out = lateral + (W·softmax_S(q·k)·v + bW + x), q = f_query(x),
- *   lateral/out [B,h,w,C] NHWC (may alias); q_out/ctx_out [B,h*w,ch]
+ *   lateral/out [B,h,w,C] NHWC (may alias; lateral nullable = 0, which with
+ *   hs == h, ws == w is the standalone NLM.forward); q_out/ctx_out [B,h*w,ch]
  *   (nullable) keep q and the attention context for the backward. */
 int jabd_nlm_pool_f32(const float* src, int64_t src_bs, int32_t src_ps, int32_t B, int32_t hs,
                       int32_t ws, int32_t C, int32_t h, int32_t w, const float* wk,
@@ -483,6 +485,45 @@ int jabd_upsample_nearest_bwd_f32(const float* dxup, int32_t B, int32_t h, int32
 /* F.interpolate(mode='nearest', size=(h,w)) of an NHWC tensor. */
 int jabd_upsample_nearest_f32(const float* src, int32_t B, int32_t hs, int32_t ws, int32_t h,
                               int32_t w, int32_t C, float* dst, jabd_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * Module-level ops — what the reference's individual nn.Modules compute when
+ * a caller runs them one by one (nn.Sequential children, the body of a
+ * torchvision IntermediateLayerGetter, a standalone eca_block / PSPModule /
+ * SeModule) instead of inside the fused RetinaFace plan.
+ * act / act_bwd: nn.ReLU / LeakyReLU(slope) / Hardswish / Hardsigmoid /
+ *   Sigmoid (nets/mobilenetV3.py:43-56, nets/layers.py:10-34) over n dense
+ *   floats (any layout); act_bwd takes the forward INPUT x.
+ * bn_eval: eval-mode nn.BatchNorm2d/1d with running statistics (+ act) over
+ *   x [M][C] (NHWC rows, or [B][C]); any C.
+ * channel_scale: y = x * s[b][c] (eca_block / SeModule gate application,
+ *   nets/mobilenetV3.py:31-32,343-348), NHWC, C % 4 == 0.
+ * adaptive_pool: cat over sizes[] of nn.AdaptiveAvgPool2d((s, s)) of NHWC x
+ *   -> out [B][S][C], S = sum s^2 (PSPModule, nets/retinaface_r.py:85-104);
+ *   bin [floor(i*H/s), ceil((i+1)*H/s)), sum / count.  _bwd gathers dy
+ *   [B][S][C] back onto every pixel (no atomics).
+ * ------------------------------------------------------------------------ */
+int jabd_act_f32(const float* x, int64_t n, int32_t act, float slope, float* y,
+                 jabd_stream_t stream);
+int jabd_act_bwd_f32(const float* x, const float* dy, int64_t n, int32_t act, float slope,
+                     float* dx, jabd_stream_t stream);
+int jabd_bn_eval_f32(const float* x, int64_t M, int32_t C, const float* running_mean,
+                     const float* running_var, float eps, const float* gamma, const float* beta,
+                     int32_t act, float slope, float* y, jabd_stream_t stream);
+int jabd_channel_scale_f32(const float* x, int64_t B, int64_t HW, int32_t C, const float* scale,
+                           float* y, jabd_stream_t stream);
+int jabd_adaptive_pool_f32(const float* x, int64_t x_bs, int32_t B, int32_t H, int32_t W,
+                           int32_t C, const int32_t* sizes, int32_t nsizes, float* out,
+                           jabd_stream_t stream);
+/* out = lateral + F.interpolate(src, size=(h, w), mode='nearest') — the
+ * plain FPN's up-sample and add (nets/layers.py:106-117); NHWC, C % 4 == 0.
+ * Backward: jabd_upsample_nearest_bwd_f32. */
+int jabd_upsample_nearest_add_f32(const float* src, int32_t B, int32_t hs, int32_t ws, int32_t h,
+                                  int32_t w, int32_t C, const float* lateral, float* out,
+                                  jabd_stream_t stream);
+int jabd_adaptive_pool_bwd_f32(const float* dy, int32_t B, int32_t H, int32_t W, int32_t C,
+                               const int32_t* sizes, int32_t nsizes, float* dx,
+                               jabd_stream_t stream);
 
 #ifdef __cplusplus
 }

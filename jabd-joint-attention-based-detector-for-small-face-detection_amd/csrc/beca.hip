@@ -146,7 +146,7 @@ extern "C" int jabd_beca_fwd_f32(const float* x, int64_t batch, int64_t pixels, 
                                  jabd_stream_t stream) {
   JABD_REQUIRE(batch >= 0 && pixels > 0 && C > 0 && k > 0 && (k & 1), "beca: bad size");
   if (batch == 0) return JABD_OK;
-  JABD_REQUIRE(x && w && y && stats, "beca: null pointer");
+  JABD_REQUIRE(x && w && stats, "beca: null pointer");
   hipStream_t st = as_stream(stream);
   const int64_t BC = batch * C, total = BC * pixels;
   float *mean = stats, *sd = stats + BC, *v = stats + 2 * BC, *gate = stats + 3 * BC;
@@ -155,6 +155,7 @@ extern "C" int jabd_beca_fwd_f32(const float* x, int64_t batch, int64_t pixels, 
   if (int e = check_launch("beca_stats")) return e;
   beca_gate_kernel<<<(unsigned)cdiv(BC, 256), 256, 0, st>>>(sd, w, k, C, BC, v, gate);
   if (int e = check_launch("beca_gate")) return e;
+  if (!y) return JABD_OK;  // gate only: stats[3] = the [B][C] gate
   beca_apply_kernel<<<(unsigned)cdiv(total, 256), 256, 0, st>>>(x, gate, C, pixels, total, y);
   return check_launch("beca_apply");
 }

@@ -326,7 +326,8 @@ __global__ __launch_bounds__(256) void nlm_apply_kernel(
   const int64_t opix = ((int64_t)b * h * w + pix) * C;
   for (int c = 4 * r; c < C; c += 16) {
     const float4 x = *reinterpret_cast<const float4*>(xp + c);
-    const float4 lt = *reinterpret_cast<const float4*>(lateral + opix + c);
+    const float4 lt = lateral ? *reinterpret_cast<const float4*>(lateral + opix + c)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);  // standalone NLM
     float v[4] = {x.x, x.y, x.z, x.w};
     float lv[4] = {lt.x, lt.y, lt.z, lt.w};
     float rr[4];
@@ -505,8 +506,7 @@ extern "C" int jabd_nlm_apply_f32(const float* src, int64_t src_bs, int32_t src_
                                   const float* vpool, int32_t S, int32_t ch, const float* wW,
                                   const float* bW, const float* lateral, float* out,
                                   float* q_out, float* ctx_out, jabd_stream_t stream) {
-  JABD_REQUIRE(src && wq && bq && kpool && vpool && wW && bW && lateral && out,
-               "nlm_apply: null pointer");
+  JABD_REQUIRE(src && wq && bq && kpool && vpool && wW && bW && out, "nlm_apply: null pointer");
   JABD_REQUIRE(ch == 4, "nlm_apply: only ch=4 (the JABD NLM) is built");
   JABD_REQUIRE(C > 0 && C % 4 == 0 && src_ps % 4 == 0 && S > 0, "nlm_apply: bad sizes");
   const size_t smem = (2 * (size_t)S * ch + 2 * (size_t)ch * C + C) * sizeof(float);

@@ -178,6 +178,18 @@ SIGNATURES = {
     "jabd_adam_fill_chunks": [c_vp, c_i64, c_vp],
     "jabd_adam_step_f32": [c_vp, c_vp, c_i64, c_f64, c_f64, c_f64, c_f64, c_f64, c_f64, c_f64,
                            c_vp],
+    # module-level ops (csrc/modules.hip)
+    "jabd_act_f32": [c_vp, c_i64, c_i32, c_f32, c_vp, c_vp],
+    "jabd_act_bwd_f32": [c_vp, c_vp, c_i64, c_i32, c_f32, c_vp, c_vp],
+    "jabd_bn_eval_f32": [c_vp, c_i64, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_i32, c_f32, c_vp,
+                         c_vp],
+    "jabd_channel_scale_f32": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp],
+    "jabd_adaptive_pool_f32": [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_i32),
+                               c_i32, c_vp, c_vp],
+    "jabd_upsample_nearest_add_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp,
+                                      c_vp],
+    "jabd_adaptive_pool_bwd_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_i32),
+                                   c_i32, c_vp, c_vp],
 }
 _RESTYPE = {"jabd_version": ctypes.c_char_p, "jabd_dw_nblk": ctypes.c_int64,
             "jabd_expand_dw_nblk": ctypes.c_int64,

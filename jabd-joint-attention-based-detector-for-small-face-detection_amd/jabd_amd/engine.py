@@ -30,83 +30,134 @@ NLM_SIZES_DEFAULT = (1, 4, 8, 12)
 FUSE_EXPAND_DW = os.environ.get("JABD_FUSE_EXPAND_DW", "1") != "0"
 
 
-def _params_signature(module):
-    return tuple(t._version for t in module.parameters()) + tuple(
-        t._version for t in module.buffers()) + tuple(
-        t.data_ptr() for t in module.parameters())
-
-
 def _w1d(eca):
     return eca.conv.weight.detach().reshape(-1).float().contiguous()
 
 
-class _Head:
-    """ECA -> FPN(+NLM) -> ECA -> SSH -> heads, shared by both detectors."""
+class SSHPack:
+    """Eval packs of one SSH (nets/layers.py:37-68): the two branches that read
+    the input (conv3X3, conv5X5_1) and the two that read t (conv5X5_2,
+    conv7X7_2) run as one GEMM each with a split output (fused along N);
+    every part's output channels are padded to a multiple of 4 for the vector
+    epilogue (10-channel branches are stored as 12)."""
 
-    def __init__(self, m, eca_names, nlm):
-        fpn = m.fpn
+    def __init__(self, s):
+        self.leaky = s.leaky
+        q = s.conv5X5_1[0].out_channels
+        self.q = q
+        self.C = 2 * s.conv3X3[0].out_channels
+        qp = (q + 3) // 4 * 4 if q % 4 else None
+        q4 = (q + 3) // 4 * 4
+        h2 = s.conv3X3[0].out_channels
+        # (R50's 256-channel SSH keeps five GEMMs: each takes the 32x32 k x k
+        # kernel, which the split output does not)
+        self.split = h2 % 4 == 0 and s.conv3X3[0].in_channels % 32 != 0
+        if self.split:
+            self.packs = (
+                F.pack_conv_cat([(s.conv3X3[0], s.conv3X3[1], None),
+                                 (s.conv5X5_1[0], s.conv5X5_1[1], qp)]),
+                F.pack_conv_cat([(s.conv5X5_2[0], s.conv5X5_2[1], q4),
+                                 (s.conv7X7_2[0], s.conv7X7_2[1], qp)], cin_pad=qp),
+                F.pack_conv(s.conv7x7_3[0], s.conv7x7_3[1], cin_pad=qp))
+        else:
+            self.packs = (F.pack_conv(s.conv3X3[0], s.conv3X3[1]),
+                          F.pack_conv(s.conv5X5_1[0], s.conv5X5_1[1], cout_pad=qp),
+                          F.pack_conv(s.conv5X5_2[0], s.conv5X5_2[1], cin_pad=qp),
+                          F.pack_conv(s.conv7X7_2[0], s.conv7X7_2[1], cin_pad=qp, cout_pad=qp),
+                          F.pack_conv(s.conv7x7_3[0], s.conv7x7_3[1], cin_pad=qp))
+
+    def forward(self, o, sc=None):
+        """o NHWC [B,h,w,Cin] (ECA gate `sc` [B,Cin] applied on load) -> relu(cat) NHWC."""
+        B, h, w, _ = o.shape
+        C = self.C
+        dev = o.device
+        feat = torch.empty((B, h, w, C), dtype=torch.float32, device=dev)
+        if self.split:
+            # feat = [conv3X3 (C/2) | conv5X5_2 (C/4) | conv7x7_3 (C/4)]; the
+            # fused middle GEMM writes conv5X5_2 padded to a multiple of 4,
+            # whose zero pad channels conv7x7_3 overwrites right after
+            ca, cb, c73 = self.packs
+            qp_ = cb.Cin
+            t = torch.empty((B, h, w, qp_), dtype=torch.float32, device=dev)
+            t2 = torch.empty((B, h, w, qp_), dtype=torch.float32, device=dev)
+            F.conv(o, ca, pad=1, act="relu", ascale=sc, out=feat, out_c0=0, y2=t,
+                   nsplit=C // 2, act2="leaky", slope2=self.leaky)
+            F.conv(t, cb, pad=1, act="relu", out=feat, out_c0=C // 2, y2=t2,
+                   nsplit=cb.Cout - qp_, act2="leaky", slope2=self.leaky)
+            F.conv(t2, c73, pad=1, act="relu", out=feat, out_c0=3 * C // 4)
+        else:
+            c3, c51, c52, c72, c73 = self.packs
+            F.conv(o, c3, pad=1, act="relu", ascale=sc, out=feat, out_c0=0)
+            t = F.conv(o, c51, pad=1, act="leaky", slope=self.leaky, ascale=sc)
+            F.conv(t, c52, pad=1, act="relu", out=feat, out_c0=C // 2)
+            t2 = F.conv(t, c72, pad=1, act="leaky", slope=self.leaky)
+            F.conv(t2, c73, pad=1, act="relu", out=feat, out_c0=3 * C // 4)
+        return feat
+
+
+class FPNPack:
+    """Eval packs of an FPN (nets/retinaface_r.py:154-207 with NLM `nlm`,
+    nets/layers.py:70-119 with nlm=None): 1x1 laterals (+BN+leaky), nearest
+    up-sample (+NLM) + add, 3x3 merges."""
+
+    def __init__(self, fpn, nlm):
         self.leaky = fpn.leaky
-        self.eca_in = [_w1d(getattr(m, n)) for n in eca_names]
         self.lat = [F.pack_conv(o[0], o[1]) for o in (fpn.output1, fpn.output2, fpn.output3)]
         self.merge1 = F.pack_conv(fpn.merge1[0], fpn.merge1[1])
         self.merge2 = F.pack_conv(fpn.merge2[0], fpn.merge2[1])
-        self.nlm_sizes = tuple(nlm.psp.sizes)
-        C, ch = nlm.in_channels, nlm.ch
-        d = lambda t: t.detach().float().contiguous()  # noqa: E731
-        self.nlm_w = (d(nlm.f_query.weight.view(ch, C)), d(nlm.f_query.bias),
-                      d(nlm.f_key.weight.view(ch, C)), d(nlm.f_key.bias),
-                      d(nlm.f_value.weight.view(ch, C)), d(nlm.f_value.bias),
-                      d(nlm.W.weight.view(C, ch)), d(nlm.W.bias))
+        self.nlm_w = None
+        if nlm is not None:
+            self.nlm_sizes = tuple(nlm.psp.sizes)
+            self.nlm_w = nlm_weights(nlm)
+
+    def _up(self, src, lateral):
+        if self.nlm_w is not None:
+            return F.nlm_fused(src, lateral, self.nlm_w, self.nlm_sizes)
+        return F.upsample_add(src, lateral)
+
+    def forward(self, feats, scales=(None, None, None)):
+        o1, o2, o3 = [F.conv(f, pk, act="leaky", slope=self.leaky, ascale=sc)
+                      for f, pk, sc in zip(feats, self.lat, scales)]
+        o2 = F.conv(self._up(o3, o2), self.merge2, pad=1, act="leaky", slope=self.leaky)
+        o1 = F.conv(self._up(o2, o1), self.merge1, pad=1, act="leaky", slope=self.leaky)
+        return [o1, o2, o3]
+
+
+def nlm_weights(nlm):
+    C, ch = nlm.in_channels, nlm.ch
+    d = lambda t: t.detach().float().contiguous()  # noqa: E731
+    return (d(nlm.f_query.weight.view(ch, C)), d(nlm.f_query.bias),
+            d(nlm.f_key.weight.view(ch, C)), d(nlm.f_key.bias),
+            d(nlm.f_value.weight.view(ch, C)), d(nlm.f_value.bias),
+            d(nlm.W.weight.view(C, ch)), d(nlm.W.bias))
+
+
+def heads_pack(m, i):
+    convs = (m.BboxHead[i].conv1x1, m.ClassHead[i].conv1x1, m.LandmarkHead[i].conv1x1)
+    w = torch.cat([c.weight.detach().float().reshape(c.weight.shape[0], -1) for c in convs])
+    b = torch.cat([c.bias.detach().float() for c in convs])
+    return w.contiguous(), b.contiguous()
+
+
+class _Head:
+    """ECA -> FPN(+NLM) -> ECA -> SSH -> heads, shared by both detectors.
+    The FPN and SSH packs are the modules' own cached packs (also used when
+    those modules run standalone)."""
+
+    def __init__(self, m, eca_names, nlm_name, dev):
+        self.eca_in = [_w1d(getattr(m, n)) for n in eca_names]
+        self.fpn = m.fpn._jabd_cached(dev, lambda: FPNPack(m.fpn, getattr(m.fpn, nlm_name)))
         self.eca_fpn = _w1d(m.eca_fpn)
-        self.ssh = []
-        q = m.ssh1.conv5X5_1[0].out_channels
-        qp = (q + 3) // 4 * 4 if q % 4 else None  # 10-channel branches stored as 12
-        # SSH (nets/layers.py:37-68): the two branches that read `o` (conv3X3,
-        # conv5X5_1) and the two that read t (conv5X5_2, conv7X7_2) run as one
-        # GEMM each with a split output (fused along N); every part's output
-        # channels are padded to a multiple of 4 for the vector epilogue.
-        q4 = (q + 3) // 4 * 4
-        h2 = m.ssh1.conv3X3[0].out_channels
-        # (R50's 256-channel SSH keeps five GEMMs: each takes the 32x32 k x k
-        # kernel, which the split output does not)
-        self.ssh_split = h2 % 4 == 0 and m.ssh1.conv3X3[0].in_channels % 32 != 0
-        for s in (m.ssh1, m.ssh2, m.ssh3):
-            if self.ssh_split:
-                self.ssh.append((
-                    F.pack_conv_cat([(s.conv3X3[0], s.conv3X3[1], None),
-                                     (s.conv5X5_1[0], s.conv5X5_1[1], qp)]),
-                    F.pack_conv_cat([(s.conv5X5_2[0], s.conv5X5_2[1], q4),
-                                     (s.conv7X7_2[0], s.conv7X7_2[1], qp)], cin_pad=qp),
-                    F.pack_conv(s.conv7x7_3[0], s.conv7x7_3[1], cin_pad=qp)))
-                continue
-            self.ssh.append((F.pack_conv(s.conv3X3[0], s.conv3X3[1]),
-                             F.pack_conv(s.conv5X5_1[0], s.conv5X5_1[1], cout_pad=qp),
-                             F.pack_conv(s.conv5X5_2[0], s.conv5X5_2[1], cin_pad=qp),
-                             F.pack_conv(s.conv7X7_2[0], s.conv7X7_2[1], cin_pad=qp,
-                                         cout_pad=qp),
-                             F.pack_conv(s.conv7x7_3[0], s.conv7x7_3[1], cin_pad=qp)))
-        self.heads = []
-        for i in range(3):
-            convs = (m.BboxHead[i].conv1x1, m.ClassHead[i].conv1x1, m.LandmarkHead[i].conv1x1)
-            w = torch.cat([c.weight.detach().float().reshape(c.weight.shape[0], -1) for c in convs])
-            b = torch.cat([c.bias.detach().float() for c in convs])
-            self.heads.append((w.contiguous(), b.contiguous()))
+        self.ssh = [s._jabd_cached(dev, lambda s=s: SSHPack(s)) for s in (m.ssh1, m.ssh2, m.ssh3)]
+        self.heads = [heads_pack(m, i) for i in range(3)]
 
     def forward(self, feats, softmax):
         B = feats[0].shape[0]
-        lat = []
-        for f, w1d, pk in zip(feats, self.eca_in, self.lat):
-            hw = f.shape[1] * f.shape[2]
-            sc = F.eca_gate(F.channel_sums(f), hw, w1d, "sigmoid")
-            lat.append(F.conv(f, pk, act="leaky", slope=self.leaky, ascale=sc))
-        o1, o2, o3 = lat
-        m2 = F.nlm_fused(o3, o2, self.nlm_w, self.nlm_sizes)
-        o2 = F.conv(m2, self.merge2, pad=1, act="leaky", slope=self.leaky)
-        m1 = F.nlm_fused(o2, o1, self.nlm_w, self.nlm_sizes)
-        o1 = F.conv(m1, self.merge1, pad=1, act="leaky", slope=self.leaky)
-        levels = [o1, o2, o3]
+        scales = [F.eca_gate(F.channel_sums(f), f.shape[1] * f.shape[2], w1d, "sigmoid")
+                  for f, w1d in zip(feats, self.eca_in)]
+        levels = self.fpn.forward(feats, scales)
         A = sum(2 * o.shape[1] * o.shape[2] for o in levels)
-        dev = o1.device
+        dev = levels[0].device
         loc = torch.empty((B, A, 4), dtype=torch.float32, device=dev)
         conf = torch.empty((B, A, 2), dtype=torch.float32, device=dev)
         landm = torch.empty((B, A, 10), dtype=torch.float32, device=dev)
@@ -114,27 +165,7 @@ class _Head:
         for i, o in enumerate(levels):
             _, h, w, C = o.shape
             sc = F.eca_gate(F.channel_sums(o), h * w, self.eca_fpn, "sigmoid")
-            feat = torch.empty((B, h, w, C), dtype=torch.float32, device=dev)
-            if self.ssh_split:
-                # feat = [conv3X3 (C/2) | conv5X5_2 (C/4) | conv7x7_3 (C/4)]; the
-                # fused middle GEMM writes conv5X5_2 padded to a multiple of 4,
-                # whose zero pad channels conv7x7_3 overwrites right after
-                ca, cb, c73 = self.ssh[i]
-                qp_ = cb.Cin
-                t = torch.empty((B, h, w, qp_), dtype=torch.float32, device=dev)
-                t2 = torch.empty((B, h, w, qp_), dtype=torch.float32, device=dev)
-                F.conv(o, ca, pad=1, act="relu", ascale=sc, out=feat, out_c0=0, y2=t,
-                       nsplit=C // 2, act2="leaky", slope2=self.leaky)
-                F.conv(t, cb, pad=1, act="relu", out=feat, out_c0=C // 2, y2=t2,
-                       nsplit=cb.Cout - qp_, act2="leaky", slope2=self.leaky)
-                F.conv(t2, c73, pad=1, act="relu", out=feat, out_c0=3 * C // 4)
-            else:
-                c3, c51, c52, c72, c73 = self.ssh[i]
-                F.conv(o, c3, pad=1, act="relu", ascale=sc, out=feat, out_c0=0)
-                t = F.conv(o, c51, pad=1, act="leaky", slope=self.leaky, ascale=sc)
-                F.conv(t, c52, pad=1, act="relu", out=feat, out_c0=C // 2)
-                t2 = F.conv(t, c72, pad=1, act="leaky", slope=self.leaky)
-                F.conv(t2, c73, pad=1, act="relu", out=feat, out_c0=3 * C // 4)
+            feat = self.ssh[i].forward(o, sc)
             wt, bs = self.heads[i]
             F.heads(feat, wt, bs, loc, conf, landm, a_off, softmax)
             a_off += 2 * h * w
@@ -142,11 +173,20 @@ class _Head:
 
 
 class _MNv3Block:
+    """Eval plan of one MobileNetV3 inverted-residual block (nets/mobilenetV3.py:
+    Block_eca :94-150, Block :35-91, Block_eca_G :152-208): fused expand 1x1 +
+    depthwise kxk (+ECA pool partials), the channel gate (ECA / SE / BECA) as a
+    [B, E] scale the project GEMM applies on its operand load, the skip branch
+    K-concatenated or added in the project GEMM's epilogue."""
+
     def __init__(self, blk):
         self.k, self.stride, self.act = blk.kernel_size, blk.stride, blk.act_name
         self.expand = F.pack_conv(blk.conv1, blk.bn1)
         self.dw_w, self.dw_b = F.pack_dw(blk.conv2, blk.bn2)
-        self.eca = _w1d(blk.eca)
+        self.gate = getattr(blk, "gate_kind", "eca")
+        self.blk = blk
+        if self.gate in ("eca", "beca"):
+            self.eca = _w1d(blk.eca)
         sk = blk.skip
         self.skip_dw = None
         if sk is None:
@@ -168,15 +208,25 @@ class _MNv3Block:
             self.skip_dw = F.pack_dw(sk[0], sk[1])
             self.project = F.pack_conv(blk.conv3, blk.bn3)
 
+    def _scale(self, d, part):
+        if self.gate == "eca":
+            return F.eca_gate(part, d.shape[1] * d.shape[2], self.eca, "hsigmoid")
+        from . import modules as M
+        if self.gate == "se":
+            return M.se_scale_eval(self.blk.se, d, self.blk)
+        if self.gate == "beca":
+            return M.beca_gate(d, self.eca)
+        return None
+
     def forward(self, x):
         if FUSE_EXPAND_DW:
             d, part = F.expand_dw(x, self.expand, self.dw_w, self.dw_b, self.k, self.stride,
-                                  act=self.act)
+                                  act=self.act, partials=self.gate == "eca")
         else:
             e = F.conv(x, self.expand, act=self.act)
             d, part = F.dwconv(e, self.dw_w, self.dw_b, self.k, self.stride, act=self.act,
-                               partials=True)
-        sc = F.eca_gate(part, d.shape[1] * d.shape[2], self.eca, "hsigmoid")
+                               partials=self.gate == "eca")
+        sc = self._scale(d, part)
         if self.kind == "identity":
             return F.conv(d, self.project, act=self.act, ascale=sc, res=x)
         if self.kind == "concat":
@@ -210,41 +260,26 @@ class _R50Block:
 
 
 class Engine:
-    def __init__(self, model, kind):
-        self.model, self.kind = model, kind
-        self.sig = None
+    """The eval-mode plan of one RetinaFace on one device (packs built once per
+    generation, see hipmodule.py)."""
 
-    def _refresh(self):
-        m = self.model
-        with torch.no_grad():
-            if self.kind == "mnv3":
-                s_, t_ = F.bn_fold(m.body.bn1)
-                self.stem = ((F.conv_weight_2d(m.body.conv1.weight.detach().float())
-                              * s_[None, :]).contiguous(), t_.detach().contiguous())
-                self.layers = [[_MNv3Block(b) for b in getattr(m.body, f"layer{i}")]
-                               for i in (1, 2, 3)]
-                self.head = _Head(m, ("eca_40", "eca_80", "eca_160"), m.fpn.nlm)
-            else:
-                self.stem = F.pack_conv(m.body.conv1, m.body.bn1)
-                self.layers = [[_R50Block(b) for b in getattr(m.body, f"layer{i}")]
-                               for i in (1, 2, 3, 4)]
-                self.head = _Head(m, ("eca_64", "eca_128", "eca_256"), m.fpn.Nlm)
+    def __init__(self, model, kind, dev):
+        m = model
+        self.kind = kind
+        if kind == "mnv3":
+            s_, t_ = F.bn_fold(m.body.bn1)
+            self.stem = ((F.conv_weight_2d(m.body.conv1.weight.detach().float())
+                          * s_[None, :]).contiguous(), t_.detach().contiguous())
+            self.layers = [[b._jabd_cached(dev, lambda b=b: _MNv3Block(b))
+                            for b in getattr(m.body, f"layer{i}")] for i in (1, 2, 3)]
+            self.head = _Head(m, ("eca_40", "eca_80", "eca_160"), "nlm", dev)
+        else:
+            self.stem = F.pack_conv(m.body.conv1, m.body.bn1)
+            self.layers = [[b._jabd_cached(dev, lambda b=b: _R50Block(b))
+                            for b in getattr(m.body, f"layer{i}")] for i in (1, 2, 3, 4)]
+            self.head = _Head(m, ("eca_64", "eca_128", "eca_256"), "Nlm", dev)
 
-    def forward(self, x):
-        m = self.model
-        if not isinstance(x, torch.Tensor) or not x.is_cuda or x.dtype != torch.float32:
-            raise RuntimeError("RetinaFace.forward on the JABD HIP path needs a float32 GPU "
-                               "tensor [B,3,H,W]; there is no CPU fallback")
-        if x.dim() != 4 or x.shape[1] != 3:
-            raise ValueError(f"expected input [B,3,H,W], got {tuple(x.shape)}")
-        if m.training:
-            from .train import train_forward
-            return train_forward(m, self.kind, x)
-        sig = _params_signature(m)
-        if sig != self.sig:
-            self._refresh()
-            self.sig = _params_signature(m)
-        x = x.contiguous()
+    def run(self, x, softmax):
         with torch.no_grad():
             if self.kind == "mnv3":
                 s = F.stem(x, self.stem[0], self.stem[1], "hswish")
@@ -262,12 +297,27 @@ class Engine:
                         s = blk.forward(s)
                     if li >= 1:
                         feats.append(s)
-            return self.head.forward(feats, softmax=(m.mode != "train"))
+            return self.head.forward(feats, softmax=softmax)
 
 
-def get_engine(model, kind):
-    eng = model.__dict__.get("_engine")
-    if eng is None or eng.kind != kind:
-        eng = Engine(model, kind)
-        model.__dict__["_engine"] = eng
-    return eng
+def _check_input(x):
+    if not isinstance(x, torch.Tensor) or not x.is_cuda or x.dtype != torch.float32:
+        raise RuntimeError("RetinaFace.forward on the JABD HIP path needs a float32 GPU "
+                           "tensor [B,3,H,W]; there is no CPU fallback")
+    if x.dim() != 4 or x.shape[1] != 3:
+        raise ValueError(f"expected input [B,3,H,W], got {tuple(x.shape)}")
+
+
+def retinaface_forward(model, kind, x):
+    """RetinaFace.forward: the fused eval plan, or the training graph.
+
+    `model` is the module being called — under nn.DataParallel that is the
+    replica on x's device, so training binds autograd to the replica's
+    broadcast parameters and eval uses packs built from them (cached per
+    device on the shared cache of the original)."""
+    _check_input(x)
+    if model.training:
+        from .train import train_forward
+        return train_forward(model, kind, x)
+    eng = model._jabd_cached(x.device, lambda: Engine(model, kind, x.device), tag="engine")
+    return eng.run(x.contiguous(), softmax=(model.mode != "train"))

@@ -291,11 +291,12 @@ def eca_gate(part, hw, w1d, gate, return_mean=False):
 
 
 def nlm_fused(src, lateral, nlm_w, sizes, save=False):
-    """lateral + NLM(nearest(src -> lateral's size)); all NHWC.
+    """lateral + NLM(nearest(src -> lateral's size)); all NHWC.  lateral=None
+    is the standalone NLM.forward(src) (no up-sample, no add).
 
     save=True also returns (q, ctx, kpool, vpool) for the backward."""
     B, hs, ws, C = src.shape
-    _, h, w, _ = lateral.shape
+    h, w = (hs, ws) if lateral is None else (lateral.shape[1], lateral.shape[2])
     wq, bq, wk, bk, wv, bv, wW, bW = nlm_w
     ch = wq.shape[0]
     S = sum(s * s for s in sizes)
@@ -306,16 +307,27 @@ def nlm_fused(src, lateral, nlm_w, sizes, save=False):
     call("jabd_nlm_pool_f32", src.data_ptr(), src.stride(0), C, B, hs, ws, C, h, w,
          wk.data_ptr(), bk.data_ptr(), wv.data_ptr(), bv.data_ptr(), ch, arr, len(sizes),
          kp.data_ptr(), vp.data_ptr(), kv.data_ptr(), _stream())
-    out = torch.empty_like(lateral)
+    out = torch.empty((B, h, w, C), dtype=torch.float32, device=src.device)
     q = ctx = None
     if save:
         q = torch.empty((B, h * w, ch), dtype=torch.float32, device=src.device)
         ctx = torch.empty_like(q)
     call("jabd_nlm_apply_f32", src.data_ptr(), src.stride(0), C, B, hs, ws, C, h, w,
          wq.data_ptr(), bq.data_ptr(), kp.data_ptr(), vp.data_ptr(), S, ch, wW.data_ptr(),
-         bW.data_ptr(), lateral.data_ptr(), out.data_ptr(), _ptr(q), _ptr(ctx), _stream())
+         bW.data_ptr(), _ptr(lateral), out.data_ptr(), _ptr(q), _ptr(ctx), _stream())
     if save:
         return out, (q, ctx, kp, vp)
+    return out
+
+
+def upsample_add(src, lateral):
+    """lateral + F.interpolate(src, size=lateral's, mode='nearest'), NHWC."""
+    _check("upsample_add.src", src)
+    B, hs, ws, C = src.shape
+    _, h, w, _ = lateral.shape
+    out = torch.empty_like(lateral)
+    call("jabd_upsample_nearest_add_f32", src.data_ptr(), B, hs, ws, h, w, C, lateral.data_ptr(),
+         out.data_ptr(), _stream())
     return out
 
 

@@ -6,16 +6,20 @@ The reference wraps the model in nn.DataParallel (train_mobilenetV3_ecagai.py:
 shard, the loss is computed on the gathered global batch (so its
 normalisers are global positive counts) and gradients are summed onto GPU 0;
 only GPU 0's BN running buffers survive.  Here each rank holds a full
-replica, MultiBoxLoss all-reduces the positive counts (nets/
-retinaface_training.py), and this module:
+replica and:
 
-  * all-reduces gradients with SUM (not DDP's mean) in flat buckets sized for
-    xGMI ring all-reduce — parameters without a gradient (the built-but-unused
-    SeModule weights) are skipped;
-  * broadcasts BN running buffers from rank 0 after each step.
+  * MultiBoxLoss all-reduces the positive counts `(sum pos, sum pos1)` over
+    the group (`MultiBoxLoss.global_counts(True, group)`, entered by
+    train_step) before normalising — 16 bytes, latency-bound.  Outside it the
+    loss normalises by its own batch's counts, as the reference's;
+  * GradAllReduce SUM-all-reduces gradients (not DDP's mean) in flat buckets
+    sized for xGMI ring all-reduce.  Buckets are launched from gradient hooks
+    while backward is still running (overlap), in one fixed order on every
+    rank; parameters that never get a gradient (the reference's built-but-
+    unused SeModule weights) are found on the first step and left out;
+  * broadcast_buffers copies rank 0's BN running buffers to every rank.
 
-Collectives run on torch.distributed ("nccl" = RCCL on ROCm, or "gloo" in
-the CPU tests).
+Collectives run on torch.distributed ("nccl" = RCCL on ROCm, or "gloo").
 """
 import torch
 import torch.distributed as dist
@@ -23,43 +27,124 @@ import torch.distributed as dist
 BUCKET_BYTES = 32 << 20  # per all-reduce: large enough to amortise the ring's latency
 
 
+def _world(group):
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+
+
 class GradAllReduce:
-    def __init__(self, model, group=None, bucket_bytes=BUCKET_BYTES):
+    """SUM all-reduce of every gradient after backward.
+
+    overlap=True: after a first synchronous step (which finds the parameters
+    that receive gradients), buckets are filled by post-accumulate-grad hooks
+    and their all-reduces launched asynchronously during backward — bucket i
+    only after buckets 0..i-1, so every rank issues the same collective
+    sequence.  Call the object after loss.backward() to wait for the
+    collectives and write the sums back into .grad."""
+
+    def __init__(self, model, group=None, bucket_bytes=BUCKET_BYTES, overlap=True):
         self.model = model
         self.group = group
         self.bucket_bytes = bucket_bytes
+        self.overlap = overlap
+        self.buckets = None      # [[param, ...], ...] in launch order
+        self.hooks = []
+        self._reset()
 
-    def _buckets(self, params):
-        bucket, size = [], 0
-        for p in params:
-            nbytes = p.grad.numel() * p.grad.element_size()
-            if bucket and size + nbytes > self.bucket_bytes:
-                yield bucket
-                bucket, size = [], 0
-            bucket.append(p)
+    # ---------------------------------------------------------------- buckets
+    def _plan(self, params):
+        """Buckets over `params` in reverse registration order (backward
+        produces the last layers' gradients first)."""
+        buckets, cur, size = [], [], 0
+        for p in reversed(params):
+            nbytes = p.numel() * p.element_size()
+            if cur and size + nbytes > self.bucket_bytes:
+                buckets.append(cur)
+                cur, size = [], 0
+            cur.append(p)
             size += nbytes
-        if bucket:
-            yield bucket
+        if cur:
+            buckets.append(cur)
+        return buckets
+
+    def _reset(self):
+        self.pending = {}
+        self.flat = {}
+        self.works = {}
+        self.next_launch = 0
+
+    def _install(self, params):
+        self.buckets = self._plan(params)
+        self.where = {}
+        for bi, b in enumerate(self.buckets):
+            for p in b:
+                self.where[p] = bi
+        for p in params:
+            self.hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    def _on_grad(self, p):
+        bi = self.where[p]
+        left = self.pending.get(bi, len(self.buckets[bi])) - 1
+        self.pending[bi] = left
+        if left == 0:
+            b = self.buckets[bi]
+            self.flat[bi] = torch.cat([q.grad.reshape(-1) for q in b])
+            while self.next_launch in self.flat and self.next_launch not in self.works:
+                i = self.next_launch
+                self.works[i] = dist.all_reduce(self.flat[i], op=dist.ReduceOp.SUM,
+                                                group=self.group, async_op=True)
+                self.next_launch += 1
+
+    def _sync_all(self, params):
+        for b in self._plan(params):
+            flat = torch.cat([p.grad.reshape(-1) for p in b])
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+            self._scatter(b, flat)
+
+    @staticmethod
+    def _scatter(bucket, flat):
+        off = 0
+        for p in bucket:
+            n = p.grad.numel()
+            p.grad.copy_(flat[off:off + n].view_as(p.grad))
+            off += n
 
     def __call__(self):
-        """SUM-all-reduce every existing gradient (call after backward)."""
-        if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+        """Finish the step's gradient SUM all-reduce (call after backward)."""
+        if not _world(self.group):
+            self._reset()
             return
-        params = [p for p in self.model.parameters() if p.grad is not None]
-        # identical order on every rank: parameters() order is deterministic
-        for bucket in self._buckets(params):
-            flat = torch.cat([p.grad.reshape(-1) for p in bucket])
-            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
-            off = 0
-            for p in bucket:
-                n = p.grad.numel()
-                p.grad.copy_(flat[off:off + n].view_as(p.grad))
-                off += n
+        if self.buckets is None:
+            # first step: the parameters with a gradient define the buckets
+            # (identical on every rank: same model, same graph)
+            params = [p for p in self.model.parameters() if p.grad is not None]
+            self._sync_all(params)
+            if self.overlap:
+                self._install(params)
+            else:
+                self.buckets = []
+                self.static = params
+            self._reset()
+            return
+        if not self.overlap:
+            self._sync_all(self.static)
+            return
+        if len(self.works) != len(self.buckets):
+            raise RuntimeError("GradAllReduce: not every bucket received its gradients this "
+                               "step (the set of parameters with gradients changed)")
+        for i, b in enumerate(self.buckets):
+            self.works[i].wait()
+            self._scatter(b, self.flat[i])
+        self._reset()
+
+    def remove(self):
+        for h in self.hooks:
+            h.remove()
+        self.hooks = []
 
 
 def broadcast_buffers(model, src=0, group=None):
     """Rank 0's BN running buffers win (DataParallel keeps only replica 0's)."""
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not _world(group):
         return
     bufs = [b for b in model.buffers() if b.is_floating_point()]
     if not bufs:
@@ -84,15 +169,18 @@ def shard(batch_images, batch_targets, rank, world):
 def train_step(model, criterion, optimizer, images, targets, priors, loc_weight=2.0,
                reducer=None):
     """One fit_one_epoch iteration (train_mobilenetV3_ecagai.py:518-533) on
-    this rank's shard: zero_grad -> forward -> MultiBoxLoss -> backward ->
-    gradient SUM all-reduce -> optimizer step -> rank-0 BN buffers."""
+    this rank's shard: zero_grad -> forward -> MultiBoxLoss with global
+    positive counts -> backward (bucketed gradient SUM all-reduce overlapped)
+    -> optimizer step -> rank-0 BN buffers."""
+    group = reducer.group if reducer is not None else None
     optimizer.zero_grad()
     out = model(images)
-    r_loss, c_loss, landm_loss = criterion(out, priors, targets)
+    with criterion.global_counts(reducer is not None and _world(group), group):
+        r_loss, c_loss, landm_loss = criterion(out, priors, targets)
     loss = loc_weight * r_loss + c_loss + landm_loss
     loss.backward()
     if reducer is not None:
         reducer()
     optimizer.step()
-    broadcast_buffers(model)
+    broadcast_buffers(model, group=group)
     return loss.detach(), (r_loss.detach(), c_loss.detach(), landm_loss.detach())

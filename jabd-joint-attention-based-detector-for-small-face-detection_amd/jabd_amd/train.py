@@ -173,8 +173,10 @@ class ConvFn(torch.autograd.Function):
         stride, pad, nchw_in, has_bias, H, W = ctx.cfg
         dy = dy.contiguous()
         dx = None
-        if ctx.needs_input_grad[0] and not nchw_in:
+        if ctx.needs_input_grad[0]:
             dx = _dgrad(dy, weight, stride, pad, H, W)
+            if nchw_in:  # a network input that requires grad: hand it back as NCHW
+                dx = dx.permute(0, 3, 1, 2).contiguous()
         dw = _wgrad(x, dy, weight, stride, pad, nchw_in) if ctx.needs_input_grad[1] else None
         db = _chan_sum(dy) if has_bias and ctx.needs_input_grad[2] else None
         return dx, dw, db, None, None, None
@@ -298,28 +300,33 @@ class DwConvFn(torch.autograd.Function):
 
 
 class NlmFn(torch.autograd.Function):
-    """lateral + NLM(nearest(src -> lateral size)) (nets/retinaface_r.py:192-203)."""
+    """lateral + NLM(nearest(src -> lateral size)) (nets/retinaface_r.py:192-203);
+    lateral=None is the standalone NLM.forward(src) (:124-152)."""
 
     @staticmethod
     def forward(ctx, src, lateral, wq, bq, wk, bk, wv, bv, wW, bW, sizes):
         B, hs, ws, C = src.shape
-        _, h, w, _ = lateral.shape
         ch = wq.shape[0]
         d = lambda t, *s: t.detach().float().reshape(*s).contiguous()  # noqa: E731
         W = (d(wq, ch, C), d(bq, ch), d(wk, ch, C), d(bk, ch), d(wv, ch, C), d(bv, ch),
              d(wW, C, ch), d(bW, C))
-        out, (q, cx, kp, vp) = F.nlm_fused(src, lateral.contiguous(), W, sizes, save=True)
-        xup = torch.empty((B, h, w, C), dtype=torch.float32, device=src.device)
-        call("jabd_upsample_nearest_f32", src.data_ptr(), B, hs, ws, h, w, C, xup.data_ptr(),
-             _st())
+        lat = lateral.contiguous() if lateral is not None else None
+        out, (q, cx, kp, vp) = F.nlm_fused(src, lat, W, sizes, save=True)
+        if lateral is None:
+            xup = src
+        else:
+            _, h, w, _ = lateral.shape
+            xup = torch.empty((B, h, w, C), dtype=torch.float32, device=src.device)
+            call("jabd_upsample_nearest_f32", src.data_ptr(), B, hs, ws, h, w, C, xup.data_ptr(),
+                 _st())
         ctx.save_for_backward(xup, q, cx, kp, vp, *W)
-        ctx.cfg = (tuple(sizes), hs, ws)
+        ctx.cfg = (tuple(sizes), hs, ws, lateral is not None)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         xup, q, cx, kp, vp, wq, bq, wk, bk, wv, bv, wW, bW = ctx.saved_tensors
-        sizes, hs, ws = ctx.cfg
+        sizes, hs, ws, has_lat = ctx.cfg
         dout = dout.contiguous()
         B, h, w, C = dout.shape
         ch = wq.shape[0]
@@ -338,9 +345,12 @@ class NlmFn(torch.autograd.Function):
         arr = (ctypes.c_int32 * len(sizes))(*sizes)
         call("jabd_nlm_bwd_proj_f32", dk.data_ptr(), dv.data_ptr(), B, S, arr, len(sizes), h, w,
              C, wk.data_ptr(), wv.data_ptr(), dkv.data_ptr(), dxup.data_ptr(), _st())
-        dsrc = torch.empty((B, hs, ws, C), dtype=torch.float32, device=dev)
-        call("jabd_upsample_nearest_bwd_f32", dxup.data_ptr(), B, h, w, hs, ws, C, 0,
-             dsrc.data_ptr(), _st())
+        if has_lat:
+            dsrc = torch.empty((B, hs, ws, C), dtype=torch.float32, device=dev)
+            call("jabd_upsample_nearest_bwd_f32", dxup.data_ptr(), B, h, w, hs, ws, C, 0,
+                 dsrc.data_ptr(), _st())
+        else:
+            dsrc = dxup  # no up-sample: x itself is the source
         # weight gradients = 1x1-conv weight gradients of the saved per-pixel tensors
         ctxv = cx.view(B, h, w, ch)
         dWW = _wgrad(ctxv, dout, torch.empty((C, ch, 1, 1), device=dev), 1, 0)
@@ -351,7 +361,27 @@ class NlmFn(torch.autograd.Function):
         dWv = _wgrad(xup, dv_only, torch.empty((ch, C, 1, 1), device=dev), 1, 0)
         g = (dWq, _chan_sum(dq), dWk, _chan_sum(dk_only), dWv, _chan_sum(dv_only), dWW,
              _chan_sum(dout))
-        return (dsrc, dout) + g + (None,)
+        return (dsrc, dout if has_lat else None) + g + (None,)
+
+
+class UpAddFn(torch.autograd.Function):
+    """lateral + F.interpolate(src, size=lateral's, mode='nearest') — the plain
+    FPN's merge input (nets/layers.py:106-117)."""
+
+    @staticmethod
+    def forward(ctx, src, lateral):
+        ctx.src_hw = (src.shape[1], src.shape[2])
+        return F.upsample_add(src, lateral.contiguous())
+
+    @staticmethod
+    def backward(ctx, dout):
+        dout = dout.contiguous()
+        B, h, w, C = dout.shape
+        hs, ws = ctx.src_hw
+        dsrc = torch.empty((B, hs, ws, C), dtype=torch.float32, device=dout.device)
+        call("jabd_upsample_nearest_bwd_f32", dout.data_ptr(), B, h, w, hs, ws, C, 0,
+             dsrc.data_ptr(), _st())
+        return dsrc, dout
 
 
 class SshTailFn(torch.autograd.Function):
@@ -521,10 +551,23 @@ def conv(x, m, stride=1, pad=0, nchw_in=False):
 
 
 def _mnv3_block(blk, s):
+    """Training graph of Block_eca / Block / Block_eca_G (nets/mobilenetV3.py:
+    :140-150, :81-91, :198-208): the gate is ECA on the project conv's load,
+    SE or BECA applied explicitly, or none."""
     act = blk.act_name
     e = bn_act(conv(s, blk.conv1), blk.bn1, act)
     d = bn_act(DwConvFn.apply(e, blk.conv2.weight, blk.stride), blk.bn2, act)
-    p = EcaConvFn.apply(d, blk.eca.conv.weight, blk.conv3.weight, 1, 0, "hsigmoid")
+    gate = getattr(blk, "gate_kind", "eca")
+    if gate == "eca":
+        p = EcaConvFn.apply(d, blk.eca.conv.weight, blk.conv3.weight, 1, 0, "hsigmoid")
+    else:
+        if gate == "se":
+            from .modules import ScaleFn, se_scale_train
+            d = ScaleFn.apply(d, se_scale_train(blk.se, d))
+        elif gate == "beca":
+            from .ops import BecaFn
+            d = BecaFn.apply(d, blk.eca.conv.weight.reshape(-1))
+        p = conv(d, blk.conv3)
     sk = blk.skip
     if sk is None:
         res = s
@@ -549,71 +592,93 @@ def _r50_block(blk, x):
     return bn_act(t, blk.bn3, "relu", res=idn)
 
 
-def _head(m, feats, eca_names, nlm):
-    fpn = m.fpn
-    lk = fpn.leaky
-    outs = (fpn.output1, fpn.output2, fpn.output3)
-    lat = [bn_act(EcaConvFn.apply(f, getattr(m, n).conv.weight, o[0].weight, 1, 0, "sigmoid"),
-                  o[1], "leaky", lk) for f, n, o in zip(feats, eca_names, outs)]
-    o1, o2, o3 = lat
+def nlm_train(nlm, src, lateral=None):
     nw = (nlm.f_query.weight, nlm.f_query.bias, nlm.f_key.weight, nlm.f_key.bias,
           nlm.f_value.weight, nlm.f_value.bias, nlm.W.weight, nlm.W.bias)
-    sizes = tuple(nlm.psp.sizes)
-    m2 = NlmFn.apply(o3, o2, *nw, sizes)
-    o2 = bn_act(conv(m2, fpn.merge2[0], 1, 1), fpn.merge2[1], "leaky", lk)
-    m1 = NlmFn.apply(o2, o1, *nw, sizes)
-    o1 = bn_act(conv(m1, fpn.merge1[0], 1, 1), fpn.merge1[1], "leaky", lk)
-    feats_out = []
-    ew = m.eca_fpn.conv.weight
-    for o, ssh in zip((o1, o2, o3), (m.ssh1, m.ssh2, m.ssh3)):
-        q = ssh.conv5X5_1[0].out_channels
-        qp = _pad_to4(q)
-        a = EcaConvFn.apply(o, ew, ssh.conv3X3[0].weight, 1, 1, "sigmoid")
-        b1 = bn_act(EcaConvFn.apply(o, ew, _padw(ssh.conv5X5_1[0].weight, cout=qp), 1, 1,
-                                    "sigmoid"), ssh.conv5X5_1[1], "leaky", ssh.leaky)
-        b = ConvFn.apply(b1, _padw(ssh.conv5X5_2[0].weight, cout=qp, cin=qp), None, 1, 1, False)
-        c1 = bn_act(ConvFn.apply(b1, _padw(ssh.conv7X7_2[0].weight, cout=qp, cin=qp), None, 1, 1,
-                                 False), ssh.conv7X7_2[1], "leaky", ssh.leaky)
-        c = ConvFn.apply(c1, _padw(ssh.conv7x7_3[0].weight, cout=qp, cin=qp), None, 1, 1, False)
-        stats = []
-        bns = (ssh.conv3X3[1], ssh.conv5X5_2[1], ssh.conv7x7_3[1])
-        gb = []
-        for bn, t in zip(bns, (a, b, c)):
-            C = t.shape[3]
-            pad = C - bn.weight.shape[0]
-            if pad:
-                g = torch.cat([bn.weight, bn.weight.new_zeros(pad)])
-                bt = torch.cat([bn.bias, bn.bias.new_zeros(pad)])
-                stats.append((None, None, bn.momentum, bn.eps))  # updated below
-            else:
-                g, bt = bn.weight, bn.bias
-                stats.append((bn.running_mean, bn.running_var, bn.momentum, bn.eps))
-            gb += [g, bt]
-            if bn.num_batches_tracked is not None:
-                bn.num_batches_tracked.add_(1)
-        if qp != q:
-            # padded branches: track running stats on padded copies, then copy back
-            padded = []
-            for i, (bn, t) in enumerate(zip(bns, (a, b, c))):
-                if stats[i][0] is None:
-                    pad = t.shape[3] - bn.weight.shape[0]
-                    rm = torch.cat([bn.running_mean, bn.running_mean.new_zeros(pad)])
-                    rv = torch.cat([bn.running_var, bn.running_var.new_ones(pad)])
-                    stats[i] = (rm, rv, bn.momentum, bn.eps)
-                    padded.append((bn, rm, rv))
-            f = SshTailFn.apply(a, b, c, *gb, stats)
-            with torch.no_grad():
-                for bn, rm, rv in padded:
-                    bn.running_mean.copy_(rm[: bn.running_mean.shape[0]])
-                    bn.running_var.copy_(rv[: bn.running_var.shape[0]])
-            # drop the zero pad channels of the 10-channel branches
-            C = o.shape[3]
-            half, quarter = C // 2, q
-            f = torch.cat([f[..., :half], f[..., half:half + quarter],
-                           f[..., half + qp:half + qp + quarter]], -1)
+    return NlmFn.apply(src, lateral, *nw, tuple(nlm.psp.sizes))
+
+
+def fpn_train(fpn, feats, nlm=None, eca_ws=None):
+    """FPN forward (nets/retinaface_r.py:169-207; nlm=None: nets/layers.py:83-119)
+    in training mode; eca_ws: the three input ECA Conv1d weights, applied on
+    the lateral convs' operand load (nets/retinaface_r.py:313-315)."""
+    lk = fpn.leaky
+    outs = (fpn.output1, fpn.output2, fpn.output3)
+    lat = []
+    for i, (f, o) in enumerate(zip(feats, outs)):
+        if eca_ws is not None:
+            y = EcaConvFn.apply(f, eca_ws[i], o[0].weight, 1, 0, "sigmoid")
         else:
-            f = SshTailFn.apply(a, b, c, *gb, stats)
-        feats_out.append(f.contiguous())
+            y = conv(f, o[0])
+        lat.append(bn_act(y, o[1], "leaky", lk))
+    o1, o2, o3 = lat
+    up = (lambda s_, l_: nlm_train(nlm, s_, l_)) if nlm is not None else UpAddFn.apply
+    o2 = bn_act(conv(up(o3, o2), fpn.merge2[0], 1, 1), fpn.merge2[1], "leaky", lk)
+    o1 = bn_act(conv(up(o2, o1), fpn.merge1[0], 1, 1), fpn.merge1[1], "leaky", lk)
+    return [o1, o2, o3]
+
+
+def ssh_train(ssh, o, eca_w=None):
+    """SSH forward (nets/layers.py:56-68) in training mode; eca_w: the head's
+    eca_fpn Conv1d weight applied on the two input convs' operand load."""
+    q = ssh.conv5X5_1[0].out_channels
+    qp = _pad_to4(q)
+
+    def first(w):
+        if eca_w is not None:
+            return EcaConvFn.apply(o, eca_w, w, 1, 1, "sigmoid")
+        return ConvFn.apply(o, w, None, 1, 1, False)
+
+    a = first(ssh.conv3X3[0].weight)
+    b1 = bn_act(first(_padw(ssh.conv5X5_1[0].weight, cout=qp)), ssh.conv5X5_1[1], "leaky",
+                ssh.leaky)
+    b = ConvFn.apply(b1, _padw(ssh.conv5X5_2[0].weight, cout=qp, cin=qp), None, 1, 1, False)
+    c1 = bn_act(ConvFn.apply(b1, _padw(ssh.conv7X7_2[0].weight, cout=qp, cin=qp), None, 1, 1,
+                             False), ssh.conv7X7_2[1], "leaky", ssh.leaky)
+    c = ConvFn.apply(c1, _padw(ssh.conv7x7_3[0].weight, cout=qp, cin=qp), None, 1, 1, False)
+    stats = []
+    bns = (ssh.conv3X3[1], ssh.conv5X5_2[1], ssh.conv7x7_3[1])
+    gb = []
+    for bn, t in zip(bns, (a, b, c)):
+        C = t.shape[3]
+        pad = C - bn.weight.shape[0]
+        if pad:
+            g = torch.cat([bn.weight, bn.weight.new_zeros(pad)])
+            bt = torch.cat([bn.bias, bn.bias.new_zeros(pad)])
+            stats.append((None, None, bn.momentum, bn.eps))  # updated below
+        else:
+            g, bt = bn.weight, bn.bias
+            stats.append((bn.running_mean, bn.running_var, bn.momentum, bn.eps))
+        gb += [g, bt]
+        if bn.num_batches_tracked is not None:
+            bn.num_batches_tracked.add_(1)
+    if qp == q:
+        return SshTailFn.apply(a, b, c, *gb, stats)
+    # padded branches: track running stats on padded copies, then copy back
+    padded = []
+    for i, (bn, t) in enumerate(zip(bns, (a, b, c))):
+        if stats[i][0] is None:
+            pad = t.shape[3] - bn.weight.shape[0]
+            rm = torch.cat([bn.running_mean, bn.running_mean.new_zeros(pad)])
+            rv = torch.cat([bn.running_var, bn.running_var.new_ones(pad)])
+            stats[i] = (rm, rv, bn.momentum, bn.eps)
+            padded.append((bn, rm, rv))
+    f = SshTailFn.apply(a, b, c, *gb, stats)
+    with torch.no_grad():
+        for bn, rm, rv in padded:
+            bn.running_mean.copy_(rm[: bn.running_mean.shape[0]])
+            bn.running_var.copy_(rv[: bn.running_var.shape[0]])
+    # drop the zero pad channels of the 10-channel branches
+    half = a.shape[3]
+    f = torch.cat([f[..., :half], f[..., half:half + q], f[..., half + qp:half + qp + q]], -1)
+    return f.contiguous()
+
+
+def _head(m, feats, eca_names, nlm):
+    o1, o2, o3 = fpn_train(m.fpn, feats, nlm,
+                           [getattr(m, n).conv.weight for n in eca_names])
+    ew = m.eca_fpn.conv.weight
+    feats_out = [ssh_train(ssh, o, ew) for o, ssh in zip((o1, o2, o3), (m.ssh1, m.ssh2, m.ssh3))]
     wb = []
     for i in range(3):
         for h in (m.BboxHead[i], m.ClassHead[i], m.LandmarkHead[i]):

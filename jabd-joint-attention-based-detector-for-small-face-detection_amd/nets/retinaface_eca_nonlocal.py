@@ -1,18 +1,24 @@
 """RetinaFace-R50 + ECA + NLM — drop-in for the reference
 nets/retinaface_eca_nonlocal.py:37-359 (the model predict.py loads).
-Same names/keys (incl. the unused `Nlm` and `IouHead` modules); forward runs
-the fused HIP plan (jabd_amd/engine.py)."""
-import math
-
+Same names/keys (incl. the unused `Nlm` and `IouHead` modules).
+RetinaFace.forward runs the fused HIP plan (jabd_amd/engine.py); the other
+modules have HIP forwards of their own (jabd_amd/modules.py)."""
 import torch.nn as nn
 
+from jabd_amd import modules as M
+from jabd_amd.engine import retinaface_forward
+from jabd_amd.hipmodule import HipModule
 from nets._getter import IntermediateLayerGetter
-from nets.layers import SSH, conv_bn, conv_bn1X1
+from nets.layers import SSH, conv_bn, conv_bn1X1, fpn_forward
 from nets.resnet_pytorch_r import resnet50
-from nets.retinaface_r import BboxHead, ClassHead, LandmarkHead, NLM, PSPModule  # noqa: F401
+from nets.retinaface_r import (BboxHead, ClassHead, LandmarkHead, NLM, PSPModule,  # noqa: F401
+                               _Head1x1)
+from nets.retinaface_r import eca_block as _eca_sigmoid
 
 
-class FPN(nn.Module):
+class FPN(HipModule):
+    """Laterals, nearest up-sample -> shared NLM(256) -> add, merges (reference :37-90)."""
+
     def __init__(self, in_channels_list, out_channels):
         super().__init__()
         self.leaky = 0.1 if out_channels <= 64 else 0.0
@@ -23,28 +29,23 @@ class FPN(nn.Module):
         self.merge2 = conv_bn(out_channels, out_channels, leaky=self.leaky)
         self.Nlm = NLM(256)
 
+    def forward(self, inputs):
+        return fpn_forward(self, inputs, self.Nlm)
 
-class IOUHead(nn.Module):
+
+class IOUHead(_Head1x1):
+    k = 1
+
     def __init__(self, inchannels=512, num_anchors=2):
         super().__init__()
-        self.conv1x1 = nn.Conv2d(inchannels, num_anchors, kernel_size=(1, 1), stride=1, padding=0)
+        self.conv1x1 = M.Conv2d(inchannels, num_anchors, kernel_size=(1, 1), stride=1, padding=0)
 
 
-class eca_block(nn.Module):
-    """Sigmoid-gated ECA (reference :203-219)."""
-    gate = "sigmoid"
-
-    def __init__(self, channel, b=1, gamma=2):
-        super().__init__()
-        k = int(abs((math.log(channel, 2) + b) / gamma))
-        k = k if k % 2 else k + 1
-        self.avg_pool = nn.AdaptiveAvgPool2d(1)
-        self.conv = nn.Conv1d(1, 1, kernel_size=k, padding=(k - 1) // 2, bias=False)
-        self.sigmoid = nn.Sigmoid()
-        self.Hsigmoid = nn.Hardsigmoid()
+class eca_block(_eca_sigmoid):
+    """Sigmoid-gated ECA (reference :203-219), same as nets/retinaface_r.py's."""
 
 
-class RetinaFace(nn.Module):
+class RetinaFace(HipModule):
     def __init__(self, cfg=None, pretrained=False, mode="train"):
         super().__init__()
         if cfg["name"] != "Resnet50":
@@ -68,8 +69,6 @@ class RetinaFace(nn.Module):
         self.eca_fpn = eca_block(256)
         self.mode = mode
         self.cfg = cfg
-        self._engine = None
 
     def forward(self, inputs):
-        from jabd_amd.engine import get_engine
-        return get_engine(self, "r50").forward(inputs)
+        return retinaface_forward(self, "r50", inputs)

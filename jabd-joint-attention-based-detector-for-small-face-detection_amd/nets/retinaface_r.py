@@ -1,52 +1,93 @@
 """JABD-MobileNetV3 RetinaFace — drop-in for the reference
-nets/retinaface_r.py:17-343 (same class names, constructor signature and
-state_dict keys).  `RetinaFace.forward(x[B,3,H,W] fp32 GPU)` runs the whole
-detector as one fused HIP plan (jabd_amd/engine.py) and returns
-(loc [B,A,4], conf [B,A,2] (softmaxed iff mode != 'train'), landm [B,A,10]).
+nets/retinaface_r.py:17-343 (same class names, constructor signatures and
+state_dict keys).
+
+`RetinaFace.forward(x[B,3,H,W] fp32 GPU)` runs the whole detector as one fused
+HIP plan (jabd_amd/engine.py in eval mode, jabd_amd/train.py's autograd graph
+in training mode) and returns (loc [B,A,4], conf [B,A,2] (softmaxed iff
+mode != 'train'), landm [B,A,10]).  Every other class here also has a forward
+of its own over libjabd kernels (jabd_amd/modules.py), so a script that
+composes them itself — as train_mobilenetV3_ecagai.py:319-435 does — runs on
+the same kernels.
 """
 import math
 
 import torch
 import torch.nn as nn
 
+from jabd_amd import modules as M
+from jabd_amd import train as T
+from jabd_amd.engine import nlm_weights, retinaface_forward
+from jabd_amd.functional import nlm_fused
+from jabd_amd.hipmodule import HipModule
 from nets._getter import IntermediateLayerGetter
-from nets.layers import SSH, conv_bn, conv_bn1X1, conv_bn_no_relu  # noqa: F401
+from nets.layers import SSH, conv_bn, conv_bn1X1, conv_bn_no_relu, fpn_forward  # noqa: F401
 from nets.mobilenetV3 import MobileNetV3_Large_eca
 
 
-class ClassHead(nn.Module):
+class _Head1x1(HipModule):
+    """1x1 conv (with bias) -> permute(0,2,3,1) -> view(B, -1, k): the NHWC
+    conv output already is the permuted tensor (no copy)."""
+    k = 1
+
+    def forward(self, x):
+        xh = M.nhwc(x, f"{type(self).__name__} input")
+        with M._Mode(self):
+            if self.training:
+                y = T.ConvFn.apply(xh, self.conv1x1.weight, self.conv1x1.bias, 1, 0, False)
+            else:
+                pk = self._jabd_cached(x.device, lambda: M.F.pack_conv(self.conv1x1))
+                y = M.F.conv(xh, pk)
+        return y.view(y.shape[0], -1, self.k)
+
+
+class ClassHead(_Head1x1):
+    k = 2
+
     def __init__(self, inchannels=512, num_anchors=2):
         super().__init__()
         self.num_anchors = num_anchors
-        self.conv1x1 = nn.Conv2d(inchannels, num_anchors * 2, kernel_size=(1, 1), stride=1,
-                                 padding=0)
+        self.conv1x1 = M.Conv2d(inchannels, num_anchors * 2, kernel_size=(1, 1), stride=1,
+                                padding=0)
 
 
-class BboxHead(nn.Module):
+class BboxHead(_Head1x1):
+    k = 4
+
     def __init__(self, inchannels=512, num_anchors=2):
         super().__init__()
-        self.conv1x1 = nn.Conv2d(inchannels, num_anchors * 4, kernel_size=(1, 1), stride=1,
-                                 padding=0)
+        self.conv1x1 = M.Conv2d(inchannels, num_anchors * 4, kernel_size=(1, 1), stride=1,
+                                padding=0)
 
 
-class LandmarkHead(nn.Module):
+class LandmarkHead(_Head1x1):
+    k = 10
+
     def __init__(self, inchannels=512, num_anchors=2):
         super().__init__()
-        self.conv1x1 = nn.Conv2d(inchannels, num_anchors * 10, kernel_size=(1, 1), stride=1,
-                                 padding=0)
+        self.conv1x1 = M.Conv2d(inchannels, num_anchors * 10, kernel_size=(1, 1), stride=1,
+                                padding=0)
 
 
-class PSPModule(nn.Module):
-    """Adaptive-average pools at `sizes`, concatenated (reference :85-104)."""
+class PSPModule(HipModule):
+    """Adaptive-average pools at `sizes`, concatenated: [n, c, S] (reference :85-104)."""
 
     def __init__(self, sizes=(1, 3, 6, 8), dimension=2):
         super().__init__()
+        if dimension != 2:
+            raise NotImplementedError("PSPModule: the 2-D pools are the ones JABD uses")
         self.sizes = tuple(sizes)
-        self.stages = nn.ModuleList([nn.AdaptiveAvgPool2d((s, s)) for s in sizes])
+        self.stages = nn.ModuleList([M.AdaptiveAvgPool2d((s, s)) for s in sizes])
+
+    def forward(self, feats):
+        with M._Mode(self):
+            out = M.AdaptivePoolFn.apply(M.nhwc(feats, "PSPModule input"), self.sizes)
+        return out.permute(0, 2, 1)
 
 
-class NLM(nn.Module):
-    """PSP-pooled non-local block, the CSAF attention (reference :107-152)."""
+class NLM(HipModule):
+    """PSP-pooled non-local block, the CSAF attention (reference :107-152):
+    x + W(softmax(q(x) . psp(k(x))) . psp(v(x)))."""
 
     def __init__(self, in_channels, scale=1, psp_size=(1, 4, 8, 12), ch=4):
         super().__init__()
@@ -54,16 +95,26 @@ class NLM(nn.Module):
             raise NotImplementedError("NLM scale > 1 is not used by any JABD model")
         self.scale, self.in_channels, self.ch = scale, in_channels, ch
         self.pool = nn.MaxPool2d(kernel_size=(scale, scale))
-        self.f_query = nn.Conv2d(in_channels, ch, kernel_size=1)
-        self.f_key = nn.Conv2d(in_channels, ch, kernel_size=1)
-        self.f_value = nn.Conv2d(in_channels, ch, kernel_size=1)
+        self.f_query = M.Conv2d(in_channels, ch, kernel_size=1)
+        self.f_key = M.Conv2d(in_channels, ch, kernel_size=1)
+        self.f_value = M.Conv2d(in_channels, ch, kernel_size=1)
         self.psp = PSPModule(psp_size)
-        self.W = nn.Conv2d(ch, in_channels, kernel_size=1)
+        self.W = M.Conv2d(ch, in_channels, kernel_size=1)
         nn.init.constant_(self.W.weight, 0)
         nn.init.constant_(self.W.bias, 0)
 
+    def forward(self, x):
+        xh = M.nhwc(x, "NLM input").contiguous()
+        if self.training:
+            return M.nchw(T.nlm_train(self, xh))
+        w = self._jabd_cached(x.device, lambda: nlm_weights(self))
+        with torch.no_grad():
+            return M.nchw(nlm_fused(xh, None, w, self.psp.sizes))
 
-class FPN(nn.Module):
+
+class FPN(HipModule):
+    """Laterals, nearest up-sample -> shared NLM -> add, merges (reference :154-207)."""
+
     def __init__(self, in_channels_list, out_channels):
         super().__init__()
         self.leaky = 0.1 if out_channels <= 64 else 0.0
@@ -74,22 +125,30 @@ class FPN(nn.Module):
         self.merge2 = conv_bn(out_channels, out_channels, leaky=self.leaky)
         self.nlm = NLM(40)
 
+    def forward(self, inputs):
+        return fpn_forward(self, inputs, self.nlm)
 
-class eca_block(nn.Module):
-    """Head ECA with a Sigmoid gate (reference :208-224)."""
+
+class eca_block(HipModule):
+    """Head ECA with a Sigmoid gate (reference :208-224): x * sigmoid(conv1d(GAP(x)))."""
     gate = "sigmoid"
 
     def __init__(self, channel, b=1, gamma=2):
         super().__init__()
         k = int(abs((math.log(channel, 2) + b) / gamma))
         k = k if k % 2 else k + 1
-        self.avg_pool = nn.AdaptiveAvgPool2d(1)
+        self.avg_pool = M.AdaptiveAvgPool2d(1)
         self.conv = nn.Conv1d(1, 1, kernel_size=k, padding=(k - 1) // 2, bias=False)
-        self.sigmoid = nn.Sigmoid()
-        self.Hsigmoid = nn.Hardsigmoid()
+        self.sigmoid = M.Sigmoid()
+        self.Hsigmoid = M.Hardsigmoid()
+
+    def forward(self, x):
+        with M._Mode(self):
+            return M.nchw(M.EcaScaleFn.apply(M.nhwc(x, "eca_block input").contiguous(),
+                                             self.conv.weight, self.gate))
 
 
-class RetinaFace(nn.Module):
+class RetinaFace(HipModule):
     def __init__(self, cfg=None, pretrained=False, mode="train"):
         super().__init__()
         if cfg["name"] != "mobilenet0.25":
@@ -114,8 +173,6 @@ class RetinaFace(nn.Module):
         self.eca_fpn = eca_block(40)
         self.mode = mode
         self.cfg = cfg
-        self._engine = None
 
     def forward(self, inputs):
-        from jabd_amd.engine import get_engine
-        return get_engine(self, "mnv3").forward(inputs)
+        return retinaface_forward(self, "mnv3", inputs)

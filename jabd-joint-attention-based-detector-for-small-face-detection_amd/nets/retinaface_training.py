@@ -5,10 +5,13 @@ nets/retinaface_training.py:1-323.
 the device: one batched match/encode kernel for all images (replacing the
 reference's per-image Python loop and host round trips, :201-227), then the
 loss kernel with on-device hard-negative mining, and a backward kernel wired
-through autograd.  Under torch.distributed the positive counts that
-normalise the loss are all-reduced so the gradient equals the reference's
-DataParallel gradient of the global-batch loss.
+through autograd.  In jabd_amd.parallel's data-parallel step the positive
+counts that normalise the loss are all-reduced (MultiBoxLoss.global_counts)
+so the summed gradient equals the reference's DataParallel gradient of the
+global-batch loss.
 """
+import contextlib
+
 import torch
 import torch.nn as nn
 
@@ -20,9 +23,9 @@ class _MultiBoxLossFn(torch.autograd.Function):
     def forward(ctx, loc, conf, landm, loc_t, conf_t, landm_t, neg_pos, group, diou=None):
         sums, counts, sel = ops.multibox_sums(loc, conf, landm, loc_t, conf_t, landm_t, neg_pos,
                                               diou)
-        if group is not None:
+        if group is not None:  # (process group,) — see MultiBoxLoss.global_counts
             import torch.distributed as dist
-            dist.all_reduce(counts, group=group)
+            dist.all_reduce(counts, group=group[0])
         loss = ops.multibox_normalize(sums, counts)
         ctx.save_for_backward(loc, conf, landm, loc_t, conf_t, landm_t, sel, counts)
         ctx.diou = diou
@@ -55,8 +58,16 @@ def log_sum_exp(x):
 
 
 class MultiBoxLoss(nn.Module):
-    def __init__(self, num_classes, overlap_thresh, neg_pos, variance, cuda=True,
-                 process_group="auto"):
+    """nets/retinaface_training.py:165-303.  Normalisers are this call's own
+    positive counts, as the reference's.  Under one-process-per-GPU data
+    parallelism with SUM-reduced gradients (jabd_amd.parallel.train_step), the
+    counts must be the global batch's: that step enters
+    `with criterion.global_counts(True, group):` and the counts are
+    all-reduced before normalising.  (Never enable it under DDP, which
+    averages gradients: the global normaliser would then shrink the gradient
+    by the world size.)"""
+
+    def __init__(self, num_classes, overlap_thresh, neg_pos, variance, cuda=True):
         super().__init__()
         if num_classes != 2:
             raise ValueError("the JABD loss kernel is built for 2 classes (face/background)")
@@ -65,15 +76,16 @@ class MultiBoxLoss(nn.Module):
         self.negpos_ratio = neg_pos
         self.variance = variance
         self.cuda = cuda
-        self.process_group = process_group
+        self._count_group = None   # (group,) while global_counts is active
 
-    def _group(self):
-        if self.process_group != "auto":
-            return self.process_group
-        import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            return dist.group.WORLD
-        return None
+    @contextlib.contextmanager
+    def global_counts(self, enabled=True, group=None):
+        prev = self._count_group
+        self._count_group = (group,) if enabled else None
+        try:
+            yield self
+        finally:
+            self._count_group = prev
 
     def forward(self, predictions, priors, targets):
         loc_data, conf_data, landm_data = predictions
@@ -83,7 +95,7 @@ class MultiBoxLoss(nn.Module):
             loc_t, conf_t, landm_t = ops.match_encode(tg, priors, self.threshold, self.variance)
         return _MultiBoxLossFn.apply(loc_data.contiguous(), conf_data.contiguous(),
                                      landm_data.contiguous(), loc_t, conf_t, landm_t,
-                                     int(self.negpos_ratio), self._group())
+                                     int(self.negpos_ratio), self._count_group)
 
 
 def weights_init(net, init_type="normal", init_gain=0.02):

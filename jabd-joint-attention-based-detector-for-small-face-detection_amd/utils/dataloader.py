@@ -83,3 +83,105 @@ def get_random_data(image, targets, input_shape, jitter=.3, hue=.1, sat=1.5, val
     out = ops.augment(img, input_shape, p["nw"], p["nh"], p["dx"], p["dy"], p["flip"],
                       p["hue"], p["sat"], p["val"])
     return out, remap_targets(targets, iw, ih, input_shape, p)
+
+
+def _annotations(labels):
+    """WIDER label rows -> [n, 15] targets (utils/dataloader.py:27-58): corners,
+    the five landmark points (columns 4,5,7,8,10,11,13,14,16,17), label -1
+    when the first landmark is missing (< 0), else 1."""
+    ann = np.zeros((0, 15))
+    for label in labels:
+        a = np.zeros((1, 15))
+        a[0, 0], a[0, 1] = label[0], label[1]
+        a[0, 2], a[0, 3] = label[0] + label[2], label[1] + label[3]
+        for k, col in enumerate((4, 5, 7, 8, 10, 11, 13, 14, 16, 17)):
+            a[0, 4 + k] = label[col]
+        a[0, 14] = -1 if a[0, 4] < 0 else 1
+        ann = np.append(ann, a, axis=0)
+    return ann
+
+
+def process_labels(txt_path):
+    """WIDER `label.txt` -> (image paths, per-image label rows) (:151-174)."""
+    imgs_path, words, labels = [], [], []
+    first = True
+    with open(txt_path, "r") as f:
+        for line in f.readlines():
+            line = line.rstrip()
+            if line.startswith("#"):
+                if first:
+                    first = False
+                else:
+                    words.append(labels.copy())
+                    labels.clear()
+                imgs_path.append(txt_path.replace("label.txt", "images/") + line[2:])
+            else:
+                labels.append([float(x) for x in line.split(" ")])
+    words.append(labels)
+    return imgs_path, words
+
+
+class DataGenerator(torch.utils.data.Dataset):
+    """Drop-in for the reference DataGenerator (utils/dataloader.py:8-69): WIDER
+    label parsing on the host, the augmentation's pixel work on the device
+    (get_random_data above).
+
+    output="numpy" (default) returns the image as the reference does (a
+    float32 CHW numpy array, what fit_one_epoch's torch.from_numpy expects);
+    output="device" keeps it on the GPU (no round trip; detection_collate then
+    stacks device tensors).  The device work cannot run in forked DataLoader
+    workers (HIP is not fork-safe): use num_workers=0 — one image costs
+    ~30 us on the device, so workers buy nothing."""
+
+    def __init__(self, txt_path, img_size, output="numpy", device="cuda"):
+        if output not in ("numpy", "device"):
+            raise ValueError("output must be 'numpy' or 'device'")
+        self.img_size = img_size
+        self.txt_path = txt_path
+        self.output = output
+        self.device = device
+        self.imgs_path, self.words = process_labels(txt_path)
+
+    def __len__(self):
+        return len(self.imgs_path)
+
+    def get_len(self):
+        return len(self.imgs_path)
+
+    def __getitem__(self, index):
+        if torch.utils.data.get_worker_info() is not None:
+            raise RuntimeError("DataGenerator runs its augmentation on the HIP device, which "
+                               "forked DataLoader workers cannot use: pass num_workers=0")
+        from PIL import Image
+        img = Image.open(self.imgs_path[index]).convert("RGB")
+        labels = self.words[index]
+        if len(labels) == 0:
+            return img, np.zeros((0, 15))
+        out, target = get_random_data(img, _annotations(labels), [self.img_size, self.img_size],
+                                      device=self.device)
+        if self.output == "numpy":
+            out = out.cpu().numpy()
+        return out, target
+
+    def rand(self, a=0, b=1):
+        return _rand(a, b)
+
+    def get_random_data(self, image, targets, input_shape, jitter=.3, hue=.1, sat=1.5, val=1.5):
+        return get_random_data(image, targets, input_shape, jitter, hue, sat, val, self.device)
+
+    def process_labels(self):
+        return process_labels(self.txt_path)
+
+
+def detection_collate(batch):
+    """Drop images without targets and stack (:177-186): numpy images as the
+    reference does, device tensors with torch.stack."""
+    images, targets = [], []
+    for img, box in batch:
+        if len(box) == 0:
+            continue
+        images.append(img)
+        targets.append(box)
+    if images and isinstance(images[0], torch.Tensor):
+        return torch.stack(images), targets
+    return np.array(images), targets

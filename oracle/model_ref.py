@@ -150,15 +150,20 @@ def conv_bn_act(ctx, x, pre, leaky, padding=0, act=True):
     return F.leaky_relu(y, leaky) if act else y
 
 
-def fpn(ctx, feats, leaky, nlm_name):
-    """FPN.forward (nets/retinaface_r.py:169-207)."""
-    o1 = conv_bn_act(ctx, feats[0], "fpn.output1", leaky)
-    o2 = conv_bn_act(ctx, feats[1], "fpn.output2", leaky)
-    o3 = conv_bn_act(ctx, feats[2], "fpn.output3", leaky)
+def fpn(ctx, feats, leaky, nlm_name, pre="fpn.", sizes=(1, 4, 8, 12)):
+    """FPN.forward (nets/retinaface_r.py:169-207); nlm_name=None is the plain
+    FPN of nets/layers.py:83-119 (up-sample + add, no NLM)."""
+    o1 = conv_bn_act(ctx, feats[0], pre + "output1", leaky)
+    o2 = conv_bn_act(ctx, feats[1], pre + "output2", leaky)
+    o3 = conv_bn_act(ctx, feats[2], pre + "output3", leaky)
     up3 = F.interpolate(o3, size=[o2.shape[2], o2.shape[3]], mode="nearest")
-    o2 = conv_bn_act(ctx, o2 + nlm(ctx, up3, nlm_name), "fpn.merge2", leaky, 1)
+    if nlm_name is not None:
+        up3 = nlm(ctx, up3, nlm_name, sizes)
+    o2 = conv_bn_act(ctx, o2 + up3, pre + "merge2", leaky, 1)
     up2 = F.interpolate(o2, size=[o1.shape[2], o1.shape[3]], mode="nearest")
-    o1 = conv_bn_act(ctx, o1 + nlm(ctx, up2, nlm_name), "fpn.merge1", leaky, 1)
+    if nlm_name is not None:
+        up2 = nlm(ctx, up2, nlm_name, sizes)
+    o1 = conv_bn_act(ctx, o1 + up2, pre + "merge1", leaky, 1)
     return [o1, o2, o3]
 
 
@@ -208,3 +213,102 @@ def retinaface_r50(P, x, mode="eval", train_bn=False):
     f = fpn(ctx, feats, 0.0, "fpn.Nlm.")
     f = [ssh(ctx, eca(ctx, f[i], "eca_fpn", "sigmoid"), f"ssh{i + 1}.", 0.0) for i in range(3)]
     return heads(ctx, f, mode)
+
+
+# ----------------------------------------------------------------------------- module-level
+# restatements for the module surface (nets/* forwards run one by one)
+def se(ctx, x, pre):
+    """SeModule.forward (nets/mobilenetV3.py:18-32): x * hsigmoid(conv(relu(bn(conv(GAP(x))))))."""
+    y = F.adaptive_avg_pool2d(x, 1)
+    y = F.relu(ctx.bn(ctx.conv(y, pre + "se.1"), pre + "se.2"))
+    y = F.hardsigmoid(ctx.conv(y, pre + "se.4"))
+    return x * y
+
+
+def stdv_eca(ctx, x, pre):
+    """eca_block_G.forward (nets/mobilenetV3.py:350-377): population std over H*W
+    (mean_channels / stdv_channels), Conv1d over channels, Hardsigmoid, x*y."""
+    w = ctx.P[pre + "conv.weight"]
+    k = w.shape[-1]
+    mean = x.sum(3, keepdim=True).sum(2, keepdim=True) / (x.shape[2] * x.shape[3])
+    var = (x - mean).pow(2).sum(3, keepdim=True).sum(2, keepdim=True) / (x.shape[2] * x.shape[3])
+    y = var.pow(0.5)
+    y = F.conv1d(y.squeeze(-1).transpose(-1, -2), w, padding=(k - 1) // 2)
+    y = F.hardsigmoid(y.transpose(-1, -2).unsqueeze(-1))
+    return x * y
+
+
+def block(ctx, x, pre, spec, gate="eca"):
+    """Block (gate "se"/"none", nets/mobilenetV3.py:35-91), Block_eca ("eca",
+    :94-150), Block_eca_G ("beca", :152-208)."""
+    if gate == "eca":
+        return block_eca(ctx, x, pre, spec)
+    k, cin, exp, cout, act, _se, stride = spec
+    out = _act(ctx.bn(ctx.conv(x, pre + "conv1"), pre + "bn1"), act)
+    out = _act(ctx.bn(ctx.conv(out, pre + "conv2", stride, k // 2, exp), pre + "bn2"), act)
+    if gate == "se":
+        out = se(ctx, out, pre + "se.")
+    elif gate == "beca":
+        out = stdv_eca(ctx, out, pre + "eca.")
+    out = ctx.bn(ctx.conv(out, pre + "conv3"), pre + "bn3")
+    skip = x
+    if stride == 1 and cin != cout:
+        skip = ctx.bn(ctx.conv(x, pre + "skip.0"), pre + "skip.1")
+    elif stride == 2 and cin != cout:
+        s = ctx.bn(ctx.conv(x, pre + "skip.0", 2, 1, cin), pre + "skip.1")
+        skip = ctx.bn(ctx.conv(s, pre + "skip.2"), pre + "skip.3")
+    elif stride == 2:
+        skip = ctx.bn(ctx.conv(x, pre + "skip.0", 2, 1, cin), pre + "skip.1")
+    return _act(out + skip, act)
+
+
+def bn1d(ctx, x, name):
+    P = ctx.P
+    return F.batch_norm(x, P[name + ".running_mean"], P[name + ".running_var"],
+                        P[name + ".weight"], P[name + ".bias"], ctx.train, ctx.momentum, ctx.eps)
+
+
+def mobilenetv3(P, x, stages, train_bn=False):
+    """MobileNetV3_{Small,Large,Large_eca,...}.forward (nets/mobilenetV3.py:257-265,
+    510-522): stem, stages = [(prefix, [(spec, gate), ...]), ...], conv2+bn2+hs,
+    GAP, linear3+bn3+hs (dropout: identity in eval), linear4."""
+    ctx = Ctx(P, train_bn)
+    x = F.hardswish(ctx.bn(ctx.conv(x, "conv1", 2, 1), "bn1"))
+    for pre, blocks in stages:
+        for bi, (spec, gate) in enumerate(blocks):
+            x = block(ctx, x, f"{pre}.{bi}.", spec, gate)
+    x = F.hardswish(ctx.bn(ctx.conv(x, "conv2"), "bn2"))
+    x = F.adaptive_avg_pool2d(x, 1).flatten(1)
+    x = F.hardswish(bn1d(ctx, F.linear(x, P["linear3.weight"]), "bn3"))
+    return F.linear(x, P["linear4.weight"], P["linear4.bias"])
+
+
+def mobilenetv1_stage(ctx, x, pre, specs):
+    """conv_bn / conv_dw Sequentials (nets/mobilenet025.py:3-19): specs =
+    [(kind, cin, cout, stride), ...]."""
+    for i, (kind, cin, cout, stride) in enumerate(specs):
+        p = f"{pre}.{i}."
+        if kind == "bn":
+            x = F.leaky_relu(ctx.bn(ctx.conv(x, p + "0", stride, 1), p + "1"), 0.1)
+        else:
+            x = F.leaky_relu(ctx.bn(ctx.conv(x, p + "0", stride, 1, cin), p + "1"), 0.1)
+            x = F.leaky_relu(ctx.bn(ctx.conv(x, p + "3"), p + "4"), 0.1)
+    return x
+
+
+MNV1_STAGES = [
+    [("bn", 3, 8, 2), ("dw", 8, 16, 1), ("dw", 16, 32, 2), ("dw", 32, 32, 1),
+     ("dw", 32, 64, 2), ("dw", 64, 64, 1)],
+    [("dw", 64, 128, 2)] + [("dw", 128, 128, 1)] * 5,
+    [("dw", 128, 256, 2), ("dw", 256, 256, 1)],
+]
+
+
+def resnet_classifier(P, x, layers=R50_LAYERS, train_bn=False):
+    """ResNet._forward_impl (nets/resnet_pytorch_r.py:232-250) for Bottleneck nets."""
+    ctx = Ctx(P, train_bn)
+    P2 = {("body." + k): v for k, v in P.items()}
+    c = Ctx(P2, train_bn)
+    feats = r50_body(c, x)
+    x = F.adaptive_avg_pool2d(feats[-1], 1).flatten(1)
+    return F.linear(x, ctx.P["fc.weight"], ctx.P["fc.bias"])

@@ -61,3 +61,53 @@ def test_grad_allreduce_and_buffers_gloo():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def _overlap_worker(rank, world, port, q):
+    """Two real backward passes through GradAllReduce(overlap=True): step 1 is
+    synchronous and installs the hooks, step 2 all-reduces from the hooks
+    during backward.  Both must equal the sum of the per-rank gradients."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from jabd_amd.parallel import GradAllReduce
+        torch.manual_seed(0)
+        m = torch.nn.Sequential(torch.nn.Linear(8, 64), torch.nn.ReLU(), torch.nn.Linear(64, 64),
+                                torch.nn.ReLU(), torch.nn.Linear(64, 3))
+        unused = torch.nn.Linear(3, 3)  # parameters that never get a gradient
+        m.add_module("unused", unused)
+        red = GradAllReduce(m, bucket_bytes=4096)  # several buckets
+        ok = True
+        for step in range(3):
+            x = torch.randn(5, 8, generator=torch.Generator().manual_seed(10 * step + rank))
+            m.zero_grad()
+            m[4](m[3](m[2](m[1](m[0](x))))).square().sum().backward()
+            mine = [p.grad.clone() for p in m.parameters() if p.grad is not None]
+            allg = [torch.zeros_like(t) for t in mine]
+            for t, a in zip(mine, allg):  # reference: explicit sum of both ranks' grads
+                lst = [torch.zeros_like(t) for _ in range(world)]
+                dist.all_gather(lst, t)
+                a.copy_(sum(lst))
+            red()
+            got = [p.grad for p in m.parameters() if p.grad is not None]
+            ok &= len(got) == 6 and all(torch.allclose(g, a, rtol=1e-6, atol=1e-6)
+                                         for g, a in zip(got, allg))
+            ok &= unused.weight.grad is None
+            ok &= (red.hooks != []) == (step >= 0)
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_overlap_hooks_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}
