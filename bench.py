@@ -164,6 +164,29 @@ def r50_roofline(device, size, batch=16, steps=3):
             "conv_ms_per_step": t_ms, "conv_gflop_per_step": flops / 1e9}
 
 
+def o1_activation_c2(device, x, steps, warmup):
+    """C2 images/s with weights that keep activations O(1) through the network."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _util import init_for_parity
+    from nets.retinaface_r import RetinaFace
+    from utils.config import cfg_mnet
+    m = init_for_parity(RetinaFace(cfg=cfg_mnet, mode="eval"), seed=1).eval().to(device)
+    with torch.no_grad():
+        for _ in range(warmup):
+            m(x)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            m(x)
+        torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    del m
+    torch.cuda.empty_cache()
+    return {"images_per_sec": x.shape[0] * steps / el, "ms_per_step": el / steps * 1e3,
+            "init": "tests/_util.py init_for_parity (conv weights N(0, 1/fan_in), BN running "
+                    "stats non-trivial)"}
+
+
 def forward_flops(model, size, batch):
     """Algorithmic FLOPs (2*MAC) of the whole forward, from the layer shapes."""
     from jabd_amd import functional as F
@@ -201,7 +224,13 @@ def forward_flops(model, size, batch):
     return tot[0]
 
 
+NMS_OPS_PER_PAIR = 13  # fp32 ops of one exact IoU test: 4 min/max, 2 sub, 2 clamp, mul, 2 add/sub, div, cmp
+
+
 def nms_bench(device, reps=5):
+    """C5: batched NMS over 8 x 100k clustered boxes (seed 99), boxes/s; the IoU
+    tests the mask producer made (kernel counters, jabd_nms_pair_stats) as
+    pairs/s against the VALU fp32 peak (the scan after it is latency-bound)."""
     from jabd_amd import ops, synth
     from oracle import box_ref
     B, n = 8, 100_000
@@ -212,14 +241,25 @@ def nms_bench(device, reps=5):
     torch.cuda.synchronize()
     ref0 = box_ref.nms(bx[0], sc[0], 0.3)
     exact = keep[0, : int(nk[0])].cpu().numpy().tolist() == ref0.tolist()
+    _, _, tested, dense = ops.batched_nms_stats(b, s, 0.3)
     t0 = time.perf_counter()
     for _ in range(reps):
         ops.batched_nms(b, s, 0.3)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
+    pairs = int(tested.sum())
+    pps = pairs / dt
     return {"config": "C5: 8 images x 100k clustered boxes, iou 0.3", "boxes_per_sec":
             B * n / dt, "ms_per_call": dt * 1e3, "kept_img0": int(nk[0]),
-            "bit_exact_img0_vs_oracle": bool(exact)}
+            "bit_exact_img0_vs_oracle": bool(exact),
+            "iou_pairs_tested_per_image": [int(v) for v in tested],
+            "dense_fallback_images": int(dense.sum()),
+            "all_pairs_per_image": n * (n - 1) // 2,
+            "iou_pairs_per_sec": pps, "ops_per_pair": NMS_OPS_PER_PAIR,
+            "valu_peak_tflops": PEAK_FP32_MFMA_TFLOPS,
+            "valu_frac": pps * NMS_OPS_PER_PAIR / (PEAK_FP32_MFMA_TFLOPS * 1e12),
+            "algorithmic_bytes": B * (20 * n + 8 * int(nk.sum()) // B),
+            "note": "bytes = 20 B read per box + 8 B per kept index; sort/scan passes extra"}
 
 
 def augment_bench(device, reps=20):
@@ -247,7 +287,7 @@ def augment_bench(device, reps=20):
             "algorithmic_bytes": nbytes, "achieved_gbs": nbytes / (ms * 1e-3) / 1e9}
 
 
-def train_bench(kind, batch, size, steps, warmup, device, dist, rank):
+def train_bench(kind, batch, size, steps, warmup, device, dist, rank, conv_roofline_steps=0):
     """steps timed training iterations (parallel.train_step) on this rank."""
     from jabd_amd import optim, parallel, synth
     from nets.retinaface_training import MultiBoxLoss, weights_init
@@ -278,6 +318,20 @@ def train_bench(kind, batch, size, steps, warmup, device, dist, rank):
     for _ in range(warmup):
         parallel.train_step(model, crit, opt, x, tg, pri, reducer=reducer)
     torch.cuda.synchronize()
+    conv = None
+    if conv_roofline_steps:
+        with TrainConvTimer() as tm:
+            for _ in range(conv_roofline_steps):
+                parallel.train_step(model, crit, opt, x, tg, pri, reducer=reducer)
+        c_ms, c_gf, c_n = tm.summary(conv_roofline_steps)
+        ach = c_gf / c_ms  # GFLOP/ms = TFLOP/s
+        conv = {"bound": "mfma", "kernel": f"training-step conv stack: forward, data-gradient "
+                f"and weight-gradient convolutions ({c_n} launches/step)",
+                "workload": f"{kind} training bs{batch} {size}x{size}", "achieved": ach,
+                "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                "frac": ach / PEAK_FP32_MFMA_TFLOPS, "conv_ms_per_step": c_ms,
+                "conv_gflop_per_step": c_gf}
+        torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -296,9 +350,59 @@ def train_bench(kind, batch, size, steps, warmup, device, dist, rank):
     mem = torch.cuda.max_memory_allocated(device) / 2**30
     del model, opt, x, tg
     torch.cuda.empty_cache()
-    return {"images_per_sec": batch * steps * world / el, "ms_per_step": el / steps * 1e3,
-            "per_gpu_batch": batch, "global_batch": batch * world, "image_size": size,
-            "steps": steps, "warmup": warmup, "loss_last": float(loss), "max_mem_gib": mem}
+    out = {"images_per_sec": batch * steps * world / el, "ms_per_step": el / steps * 1e3,
+           "per_gpu_batch": batch, "global_batch": batch * world, "image_size": size,
+           "steps": steps, "warmup": warmup, "loss_last": float(loss), "max_mem_gib": mem}
+    if conv is not None:
+        out["conv_roofline"] = conv
+    return out
+
+
+class TrainConvTimer:
+    """HIP events around every libjabd convolution call of a training step
+    (forward conv, data-gradient conv, weight-gradient kernel), on torch's
+    current stream (the launch stream); algorithmic FLOPs from the call's
+    jabd_conv_args: 2 * pixels * (KH*KW*Cin + Cin2) * Cout of the forward
+    convolution each call computes or differentiates."""
+    NAMES = ("jabd_conv2d_nhwc_f32", "jabd_conv_wgrad_f32")
+
+    def __init__(self):
+        self.recs = []
+
+    def __enter__(self):
+        from jabd_amd import functional, train, _lib
+        self.mods = (functional, train)
+        self.orig = _lib.call
+
+        def timed(name, *args):
+            if name not in self.NAMES:
+                return self.orig(name, *args)
+            a = args[0]._obj
+            if name == "jabd_conv_wgrad_f32" or not a.tconv:
+                px = a.B * a.OH * a.OW
+                flops = 2.0 * px * (a.KH * a.KW * a.Cin + a.Cin2) * a.Cout
+            else:  # data gradient of a stride-s conv: x = dY (H x W), out = dX
+                flops = 2.0 * a.B * a.H * a.W * a.KH * a.KW * a.Cin * a.Cout
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            r = self.orig(name, *args)
+            e1.record()
+            self.recs.append((e0, e1, flops))
+            return r
+        for m in self.mods:
+            m.call = timed
+        return self
+
+    def __exit__(self, *exc):
+        for m in self.mods:
+            m.call = self.orig
+
+    def summary(self, steps):
+        torch.cuda.synchronize()
+        ms = sum(a.elapsed_time(b) for a, b, _ in self.recs) / steps
+        gf = sum(f for _, _, f in self.recs) / steps / 1e9
+        return ms, gf, len(self.recs) // steps
 
 
 def pmc_traffic():
@@ -312,31 +416,89 @@ def pmc_traffic():
         return json.load(f)
 
 
+def host_cores():
+    """(threads this process may use, physical cores per lscpu)."""
+    import subprocess
+    phys = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        kv = dict(l.split(":", 1) for l in out.splitlines() if ":" in l)
+        phys = int(kv["Core(s) per socket"].strip()) * int(kv["Socket(s)"].strip())
+    except Exception:
+        pass
+    return torch.get_num_threads(), phys
+
+
+def _time_bounded(fn, seconds, min_iters=1):
+    fn()  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while n < min_iters or time.perf_counter() - t0 < seconds:
+        fn()
+        n += 1
+    return n, time.perf_counter() - t0
+
+
 def cpu_baseline(size, seconds):
-    from oracle import model_ref
+    """The oracle's PyTorch-CPU restatement timed on this host (rank 0, N=1):
+    headline leg C2 (MNv3 eval forward, bs1 1024^2) plus the legs BASELINE.md
+    plans — C1 end to end (640^2 bs1: preprocess, forward, decode, score
+    filter, torchvision-CPU NMS), C2/C3 forwards at bs4, C3 (R50) at bs1, and
+    C5's NMS over one 100k-box image (oracle/nms_ref.c) — each a bounded
+    sample of a few seconds."""
+    from oracle import box_ref, model_ref, prep_ref
     from nets.retinaface_r import RetinaFace
+    from nets.retinaface_eca_nonlocal import RetinaFace as R50
     from nets.retinaface_training import weights_init
-    from utils.config import cfg_mnet
+    from utils.config import cfg_mnet, cfg_re50
+    from jabd_amd import synth
     import contextlib
     import io
+    import numpy as np
+    threads, phys = host_cores()
     torch.manual_seed(0)
-    m = RetinaFace(cfg=cfg_mnet, mode="eval")
     with contextlib.redirect_stdout(io.StringIO()):
+        m = RetinaFace(cfg=cfg_mnet, mode="eval")
         weights_init(m)
+        r = R50(cfg=cfg_re50, mode="eval")
+        weights_init(r)
     sd = {k: v.float() for k, v in m.eval().state_dict().items()}
-    x = torch.randn(1, 3, size, size)
+    sdr = {k: v.float() for k, v in r.eval().state_dict().items()}
+    legs = {}
     with torch.no_grad():
-        model_ref.retinaface_mnv3(sd, x)  # warm-up
-        n, t0 = 0, time.perf_counter()
-        while True:
-            model_ref.retinaface_mnv3(sd, x)
-            n += 1
-            if time.perf_counter() - t0 > seconds:
-                break
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "images/sec", "cores": torch.get_num_threads(),
-            "kind": "port", "sample": f"{n} images, bs1 {size}x{size}, oracle "
-            "model_ref.retinaface_mnv3 (PyTorch-CPU fp32 restatement)"}
+        x1 = synth.images(1, size, seed=1234)
+        n, dt = _time_bounded(lambda: model_ref.retinaface_mnv3(sd, x1), seconds)
+        head = {"value": n / dt, "unit": "images/sec", "cores": threads,
+                "host_physical_cores": phys, "kind": "port",
+                "sample": f"{n} images, bs1 {size}x{size}, oracle model_ref.retinaface_mnv3 "
+                          "(PyTorch-CPU fp32 restatement)"}
+        x4 = synth.images(4, size, seed=1234)
+        n, dt = _time_bounded(lambda: model_ref.retinaface_mnv3(sd, x4), 3.0)
+        legs["C2_mnv3_bs4"] = {"images_per_sec": 4 * n / dt, "batches": n}
+        n, dt = _time_bounded(lambda: model_ref.retinaface_r50(sdr, x1), 3.0)
+        legs["C3_r50_bs1"] = {"images_per_sec": n / dt, "batches": n}
+        n, dt = _time_bounded(lambda: model_ref.retinaface_r50(sdr, x4), 3.0)
+        legs["C3_r50_bs4"] = {"images_per_sec": 4 * n / dt, "batches": n}
+        img = np.random.default_rng(640).integers(0, 256, (480, 640, 3)).astype(np.float32)
+        pri = box_ref.anchors(cfg_mnet, (640, 640))
+
+        def c1():
+            xx = torch.from_numpy(prep_ref.preprocess(img, (640, 640)))[None]
+            loc, conf, landm = model_ref.retinaface_mnv3(sd, xx, "eval")
+            det = torch.cat([box_ref.decode(loc[0], pri, cfg_mnet["variance"]), conf[0][:, 1:2],
+                             box_ref.decode_landm(landm[0], pri, cfg_mnet["variance"])], -1)
+            rows = box_ref.non_max_suppression(det, 0.5, 0.3)
+            if len(rows):
+                prep_ref.correct_rows(np.asarray(rows, np.float32), (640, 640), (480, 640))
+        n, dt = _time_bounded(c1, 3.0)
+        legs["C1_detect_image_640"] = {"images_per_sec": n / dt, "images": n,
+                                       "stages": "letterbox+preprocess, forward, decode, "
+                                                 ">=0.5 filter, NMS 0.3, correct_boxes"}
+    bx, sc = synth.nms_boxes(1, 100_000, seed=99)
+    n, dt = _time_bounded(lambda: box_ref.nms(bx[0], sc[0], 0.3), 1.0)
+    legs["C5_nms_100k"] = {"boxes_per_sec": 100_000 * n / dt, "images": n,
+                           "kind": "oracle/nms_ref.c (torchvision-CPU NMS restated in C), 1 thread"}
+    head["legs"] = legs
+    return head
 
 
 def main():
@@ -403,14 +565,19 @@ def main():
             "achieved_hbm_gbs": alg_bytes / (t_ms * 1e-3) / 1e9,
             "hbm_frac": alg_bytes / (t_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
             "conv_ms_per_step": t_ms, "conv_gflop_per_step": flops_step / 1e9}
+        # the same C2 step with O(1)-activation weights (tests/_util.py init):
+        # weights_init's N(0, 0.02) convs make deep activations vanish, and
+        # MFMA loops over near-zero data hold higher clocks (DVFS)
+        extra["c2_o1_activations"] = o1_activation_c2(device, x, args.steps, args.warmup)
         if world == 1 and args.r50_batch > 0:
-            extra["roofline_r50"] = r50_roofline(device, args.size)
+            extra["roofline_r50_eval"] = r50_roofline(device, args.size)
     if not args.no_train:
         tr = {"C4_mnv3": train_bench("mnv3", args.batch, args.size, args.train_steps, 3, device,
-                                     dist, rank)}
+                                     dist, rank, conv_roofline_steps=1 if rank == 0 else 0)}
         if world == 1 and args.r50_batch > 0:
             tr["C3_r50"] = train_bench("r50", args.r50_batch, args.size, max(2, args.train_steps // 2),
-                                       2, device, None, rank)
+                                       2, device, None, rank, conv_roofline_steps=1)
+            extra["roofline_r50"] = tr["C3_r50"].get("conv_roofline")
         extra["train"] = tr
     if rank == 0:
         extra["forward_gflop_per_image"] = forward_flops(model, args.size, 1) / 1e9

@@ -71,6 +71,14 @@ int jabd_batched_nms_f32(const float* boxes, int64_t box_stride,
                          int64_t* keep, int64_t* n_keep, void* ws,
                          size_t ws_bytes, jabd_stream_t stream);
 
+/* Measurement helper: after jabd_batched_nms_f32 with the same (batch, n,
+ * ws), copy to host arrays each image's number of exact IoU tests made by
+ * the grid producer (candidate pairs), its off-block suppressing pairs, and
+ * its producer (0 = grid, != 0 = dense: every pair tested).  Synchronises
+ * the stream; batch <= 254. */
+int jabd_nms_pair_stats(const void* ws, size_t ws_bytes, int64_t batch, int64_t n,
+                        int64_t* tested, int32_t* hits, int32_t* dense, jabd_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * predict.py:162-181 fused: decode + decode_landm + conf[:,1] + score filter
  * + NMS, for B images at once.  conf is the eval-mode softmax [B,A,2].

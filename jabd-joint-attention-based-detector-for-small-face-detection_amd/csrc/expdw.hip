@@ -45,7 +45,7 @@ struct XdCfg {
   static constexpr int IH = (TH - 1) * S + K, IW = (TW - 1) * S + K;
   static constexpr int IPX = IH * IW;
   static constexpr int IPAD = (IPX + 15) / 16 * 16;
-  static constexpr int XP = 20;      // staged-input pitch (16 channels + 4)
+  static constexpr int XP = 16;      // staged input: 4 quad planes of IPAD float4
   static constexpr int EP = EC + 4;  // expanded-tile pitch
   static constexpr int NPB = IPAD / 16, NNT = EC / 16, NBLK = NPB * NNT;
   static constexpr int BPW = (NBLK + 3) / 4;  // MFMA blocks per wave
@@ -57,19 +57,13 @@ struct XdCfg {
   static_assert(TW % PW == 0 && 256 % NC4 == 0, "tile shape");
   static_assert(LDS * 4 <= 160 * 1024, "LDS");
   static_assert((K * K + 1) * NC4 <= 256, "dw taps: one float4 per thread");
-  static_assert(64 % NC4 == 0, "channel quads must tile a wave");
+  static_assert(NC4 == 4 || NC4 == 8, "dw_lane: 16- or 32-channel chunks");
 };
 
-// Persistent: workgroup L walks work items i = L, L + G, ... (G = grid, a
-// multiple of 8, so every item of a WG stays on that WG's XCD).  Item i ->
-// (tile, EC-chunk) with the chunks of one tile on one XCD.  A work item is
-// Kc stages (16 input channels each); the global loads of the next stage
-// (possibly the next item's first) are issued into registers before the
-// current stage's MFMAs / depthwise phase, so HBM latency overlaps compute.
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() is also a
 // workgroup-scope fence on global memory, so the compiler drains every
 // outstanding global load (s_waitcnt vmcnt(0)) before it — which would
-// retire the next item's register prefetch at the first barrier after it is
+// retire an in-flight register prefetch at the first barrier after it is
 // issued.  The LDS ordering this kernel needs is just lgkmcnt(0) + s_barrier.
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -122,237 +116,40 @@ __device__ __forceinline__ bool xd_item(const jabd_expdw_args& p, int i, const X
   return true;
 }
 
-template <int K, int S, int TH, int TW, int EC, int ACT>
-__global__ __launch_bounds__(256, EC == 16 ? 3 : 2) void expdw_kernel(const jabd_expdw_args p, const XdDivs dv,
-                                                       int nitems) {
-  using C = XdCfg<K, S, TH, TW, EC>;
-  constexpr int NPF = (C::IPAD * 4 + 255) / 256;  // prefetched float4 per thread per stage
-  __shared__ __attribute__((aligned(16))) float lds[C::LDS];
-  __shared__ float4 wsh[K * K + 1][C::NC4];  // this chunk's dw taps + bias (row K*K)
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, j = lane & 15, g = lane >> 4;
-  const f32x4* wpk = reinterpret_cast<const f32x4*>(p.we);
-  const int G = gridDim.x;
-
-  // tiles that straddle the 8-aligned tile padding are skipped: advance to
-  // the next real item (uniform per workgroup)
-  auto next_item = [&](int i, XdItem& it) -> int {
-    while (i < nitems && !xd_item<K, S, TH, TW, EC>(p, i, dv, nitems, it))
-      i += G;
-    return i;
-  };
-  float4 pf[NPF];
-  // this thread's (tile row, tile col) of each prefetch slot; rr = -1 marks
-  // padding slots.  The channel quad (t & 3) is the same for every slot.
-  int pr[NPF], pc[NPF];
-#pragma unroll
-  for (int u = 0; u < NPF; ++u) {
-    const int px = (u * 256 + t) >> 2;
-    pr[u] = px < C::IPX ? px / C::IW : -1;
-    pc[u] = px < C::IPX ? px - (px / C::IW) * C::IW : 0;
-  }
-  const int cq = (t & 3) * 4;
-  const int c4 = t % C::NC4, chl = 4 * c4;
-  // expand-GEMM channel block of this wave (blk = wave + 4u -> nt = blk % NNT)
-  const int ntw = wave % C::NNT;
-  constexpr int NWD = (K * K + 1) * C::NC4;  // dw taps + bias float4 of one chunk
-  // Register prefetch of everything a stage / item reads from global memory:
-  // input pixels (pf), this wave's packed expand weights (pa), and at an
-  // item's first stage its expand bias (pbi) and dw taps (pwd), so no global
-  // load latency is exposed between the barriers of an item.
-  f32x4 pa_n = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float4 pbi_n = make_float4(0.f, 0.f, 0.f, 0.f), pwd_n = pbi_n;
-  auto prefetch = [&](const XdItem& it, int kc) {
-    const float* xb = p.x + (int64_t)it.b * p.x_bs + 16 * kc + cq;
-    const bool cv = 16 * kc + cq < p.Cin;
-#pragma unroll
-    for (int u = 0; u < NPF; ++u) {
-      const int ih = it.ih0 + pr[u], iw = it.iw0 + pc[u];
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (cv && pr[u] >= 0 && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W)
-        v = *reinterpret_cast<const float4*>(xb + (ih * p.W + iw) * p.x_ps);
-      pf[u] = v;
-    }
-    const int nt = it.c0 / 16 + ntw;
-    if (nt < p.Ntiles) pa_n = wpk[(kc * p.Ntiles + nt) * 64 + lane];
-    if (kc == 0) {
-      const int ch = it.c0 + 16 * ntw + 4 * g;
-      if (ch < p.E) pbi_n = *reinterpret_cast<const float4*>(p.be + ch);
-      if (t < NWD) {
-        const int tp = t / C::NC4, cc = it.c0 + 4 * (t - tp * C::NC4);
-        pwd_n = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (cc < p.E)
-          pwd_n = *reinterpret_cast<const float4*>((tp < K * K ? p.wd + tp * p.E : p.bd) + cc);
-      }
-    }
-  };
-
-  XdItem cur, nxt;
-  int ci_idx = next_item(blockIdx.x, cur);
-  if (ci_idx >= nitems) return;
-  prefetch(cur, 0);
-  float4 pbi = pbi_n, pwd = pwd_n;
-
-  while (true) {
-    f32x4 acc[C::BPW];
-#pragma unroll
-    for (int u = 0; u < C::BPW; ++u) acc[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int nt0 = cur.c0 / 16;
-    int nx_idx = -1;
-    for (int kc = 0; kc < p.Kc; ++kc) {
-      // regs -> LDS (this stage's input channels)
-#pragma unroll
-      for (int u = 0; u < NPF; ++u) {
-        const int idx = u * 256 + t;
-        if (idx < C::IPAD * 4)
-          *reinterpret_cast<float4*>(lds + (idx >> 2) * C::XP + (idx & 3) * 4) = pf[u];
-      }
-      const f32x4 a = pa_n;
-      lds_barrier();
-      // issue the next stage's loads
-      if (kc + 1 < p.Kc) {
-        prefetch(cur, kc + 1);
-      } else {
-        nx_idx = next_item(ci_idx + G, nxt);
-        if (nx_idx < nitems) prefetch(nxt, 0);
-      }
-      if (nt0 + ntw < p.Ntiles) {
-#pragma unroll
-        for (int u = 0; u < C::BPW; ++u) {
-          const int blk = wave + 4 * u;
-          if (blk < C::NBLK) {
-            const int pb = blk / C::NNT;
-            const f32x4 bv =
-                *reinterpret_cast<const f32x4*>(lds + (pb * 16 + j) * C::XP + 4 * g);
-            acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bv.x, acc[u], 0, 0, 0);
-            acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bv.y, acc[u], 0, 0, 0);
-            acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bv.z, acc[u], 0, 0, 0);
-            acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bv.w, acc[u], 0, 0, 0);
-          }
-        }
-      }
-      lds_barrier();
-    }
-    // acc[u][r] = expanded channel 16nt + 4g + r of tile pixel 16pb + j
-#pragma unroll
-    for (int u = 0; u < C::BPW; ++u) {
-      const int blk = wave + 4 * u;
-      if (blk < C::NBLK) {
-        const int pb = blk / C::NNT, nt = blk - pb * C::NNT;
-        const int px = pb * 16 + j, ch = 16 * nt + 4 * g;
-        float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (px < C::IPX && cur.c0 + ch < p.E) {
-          const int r = px / C::IW, cc = px - r * C::IW;
-          const int ih = cur.ih0 + r, iw = cur.iw0 + cc;
-          if (ih >= 0 && ih < p.H && iw >= 0 && iw < p.W) {
-            const float4 bi = pbi;  // ch = 16*ntw + 4g for every block of this wave
-            o.x = xd_act<ACT>(acc[u][0] + bi.x);
-            o.y = xd_act<ACT>(acc[u][1] + bi.y);
-            o.z = xd_act<ACT>(acc[u][2] + bi.z);
-            o.w = xd_act<ACT>(acc[u][3] + bi.w);
-          }
-        }
-        *reinterpret_cast<float4*>(lds + px * C::EP + ch) = o;
-      }
-    }
-    if (t < NWD) wsh[t / C::NC4][t % C::NC4] = pwd;
-    lds_barrier();
-
-    // depthwise phase
-    const bool chv = cur.c0 + chl < p.E;
-    float4 psum = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (chv) {
-      const float4 bias2 = wsh[K * K][c4];
-      float* yb = p.y + (int64_t)cur.b * p.y_bs + cur.c0 + chl;
-#pragma unroll 1
-      for (int itm = t; itm < C::ITEMS; itm += 256) {
-        const int strip = itm / C::NC4;
-        const int orow = strip / C::NSTRIP, st = strip - orow * C::NSTRIP;
-        const int oh = cur.oh0 + orow, owb = cur.ow0 + st * C::PW;
-        if (oh >= p.OH || owb >= p.OW) continue;
-        float4 a2[C::PW];
-#pragma unroll
-        for (int o = 0; o < C::PW; ++o) a2[o] = bias2;
-#pragma unroll 1
-        for (int kh = 0; kh < K; ++kh) {
-          const float* rowp = lds + ((orow * S + kh) * C::IW + st * C::PW * S) * C::EP + chl;
-          float4 row[C::SPAN];
-#pragma unroll
-          for (int c = 0; c < C::SPAN; ++c)
-            row[c] = *reinterpret_cast<const float4*>(rowp + c * C::EP);
-          float4 wk[K];
-#pragma unroll
-          for (int kw = 0; kw < K; ++kw) wk[kw] = wsh[kh * K + kw][c4];
-#pragma unroll
-          for (int o = 0; o < C::PW; ++o)
-#pragma unroll
-            for (int kw = 0; kw < K; ++kw) {
-              const float4 xv = row[o * S + kw], wv = wk[kw];
-              a2[o].x = fmaf(xv.x, wv.x, a2[o].x);
-              a2[o].y = fmaf(xv.y, wv.y, a2[o].y);
-              a2[o].z = fmaf(xv.z, wv.z, a2[o].z);
-              a2[o].w = fmaf(xv.w, wv.w, a2[o].w);
-            }
-        }
-#pragma unroll
-        for (int o = 0; o < C::PW; ++o) {
-          if (owb + o >= p.OW) break;
-          float4 v;
-          v.x = xd_act<ACT>(a2[o].x);
-          v.y = xd_act<ACT>(a2[o].y);
-          v.z = xd_act<ACT>(a2[o].z);
-          v.w = xd_act<ACT>(a2[o].w);
-          *reinterpret_cast<float4*>(yb + ((int64_t)oh * p.OW + owb + o) * p.y_ps) = v;
-          psum.x += v.x; psum.y += v.y; psum.z += v.z; psum.w += v.w;
-        }
-      }
-    }
-    if (p.part) {
-      // threads with the same channel quad sit at lanes c4, c4 + NC4, ...:
-      // butterfly over the lane bits above log2(NC4) (fixed order), then
-      // combine the 4 waves' results in LDS
-#pragma unroll
-      for (int off = C::NC4; off < 64; off <<= 1) {
-        psum.x += __shfl_xor(psum.x, off);
-        psum.y += __shfl_xor(psum.y, off);
-        psum.z += __shfl_xor(psum.z, off);
-        psum.w += __shfl_xor(psum.w, off);
-      }
-      lds_barrier();
-      float4* red = reinterpret_cast<float4*>(lds);
-      if (lane < C::NC4) red[wave * C::NC4 + lane] = psum;
-      lds_barrier();
-      if (t < C::NC4 && cur.c0 + 4 * t < p.E) {
-        const float4 a0 = red[t], a1 = red[C::NC4 + t], a2 = red[2 * C::NC4 + t],
-                     a3 = red[3 * C::NC4 + t];
-        float4 sm;
-        sm.x = (a0.x + a1.x) + (a2.x + a3.x);
-        sm.y = (a0.y + a1.y) + (a2.y + a3.y);
-        sm.z = (a0.z + a1.z) + (a2.z + a3.z);
-        sm.w = (a0.w + a1.w) + (a2.w + a3.w);
-        *reinterpret_cast<float4*>(p.part + ((int64_t)cur.b * (int)dv.tiles_img.d + cur.t_in) * p.E +
-                                   cur.c0 + 4 * t) = sm;
-      }
-    }
-    lds_barrier();  // LDS (Es / red) free for the next item's staging
-    if (nx_idx >= nitems) break;
-    cur = nxt;
-    ci_idx = nx_idx;
-    pbi = pbi_n;
-    pwd = pwd_n;
+// ---------------------------------------------------------------------------
+// One workgroup per work item (tile x EC-chunk), no state carried across
+// items (a persistent cross-item-prefetch form measured 5-30% slower on every
+// layer: SGPR spills, loop-carried operand copies).  The item is decoded
+// once; loads go through a buffer descriptor whose range check zeroes
+// out-of-image pixels (no branch per load); the expanded tile is built with
+// selects.  Latency hiding comes from the resident workgroups.
+//
+// LDS layouts (bank rules: MI355X_MICROARCH.md §LDS), all conflict-free:
+//  * staged input, channel-quad-major Xs[q][px][4] (q = 4 channels of the
+//    16-channel stage): an MFMA B read (pixel j, quad g per lane) hits slot
+//    px mod 16 in every ds_read_b128 lane group, and the stage stores (8
+//    contiguous lanes = 8 consecutive pixels of one quad) hit 8 distinct slots;
+//  * expanded tile [px][EC + 4]: the epilogue's 8-lane store groups are
+//    consecutive pixels (odd pitch in slots); the depthwise reads assign
+//    lanes to (strip, channel quad) so that each ds_read_b128 lane group
+//    reads 4 strips of one output row x 4 channel quads (dw_lane()).
+// ---------------------------------------------------------------------------
+// Depthwise-phase lane assignment.  The four ds_read_b128 lane groups are the
+// lane quads q = (l >> 2) & 7 of even popcount {0,3,5,6} and odd popcount
+// {1,2,4,7}, in each 32-lane half.  EC = 32 (8 channel quads): the parity
+// picks channel quads 0-3 / 4-7 and q >> 1 the strip; EC = 16: the group
+// picks the strip row.  Returns (channel quad, strip within the wave's slice).
+template <int NC4>
+__device__ __forceinline__ void dw_lane(int l, int& c4, int& sl) {
+  const int h = l >> 5, q = (l >> 2) & 7, par = __builtin_popcount(q) & 1, k = q >> 1;
+  if (NC4 == 8) {
+    c4 = (l & 3) + 4 * par;
+    sl = 4 * h + k;
+  } else {
+    c4 = l & 3;
+    sl = 4 * (2 * h + par) + k;
   }
 }
-
-
-// ---------------------------------------------------------------------------
-// Non-persistent form: one workgroup per work item (tile x EC-chunk), no
-// state carried across items.  The persistent kernel above spends ~1100
-// instructions per item-wave (SGPR spills to VGPR lanes, loop-carried copies
-// of the prefetched operands, a branch per epilogue block); this one decodes
-// its item once, loads through a buffer descriptor whose range check zeroes
-// out-of-image pixels (no branch per load), and builds the expanded tile with
-// selects.  Latency hiding comes from the resident workgroups instead of a
-// cross-item register prefetch.
-// ---------------------------------------------------------------------------
 template <int K, int S, int TH, int TW, int EC, int ACT, int KP>
 __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p, const XdDivs dv,
                                                        int nitems) {
@@ -388,7 +185,9 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
   // voffset 0xFFFFFFF0 and reads zeros (host: x < 4 GiB)
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(p.x), (short)0, (int)(uint32_t)((int64_t)p.B * p.x_bs * 4), 0x00020000);
-  const int cq = (t & 3) * 4;
+  // stage slot u of this thread: pixel u*64 + (t>>6)*16 + (t&15), channel quad (t>>4)&3
+  const int cq = ((t >> 4) & 3) * 4;
+  const int spx0 = (t >> 6) * 16 + (t & 15);
   // KP-deep register ring of input stages: stage kc + KP is issued as soon
   // as stage kc has been written to LDS, and the raw LDS barriers below keep
   // it in flight across the MFMA phase (a __syncthreads() would drain it).
@@ -399,7 +198,7 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
     const bool cok = cofs < p.Cin;
 #pragma unroll
     for (int u = 0; u < NPF; ++u) {
-      const int px = (u * 256 + t) >> 2;
+      const int px = u * 64 + spx0;
       const int r = px / C::IW, c = px - r * C::IW;
       const int ih = it.ih0 + r, iw = it.iw0 + c;
       const bool ok = px < C::IPX && cok &&
@@ -424,9 +223,8 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
       f32x4 a = wpk[(kc * p.Ntiles + ntc) * 64 + lane];
 #pragma unroll
       for (int u = 0; u < NPF; ++u) {
-        const int idx = u * 256 + t;
-        if (idx < C::IPAD * 4)
-          *reinterpret_cast<float4*>(lds + (idx >> 2) * C::XP + (idx & 3) * 4) = pf[s][u];
+        if (u * 64 + spx0 < C::IPAD)
+          *reinterpret_cast<float4*>(lds + (cq / 4 * C::IPAD + u * 64 + spx0) * 4) = pf[s][u];
       }
       // retire the weight load here, before the next stage's loads are in
       // flight: the compiler's vmcnt tracking cannot count through the
@@ -444,7 +242,7 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
           const int blk = wave + 4 * u;
           if (blk < C::NBLK) {
             const int pb = blk / C::NNT;
-            const f32x4 bv = *reinterpret_cast<const f32x4*>(lds + (pb * 16 + j) * C::XP + 4 * g);
+            const f32x4 bv = *reinterpret_cast<const f32x4*>(lds + (g * C::IPAD + pb * 16 + j) * 4);
             acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bv.x, acc[u], 0, 0, 0);
             acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bv.y, acc[u], 0, 0, 0);
             acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bv.z, acc[u], 0, 0, 0);
@@ -496,15 +294,19 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
   __syncthreads();
 
   // depthwise phase
-  const int c4 = t % C::NC4, chl = 4 * c4;
+  int c4, sl;
+  dw_lane<C::NC4>(lane, c4, sl);
+  const int chl = 4 * c4;
   const bool chv = it.c0 + chl < p.E;
+  constexpr int SPW = 64 / C::NC4;  // strips per wave per pass
   float4 psum = make_float4(0.f, 0.f, 0.f, 0.f);
   if (chv) {
     const float4 bias2 = wsh[K * K][c4];
     float* yb = p.y + (int64_t)it.b * p.y_bs + it.c0 + chl;
 #pragma unroll 1
-    for (int itm = t; itm < C::ITEMS; itm += 256) {
-      const int strip = itm / C::NC4;
+    for (int pass = 0; pass * 256 < C::ITEMS; ++pass) {
+      const int strip = (pass * 4 + wave) * SPW + sl;
+      if (strip >= TH * C::NSTRIP) break;
       const int orow = strip / C::NSTRIP, st = strip - orow * C::NSTRIP;
       const int oh = it.oh0 + orow, owb = it.ow0 + st * C::PW;
       if (oh >= p.OH || owb >= p.OW) continue;
@@ -546,8 +348,15 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
     }
   }
   if (p.part) {
+    // sum the lanes holding the same channel quad (dw_lane): EC = 32 -> lane
+    // xor 12, 20 (the even-popcount quad permutations) and 32; EC = 16 ->
+    // xor 4, 8, 16, 32.  Fixed order: deterministic.  Lanes 0..NC4-1 then
+    // hold channel quads 0..NC4-1.
+    constexpr int NX = C::NC4 == 8 ? 3 : 4;
+    constexpr int X8[3] = {12, 20, 32}, X4[4] = {4, 8, 16, 32};
 #pragma unroll
-    for (int off = C::NC4; off < 64; off <<= 1) {
+    for (int r = 0; r < NX; ++r) {
+      const int off = C::NC4 == 8 ? X8[r] : X4[r];
       psum.x += __shfl_xor(psum.x, off);
       psum.y += __shfl_xor(psum.y, off);
       psum.z += __shfl_xor(psum.z, off);
@@ -572,22 +381,6 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
 }
 
 
-static int64_t xd_grid(const void* fn, int64_t nitems) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cus = 256;
-  }
-  int per = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 256, 0) != hipSuccess || per < 1)
-    per = 1;
-  int64_t grid = (int64_t)per * cus / 8 * 8;
-  if (grid < 8) grid = 8;
-  return grid < nitems ? grid : nitems;  // nitems is a multiple of 8
-}
-
 struct XdTile {
   int th, tw;
 };
@@ -600,15 +393,6 @@ static XdTile xd_tile(int k, int s) {
 }  // namespace jabd
 
 using namespace jabd;
-
-static int xd_version() {
-  static int xdv = -1;  // JABD_EXPDW_V=1: the persistent kernel (A/B), else workgroup-per-item
-  if (xdv < 0) {
-    const char* e = getenv("JABD_EXPDW_V");
-    xdv = e && e[0] == '1' ? 1 : 2;
-  }
-  return xdv;
-}
 
 // JABD_EXPDW_KP=2|3: input register ring depth (A/B).  Default 1: deeper
 // rings measured 0-7% slower (b3/b4/b11/b12 in tools/convbench.py --set xd),
@@ -662,26 +446,19 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
   hipStream_t st = as_stream(stream);
   const XdDivs dv{make_fastdiv((uint32_t)nch), make_fastdiv((uint32_t)tiles_img),
                   make_fastdiv((uint32_t)tiles_w)};
-  // persistent grid = the workgroups that are resident at once (a multiple of
-  // 8 for XCD-stable item ownership; any more would run as a late tail)
-  const bool v2 = xd_version() != 1 && (int64_t)a.B * a.x_bs * 4 < ((int64_t)1 << 32) - 16;
+  JABD_REQUIRE((int64_t)a.B * a.x_bs * 4 < ((int64_t)1 << 32) - 16,
+               "expand_dw: input must be < 4 GiB (buffer-descriptor offsets)");
 #define XD_LAUNCH(K_, S_, TH_, TW_, EC_, ACT_)                                                \
   do {                                                                                        \
-    if (v2) {                                                                                 \
-      if (a.Kc == 1 || xd_kp() == 1)                                                          \
-        expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1><<<(unsigned)nitems, 256, 0, st>>>(     \
-            a, dv, (int)nitems);                                                              \
-      else if (a.Kc == 2 || xd_kp() == 2)                                                     \
-        expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 2><<<(unsigned)nitems, 256, 0, st>>>(     \
-            a, dv, (int)nitems);                                                              \
-      else                                                                                    \
-        expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 3><<<(unsigned)nitems, 256, 0, st>>>(     \
-            a, dv, (int)nitems);                                                              \
-      break;                                                                                  \
-    }                                                                                         \
-    const int64_t grid = xd_grid((const void*)expdw_kernel<K_, S_, TH_, TW_, EC_, ACT_>, nitems); \
-    expdw_kernel<K_, S_, TH_, TW_, EC_, ACT_><<<(unsigned)grid, 256, 0, st>>>(a, dv,         \
-                                                                             (int)nitems);    \
+    if (a.Kc == 1 || xd_kp() == 1)                                                            \
+      expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1><<<(unsigned)nitems, 256, 0, st>>>(       \
+          a, dv, (int)nitems);                                                                \
+    else if (a.Kc == 2 || xd_kp() == 2)                                                       \
+      expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 2><<<(unsigned)nitems, 256, 0, st>>>(       \
+          a, dv, (int)nitems);                                                                \
+    else                                                                                      \
+      expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 3><<<(unsigned)nitems, 256, 0, st>>>(       \
+          a, dv, (int)nitems);                                                                \
   } while (0)
 #define XD_CASE(K_, S_, TH_, TW_, EC_)                                    \
   if (a.k == K_ && a.stride == S_ && EC == EC_) {                         \

@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <vector>
 
 #include "common.h"
 #include "nms_internal.h"
@@ -375,7 +376,7 @@ __global__ __launch_bounds__(256) void grid_pairs(
     float inv_w, float fcell, const unsigned* __restrict__ ext, const int* __restrict__ nact,
     double thr, int64_t cap, int* __restrict__ dense, uint64_t* __restrict__ diag,
     int* __restrict__ npairs, int* __restrict__ rowcnt, int* __restrict__ prow,
-    int* __restrict__ pcol, int* __restrict__ pslot) {
+    int* __restrict__ pcol, int* __restrict__ pslot, unsigned long long* __restrict__ tested) {
   const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
   if (p >= total) return;
@@ -442,6 +443,7 @@ __global__ __launch_bounds__(256) void grid_pairs(
   // own class, then the forward half of the neighbour classes:
   // (0, 1..kK) and (1..kK, -kK..kK)
   constexpr int NNB = kK + kK * (2 * kK + 1);
+  unsigned ntest = 0;
   for (int nbr = 0; nbr <= NNB; ++nbr) {
     int cw2, ch2;
     if (nbr <= kK) {
@@ -464,6 +466,7 @@ __global__ __launch_bounds__(256) void grid_pairs(
         const int j = sval[q];
         // same class: each pair once, from the lower rank
         bool hit = !(nbr == 0 && j <= i);
+        ntest += hit;
         if (hit) hit = iou_gt(bi.x, bi.y, bi.z, bi.w, ai, gbox[q], garea[q], thr, thrf, true);
         if (hit) {
           const int row = i < j ? i : j, col = i < j ? j : i;
@@ -485,6 +488,9 @@ __global__ __launch_bounds__(256) void grid_pairs(
     }
   }
   flush();
+  // per-lane counter slots (64 per image): a single address per image would
+  // serialise ~100k L2 atomics; lanes that returned early take no part
+  if (ntest) atomicAdd(&tested[(int64_t)b * 64 + lane], (unsigned long long)ntest);
 }
 
 // CSR of each row's off-block columns: csr[rowoff[row] + slot] = col.
@@ -636,6 +642,7 @@ struct NmsWs {
   // grid path
   unsigned* ext;
   int *dense, *nact, *npairs, *gval_in, *gval_out, *rowcnt, *rowoff, *prow, *pcol, *pslot, *csr;
+  unsigned long long* tested;  // grid candidates IoU-tested per image (measurement)
   float4* gbox;
   float* garea;
   int64_t cap;
@@ -669,6 +676,7 @@ static void carve_nms(A& a, int64_t batch, int64_t n, NmsWs* w) {
   T(int, bc, dense);
   T(int, bc, nact);
   T(int, bc, npairs);
+  T(unsigned long long, bc * 64, tested);
   T(int, bc * n, gval_in);
   T(int, bc * n, gval_out);
   T(int, bc * n, rowcnt);
@@ -746,6 +754,7 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
       JABD_HIP(hipMemsetAsync(w.dense, 0, sizeof(int) * bc, st));
       JABD_HIP(hipMemsetAsync(w.nact, 0, sizeof(int) * bc, st));
       JABD_HIP(hipMemsetAsync(w.npairs, 0, sizeof(int) * bc, st));
+      JABD_HIP(hipMemsetAsync(w.tested, 0, sizeof(unsigned long long) * bc * 64, st));
       JABD_HIP(hipMemsetAsync(w.ext, 0, sizeof(unsigned) * bc * 2 * kNC, st));
       JABD_HIP(hipMemsetAsync(w.diag, 0, sizeof(uint64_t) * bc * n, st));
       JABD_HIP(hipMemsetAsync(w.rowcnt, 0, sizeof(int) * bc * n, st));
@@ -761,7 +770,8 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
       if (int e = check_launch("grid_gather")) return e;
       grid_pairs<<<(unsigned)cdiv((int64_t)bc * n, 256), 256, 0, st>>>(
           w.kout, w.gval_out, (int64_t)bc * n, w.gbox, w.garea, n, bc, inv_w, fcell, w.ext, w.nact,
-          iou_thr, w.cap, w.dense, w.diag, w.npairs, w.rowcnt, w.prow, w.pcol, w.pslot);
+          iou_thr, w.cap, w.dense, w.diag, w.npairs, w.rowcnt, w.prow, w.pcol, w.pslot,
+          w.tested);
       if (int e = check_launch("grid_pairs")) return e;
       JABD_HIP(hipcub::DeviceScan::ExclusiveSum(w.tmp, w.tmp_bytes, w.rowcnt, w.rowoff,
                                                 (int)(bc * n), st));
@@ -810,4 +820,34 @@ extern "C" int jabd_batched_nms_f32(const float* boxes, int64_t box_stride,
   return jabd::nms_core(boxes, box_stride, box_bstride, scores, score_stride, score_bstride,
                         n_valid, batch, n, iou_threshold, score_threshold, keep, n_keep, ws,
                         ws_bytes, jabd::as_stream(stream));
+}
+
+// Measurement helper (bench.py's IoU-pair count): after jabd_batched_nms_f32
+// with this (batch, n, ws), copy each image's number of exact IoU tests of the
+// grid producer (candidate pairs), its off-block suppressing pairs, and the
+// producer (0 = grid, != 0 = dense: that image tested every pair) to the host.
+// Synchronises `stream`.  Valid for batch <= 254 (one pass holds every image).
+extern "C" int jabd_nms_pair_stats(const void* ws, size_t ws_bytes, int64_t batch, int64_t n,
+                                   int64_t* tested, int32_t* hits, int32_t* dense,
+                                   jabd_stream_t stream) {
+  using namespace jabd;
+  JABD_REQUIRE(ws && tested && hits && dense && batch > 0 && n > 0, "nms_pair_stats: bad args");
+  JABD_REQUIRE(images_per_pass(batch, n) == batch, "nms_pair_stats: batch spans several passes");
+  Carve cv(const_cast<void*>(ws), ws_bytes);
+  NmsWs w;
+  carve_nms(cv, batch, n, &w);
+  JABD_REQUIRE(cv.ok(), "nms_pair_stats: workspace too small");
+  hipStream_t st = as_stream(stream);
+  std::vector<unsigned long long> slots((size_t)batch * 64);
+  JABD_HIP(hipMemcpyAsync(slots.data(), w.tested, sizeof(unsigned long long) * batch * 64,
+                          hipMemcpyDeviceToHost, st));
+  JABD_HIP(hipMemcpyAsync(hits, w.npairs, sizeof(int32_t) * batch, hipMemcpyDeviceToHost, st));
+  JABD_HIP(hipMemcpyAsync(dense, w.dense, sizeof(int32_t) * batch, hipMemcpyDeviceToHost, st));
+  JABD_HIP(hipStreamSynchronize(st));
+  for (int64_t b = 0; b < batch; ++b) {
+    unsigned long long t = 0;
+    for (int l = 0; l < 64; ++l) t += slots[(size_t)b * 64 + l];
+    tested[b] = (int64_t)t;
+  }
+  return JABD_OK;
 }

@@ -91,6 +91,7 @@ SIGNATURES = {
     "jabd_nms_workspace_size": [c_i64, c_i64, c_sizep],
     "jabd_batched_nms_f32": [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
                              c_f64, c_f32, c_vp, c_vp, c_vp, c_size, c_vp],
+    "jabd_nms_pair_stats": [c_vp, c_size, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp],
     "jabd_detect_workspace_size": [c_i64, c_i64, c_sizep],
     "jabd_detect_f32": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f64,
                         c_vp, c_vp, c_vp, c_size, c_vp],

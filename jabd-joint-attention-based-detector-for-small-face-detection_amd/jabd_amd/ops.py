@@ -100,6 +100,31 @@ def batched_nms(boxes, scores, iou_threshold, score_threshold=-math.inf, n_valid
     return keep, n_keep
 
 
+def batched_nms_stats(boxes, scores, iou_threshold):
+    """batched_nms plus per-image measurement counters: (keep, n_keep,
+    tested int64[B], dense bool[B]) where `tested` is the number of exact
+    fp32 IoU evaluations the mask producer made (grid: its candidate pairs;
+    dense: every pair).  Synchronises (measurement only)."""
+    B, N = boxes.shape[0], boxes.shape[1]
+    dev = boxes.device
+    boxes = _dev("nms.boxes", boxes)
+    scores = _dev("nms.scores", scores)
+    keep = torch.empty((B, N), dtype=torch.int64, device=dev)
+    n_keep = torch.zeros((B,), dtype=torch.int64, device=dev)
+    ws = _ws(_size_query("jabd_nms_workspace_size", B, N), dev)
+    C = boxes.shape[-1]
+    call("jabd_batched_nms_f32", _p(boxes), C, N * C, _p(scores), 1, N, None, B, N,
+         float(iou_threshold), float(-math.inf), _p(keep), _p(n_keep), _p(ws), ws.numel(),
+         _stream())
+    tested = np.zeros(B, np.int64)
+    hits = np.zeros(B, np.int32)
+    dense = np.zeros(B, np.int32)
+    call("jabd_nms_pair_stats", _p(ws), ws.numel(), B, N, tested.ctypes.data, hits.ctypes.data,
+         dense.ctypes.data, _stream())
+    tested = np.where(dense != 0, N * (N - 1) // 2, tested)
+    return keep, n_keep, tested, dense != 0
+
+
 def nms(boxes, scores, iou_threshold):
     """torchvision.ops.nms(boxes[N,4], scores[N], iou_threshold) -> int64[K].
 
