@@ -16,7 +16,8 @@ import threading
 import torch  # noqa: F401  (load torch's HIP runtime first; see docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libjabd.so")
+# JABD_LIB: an alternative build of the same ABI (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("JABD_LIB") or os.path.join(_HERE, "libjabd.so")
 
 c_i64 = ctypes.c_int64
 c_int = ctypes.c_int
