@@ -183,6 +183,28 @@ int jabd_upsample_bicubic_ac_bwd_f32(const float* grad_y, int64_t batch, int H,
                                      int W, int C, float* grad_x, int OH, int OW,
                                      jabd_stream_t stream);
 
+/* General-width NLM attention core (the BECA variant's NLM(40): ch = 40, PSP
+ * (1,3,6,8), S = 110; train_mobilenetV3_ecagai.py:182-234, replacing its
+ * torch.matmul -> F.softmax -> torch.matmul at :220-226).  q [B, P, ch]
+ * (f_query of the up-sampled map, NHWC), kp / vp [B, S, ch] (f_key / f_value
+ * of the PSP-pooled rows).  Forward: ctx [B, P, ch] = softmax(q kp^T) vp and
+ * lse [B, P] (log-sum-exp per pixel; may be NULL for inference).  Backward
+ * from dctx: dq [B, P, ch], and pmat / dsmat [B, S, P] (softmax and its
+ * pre-softmax gradient, S-major) for dK = dsmat . q, dV = pmat . dctx.
+ * ch a multiple of 4 in 8..64; S * ch * 8 bytes must fit in LDS (160 KiB). */
+int jabd_nlm_attn_fwd_f32(const float* q, const float* kp, const float* vp, int32_t B,
+                          int32_t P, int32_t S, int32_t ch, float* ctx, float* lse,
+                          jabd_stream_t stream);
+int jabd_nlm_attn_bwd_f32(const float* q, const float* kp, const float* vp, const float* ctx,
+                          const float* lse, const float* dctx, int32_t B, int32_t P, int32_t S,
+                          int32_t ch, float* dq, float* pmat, float* dsmat,
+                          jabd_stream_t stream);
+/* y = a + b (+ c if non-NULL), n floats (n % 4 == 0, 16-byte aligned): the
+ * NLM residual + FPN lateral add of the bicubic variant
+ * (train_mobilenetV3_ecagai.py:233, 271). */
+int jabd_add3_f32(const float* a, const float* b, const float* c, int64_t n, float* y,
+                  jabd_stream_t stream);
+
 /* BECA gate — the contrast-ECA block of the bicubic variant
  * (train_mobilenetV3_ecagai.py:286-316): y = x * Hardsigmoid(conv1d_k(std_hw(x)))
  * on NHWC fp32 [batch, pixels, C]; w float[k] (k odd, no bias).  stats

@@ -117,6 +117,10 @@ SIGNATURES = {
     "jabd_upsample_bicubic_ac_f32": [c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_int, c_vp],
     "jabd_upsample_bicubic_ac_bwd_f32": [c_vp, c_i64, c_int, c_int, c_int, c_vp, c_int, c_int,
                                          c_vp],
+    "jabd_nlm_attn_fwd_f32": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],
+    "jabd_nlm_attn_bwd_f32": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32,
+                              c_vp, c_vp, c_vp, c_vp],
+    "jabd_add3_f32": [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
     "jabd_beca_fwd_f32": [c_vp, c_i64, c_i64, c_int, c_vp, c_int, c_vp, c_vp, c_vp],
     "jabd_beca_bwd_f32": [c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp,
                           c_vp],

@@ -15,6 +15,9 @@ forward as a fixed sequence of libjabd kernels on NHWC fp32 activations:
   RetinaFace-R50 (nets/retinaface_eca_nonlocal.py:314-359): 7x7 stem +
     maxpool, bottlenecks with the downsample folded into conv3's GEMM, then
     the same head.
+  MobileNetV3-BECA (train_mobilenetV3_ecagai.py:319-435): the MobileNetV3
+    plan with BECA gates (std pool + Hardsigmoid) on the head, bicubic
+    up-sampling and the ch=40 NLM in the FPN.
 
 There is no CPU path: inputs must be float32 tensors on the GPU.
 """
@@ -95,25 +98,62 @@ class SSHPack:
         return feat
 
 
+class NlmPack:
+    """Eval form of an NLM of any width (nets/retinaface_r.py:107-152;
+    train_mobilenetV3_ecagai.py:182-234 for ch=40).  ch=4: the fused
+    pool / apply kernels (head.hip).  Other widths: f_query as a 1x1 GEMM,
+    PSP pooling of x then f_key / f_value on the S pooled rows (pooling is
+    linear with unit-sum bins), the attention core (nlm_attn.hip), then W as a
+    1x1 GEMM with the residual x added in its epilogue."""
+
+    def __init__(self, nlm):
+        self.ch = nlm.ch
+        self.sizes = tuple(nlm.psp.sizes)
+        if self.ch == 4:
+            self.w = nlm_weights(nlm)
+        else:
+            self.q, self.k, self.v, self.W = (F.pack_conv(c) for c in
+                                              (nlm.f_query, nlm.f_key, nlm.f_value, nlm.W))
+
+    def forward(self, x, lateral=None):
+        """NLM(x) (+ lateral), NHWC."""
+        if self.ch == 4:
+            y = F.nlm_fused(x, None, self.w, self.sizes)
+            return F.add3(y, lateral, out=y) if lateral is not None else y
+        B, h, w, C = x.shape
+        S = sum(s * s for s in self.sizes)
+        q = F.conv(x, self.q)
+        pooled = F.adaptive_pool(x, self.sizes).view(B, S, 1, C)
+        kp = F.conv(pooled, self.k).view(B, S, self.ch)
+        vp = F.conv(pooled, self.v).view(B, S, self.ch)
+        y = F.conv(F.nlm_attn(q, kp, vp), self.W, res=x)
+        return F.add3(y, lateral, out=y) if lateral is not None else y
+
+
 class FPNPack:
     """Eval packs of an FPN (nets/retinaface_r.py:154-207 with NLM `nlm`,
-    nets/layers.py:70-119 with nlm=None): 1x1 laterals (+BN+leaky), nearest
-    up-sample (+NLM) + add, 3x3 merges."""
+    nets/layers.py:70-119 with nlm=None, train_mobilenetV3_ecagai.py:237-285
+    with bicubic up-sampling): 1x1 laterals (+BN+leaky), up-sample (+NLM) +
+    add, 3x3 merges."""
 
     def __init__(self, fpn, nlm):
         self.leaky = fpn.leaky
+        self.mode = getattr(fpn, "upsample_mode", "nearest")
         self.lat = [F.pack_conv(o[0], o[1]) for o in (fpn.output1, fpn.output2, fpn.output3)]
         self.merge1 = F.pack_conv(fpn.merge1[0], fpn.merge1[1])
         self.merge2 = F.pack_conv(fpn.merge2[0], fpn.merge2[1])
-        self.nlm_w = None
-        if nlm is not None:
-            self.nlm_sizes = tuple(nlm.psp.sizes)
-            self.nlm_w = nlm_weights(nlm)
+        self.nlm = NlmPack(nlm) if nlm is not None else None
 
     def _up(self, src, lateral):
-        if self.nlm_w is not None:
-            return F.nlm_fused(src, lateral, self.nlm_w, self.nlm_sizes)
-        return F.upsample_add(src, lateral)
+        _, h, w, _ = lateral.shape
+        if self.nlm is not None:
+            if self.mode == "nearest" and self.nlm.ch == 4:  # one fused kernel pair
+                return F.nlm_fused(src, lateral, self.nlm.w, self.nlm.sizes)
+            return self.nlm.forward(F.upsample(src, h, w, self.mode), lateral)
+        if self.mode == "nearest":
+            return F.upsample_add(src, lateral)
+        up = F.upsample(src, h, w, self.mode)
+        return F.add3(up, lateral, out=up)
 
     def forward(self, feats, scales=(None, None, None)):
         o1, o2, o3 = [F.conv(f, pk, act="leaky", slope=self.leaky, ascale=sc)
@@ -144,17 +184,23 @@ class _Head:
     The FPN and SSH packs are the modules' own cached packs (also used when
     those modules run standalone)."""
 
-    def __init__(self, m, eca_names, nlm_name, dev):
+    def __init__(self, m, eca_names, nlm_name, dev, gate="sigmoid"):
+        self.gate = gate  # "sigmoid": mean-pool ECA; "beca": std-pool + Hardsigmoid
         self.eca_in = [_w1d(getattr(m, n)) for n in eca_names]
         self.fpn = m.fpn._jabd_cached(dev, lambda: FPNPack(m.fpn, getattr(m.fpn, nlm_name)))
         self.eca_fpn = _w1d(m.eca_fpn)
         self.ssh = [s._jabd_cached(dev, lambda s=s: SSHPack(s)) for s in (m.ssh1, m.ssh2, m.ssh3)]
         self.heads = [heads_pack(m, i) for i in range(3)]
 
+    def _gate(self, f, w1d):
+        if self.gate == "beca":
+            from . import modules as M
+            return M.beca_gate(f, w1d)
+        return F.eca_gate(F.channel_sums(f), f.shape[1] * f.shape[2], w1d, "sigmoid")
+
     def forward(self, feats, softmax):
         B = feats[0].shape[0]
-        scales = [F.eca_gate(F.channel_sums(f), f.shape[1] * f.shape[2], w1d, "sigmoid")
-                  for f, w1d in zip(feats, self.eca_in)]
+        scales = [self._gate(f, w1d) for f, w1d in zip(feats, self.eca_in)]
         levels = self.fpn.forward(feats, scales)
         A = sum(2 * o.shape[1] * o.shape[2] for o in levels)
         dev = levels[0].device
@@ -164,7 +210,7 @@ class _Head:
         a_off = 0
         for i, o in enumerate(levels):
             _, h, w, C = o.shape
-            sc = F.eca_gate(F.channel_sums(o), h * w, self.eca_fpn, "sigmoid")
+            sc = self._gate(o, self.eca_fpn)
             feat = self.ssh[i].forward(o, sc)
             wt, bs = self.heads[i]
             F.heads(feat, wt, bs, loc, conf, landm, a_off, softmax)
@@ -272,7 +318,8 @@ class Engine:
                           * s_[None, :]).contiguous(), t_.detach().contiguous())
             self.layers = [[b._jabd_cached(dev, lambda b=b: _MNv3Block(b))
                             for b in getattr(m.body, f"layer{i}")] for i in (1, 2, 3)]
-            self.head = _Head(m, ("eca_40", "eca_80", "eca_160"), "nlm", dev)
+            self.head = _Head(m, ("eca_40", "eca_80", "eca_160"), "nlm", dev,
+                              gate=getattr(m, "head_gate", "sigmoid"))
         else:
             self.stem = F.pack_conv(m.body.conv1, m.body.bn1)
             self.layers = [[b._jabd_cached(dev, lambda b=b: _R50Block(b))

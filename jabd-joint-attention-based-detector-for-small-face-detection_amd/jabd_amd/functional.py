@@ -347,3 +347,52 @@ def heads(x, wt, bias, loc, conf, landm, a_off, softmax):
     call("jabd_heads_f32", x.data_ptr(), x.stride(0), C, B, H * W, C, wt.data_ptr(),
          bias.data_ptr(), A, a_off, 1 if softmax else 0, loc.data_ptr(), conf.data_ptr(),
          landm.data_ptr(), _stream())
+
+
+def adaptive_pool(x, sizes):
+    """cat over sizes of AdaptiveAvgPool2d((s, s)) of NHWC x -> [B, S, C]."""
+    B, H, W, C = x.shape
+    S = sum(s * s for s in sizes)
+    out = torch.empty((B, S, C), dtype=torch.float32, device=x.device)
+    arr = (ctypes.c_int32 * len(sizes))(*sizes)
+    call("jabd_adaptive_pool_f32", x.data_ptr(), x.stride(0), B, H, W, C, arr, len(sizes),
+         out.data_ptr(), _stream())
+    return out
+
+
+def upsample(src, h, w, mode):
+    """F.interpolate(src, size=(h, w), mode) on NHWC: 'nearest', or 'bicubic'
+    with align_corners=True (train_mobilenetV3_ecagai.py:270,279)."""
+    _check("upsample.src", src)
+    B, hs, ws, C = src.shape
+    out = torch.empty((B, h, w, C), dtype=torch.float32, device=src.device)
+    if mode == "nearest":
+        call("jabd_upsample_nearest_f32", src.data_ptr(), B, hs, ws, h, w, C, out.data_ptr(),
+             _stream())
+    elif mode == "bicubic":
+        call("jabd_upsample_bicubic_ac_f32", src.data_ptr(), B, hs, ws, C, out.data_ptr(), h, w,
+             _stream())
+    else:
+        raise NotImplementedError(f"up-sampling mode {mode!r}")
+    return out
+
+
+def nlm_attn(q, kp, vp, save=False):
+    """softmax(q . kp^T) . vp per pixel: q [B, h, w, ch], kp / vp [B, S, ch] ->
+    ctx [B, h, w, ch] (+ lse [B, h*w] when save)."""
+    B, h, w, ch = q.shape
+    S = kp.shape[1]
+    ctx = torch.empty_like(q)
+    lse = torch.empty((B, h * w), dtype=torch.float32, device=q.device) if save else None
+    call("jabd_nlm_attn_fwd_f32", q.data_ptr(), kp.data_ptr(), vp.data_ptr(), B, h * w, S, ch,
+         ctx.data_ptr(), _ptr(lse), _stream())
+    return (ctx, lse) if save else ctx
+
+
+def add3(a, b, c=None, out=None):
+    """a + b (+ c), same-shape dense tensors."""
+    if out is None:
+        out = torch.empty_like(a)
+    call("jabd_add3_f32", a.data_ptr(), b.data_ptr(), _ptr(c), a.numel(), out.data_ptr(),
+         _stream())
+    return out

@@ -13,6 +13,8 @@ kernels (fp32, NHWC):
   BnActFn     batch-stat BN + activation (+ the block's residual add)
   DwConvFn    depthwise conv; dgrad/wgrad kernels
   NlmFn       CSAF non-local block fused with the up-sample and lateral add
+  NlmAttnFn   attention core of the other NLM widths (ch=40, BECA variant)
+  UpsampleFn  nearest / bicubic(align_corners) up-sampling; Add3Fn adds
   SshTailFn   SSH's three BN branches written into one concatenated tensor
   HeadsFn     the three 1x1 heads of all levels -> (loc, conf, landm)
   MaxPoolFn   ResNet stem max pool
@@ -384,6 +386,75 @@ class UpAddFn(torch.autograd.Function):
         return dsrc, dout
 
 
+class UpsampleFn(torch.autograd.Function):
+    """F.interpolate(src, size, mode) on NHWC: nearest, or bicubic with
+    align_corners=True (train_mobilenetV3_ecagai.py:270,279)."""
+
+    @staticmethod
+    def forward(ctx, src, h, w, mode):
+        ctx.cfg = (tuple(src.shape), mode)
+        return F.upsample(src.contiguous(), h, w, mode)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (B, hs, ws, C), mode = ctx.cfg
+        dout = dout.contiguous()
+        _, h, w, _ = dout.shape
+        dsrc = torch.empty((B, hs, ws, C), dtype=torch.float32, device=dout.device)
+        if mode == "nearest":
+            call("jabd_upsample_nearest_bwd_f32", dout.data_ptr(), B, h, w, hs, ws, C, 0,
+                 dsrc.data_ptr(), _st())
+        else:
+            call("jabd_upsample_bicubic_ac_bwd_f32", dout.data_ptr(), B, hs, ws, C,
+                 dsrc.data_ptr(), h, w, _st())
+        return dsrc, None, None, None
+
+
+class Add3Fn(torch.autograd.Function):
+    """a + b (+ c) — the NLM residual and the FPN lateral add."""
+
+    @staticmethod
+    def forward(ctx, a, b, c):
+        ctx.has_c = c is not None
+        return F.add3(a.contiguous(), b.contiguous(), c.contiguous() if c is not None else None)
+
+    @staticmethod
+    def backward(ctx, d):
+        return d, d, (d if ctx.has_c else None)
+
+
+class NlmAttnFn(torch.autograd.Function):
+    """softmax(q . kp^T) . vp (train_mobilenetV3_ecagai.py:216-226) for NLM
+    widths other than 4: HIP forward (online softmax) and backward (dq in the
+    kernel; dK = dS . q and dV = P . dctx as per-image batched GEMMs)."""
+
+    @staticmethod
+    def forward(ctx, q, kp, vp):
+        q, kp, vp = q.contiguous(), kp.contiguous(), vp.contiguous()
+        out, lse = F.nlm_attn(q, kp, vp, save=True)
+        ctx.save_for_backward(q, kp, vp, out, lse)
+        return out
+
+    @staticmethod
+    def backward(ctx, dctx):
+        q, kp, vp, out, lse = ctx.saved_tensors
+        dctx = dctx.contiguous()
+        B, h, w, ch = q.shape
+        S = kp.shape[1]
+        P = h * w
+        dev = q.device
+        dq = torch.empty_like(q)
+        pm = torch.empty((B, S, P), dtype=torch.float32, device=dev)
+        dsm = torch.empty_like(pm)
+        call("jabd_nlm_attn_bwd_f32", q.data_ptr(), kp.data_ptr(), vp.data_ptr(), out.data_ptr(),
+             lse.data_ptr(), dctx.data_ptr(), B, P, S, ch, dq.data_ptr(), pm.data_ptr(),
+             dsm.data_ptr(), _st())
+        # [S x P] . [P x ch] per image: plain batched GEMMs (hipBLASLt)
+        dk = torch.bmm(dsm, q.view(B, P, ch))
+        dv = torch.bmm(pm, dctx.view(B, P, ch))
+        return dq, dk, dv
+
+
 class SshTailFn(torch.autograd.Function):
     """relu(cat(BN(a), BN(b), BN(c))) of SSH (nets/layers.py:56-68)."""
 
@@ -593,26 +664,64 @@ def _r50_block(blk, x):
 
 
 def nlm_train(nlm, src, lateral=None):
-    nw = (nlm.f_query.weight, nlm.f_query.bias, nlm.f_key.weight, nlm.f_key.bias,
-          nlm.f_value.weight, nlm.f_value.bias, nlm.W.weight, nlm.W.bias)
-    return NlmFn.apply(src, lateral, *nw, tuple(nlm.psp.sizes))
+    """ch=4: lateral + NLM(nearest(src)) fused (lateral=None: NLM(src)).
+    Other widths: lateral + NLM(src) composed from ConvFn / AdaptivePoolFn /
+    NlmAttnFn (src already at the output size)."""
+    if nlm.ch == 4:
+        nw = (nlm.f_query.weight, nlm.f_query.bias, nlm.f_key.weight, nlm.f_key.bias,
+              nlm.f_value.weight, nlm.f_value.bias, nlm.W.weight, nlm.W.bias)
+        return NlmFn.apply(src, lateral, *nw, tuple(nlm.psp.sizes))
+    from .modules import AdaptivePoolFn
+    x = src.contiguous()
+    B, h, w, C = x.shape
+    sizes = tuple(nlm.psp.sizes)
+    S = sum(s_ * s_ for s_ in sizes)
+    q = conv(x, nlm.f_query)
+    pooled = AdaptivePoolFn.apply(x, sizes).view(B, S, 1, C)
+    kp = conv(pooled, nlm.f_key).view(B, S, nlm.ch)
+    vp = conv(pooled, nlm.f_value).view(B, S, nlm.ch)
+    y = conv(NlmAttnFn.apply(q, kp, vp), nlm.W)
+    return Add3Fn.apply(y, x, lateral)
 
 
-def fpn_train(fpn, feats, nlm=None, eca_ws=None):
-    """FPN forward (nets/retinaface_r.py:169-207; nlm=None: nets/layers.py:83-119)
-    in training mode; eca_ws: the three input ECA Conv1d weights, applied on
-    the lateral convs' operand load (nets/retinaface_r.py:313-315)."""
+def fpn_up_train(fpn, nlm, src, lateral):
+    """lateral + [NLM](up(src -> lateral's size)) in training mode."""
+    mode = getattr(fpn, "upsample_mode", "nearest")
+    if nlm is None:
+        if mode == "nearest":
+            return UpAddFn.apply(src, lateral)
+        return Add3Fn.apply(UpsampleFn.apply(src, lateral.shape[1], lateral.shape[2], mode),
+                            lateral, None)
+    if mode == "nearest" and nlm.ch == 4:
+        return nlm_train(nlm, src, lateral)
+    up = UpsampleFn.apply(src, lateral.shape[1], lateral.shape[2], mode)
+    if nlm.ch == 4:
+        return Add3Fn.apply(nlm_train(nlm, up), lateral, None)
+    return nlm_train(nlm, up, lateral)
+
+
+def fpn_train(fpn, feats, nlm=None, eca_ws=None, gate="sigmoid"):
+    """FPN forward (nets/retinaface_r.py:169-207; nlm=None: nets/layers.py:83-119;
+    bicubic: train_mobilenetV3_ecagai.py:254-285) in training mode; eca_ws:
+    the three input ECA Conv1d weights — mean-pool ECA applied on the lateral
+    convs' operand load (nets/retinaface_r.py:313-315), or with gate="beca"
+    the std-pool BECA (train_mobilenetV3_ecagai.py:415-418)."""
     lk = fpn.leaky
     outs = (fpn.output1, fpn.output2, fpn.output3)
     lat = []
     for i, (f, o) in enumerate(zip(feats, outs)):
-        if eca_ws is not None:
+        if eca_ws is not None and gate == "beca":
+            from .ops import BecaFn
+            y = conv(BecaFn.apply(f, eca_ws[i].reshape(-1)), o[0])
+        elif eca_ws is not None:
             y = EcaConvFn.apply(f, eca_ws[i], o[0].weight, 1, 0, "sigmoid")
         else:
             y = conv(f, o[0])
         lat.append(bn_act(y, o[1], "leaky", lk))
     o1, o2, o3 = lat
-    up = (lambda s_, l_: nlm_train(nlm, s_, l_)) if nlm is not None else UpAddFn.apply
+
+    def up(s_, l_):
+        return fpn_up_train(fpn, nlm, s_, l_)
     o2 = bn_act(conv(up(o3, o2), fpn.merge2[0], 1, 1), fpn.merge2[1], "leaky", lk)
     o1 = bn_act(conv(up(o2, o1), fpn.merge1[0], 1, 1), fpn.merge1[1], "leaky", lk)
     return [o1, o2, o3]
@@ -675,10 +784,17 @@ def ssh_train(ssh, o, eca_w=None):
 
 
 def _head(m, feats, eca_names, nlm):
+    gate = getattr(m, "head_gate", "sigmoid")
     o1, o2, o3 = fpn_train(m.fpn, feats, nlm,
-                           [getattr(m, n).conv.weight for n in eca_names])
+                           [getattr(m, n).conv.weight for n in eca_names], gate)
     ew = m.eca_fpn.conv.weight
-    feats_out = [ssh_train(ssh, o, ew) for o, ssh in zip((o1, o2, o3), (m.ssh1, m.ssh2, m.ssh3))]
+    if gate == "beca":
+        from .ops import BecaFn
+        feats_out = [ssh_train(ssh, BecaFn.apply(o, ew.reshape(-1)))
+                     for o, ssh in zip((o1, o2, o3), (m.ssh1, m.ssh2, m.ssh3))]
+    else:
+        feats_out = [ssh_train(ssh, o, ew)
+                     for o, ssh in zip((o1, o2, o3), (m.ssh1, m.ssh2, m.ssh3))]
     wb = []
     for i in range(3):
         for h in (m.BboxHead[i], m.ClassHead[i], m.LandmarkHead[i]):

@@ -17,8 +17,7 @@ import torch.nn as nn
 
 from jabd_amd import modules as M
 from jabd_amd import train as T
-from jabd_amd.engine import nlm_weights, retinaface_forward
-from jabd_amd.functional import nlm_fused
+from jabd_amd.engine import NlmPack, retinaface_forward
 from jabd_amd.hipmodule import HipModule
 from nets._getter import IntermediateLayerGetter
 from nets.layers import SSH, conv_bn, conv_bn1X1, conv_bn_no_relu, fpn_forward  # noqa: F401
@@ -107,9 +106,9 @@ class NLM(HipModule):
         xh = M.nhwc(x, "NLM input").contiguous()
         if self.training:
             return M.nchw(T.nlm_train(self, xh))
-        w = self._jabd_cached(x.device, lambda: nlm_weights(self))
+        pk = self._jabd_cached(x.device, lambda: NlmPack(self))
         with torch.no_grad():
-            return M.nchw(nlm_fused(xh, None, w, self.psp.sizes))
+            return M.nchw(pk.forward(xh))
 
 
 class FPN(HipModule):

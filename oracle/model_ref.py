@@ -12,6 +12,8 @@ drives both this restatement and the product module.  Paths are relative to
   * RetinaFace-R50 + ECA + NLM — nets/retinaface_eca_nonlocal.py:235-359
     over torchvision.models.resnet50 (layout identical to
     nets/resnet_pytorch_r.py:87-303).
+  * JABD-MobileNetV3-BECA — train_mobilenetV3_ecagai.py:161-435 (defined
+    inline in that training script).
 """
 import math
 
@@ -150,17 +152,25 @@ def conv_bn_act(ctx, x, pre, leaky, padding=0, act=True):
     return F.leaky_relu(y, leaky) if act else y
 
 
-def fpn(ctx, feats, leaky, nlm_name, pre="fpn.", sizes=(1, 4, 8, 12)):
+def _up(x, ref, mode):
+    if mode == "bicubic":  # train_mobilenetV3_ecagai.py:270,279
+        return F.interpolate(x, size=[ref.shape[2], ref.shape[3]], mode="bicubic",
+                             align_corners=True)
+    return F.interpolate(x, size=[ref.shape[2], ref.shape[3]], mode="nearest")
+
+
+def fpn(ctx, feats, leaky, nlm_name, pre="fpn.", sizes=(1, 4, 8, 12), up="nearest"):
     """FPN.forward (nets/retinaface_r.py:169-207); nlm_name=None is the plain
-    FPN of nets/layers.py:83-119 (up-sample + add, no NLM)."""
+    FPN of nets/layers.py:83-119 (up-sample + add, no NLM); up="bicubic" is the
+    BECA variant's FPN (train_mobilenetV3_ecagai.py:254-285)."""
     o1 = conv_bn_act(ctx, feats[0], pre + "output1", leaky)
     o2 = conv_bn_act(ctx, feats[1], pre + "output2", leaky)
     o3 = conv_bn_act(ctx, feats[2], pre + "output3", leaky)
-    up3 = F.interpolate(o3, size=[o2.shape[2], o2.shape[3]], mode="nearest")
+    up3 = _up(o3, o2, up)
     if nlm_name is not None:
         up3 = nlm(ctx, up3, nlm_name, sizes)
     o2 = conv_bn_act(ctx, o2 + up3, pre + "merge2", leaky, 1)
-    up2 = F.interpolate(o2, size=[o1.shape[2], o1.shape[3]], mode="nearest")
+    up2 = _up(o2, o1, up)
     if nlm_name is not None:
         up2 = nlm(ctx, up2, nlm_name, sizes)
     o1 = conv_bn_act(ctx, o1 + up2, pre + "merge1", leaky, 1)
@@ -212,6 +222,20 @@ def retinaface_r50(P, x, mode="eval", train_bn=False):
              eca(ctx, c5, "eca_256", "sigmoid")]
     f = fpn(ctx, feats, 0.0, "fpn.Nlm.")
     f = [ssh(ctx, eca(ctx, f[i], "eca_fpn", "sigmoid"), f"ssh{i + 1}.", 0.0) for i in range(3)]
+    return heads(ctx, f, mode)
+
+
+def retinaface_mnv3_beca(P, x, mode="eval", train_bn=False):
+    """JABD-MobileNetV3-BECA (train_mobilenetV3_ecagai.py:319-435): the same
+    body, BECA gates (std pool -> Conv1d -> Hardsigmoid, :286-316) for
+    eca_40/80/160 and eca_fpn, FPN with bicubic align_corners up-sampling and
+    NLM(40) of ch=40 with PSP (1, 3, 6, 8) (:161-234)."""
+    ctx = Ctx(P, train_bn)
+    c3, c4, c5 = mnv3_body(ctx, x)
+    feats = [stdv_eca(ctx, c3, "eca_40."), stdv_eca(ctx, c4, "eca_80."),
+             stdv_eca(ctx, c5, "eca_160.")]
+    f = fpn(ctx, feats, 0.1, "fpn.nlm.", sizes=(1, 3, 6, 8), up="bicubic")
+    f = [ssh(ctx, stdv_eca(ctx, f[i], "eca_fpn."), f"ssh{i + 1}.", 0.1) for i in range(3)]
     return heads(ctx, f, mode)
 
 

@@ -30,7 +30,8 @@ def test_every_exported_module_runs_on_the_hip_path():
     from jabd_amd.hipmodule import HipModule
     allowed = {nn.Sequential, nn.ModuleList, nn.Identity, nn.Dropout, nn.Conv1d, nn.MaxPool2d}
     for modname in ("nets.retinaface_r", "nets.retinaface_eca_nonlocal", "nets.mobilenetV3",
-                    "nets.mobilenet025", "nets.layers", "nets.resnet_pytorch_r"):
+                    "nets.mobilenet025", "nets.layers", "nets.resnet_pytorch_r",
+                    "nets.retinaface_beca"):
         mod = importlib.import_module(modname)
         for name, cls in vars(mod).items():
             if isinstance(cls, type) and issubclass(cls, nn.Module) and \
