@@ -305,6 +305,14 @@ class _R50Block:
         return F.conv(t, self.c3, act="relu", res=x)
 
 
+def mnv3_stages(body):
+    """The three block lists of a MobileNetV3 detector body (layer1..3 of
+    MobileNetV3_Large_eca, or MobileNetV3_Small's tapped bneck)."""
+    if hasattr(body, "stages"):
+        return body.stages()
+    return [list(getattr(body, f"layer{i}")) for i in (1, 2, 3)]
+
+
 class Engine:
     """The eval-mode plan of one RetinaFace on one device (packs built once per
     generation, see hipmodule.py)."""
@@ -316,10 +324,10 @@ class Engine:
             s_, t_ = F.bn_fold(m.body.bn1)
             self.stem = ((F.conv_weight_2d(m.body.conv1.weight.detach().float())
                           * s_[None, :]).contiguous(), t_.detach().contiguous())
-            self.layers = [[b._jabd_cached(dev, lambda b=b: _MNv3Block(b))
-                            for b in getattr(m.body, f"layer{i}")] for i in (1, 2, 3)]
-            self.head = _Head(m, ("eca_40", "eca_80", "eca_160"), "nlm", dev,
-                              gate=getattr(m, "head_gate", "sigmoid"))
+            self.layers = [[b._jabd_cached(dev, lambda b=b: _MNv3Block(b)) for b in stage]
+                           for stage in mnv3_stages(m.body)]
+            self.head = _Head(m, getattr(m, "eca_names", ("eca_40", "eca_80", "eca_160")), "nlm",
+                              dev, gate=getattr(m, "head_gate", "sigmoid"))
         else:
             self.stem = F.pack_conv(m.body.conv1, m.body.bn1)
             self.layers = [[b._jabd_cached(dev, lambda b=b: _R50Block(b))

@@ -811,11 +811,13 @@ def train_forward(model, kind, x):
         body = model.body
         s = bn_act(conv(x, body.conv1, 2, 1, nchw_in=True), body.bn1, "hswish")
         feats = []
-        for i in (1, 2, 3):
-            for blk in getattr(body, f"layer{i}"):
+        from .engine import mnv3_stages
+        for stage in mnv3_stages(body):
+            for blk in stage:
                 s = _mnv3_block(blk, s)
             feats.append(s)
-        return _head(model, feats, ("eca_40", "eca_80", "eca_160"), model.fpn.nlm)
+        return _head(model, feats, getattr(model, "eca_names", ("eca_40", "eca_80", "eca_160")),
+                     model.fpn.nlm)
     body = model.body
     s = bn_act(conv(x, body.conv1, 2, 3, nchw_in=True), body.bn1, "relu")
     s = MaxPoolFn.apply(s)

@@ -11,6 +11,7 @@ composes them itself — as train_mobilenetV3_ecagai.py:319-435 does — runs on
 the same kernels.
 """
 import math
+from collections import OrderedDict
 
 import torch
 import torch.nn as nn
@@ -21,7 +22,7 @@ from jabd_amd.engine import NlmPack, retinaface_forward
 from jabd_amd.hipmodule import HipModule
 from nets._getter import IntermediateLayerGetter
 from nets.layers import SSH, conv_bn, conv_bn1X1, conv_bn_no_relu, fpn_forward  # noqa: F401
-from nets.mobilenetV3 import MobileNetV3_Large_eca
+from nets.mobilenetV3 import MobileNetV3_Large_eca, MobileNetV3_Small
 
 
 class _Head1x1(HipModule):
@@ -170,6 +171,72 @@ class RetinaFace(HipModule):
         self.eca_80 = eca_block(80)
         self.eca_160 = eca_block(160)
         self.eca_fpn = eca_block(40)
+        self.mode = mode
+        self.cfg = cfg
+
+    def forward(self, inputs):
+        return retinaface_forward(self, "mnv3", inputs)
+
+
+class MobileNetV3SmallBody(HipModule):
+    """MobileNetV3_Small's stem + `bneck` (reference nets/mobilenetV3.py:210-229)
+    as a detector body.  The reference has no detector wiring for it (its
+    blocks sit in one Sequential, which IntermediateLayerGetter cannot tap);
+    this taps bneck[2] (stride 8, 24 ch), bneck[7] (stride 16, 48 ch) and
+    bneck[10] (stride 32, 96 ch) — the last block of each resolution — and
+    returns them as IntermediateLayerGetter would.  Keys stay the
+    classifier's (`conv1`, `bn1`, `bneck.N...`) so its checkpoint loads."""
+    splits = (3, 8, 11)
+
+    def __init__(self, backbone):
+        super().__init__()
+        self.conv1, self.bn1, self.hs1 = backbone.conv1, backbone.bn1, backbone.hs1
+        self.bneck = backbone.bneck
+
+    def stages(self):
+        b = list(self.bneck)
+        lo = 0
+        out = []
+        for hi in self.splits:
+            out.append(b[lo:hi])
+            lo = hi
+        return out
+
+    def forward(self, x):
+        with M._Mode(self):
+            s = M.nchw(M.conv_bn_act(self, self.conv1, self.bn1, x, *M.act_of(self.hs1)))
+        out = OrderedDict()
+        for i, blocks in enumerate(self.stages()):
+            for b in blocks:
+                s = b(s)
+            out[i + 1] = s
+        return out
+
+
+class RetinaFace_Small(HipModule):
+    """The JABD head (ECA -> FPN + NLM -> ECA -> SSH -> heads, as RetinaFace
+    above) on a MobileNetV3_Small body: BASELINE config 1's "MobileNetV3-small
+    + ECA head" (cfg_mnv3_small).  Lateral widths 24/48/96; ECA blocks
+    eca_24 / eca_48 / eca_96 and eca_fpn."""
+    eca_names = ("eca_24", "eca_48", "eca_96")
+
+    def __init__(self, cfg=None, pretrained=False, mode="train"):
+        super().__init__()
+        if pretrained:
+            raise RuntimeError("no pretrained MobileNetV3_Small checkpoint is shipped")
+        self.body = MobileNetV3SmallBody(MobileNetV3_Small())
+        oc = cfg["out_channel"]
+        self.fpn = FPN([24, 48, 96], oc)
+        self.ssh1 = SSH(oc, oc)
+        self.ssh2 = SSH(oc, oc)
+        self.ssh3 = SSH(oc, oc)
+        self.ClassHead = nn.ModuleList([ClassHead(oc, 2) for _ in range(3)])
+        self.BboxHead = nn.ModuleList([BboxHead(oc, 2) for _ in range(3)])
+        self.LandmarkHead = nn.ModuleList([LandmarkHead(oc, 2) for _ in range(3)])
+        self.eca_24 = eca_block(24)
+        self.eca_48 = eca_block(48)
+        self.eca_96 = eca_block(96)
+        self.eca_fpn = eca_block(oc)
         self.mode = mode
         self.cfg = cfg
 

@@ -15,6 +15,10 @@ cfg_mnet = {
     "out_channel": 40,
 }
 
+# MobileNetV3_Small + the JABD ECA head (BASELINE config 1; no reference
+# counterpart — see nets.retinaface_r.RetinaFace_Small).  Same anchors as cfg_mnet.
+cfg_mnv3_small = dict(cfg_mnet, name="mobilenetv3_small", return_layers={}, in_channel=None)
+
 cfg_mnet_4 = {
     "name": "mobilenetV3",
     "min_sizes": [[4, 12], [16, 32], [64, 128], [256, 512]],

@@ -239,6 +239,38 @@ def retinaface_mnv3_beca(P, x, mode="eval", train_bn=False):
     return heads(ctx, f, mode)
 
 
+# nets/mobilenetV3.py:216-228 (MobileNetV3_Small.bneck; every block has an SE
+# flag), split where the detector body taps it (stride 8 / 16 / 32)
+MNV3_SMALL_LAYERS = [
+    [(3, 16, 16, 16, "relu", True, 2), (3, 16, 72, 24, "relu", False, 2),
+     (3, 24, 88, 24, "relu", False, 1)],
+    [(5, 24, 96, 40, "hswish", True, 2), (5, 40, 240, 40, "hswish", True, 1),
+     (5, 40, 240, 40, "hswish", True, 1), (5, 40, 120, 48, "hswish", True, 1),
+     (5, 48, 144, 48, "hswish", True, 1)],
+    [(5, 48, 288, 96, "hswish", True, 2), (5, 96, 576, 96, "hswish", True, 1),
+     (5, 96, 576, 96, "hswish", True, 1)],
+]
+
+
+def retinaface_mnv3_small(P, x, mode="eval", train_bn=False):
+    """MobileNetV3_Small body (Block with SE / no gate, nets/mobilenetV3.py:35-91,
+    210-229) tapped after bneck[2], [7], [10], under the JABD head of
+    nets/retinaface_r.py:304-343 (eca_24/48/96)."""
+    ctx = Ctx(P, train_bn)
+    x = F.hardswish(ctx.bn(ctx.conv(x, "body.conv1", 2, 1), "body.bn1"))
+    feats = []
+    i = 0
+    for layer in MNV3_SMALL_LAYERS:
+        for spec in layer:
+            x = block(ctx, x, f"body.bneck.{i}.", spec, "se" if spec[5] else "none")
+            i += 1
+        feats.append(x)
+    feats = [eca(ctx, f, n, "sigmoid") for f, n in zip(feats, ("eca_24", "eca_48", "eca_96"))]
+    f = fpn(ctx, feats, 0.1, "fpn.nlm.")
+    f = [ssh(ctx, eca(ctx, f[i], "eca_fpn", "sigmoid"), f"ssh{i + 1}.", 0.1) for i in range(3)]
+    return heads(ctx, f, mode)
+
+
 # ----------------------------------------------------------------------------- module-level
 # restatements for the module surface (nets/* forwards run one by one)
 def se(ctx, x, pre):

@@ -128,3 +128,54 @@ def test_beca_detector_training_parity(cuda):
     m = _model(mode="train", seed=22)
     x = torch.randn(2, 3, 96, 96, generator=torch.Generator().manual_seed(4)) * 50
     _train_compare(m, model_ref.retinaface_mnv3_beca, x, cuda)
+
+
+# ----------------------------------------------------------------------------- MobileNetV3_Small
+def _small(mode="eval", seed=31):
+    from nets.retinaface_r import RetinaFace_Small
+    from utils.config import cfg_mnv3_small
+    m = init_for_parity(RetinaFace_Small(cfg=cfg_mnv3_small, mode=mode), seed=seed)
+    return m.eval() if mode == "eval" else m
+
+
+def test_small_detector_layout():
+    """BASELINE config 1's MobileNetV3-small + ECA head: the classifier's keys
+    under body., taps at strides 8/16/32, the cfg_mnet anchor count."""
+    from utils.anchors import Anchors
+    from utils.config import cfg_mnv3_small
+    m = _small()
+    sd = m.state_dict()
+    for k in ("body.conv1.weight", "body.bneck.0.se.se.1.weight", "body.bneck.10.bn3.running_var",
+              "fpn.output1.0.weight", "eca_24.conv.weight", "eca_96.conv.weight"):
+        assert k in sd, k
+    assert sd["fpn.output1.0.weight"].shape[1] == 24 and sd["fpn.output3.0.weight"].shape[1] == 96
+    with torch.no_grad():
+        loc, conf, landm = model_ref.retinaface_mnv3_small(sd, torch.randn(1, 3, 640, 640))
+    assert loc.shape[1] == Anchors(cfg_mnv3_small, image_size=(640, 640)).get_anchors().shape[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,mode", [((1, 640, 640), "eval"), ((2, 96, 160), "train")])
+def test_small_detector_forward_parity(cuda, shape, mode):
+    m = _small()
+    B, H, W = shape
+    x = torch.randn(B, 3, H, W, generator=torch.Generator().manual_seed(H)) * 50
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    with torch.no_grad():
+        ref = model_ref.retinaface_mnv3_small(sd, x, mode)
+    m.mode = mode
+    mg = m.to(cuda)
+    with torch.no_grad():
+        got = mg(x.to(cuda))
+    for g_, r, name in zip(got, ref, ("loc", "conf", "landm")):
+        e = rel_err(g_, r)
+        print(f"{name}: max-norm rel {e:.2e}, elementwise {elem_rel_err(g_, r):.2e}")
+        assert e < TOL, f"{name}: rel err {e:.2e}"
+
+
+@pytest.mark.gpu
+def test_small_detector_training_parity(cuda):
+    from test_train import _train_compare
+    m = _small(mode="train", seed=32)
+    x = torch.randn(2, 3, 96, 96, generator=torch.Generator().manual_seed(6)) * 50
+    _train_compare(m, model_ref.retinaface_mnv3_small, x, cuda)
