@@ -4,8 +4,9 @@
 // one thread per output element with the channel fastest (coalesced).
 // PyTorch's algorithm: scale = (in-1)/(out-1) (0 if out == 1), src = scale*o,
 // i = floor(src), t = src - i, cubic-convolution weights with A = -0.75, taps
-// i-1..i+2 clamped to [0, in-1], x first then y.  Backward scatters the 16
-// weighted taps with fp32 atomics (one output's taps may share a clamped input).
+// i-1..i+2 clamped to [0, in-1], x first then y.  Backward gathers: each input
+// element sums the weighted gradients of the outputs that read it, in a fixed
+// order (deterministic; clamped taps that share an input are summed per axis).
 #include <math.h>
 
 #include "common.h"
@@ -63,6 +64,33 @@ __global__ __launch_bounds__(256) void upsample_bicubic_fwd(const float* __restr
   y[e] = acc;
 }
 
+// Sum of the cubic weights with which output o's four (clamped) taps read
+// input index i along one axis — the same index math as the forward.
+__device__ __forceinline__ float tap_weight(int o, float scale, int n, int i) {
+  int idx[4];
+  float w[4];
+  cubic_src(o, scale, n, idx, w);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) s += idx[k] == i ? w[k] : 0.f;
+  return s;
+}
+
+// Outputs whose taps can reach input i: floor(scale*o) in [i-2, i+1] (one
+// index of slack for rounding); the edge inputs also collect the clamped taps.
+__device__ __forceinline__ void out_range(int i, int n, int on, float scale, int& lo, int& hi) {
+  if (scale <= 0.f) {
+    lo = 0;
+    hi = on - 1;
+    return;
+  }
+  lo = i == 0 ? 0 : max(0, (int)floorf((float)(i - 2) / scale) - 1);
+  hi = i == n - 1 ? on - 1 : min(on - 1, (int)ceilf((float)(i + 2) / scale) + 1);
+}
+
+// Gather form: one thread per input element sums, in a fixed order, the
+// weighted gradients of every output that reads it — deterministic (no
+// atomics), and each grad_x element is written once.
 __global__ __launch_bounds__(256) void upsample_bicubic_bwd(const float* __restrict__ gy, int H,
                                                             int W, int C, float* __restrict__ gx,
                                                             int OH, int OW, float sh, float sw,
@@ -71,21 +99,27 @@ __global__ __launch_bounds__(256) void upsample_bicubic_bwd(const float* __restr
   if (e >= total) return;
   const int c = (int)(e % C);
   int64_t r = e / C;
-  const int ox = (int)(r % OW);
-  r /= OW;
-  const int oy = (int)(r % OH);
-  const int64_t b = r / OH;
-  int xi[4], yi[4];
-  float wx[4], wy[4];
-  cubic_src(ox, sw, W, xi, wx);
-  cubic_src(oy, sh, H, yi, wy);
-  const float g = gy[e];
-  float* gb = gx + b * H * W * C + c;
-#pragma unroll
-  for (int ky = 0; ky < 4; ++ky)
-#pragma unroll
-    for (int kx = 0; kx < 4; ++kx)
-      atomicAdd(gb + ((int64_t)yi[ky] * W + xi[kx]) * C, g * wy[ky] * wx[kx]);
+  const int ix = (int)(r % W);
+  r /= W;
+  const int iy = (int)(r % H);
+  const int64_t b = r / H;
+  int ylo, yhi, xlo, xhi;
+  out_range(iy, H, OH, sh, ylo, yhi);
+  out_range(ix, W, OW, sw, xlo, xhi);
+  const float* gb = gy + b * OH * OW * C + c;
+  float acc = 0.f;
+  for (int oy = ylo; oy <= yhi; ++oy) {
+    const float wy = tap_weight(oy, sh, H, iy);
+    if (wy == 0.f) continue;
+    const float* row = gb + (int64_t)oy * OW * C;
+    float rs = 0.f;
+    for (int ox = xlo; ox <= xhi; ++ox) {
+      const float wx = tap_weight(ox, sw, W, ix);
+      if (wx != 0.f) rs = fmaf(wx, row[(int64_t)ox * C], rs);
+    }
+    acc = fmaf(wy, rs, acc);
+  }
+  gx[e] = acc;
 }
 
 static float ac_scale(int in, int out) {
@@ -113,11 +147,10 @@ extern "C" int jabd_upsample_bicubic_ac_bwd_f32(const float* grad_y, int64_t bat
                                                 jabd_stream_t stream) {
   JABD_REQUIRE(batch >= 0 && H > 0 && W > 0 && C > 0 && OH > 0 && OW > 0,
                "upsample_bicubic_bwd: bad size");
-  const int64_t total = batch * OH * OW * C;
+  const int64_t total = batch * H * W * C;
   if (batch == 0) return JABD_OK;
   JABD_REQUIRE(grad_y && grad_x, "upsample_bicubic_bwd: null pointer");
   hipStream_t st = as_stream(stream);
-  JABD_HIP(hipMemsetAsync(grad_x, 0, sizeof(float) * batch * H * W * C, st));
   upsample_bicubic_bwd<<<(unsigned)cdiv(total, 256), 256, 0, st>>>(
       grad_y, H, W, C, grad_x, OH, OW, ac_scale(H, OH), ac_scale(W, OW), total);
   return check_launch("upsample_bicubic_bwd");

@@ -1,9 +1,11 @@
 """ORACLE (test infrastructure only) — the image part of utils/dataloader.py:71-115
 (get_random_data) + :62-64, restated in numpy for given random draws.
 
-Neither PIL's resampler nor cv2 is in this image and the reference holds no
-augmented fixture, so both restatements are parity-unpinned against those
-libraries; tests/test_augment.py pins them with hand-derived known answers.
+The reference holds no augmented fixture.  Pillow (12.2.0) is importable in
+the build container: tests/test_augment.py pins resize_bicubic and
+compose_canvas bit-exactly against Image.resize(BICUBIC) / Image.paste /
+transpose on random images.  cv2 is absent: the HSV round trip stays pinned
+only by hand-derived known answers (parity unpinned against cv2).
   * Image.resize(BICUBIC): Pillow Resample.c — precompute_coeffs (bicubic
     a = -0.5, support 2*max(scale, 1), taps [int(c - sup + .5), int(c + sup + .5)),
     double weights normalised by their sum), normalize_coeffs_8bpc (22-bit fixed
@@ -104,17 +106,24 @@ def hsv2rgb(x):
     return np.where(gray, np.stack([v, v, v], -1), rgb).astype(np.float32)
 
 
-def augment_image(img_u8, input_shape, nw, nh, dx, dy, flip, hue, sat, val):
-    """:84-115 + :62-64 for the given draws: float32 [3, h, w]."""
+def compose_canvas(rs, input_shape, dx, dy, flip):
+    """:90-98: Image.new('RGB', (w, h), (128, 128, 128)).paste(rs, (dx, dy)),
+    then transpose(FLIP_LEFT_RIGHT) if flip; uint8 [h, w, 3]."""
     h, w = input_shape
-    rs = resize_bicubic(img_u8, nw, nh)
-    canvas = np.full((h, w, 3), 128, np.uint8)                 # Image.new grey + paste
+    nh, nw = rs.shape[:2]
+    canvas = np.full((h, w, 3), 128, np.uint8)
     y0, x0 = max(dy, 0), max(dx, 0)
     y1, x1 = min(dy + nh, h), min(dx + nw, w)
     if y1 > y0 and x1 > x0:
         canvas[y0:y1, x0:x1] = rs[y0 - dy:y1 - dy, x0 - dx:x1 - dx]
     if flip:
         canvas = canvas[:, ::-1]
+    return canvas
+
+
+def augment_image(img_u8, input_shape, nw, nh, dx, dy, flip, hue, sat, val):
+    """:84-115 + :62-64 for the given draws: float32 [3, h, w]."""
+    canvas = compose_canvas(resize_bicubic(img_u8, nw, nh), input_shape, dx, dy, flip)
     x = rgb2hsv(np.array(canvas, np.float32) / np.float32(255))
     x[..., 0] += np.float32(hue * 360)
     x[..., 0][x[..., 0] > 1] -= 1

@@ -1,8 +1,9 @@
 """§8f rank 2: get_random_data's image path on the device (jabd_augment_u8)
 against the numpy restatement in oracle/aug_ref.py (PIL BICUBIC + cv2 float
-HSV).  PIL/cv2 are absent and the reference holds no augmented fixture, so the
-oracle is pinned by the hand-derived known answers below (parity unpinned
-against those libraries); GPU vs oracle is bit-exact for the resize
+HSV).  The resize and the paste/flip canvas are pinned byte-exactly against
+Pillow itself (importable in the build container; skipped where it is not);
+cv2 is absent, so the HSV path is pinned by the hand-derived known answers
+below (parity unpinned against cv2); GPU vs oracle is bit-exact for the resize
 (integer arithmetic) and within 2e-4 absolute (on a 0..255 scale) for the HSV
 round trip, whose fp32 ops the kernel issues in the same order."""
 import numpy as np
@@ -17,6 +18,32 @@ def test_bicubic_kat_identity_and_constant():
     assert np.array_equal(aug_ref.resize_bicubic(img, 7, 9), img)
     const = np.full((13, 11, 3), 77, np.uint8)            # weights sum to 1 -> constant
     assert np.all(aug_ref.resize_bicubic(const, 5, 29) == 77)
+
+
+@pytest.mark.parametrize("ih,iw,nh,nw", [(37, 53, 61, 29), (120, 90, 47, 63), (16, 16, 16, 16),
+                                         (9, 200, 31, 12), (64, 48, 256, 192), (5, 3, 2, 1)])
+def test_bicubic_oracle_pinned_to_pillow(ih, iw, nh, nw):
+    """oracle.resize_bicubic == PIL Image.resize(BICUBIC) byte for byte (the
+    reference's own resampler, utils/dataloader.py:88)."""
+    Image = pytest.importorskip("PIL.Image")
+    img = np.random.default_rng(ih * 7 + nw).integers(0, 256, (ih, iw, 3)).astype(np.uint8)
+    ref = np.asarray(Image.fromarray(img).resize((nw, nh), Image.BICUBIC))
+    assert np.array_equal(aug_ref.resize_bicubic(img, nw, nh), ref)
+
+
+@pytest.mark.parametrize("dx,dy,flip", [(5, -7, False), (-20, 3, True), (0, 0, True),
+                                        (40, 40, False), (-100, 0, False)])
+def test_canvas_oracle_pinned_to_pillow(dx, dy, flip):
+    """oracle.compose_canvas == Image.new grey + paste + FLIP_LEFT_RIGHT
+    (utils/dataloader.py:90-98)."""
+    Image = pytest.importorskip("PIL.Image")
+    rs = np.random.default_rng(abs(dx) + 50).integers(0, 256, (37, 45, 3)).astype(np.uint8)
+    h, w = 48, 64
+    new = Image.new("RGB", (w, h), (128, 128, 128))
+    new.paste(Image.fromarray(rs), (dx, dy))
+    if flip:
+        new = new.transpose(Image.FLIP_LEFT_RIGHT)
+    assert np.array_equal(aug_ref.compose_canvas(rs, (h, w), dx, dy, flip), np.asarray(new))
 
 
 def test_hsv_kat():
