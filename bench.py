@@ -287,6 +287,50 @@ def augment_bench(device, reps=20):
             "algorithmic_bytes": nbytes, "achieved_gbs": nbytes / (ms * 1e-3) / 1e9}
 
 
+def detector(kind):
+    """(RetinaFace class, cfg) of a detector kind: mnv3 (JABD-MobileNetV3),
+    beca (JABD-MobileNetV3-BECA), small (MobileNetV3_Small + ECA head), r50."""
+    from utils import config
+    if kind == "mnv3":
+        from nets.retinaface_r import RetinaFace
+        return RetinaFace, config.cfg_mnet
+    if kind == "beca":
+        from nets.retinaface_beca import RetinaFace
+        return RetinaFace, config.cfg_mnet
+    if kind == "small":
+        from nets.retinaface_r import RetinaFace_Small
+        return RetinaFace_Small, config.cfg_mnv3_small
+    from nets.retinaface_eca_nonlocal import RetinaFace
+    return RetinaFace, config.cfg_re50
+
+
+def variant_forward(kind, device, size, batch, steps, warmup=2):
+    """Eval-forward images/s of a detector variant at the C2 shape (synthetic
+    input, weights_init weights): the f4 rows (BECA, MobileNetV3_Small)."""
+    from jabd_amd import synth
+    from nets.retinaface_training import weights_init
+    import contextlib
+    import io
+    RetinaFace, cfg = detector(kind)
+    torch.manual_seed(0)
+    m = RetinaFace(cfg=cfg, mode="eval")
+    with contextlib.redirect_stdout(io.StringIO()):
+        weights_init(m)
+    m = m.eval().to(device)
+    x = synth.images(batch, size, seed=99, device=device)
+    with torch.no_grad():
+        for _ in range(warmup):
+            m(x)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            m(x)
+        torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"workload": f"{kind} eval forward bs{batch} {size}x{size}",
+            "images_per_sec": batch * steps / el, "ms_per_step": el / steps * 1e3}
+
+
 def train_bench(kind, batch, size, steps, warmup, device, dist, rank, conv_roofline_steps=0):
     """steps timed training iterations (parallel.train_step) on this rank."""
     from jabd_amd import optim, parallel, synth
@@ -294,12 +338,7 @@ def train_bench(kind, batch, size, steps, warmup, device, dist, rank, conv_roofl
     from utils.anchors import Anchors
     import contextlib
     import io
-    if kind == "mnv3":
-        from nets.retinaface_r import RetinaFace
-        from utils.config import cfg_mnet as cfg
-    else:
-        from nets.retinaface_eca_nonlocal import RetinaFace
-        from utils.config import cfg_re50 as cfg
+    RetinaFace, cfg = detector(kind)
     torch.manual_seed(0)
     model = RetinaFace(cfg=cfg, mode="train")
     with contextlib.redirect_stdout(io.StringIO()):
@@ -571,6 +610,9 @@ def main():
         extra["c2_o1_activations"] = o1_activation_c2(device, x, args.steps, args.warmup)
         if world == 1 and args.r50_batch > 0:
             extra["roofline_r50_eval"] = r50_roofline(device, args.size)
+        if world == 1:
+            extra["variants"] = {k: variant_forward(k, device, args.size, args.batch, 5)
+                                 for k in ("beca", "small")}
     if not args.no_train:
         tr = {"C4_mnv3": train_bench("mnv3", args.batch, args.size, args.train_steps, 3, device,
                                      dist, rank, conv_roofline_steps=1 if rank == 0 else 0)}

@@ -6,6 +6,8 @@
 // block partials summed in a fixed order (deterministic).
 #include <math.h>
 
+#include <algorithm>
+
 #include "common.h"
 #include "conv_args.h"
 
@@ -642,6 +644,96 @@ __global__ __launch_bounds__(256) void wgrad_reduce2_kernel(const float* __restr
   dw[((int64_t)n * Cin + ci) * KHW + tap] = s;
 }
 
+// Weight gradient of a conv over the NCHW network input with a small im2col
+// depth (the MobileNetV3 stem, 3x3/s2, 3 -> 16: K = 27, Cout = 16), where the
+// tiled kernels above would run 64x64 tiles at ~10% occupancy of the MFMA
+// block and gather x element by element.  Each wave takes segments of 64
+// consecutive output pixels of one output row: it stages the segment's input
+// window (Cin x KH rows x (63*stride + KW) columns, zero-padded) into its own
+// LDS slice with coalesced row loads, then runs 16 steps of two 16x16x4 MFMAs
+// (A = im2col rows k = 16t + i, B = dY[pixel][co], 4 pixels per step) — the
+// reduction index is the pixel.  Per-wave partials [wave][K][Cout] are summed
+// by wgrad_reduce2_kernel in a fixed order.
+constexpr int kSwPx = 64;
+
+static bool stem_wgrad_ok(const ConvArgs& a) {
+  return a.nchw_in && !a.ascale && a.KH * a.KW * a.Cin <= 32 && a.Cout <= 16 && a.stride <= 2 &&
+         a.KW <= 7 && a.Cin * a.KH * ((kSwPx - 1) * a.stride + a.KW) <= 1536;
+}
+
+static int64_t stem_wgrad_waves(const ConvArgs& a) {
+  const int64_t ntask = (int64_t)a.B * a.OH * cdiv(a.OW, kSwPx);
+  return 4 * std::min<int64_t>(2048, cdiv(ntask, 4 * 8));
+}
+
+__global__ __launch_bounds__(256) void stem_wgrad_kernel(const ConvArgs p, int64_t ntask,
+                                                         float* __restrict__ part) {
+  extern __shared__ float sw_lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int WC = (kSwPx - 1) * p.stride + p.KW;
+  const int WS = p.Cin * p.KH * WC;
+  float* win = sw_lds + wave * WS;
+  const int K = p.Cin * p.KH * p.KW;
+  int aoff[2];
+  bool aval[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int kk = 16 * t + i;  // k = tap * Cin + ci, tap = kh * KW + kw
+    aval[t] = kk < K;
+    const int tap = kk / p.Cin, ci = kk - tap * p.Cin;
+    const int kh = tap / p.KW, kw = tap - kh * p.KW;
+    aoff[t] = aval[t] ? (ci * p.KH + kh) * WC + kw : 0;
+  }
+  f32x4 acc0 = (f32x4){0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  const int nseg = (p.OW + kSwPx - 1) / kSwPx;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + wave, nw = (int64_t)gridDim.x * 4;
+  for (int64_t task = gw; task < ntask; task += nw) {
+    const int seg = (int)(task % nseg);
+    const int64_t row = task / nseg;
+    const int oy = (int)(row % p.OH);
+    const int b = (int)(row / p.OH);
+    const int ox0 = seg * kSwPx;
+    const int iy0 = oy * p.stride - p.pad, ix0 = ox0 * p.stride - p.pad;
+    const float* xb = p.x + (int64_t)b * p.x_bs;
+    for (int e = lane; e < WS; e += 64) {
+      const int r = e / WC, col = e - r * WC;
+      const int ci = r / p.KH, kh = r - ci * p.KH;
+      const int iy = iy0 + kh, ix = ix0 + col;
+      float v = 0.f;
+      if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
+        v = xb[((int64_t)ci * p.H + iy) * p.W + ix];
+      win[e] = v;
+    }
+    // the window is wave-private: LDS writes -> reads need only this wave
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const float* dyr = p.y + (int64_t)b * p.y_bs + ((int64_t)oy * p.OW) * p.y_ps + p.y_c0 + i;
+#pragma unroll 4
+    for (int q = 0; q < kSwPx / 4; ++q) {
+      const int px = 4 * q + g, ox = ox0 + px;
+      const bool v = ox < p.OW;
+      const float d = (v && i < p.Cout) ? dyr[(int64_t)ox * p.y_ps] : 0.f;
+      const float a0 = aval[0] && v ? win[aoff[0] + px * p.stride] : 0.f;
+      const float a1 = aval[1] && v ? win[aoff[1] + px * p.stride] : 0.f;
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, d, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, d, acc1, 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();  // every lane's reads done before the next staging
+  }
+  // acc_t[r] = dW[k = 16t + 4g + r][n = i]
+  float* pc = part + gw * K * p.Cout;
+  if (i < p.Cout) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k0 = 4 * g + r, k1 = 16 + 4 * g + r;
+      if (k0 < K) pc[(int64_t)k0 * p.Cout + i] = acc0[r];
+      if (k1 < K) pc[(int64_t)k1 * p.Cout + i] = acc1[r];
+    }
+  }
+}
+
 static int wv_tile(int64_t n) { return n <= 16 ? 16 : (n <= 32 ? 32 : 64); }
 
 // ---------------------------------------------------------------------------
@@ -1253,7 +1345,9 @@ extern "C" int64_t jabd_conv_wgrad_part_floats(const jabd_conv_args* args) {
   if (!args) return -1;
   ConvArgs a = *args;
   a.M = (int64_t)a.B * a.OH * a.OW;
-  return wgrad_chunks(a) * (int64_t)a.KH * a.KW * a.Cin * a.Cout;
+  const int64_t KN = (int64_t)a.KH * a.KW * a.Cin * a.Cout;
+  if (stem_wgrad_ok(a)) return stem_wgrad_waves(a) * KN;
+  return wgrad_chunks(a) * KN;
 }
 
 extern "C" int jabd_conv_wgrad_f32(const jabd_conv_args* args, float* part, float* dw,
@@ -1268,6 +1362,17 @@ extern "C" int jabd_conv_wgrad_f32(const jabd_conv_args* args, float* part, floa
   const int64_t per = cdiv(cdiv(a.M, nchunk), kWgPx) * kWgPx;
   const int64_t nch = cdiv(a.M, per);
   hipStream_t st = as_stream(stream);
+  if (stem_wgrad_ok(a)) {
+    const int64_t nwv = stem_wgrad_waves(a);
+    const int64_t ntask = (int64_t)a.B * a.OH * cdiv(a.OW, kSwPx);
+    const size_t lds = 4 * sizeof(float) * a.Cin * a.KH * ((kSwPx - 1) * a.stride + a.KW);
+    stem_wgrad_kernel<<<(unsigned)(nwv / 4), 256, lds, st>>>(a, ntask, part);
+    if (int e = check_launch("stem_wgrad")) return e;
+    const int64_t tot = (int64_t)K * a.Cout;
+    wgrad_reduce2_kernel<<<(unsigned)cdiv(tot, 16), 256, 0, st>>>(part, nwv, K, a.Cout, a.Cin,
+                                                                  a.KH * a.KW, 16, dw);
+    return check_launch("wgrad_reduce");
+  }
   if (wgrad_vec_ok(a) && wgrad32_ok(a)) {
     const int tk = wg32_tile(K), tn = wg32_tile(a.Cout);
     const int fast = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.H == a.OH &&

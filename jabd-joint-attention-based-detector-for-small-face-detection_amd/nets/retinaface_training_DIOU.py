@@ -44,5 +44,5 @@ class MultiBoxLoss(_BaseMultiBoxLoss):
                                                       raw_loc=True)
         return _MultiBoxLossFn.apply(loc_data.contiguous(), conf_data.contiguous(),
                                      landm_data.contiguous(), loc_t, conf_t, landm_t,
-                                     int(self.negpos_ratio), self._group(),
+                                     int(self.negpos_ratio), self._count_group,
                                      (priors, tuple(float(v) for v in self.variance)))

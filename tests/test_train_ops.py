@@ -50,6 +50,30 @@ def test_convfn_grads(cuda, cin, cout, k, s, h):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,k,s,h,w", [(3, 16, 3, 2, 64, 200), (3, 16, 3, 2, 37, 51),
+                                              (3, 8, 3, 1, 20, 70), (1, 16, 5, 2, 33, 129),
+                                              (3, 64, 7, 2, 40, 44)])
+def test_convfn_nchw_input_wgrad(cuda, cin, cout, k, s, h, w):
+    """Weight gradient of a conv on the NCHW network input: the MobileNetV3
+    stem shape (3x3/s2, 3 -> 16; stem_wgrad_kernel), widths/heights that are
+    not multiples of the 64-pixel segment, and the R50 7x7 stem (Cout 64:
+    the generic tiled kernel)."""
+    from jabd_amd.train import ConvFn
+    g = torch.Generator().manual_seed(cin * 100 + h)
+    x = torch.randn(2, cin, h, w, generator=g) * 50
+    wt = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
+    wr = wt.double().requires_grad_()
+    y = tF.conv2d(x.double(), wr, None, s, k // 2)
+    dy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (y * dy).sum().backward()
+    wg = torch.nn.Parameter(wt.to(cuda))
+    yg = ConvFn.apply(x.to(cuda), wg, None, s, k // 2, True)
+    assert rel_err(_nchw(yg.detach()), y.detach()) < TOL
+    (yg * _nhwc(dy.float()).to(cuda)).sum().backward()
+    _check([wg.grad], [wr.grad], ["dw"])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("c,cout,k,gate,h", [(40, 40, 1, "sigmoid", 8), (256, 128, 3, "sigmoid", 4),
                                              (72, 24, 1, "hsigmoid", 10), (2048, 256, 1, "sigmoid", 3)])
 def test_ecaconvfn_grads(cuda, c, cout, k, gate, h):

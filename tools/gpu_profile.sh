@@ -3,7 +3,7 @@
 # profiles/<round>/pmc_traffic.json), then kernel-trace stats of the C2
 # forward / training steps.  Usage on the GPU box: bash tools/gpu_profile.sh r01
 set -o pipefail
-R=${1:-r01}
+R=${1:-r02}
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/$R
@@ -16,5 +16,11 @@ timeout -k 10 500 python -u bench.py > $O/bench.log 2>&1 && tail -1 $O/bench.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_fwd -o run -- python3 bench.py --steps 10 --pmc-forward-only > $O/prof_fwd.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_tr_mnv3 -o run -- python3 tools/train_steps.py --kind mnv3 > $O/tr_mnv3.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_tr_r50 -o run -- python3 tools/train_steps.py --kind r50 --batch 64 --steps 2 > $O/tr_r50.log 2>&1 &&
-timeout -k 10 200 python3 tools/fwd_ops.py > $O/fwd_ops_c2.txt 2>&1
+timeout -k 10 200 python3 tools/fwd_ops.py > $O/fwd_ops_c2.txt 2>&1 &&
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof_nms -o run -- python3 tools/nms_steps.py --reps 5 > $O/nms_steps.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_tr_beca -o run -- python3 tools/train_steps.py --kind beca --steps 2 > $O/tr_beca.log 2>&1 &&
+for d in prof_fwd:c2_forward prof_tr_mnv3:c4_mnv3_train prof_tr_r50:c3_r50_train prof_nms:c5_nms prof_tr_beca:beca_train; do
+  python3 tools/prof_summary.py $O/${d%%:*} --csv profiles/$R/kernel_stats_${d##*:}.csv > /dev/null || exit 1
+done
+cp $O/bench_line.json $O/fwd_ops_c2.txt profiles/$R/
 echo rc=$?
