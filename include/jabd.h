@@ -210,14 +210,18 @@ int jabd_add3_f32(const float* a, const float* b, const float* c, int64_t n, flo
  * on NHWC fp32 [batch, pixels, C]; w float[k] (k odd, no bias).  stats
  * float[4, batch*C] (mean, std, pre-activation, gate) is written by the forward
  * and read by the backward; the backward's ws is float[2, batch*C].  y may be
- * NULL: the gate alone (stats row 3) for a consumer that scales on load. */
+ * NULL: the gate alone (stats row 3) for a consumer that scales on load.
+ * part / part_floats: the per-chunk reduction workspace, float
+ * [jabd_beca_ws_floats(batch, pixels, C)] (NULL or too small: a slower
+ * one-workgroup-per-image reduction). */
+int64_t jabd_beca_ws_floats(int64_t batch, int64_t pixels, int C);
 int jabd_beca_fwd_f32(const float* x, int64_t batch, int64_t pixels, int C,
-                      const float* w, int k, float* y, float* stats,
-                      jabd_stream_t stream);
+                      const float* w, int k, float* y, float* stats, float* part,
+                      int64_t part_floats, jabd_stream_t stream);
 int jabd_beca_bwd_f32(const float* x, const float* grad_y, int64_t batch,
                       int64_t pixels, int C, const float* w, int k,
                       const float* stats, float* grad_x, float* grad_w, float* ws,
-                      jabd_stream_t stream);
+                      float* part, int64_t part_floats, jabd_stream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * A9 MultiBoxLoss — nets/retinaface_training.py:183-303.
@@ -542,9 +546,14 @@ int jabd_bn_eval_f32(const float* x, int64_t M, int32_t C, const float* running_
                      int32_t act, float slope, float* y, jabd_stream_t stream);
 int jabd_channel_scale_f32(const float* x, int64_t B, int64_t HW, int32_t C, const float* scale,
                            float* y, jabd_stream_t stream);
+/* cat over `sizes` of AdaptiveAvgPool2d((s, s)) of NHWC x -> out [B, S, C]
+ * (PSPModule, nets/retinaface_r.py:85-104).  ws / ws_floats: row-pass
+ * workspace, float[jabd_adaptive_pool_ws_floats(...)] (NULL: one-pass kernel). */
+int64_t jabd_adaptive_pool_ws_floats(int32_t B, int32_t H, int32_t C, const int32_t* sizes,
+                                     int32_t nsizes);
 int jabd_adaptive_pool_f32(const float* x, int64_t x_bs, int32_t B, int32_t H, int32_t W,
                            int32_t C, const int32_t* sizes, int32_t nsizes, float* out,
-                           jabd_stream_t stream);
+                           float* ws, int64_t ws_floats, jabd_stream_t stream);
 /* out = lateral + F.interpolate(src, size=(h, w), mode='nearest') — the
  * plain FPN's up-sample and add (nets/layers.py:106-117); NHWC, C % 4 == 0.
  * Backward: jabd_upsample_nearest_bwd_f32. */

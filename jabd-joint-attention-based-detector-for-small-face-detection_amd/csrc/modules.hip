@@ -162,8 +162,66 @@ __global__ __launch_bounds__(256) void adaptive_pool_kernel(const float* __restr
   }
 }
 
+// Two-pass form (workspace): pass 1, one workgroup per (row, image), sums
+// each column bin q (q enumerates (level, bj)) of the row for every channel
+// into rowpart[b][y][q][c]; pass 2, one workgroup per (bin, image), sums the
+// bin's rows of rowpart.  x is read from HBM once (the one-pass kernel above
+// has the 1x1 bin's workgroup read the whole image alone).  Fixed order.
+__device__ __forceinline__ void col_bin(const PoolSizes& sz, int q, int& lvl, int& bj) {
+  lvl = 0;
+  while (lvl < sz.n - 1 && q >= sz.v[lvl]) {
+    q -= sz.v[lvl];
+    ++lvl;
+  }
+  bj = q;
+}
+
+__global__ __launch_bounds__(256) void pool_rows_kernel(const float* __restrict__ x,
+                                                        int64_t x_bs, int H, int W, int C,
+                                                        const PoolSizes sz, int Q,
+                                                        float* __restrict__ rowpart) {
+  const int y = blockIdx.x, b = blockIdx.y;
+  const float* xr = x + (int64_t)b * x_bs + (int64_t)y * W * C;
+  float* rp = rowpart + (((int64_t)b * H + y) * Q) * C;
+  for (int it = threadIdx.x; it < Q * C; it += blockDim.x) {
+    const int q = it / C, c = it - q * C;
+    int lvl, bj;
+    col_bin(sz, q, lvl, bj);
+    const int z = sz.v[lvl];
+    const int w0 = (bj * W) / z, w1 = ((bj + 1) * W + z - 1) / z;
+    float a = 0.f;
+    for (int j = w0; j < w1; ++j) a += xr[(int64_t)j * C + c];
+    rp[it] = a;
+  }
+}
+
+__global__ __launch_bounds__(256) void pool_bins_kernel(const float* __restrict__ rowpart, int H,
+                                                        int W, int C, const PoolSizes sz, int S,
+                                                        int Q, float* __restrict__ out) {
+  const int s = blockIdx.x, b = blockIdx.y;
+  int h0, h1, w0, w1;
+  pool_bin(sz, s, H, W, h0, h1, w0, w1);
+  // column-bin index q of this bin: levels before it, then bj
+  int base = 0, qb = 0, lvl = 0;
+  for (; lvl < sz.n - 1; ++lvl) {
+    const int n = sz.v[lvl] * sz.v[lvl];
+    if (s < base + n) break;
+    base += n;
+    qb += sz.v[lvl];
+  }
+  const int q = qb + (s - base) % sz.v[lvl];
+  const float cnt = (float)((h1 - h0) * (w1 - w0));
+  const float* rp = rowpart + ((int64_t)b * H * Q + q) * C;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float a = 0.f;
+    for (int i = h0; i < h1; ++i) a += rp[(int64_t)i * Q * C + c];
+    out[((int64_t)b * S + s) * C + c] = a / cnt;
+  }
+}
+
 // dx[b][p][c] = sum over the bins containing p of dy[b][s][c] / |bin s|
-// (gather form: every pixel owns its sum, no atomics).
+// (gather form: every pixel owns its sum, no atomics).  Per level only the
+// bins around floor(i*z/H) can hold row i (likewise for columns).
 __global__ __launch_bounds__(256) void adaptive_pool_bwd_kernel(const float* __restrict__ dy,
                                                                 int H, int W, int C,
                                                                 const PoolSizes sz, int S,
@@ -178,11 +236,12 @@ __global__ __launch_bounds__(256) void adaptive_pool_bwd_kernel(const float* __r
   int base = 0;
   for (int l = 0; l < sz.n; ++l) {
     const int z = sz.v[l];
-    // bins of this level whose row range holds i: bi with floor(bi*H/z) <= i < ceil((bi+1)H/z)
-    for (int bi = 0; bi < z; ++bi) {
+    const int bi0 = max(0, (i * z) / H - 1), bi1 = min(z - 1, (i * z) / H + 1);
+    const int bj0 = max(0, (j * z) / W - 1), bj1 = min(z - 1, (j * z) / W + 1);
+    for (int bi = bi0; bi <= bi1; ++bi) {
       const int r0 = (bi * H) / z, r1 = ((bi + 1) * H + z - 1) / z;
       if (i < r0 || i >= r1) continue;
-      for (int bj = 0; bj < z; ++bj) {
+      for (int bj = bj0; bj <= bj1; ++bj) {
         const int c0 = (bj * W) / z, c1 = ((bj + 1) * W + z - 1) / z;
         if (j < c0 || j >= c1) continue;
         a += dy[((int64_t)b * S + base + bi * z + bj) * C + c] / (float)((r1 - r0) * (c1 - c0));
@@ -314,15 +373,33 @@ static int pool_sizes(const int32_t* sizes, int32_t nsizes, PoolSizes& sz, int& 
   return JABD_OK;
 }
 
+extern "C" int64_t jabd_adaptive_pool_ws_floats(int32_t B, int32_t H, int32_t C,
+                                                const int32_t* sizes, int32_t nsizes) {
+  if (!sizes || nsizes <= 0 || B <= 0 || H <= 0 || C <= 0) return -1;
+  int64_t Q = 0;
+  for (int i = 0; i < nsizes; ++i) Q += sizes[i];
+  return (int64_t)B * H * Q * C;
+}
+
 extern "C" int jabd_adaptive_pool_f32(const float* x, int64_t x_bs, int32_t B, int32_t H,
                                       int32_t W, int32_t C, const int32_t* sizes, int32_t nsizes,
-                                      float* out, jabd_stream_t stream) {
+                                      float* out, float* ws, int64_t ws_floats,
+                                      jabd_stream_t stream) {
   JABD_REQUIRE(x && out && B > 0 && H > 0 && W > 0 && C > 0, "adaptive_pool: bad args");
   PoolSizes sz;
   int S;
   if (int e = pool_sizes(sizes, nsizes, sz, S)) return e;
-  dim3 g((unsigned)S, (unsigned)B);
-  adaptive_pool_kernel<<<g, 256, 0, as_stream(stream)>>>(x, x_bs, H, W, C, sz, S, out);
+  hipStream_t st = as_stream(stream);
+  if (ws && ws_floats >= jabd_adaptive_pool_ws_floats(B, H, C, sizes, nsizes)) {
+    int Q = 0;
+    for (int i = 0; i < nsizes; ++i) Q += sizes[i];
+    pool_rows_kernel<<<dim3((unsigned)H, (unsigned)B), 256, 0, st>>>(x, x_bs, H, W, C, sz, Q, ws);
+    if (int e = check_launch("adaptive_pool_rows")) return e;
+    pool_bins_kernel<<<dim3((unsigned)S, (unsigned)B), 256, 0, st>>>(ws, H, W, C, sz, S, Q, out);
+    return check_launch("adaptive_pool_bins");
+  }
+  adaptive_pool_kernel<<<dim3((unsigned)S, (unsigned)B), 256, 0, st>>>(x, x_bs, H, W, C, sz, S,
+                                                                      out);
   return check_launch("adaptive_pool");
 }
 

@@ -121,9 +121,10 @@ SIGNATURES = {
     "jabd_nlm_attn_bwd_f32": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32,
                               c_vp, c_vp, c_vp, c_vp],
     "jabd_add3_f32": [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
-    "jabd_beca_fwd_f32": [c_vp, c_i64, c_i64, c_int, c_vp, c_int, c_vp, c_vp, c_vp],
+    "jabd_beca_ws_floats": [c_i64, c_i64, c_int],
+    "jabd_beca_fwd_f32": [c_vp, c_i64, c_i64, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_vp],
     "jabd_beca_bwd_f32": [c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp,
-                          c_vp],
+                          c_vp, c_i64, c_vp],
     "jabd_match_iou_f32": [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_f32, c_f32, c_f32,
                            c_vp, c_vp, c_vp, c_vp, c_size, c_vp],
     "jabd_multibox_diou_loss_fwd_f32": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_f32,
@@ -190,8 +191,9 @@ SIGNATURES = {
     "jabd_bn_eval_f32": [c_vp, c_i64, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_i32, c_f32, c_vp,
                          c_vp],
     "jabd_channel_scale_f32": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp],
+    "jabd_adaptive_pool_ws_floats": [c_i32, c_i32, c_i32, ctypes.POINTER(c_i32), c_i32],
     "jabd_adaptive_pool_f32": [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_i32),
-                               c_i32, c_vp, c_vp],
+                               c_i32, c_vp, c_vp, c_i64, c_vp],
     "jabd_upsample_nearest_add_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp,
                                       c_vp],
     "jabd_adaptive_pool_bwd_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_i32),
@@ -201,7 +203,8 @@ _RESTYPE = {"jabd_version": ctypes.c_char_p, "jabd_dw_nblk": ctypes.c_int64,
             "jabd_expand_dw_nblk": ctypes.c_int64,
             "jabd_bn_nblk": ctypes.c_int64, "jabd_conv_wgrad_part_floats": ctypes.c_int64,
             "jabd_dw_wgrad_part_floats": ctypes.c_int64,
-            "jabd_adam_num_chunks": ctypes.c_int64}
+            "jabd_adam_num_chunks": ctypes.c_int64, "jabd_beca_ws_floats": ctypes.c_int64,
+            "jabd_adaptive_pool_ws_floats": ctypes.c_int64}
 
 _lock = threading.Lock()
 _lib = None

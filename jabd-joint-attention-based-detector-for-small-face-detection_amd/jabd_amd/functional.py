@@ -355,8 +355,10 @@ def adaptive_pool(x, sizes):
     S = sum(s * s for s in sizes)
     out = torch.empty((B, S, C), dtype=torch.float32, device=x.device)
     arr = (ctypes.c_int32 * len(sizes))(*sizes)
+    n = int(lib().jabd_adaptive_pool_ws_floats(B, H, C, arr, len(sizes)))
+    ws = torch.empty(max(n, 1), dtype=torch.float32, device=x.device)
     call("jabd_adaptive_pool_f32", x.data_ptr(), x.stride(0), B, H, W, C, arr, len(sizes),
-         out.data_ptr(), _stream())
+         out.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
     return out
 
 

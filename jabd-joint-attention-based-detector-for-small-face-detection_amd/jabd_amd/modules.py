@@ -122,11 +122,7 @@ class AdaptivePoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, sizes):
         B, H, W, C = x.shape
-        S = sum(s * s for s in sizes)
-        out = torch.empty((B, S, C), dtype=torch.float32, device=x.device)
-        arr = (ctypes.c_int32 * len(sizes))(*sizes)
-        call("jabd_adaptive_pool_f32", x.data_ptr(), x.stride(0), B, H, W, C, arr, len(sizes),
-             out.data_ptr(), _st())
+        out = F.adaptive_pool(x, sizes)
         ctx.cfg = (tuple(sizes), B, H, W, C)
         return out
 
@@ -471,6 +467,8 @@ def beca_gate(xh, w1d):
     B, H, W, C = xh.shape
     w = w1d.detach().reshape(-1).float().contiguous()
     stats = torch.empty((4, B * C), dtype=torch.float32, device=xh.device)
+    from .ops import beca_part
+    part = beca_part(B, H * W, C, xh.device)
     call("jabd_beca_fwd_f32", xh.data_ptr(), B, H * W, C, w.data_ptr(), w.numel(), None,
-         stats.data_ptr(), _st())
+         stats.data_ptr(), part.data_ptr(), part.numel(), _st())
     return stats[3].view(B, C)

@@ -374,6 +374,12 @@ def upsample_bicubic(x_nhwc, size):
 
 
 # --------------------------------------------------------------------------- BECA
+def beca_part(B, pixels, C, device):
+    """Reduction workspace of jabd_beca_fwd_f32 / _bwd_f32."""
+    n = int(lib().jabd_beca_ws_floats(B, pixels, C))
+    return torch.empty(max(n, 1), dtype=torch.float32, device=device)
+
+
 class BecaFn(torch.autograd.Function):
     """eca_block of the bicubic variant (train_mobilenetV3_ecagai.py:286-316) on
     NHWC x [B, H, W, C] with the conv1d weight w [k]: x * Hardsigmoid(conv1d(std))."""
@@ -385,8 +391,9 @@ class BecaFn(torch.autograd.Function):
         B, H, W, C = x.shape
         y = torch.empty_like(x)
         stats = torch.empty((4, B * C), dtype=torch.float32, device=x.device)
+        part = beca_part(B, H * W, C, x.device)
         call("jabd_beca_fwd_f32", _p(x), B, H * W, C, _p(w), w.numel(), _p(y), _p(stats),
-             _stream())
+             _p(part), part.numel(), _stream())
         ctx.save_for_backward(x, w, stats)
         return y
 
@@ -398,8 +405,9 @@ class BecaFn(torch.autograd.Function):
         gx = torch.empty_like(x)
         gw = torch.empty_like(w)
         ws = torch.empty((2, B * C), dtype=torch.float32, device=x.device)
+        part = beca_part(B, H * W, C, x.device)
         call("jabd_beca_bwd_f32", _p(x), _p(gy), B, H * W, C, _p(w), w.numel(), _p(stats),
-             _p(gx), _p(gw), _p(ws), _stream())
+             _p(gx), _p(gw), _p(ws), _p(part), part.numel(), _stream())
         return gx, gw
 
 

@@ -116,8 +116,11 @@ def stdv_channels(F):
         xh = M.nhwc(F).contiguous()
         stats = torch.empty((4, B * C), dtype=torch.float32, device=F.device)
         w = torch.zeros(1, dtype=torch.float32, device=F.device)
-        M.call("jabd_beca_fwd_f32", xh.data_ptr(), B, xh.shape[1] * xh.shape[2], C, w.data_ptr(),
-               1, None, stats.data_ptr(), M._st())
+        P = xh.shape[1] * xh.shape[2]
+        from jabd_amd.ops import beca_part
+        part = beca_part(B, P, C, F.device)
+        M.call("jabd_beca_fwd_f32", xh.data_ptr(), B, P, C, w.data_ptr(), 1, None,
+               stats.data_ptr(), part.data_ptr(), part.numel(), M._st())
     return stats[1].view(B, C, 1, 1)
 
 
