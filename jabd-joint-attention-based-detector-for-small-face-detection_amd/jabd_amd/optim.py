@@ -101,4 +101,8 @@ class Adam(torch.optim.Adam):
                           float(beta1), float(beta2), float(group["eps"]),
                           float(group["weight_decay"]), 1.0 - beta1 ** step,
                           1.0 - beta2 ** step, _stream())
+                # the kernel wrote through raw pointers: bump the version
+                # counters as an in-place torch op would, so weight caches
+                # keyed on _version (train._packed) see the new values
+                torch.autograd.graph.increment_version([t[0] for t in tensors])
         return loss

@@ -102,3 +102,29 @@ def test_adam_state_dict_roundtrip(cuda):
     back = torch.optim.Adam(ref, lr=2e-3, weight_decay=5e-4)
     back.load_state_dict(copy.deepcopy(o_got.state_dict()))
     assert float(back.state_dict()["state"][0]["step"]) == 4.0
+
+
+@pytest.mark.gpu
+def test_adam_steps_reach_the_training_convs(cuda):
+    """The fused step writes parameters through raw pointers; the training
+    convs' packed-weight cache (train._packed, keyed on _version) must see the
+    update: three train_steps with jabd Adam match three with torch.optim.Adam."""
+    from _util import init_for_parity
+    from jabd_amd import parallel, synth
+    from jabd_amd.optim import Adam
+    from nets.retinaface_r import RetinaFace
+    from nets.retinaface_training import MultiBoxLoss
+    from utils.anchors import Anchors
+    from utils.config import cfg_mnet
+    x = synth.images(2, 96, seed=5).to(cuda)
+    tg = [torch.from_numpy(t).to(cuda) for t in synth.targets(2, 96, seed=6)]
+    pri = Anchors(cfg_mnet, image_size=(96, 96)).get_anchors().to(cuda)
+    losses = {}
+    for name, mk in (("torch", torch.optim.Adam), ("jabd", Adam)):
+        m = init_for_parity(RetinaFace(cfg=cfg_mnet, mode="train"), seed=8).to(cuda).train()
+        opt = mk(m.parameters(), lr=1e-2, weight_decay=5e-4)
+        crit = MultiBoxLoss(2, 0.35, 7, cfg_mnet["variance"], True)
+        losses[name] = [float(parallel.train_step(m, crit, opt, x, tg, pri)[0]) for _ in range(3)]
+    assert losses["torch"][0] != losses["torch"][2]  # the steps do move the loss
+    for a, b in zip(losses["torch"], losses["jabd"]):
+        assert abs(a - b) <= 1e-4 * abs(a), losses
