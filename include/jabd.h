@@ -333,6 +333,15 @@ typedef struct jabd_conv_args {
 int jabd_conv_pack_tn(int cout);
 /* 32-channel N-tiles per workgroup of the 32x32x2 1x1 kernel for a Cout. */
 int jabd_conv_pack_tn32(int cout);
+/* Device-side weight packing: torch weight w [cout][cin][kh][kw] (transposed
+ * = 1: the data-gradient form, W'[ci][co] = W[co][ci]) -> wp float4
+ * [Kc][Ntiles][64] (the 16x16x4 layout above) and, if wp32 != NULL, wp32
+ * float4 [K8][NT32][64] (the 32x32x2 layout); K = kh*kw*cin' rows in tap-major
+ * order, zero padding outside.  One launch per weight (the training convs
+ * repack after every optimizer step). */
+int jabd_conv_pack_f32(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw,
+                       int32_t transposed, int32_t Kc, int32_t Ntiles, float* wp, int32_t K8,
+                       int32_t NT32, float* wp32, jabd_stream_t stream);
 int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t stream);
 
 /* A1 MobileNetV3 stem — nets/mobilenetV3.py:455-457,511: conv3x3/s2/p1 3->16

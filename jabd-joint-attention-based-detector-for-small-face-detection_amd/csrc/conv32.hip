@@ -379,3 +379,76 @@ int conv1x1_m32_dispatch(const ConvArgs& a0, hipStream_t st, bool kxk) {
 #undef M32
 }
 }  // namespace jabd
+
+// ---------------------------------------------------------------------------
+// Weight packing on the device (the training convs repack after every
+// optimizer step): straight from the torch weight [Cout][Cin][KH][KW] (or,
+// transposed = 1, the data-gradient form W'[ci][co] = W[co][ci]) to
+//   wp   float4 [Kc][Ntiles][64]:  lane 16g + j, element e = W2d[16kc+4g+e][16nt+j]
+//   wp32 float4 [K8][NT32][64]:    lane 32h + j, element e = W2d[8k8+4h+e][32nt+j]
+// with W2d[k][n], k = tap * Cin' + ci' (tap = kh * KW + kw), zero outside
+// K x N — the layouts jabd_amd.functional.PackedConv builds on the host.
+namespace jabd {
+
+__device__ __forceinline__ float w2d_at(const float* __restrict__ w, int cout, int cin, int khw,
+                                        int transposed, int k, int n) {
+  const int cinp = transposed ? cout : cin;  // the packed GEMM's input channels
+  const int ncols = transposed ? cin : cout;
+  if (k >= khw * cinp || n >= ncols) return 0.f;
+  const int tap = k / cinp, c = k - tap * cinp;
+  const int co = transposed ? c : n, ci = transposed ? n : c;
+  return w[((int64_t)co * cin + ci) * khw + tap];
+}
+
+__global__ __launch_bounds__(256) void pack_w_kernel(const float* __restrict__ w, int cout,
+                                                     int cin, int khw, int transposed, int Kc,
+                                                     int Ntiles, float* __restrict__ wp, int K8,
+                                                     int NT32, float* __restrict__ wp32) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t n16 = (int64_t)Kc * Ntiles * 64;
+  if (i < n16) {
+    const int lane = (int)(i & 63);
+    const int64_t r = i >> 6;
+    const int nt = (int)(r % Ntiles), kc = (int)(r / Ntiles);
+    const int g = lane >> 4, j = lane & 15;
+    float4 v;
+    v.x = w2d_at(w, cout, cin, khw, transposed, 16 * kc + 4 * g + 0, 16 * nt + j);
+    v.y = w2d_at(w, cout, cin, khw, transposed, 16 * kc + 4 * g + 1, 16 * nt + j);
+    v.z = w2d_at(w, cout, cin, khw, transposed, 16 * kc + 4 * g + 2, 16 * nt + j);
+    v.w = w2d_at(w, cout, cin, khw, transposed, 16 * kc + 4 * g + 3, 16 * nt + j);
+    reinterpret_cast<float4*>(wp)[i] = v;
+    return;
+  }
+  const int64_t i2 = i - n16;
+  if (!wp32 || i2 >= (int64_t)K8 * NT32 * 64) return;
+  const int lane = (int)(i2 & 63);
+  const int64_t r = i2 >> 6;
+  const int nt = (int)(r % NT32), k8 = (int)(r / NT32);
+  const int h = lane >> 5, j = lane & 31;
+  float4 v;
+  v.x = w2d_at(w, cout, cin, khw, transposed, 8 * k8 + 4 * h + 0, 32 * nt + j);
+  v.y = w2d_at(w, cout, cin, khw, transposed, 8 * k8 + 4 * h + 1, 32 * nt + j);
+  v.z = w2d_at(w, cout, cin, khw, transposed, 8 * k8 + 4 * h + 2, 32 * nt + j);
+  v.w = w2d_at(w, cout, cin, khw, transposed, 8 * k8 + 4 * h + 3, 32 * nt + j);
+  reinterpret_cast<float4*>(wp32)[i2] = v;
+}
+
+}  // namespace jabd
+
+extern "C" int jabd_conv_pack_f32(const float* w, int32_t cout, int32_t cin, int32_t kh,
+                                  int32_t kw, int32_t transposed, int32_t Kc, int32_t Ntiles,
+                                  float* wp, int32_t K8, int32_t NT32, float* wp32,
+                                  jabd_stream_t stream) {
+  using namespace jabd;
+  JABD_REQUIRE(w && wp && cout > 0 && cin > 0 && kh > 0 && kw > 0 && Kc > 0 && Ntiles > 0 &&
+                   (!wp32 || (K8 > 0 && NT32 > 0)),
+               "conv_pack: bad args");
+  const int cinp = transposed ? cout : cin, ncols = transposed ? cin : cout;
+  JABD_REQUIRE(16 * Kc >= kh * kw * cinp && 16 * Ntiles >= ncols &&
+                   (!wp32 || (8 * K8 >= kh * kw * cinp && 32 * NT32 >= ncols)),
+               "conv_pack: tile counts do not cover the weight");
+  const int64_t tot = (int64_t)Kc * Ntiles * 64 + (wp32 ? (int64_t)K8 * NT32 * 64 : 0);
+  pack_w_kernel<<<(unsigned)cdiv(tot, 256), 256, 0, as_stream(stream)>>>(
+      w, cout, cin, kh * kw, transposed, Kc, Ntiles, wp, K8, NT32, wp32);
+  return check_launch("conv_pack");
+}

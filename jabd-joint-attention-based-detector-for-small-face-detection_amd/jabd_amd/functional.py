@@ -69,6 +69,39 @@ class PackedConv:
         self.w32 = wp.view(k8, 2, 4, self.ntiles32, 32).permute(0, 3, 1, 4, 2).contiguous()
 
 
+def pack_weight_device(weight, transposed=False):
+    """PackedConv of a raw torch conv weight [Cout, Cin, KH, KW] built by one
+    device kernel (jabd_conv_pack_f32) — the same layouts as PackedConv(
+    conv_weight_2d(w), ...) without the host-side zeros / copies / permutes.
+    transposed: the data-gradient form (input and output channels swapped)."""
+    w = weight.detach()
+    if w.dtype != torch.float32 or not w.is_contiguous():
+        w = w.float().contiguous()
+    cout, cin, kh, kw = w.shape
+    pcin, pcout = (cout, cin) if transposed else (cin, cout)
+    pk = PackedConv.__new__(PackedConv)
+    pk.KH, pk.KW, pk.Cin, pk.Cin2, pk.Cout = kh, kw, pcin, 0, pcout
+    pk.tn = int(lib().jabd_conv_pack_tn(pcout))
+    tiles = (pcout + 15) // 16
+    pk.Ntiles = (tiles + pk.tn - 1) // pk.tn * pk.tn
+    K = kh * kw * pcin
+    pk.Kc = (K + 15) // 16
+    pk.bias = None
+    pk.w = torch.empty((pk.Kc, pk.Ntiles, 4, 16, 4), dtype=torch.float32, device=w.device)
+    pk.w32 = None
+    k8 = nt32 = 0
+    if (kh == 1 and kw == 1) or pcin % 32 == 0:
+        pk.tn32 = int(lib().jabd_conv_pack_tn32(pcout))
+        nt = (pcout + 31) // 32
+        pk.ntiles32 = (nt + pk.tn32 - 1) // pk.tn32 * pk.tn32
+        k8 = (K + 31) // 32 * 4
+        nt32 = pk.ntiles32
+        pk.w32 = torch.empty((k8, nt32, 2, 32, 4), dtype=torch.float32, device=w.device)
+    call("jabd_conv_pack_f32", w.data_ptr(), cout, cin, kh, kw, 1 if transposed else 0, pk.Kc,
+         pk.Ntiles, pk.w.data_ptr(), k8, nt32, _ptr(pk.w32), _stream())
+    return pk
+
+
 def conv_weight_2d(weight):
     """nn.Conv2d weight [Cout, Cin, KH, KW] -> [KH*KW*Cin, Cout] (tap-major)."""
     cout, cin, kh, kw = weight.shape

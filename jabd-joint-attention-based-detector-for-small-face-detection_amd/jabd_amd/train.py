@@ -62,11 +62,8 @@ def _packed(weight, transposed):
         pk = cache.get(key)
         if pk is not None:
             return pk
-    w = weight.detach().float()
-    if transposed:
-        w = w.transpose(0, 1)  # [Cin][Cout][KH][KW]: the dgrad GEMM's "weight"
-    kh, kw = w.shape[2], w.shape[3]
-    pk = F.PackedConv(F.conv_weight_2d(w).contiguous(), None, kh, kw, w.shape[1])
+    # transposed: [Cin][Cout][KH][KW] is the dgrad GEMM's "weight"
+    pk = F.pack_weight_device(weight, transposed)
     if cache is not None:
         if len(cache) > 4:  # stale versions
             cache.clear()
@@ -514,7 +511,9 @@ class HeadsFn(torch.autograd.Function):
     """Bbox/Class/Landmark 1x1 heads of the 3 levels -> (loc, conf, landm) logits."""
 
     @staticmethod
-    def forward(ctx, f1, f2, f3, *wb):
+    def forward(ctx, f1, f2, f3, cidx, *wb):
+        """cidx: per level None, or the channel index of each real feature
+        channel in a zero-padded feature tensor (ssh_train(padded_out=True))."""
         feats = (f1, f2, f3)
         B = f1.shape[0]
         A = sum(2 * f.shape[1] * f.shape[2] for f in feats)
@@ -526,14 +525,20 @@ class HeadsFn(torch.autograd.Function):
         cat = []
         for i, f in enumerate(feats):
             ws = wb[6 * i:6 * i + 6]  # Wb, bb, Wc, bc, Wl, bl
-            C = f.shape[3]
+            C = ws[0].shape[1]
             wt = torch.cat([ws[0].detach().reshape(8, C), ws[2].detach().reshape(4, C),
-                            ws[4].detach().reshape(20, C)]).float().contiguous()
+                            ws[4].detach().reshape(20, C)]).float()
+            if cidx[i] is not None:  # zero columns at the feature's pad channels
+                wp = wt.new_zeros((32, f.shape[3]))
+                wp[:, cidx[i]] = wt
+                wt = wp
+            wt = wt.contiguous()
             bs = torch.cat([ws[1].detach(), ws[3].detach(), ws[5].detach()]).float().contiguous()
             F.heads(f, wt, bs, loc, conf, landm, a_off, softmax=False)
             cat.append(wt)
             a_off += 2 * f.shape[1] * f.shape[2]
         ctx.save_for_backward(f1, f2, f3, *cat)
+        ctx.cidx = cidx
         return loc, conf, landm
 
     @staticmethod
@@ -555,11 +560,15 @@ class HeadsFn(torch.autograd.Function):
             wconv = wt.view(32, C, 1, 1)
             dfs.append(_dgrad(dout, wconv, 1, 0, h, w))
             dW = _wgrad(f, dout, wconv, 1, 0).view(32, C)
+            ci = ctx.cidx[len(dfs) - 1]
+            if ci is not None:
+                dW = dW[:, ci]
+                C = dW.shape[1]
             db = _chan_sum(dout)
             dws += [dW[:8].reshape(8, C, 1, 1), db[:8], dW[8:12].reshape(4, C, 1, 1), db[8:12],
                     dW[12:].reshape(20, C, 1, 1), db[12:]]
             a_off += 2 * h * w
-        return tuple(dfs) + tuple(dws)
+        return tuple(dfs) + (None,) + tuple(dws)
 
 
 class MaxPoolFn(torch.autograd.Function):
@@ -602,9 +611,33 @@ def bn_act(x, bn, act="none", slope=0.0, res=None):
             rv.copy_(rv_p[: rv.shape[0]])
     else:
         y = BnActFn.apply(x, g, b, res, rm, rv, act, slope, bn.momentum, bn.eps)
-    if bn.num_batches_tracked is not None:
-        bn.num_batches_tracked.add_(1)
+    _count_batch(bn)
     return y
+
+
+# num_batches_tracked increments of one train_forward, applied as one
+# multi-tensor add at its end (75 one-element kernels otherwise)
+_NBT = []
+
+
+def _count_batch(bn):
+    t = bn.num_batches_tracked
+    if t is None:
+        return
+    if _NBT:
+        _NBT[-1].append(t)
+    else:
+        t.add_(1)
+
+
+class _BatchCounts:
+    def __enter__(self):
+        _NBT.append([])
+
+    def __exit__(self, *exc):
+        ts = _NBT.pop()
+        if ts and exc[0] is None:
+            torch._foreach_add_(ts, 1)
 
 
 def _padw(weight, cout=None, cin=None):
@@ -727,9 +760,12 @@ def fpn_train(fpn, feats, nlm=None, eca_ws=None, gate="sigmoid"):
     return [o1, o2, o3]
 
 
-def ssh_train(ssh, o, eca_w=None):
+def ssh_train(ssh, o, eca_w=None, padded_out=False):
     """SSH forward (nets/layers.py:56-68) in training mode; eca_w: the head's
-    eca_fpn Conv1d weight applied on the two input convs' operand load."""
+    eca_fpn Conv1d weight applied on the two input convs' operand load.
+    padded_out: when the quarter branches are zero-padded to a multiple of 4
+    channels, return (padded tensor, index of each real channel) instead of
+    copying the real channels out (the heads read the padded layout)."""
     q = ssh.conv5X5_1[0].out_channels
     qp = _pad_to4(q)
 
@@ -759,10 +795,10 @@ def ssh_train(ssh, o, eca_w=None):
             g, bt = bn.weight, bn.bias
             stats.append((bn.running_mean, bn.running_var, bn.momentum, bn.eps))
         gb += [g, bt]
-        if bn.num_batches_tracked is not None:
-            bn.num_batches_tracked.add_(1)
+        _count_batch(bn)
     if qp == q:
-        return SshTailFn.apply(a, b, c, *gb, stats)
+        f = SshTailFn.apply(a, b, c, *gb, stats)
+        return (f, None) if padded_out else f
     # padded branches: track running stats on padded copies, then copy back
     padded = []
     for i, (bn, t) in enumerate(zip(bns, (a, b, c))):
@@ -777,8 +813,12 @@ def ssh_train(ssh, o, eca_w=None):
         for bn, rm, rv in padded:
             bn.running_mean.copy_(rm[: bn.running_mean.shape[0]])
             bn.running_var.copy_(rv[: bn.running_var.shape[0]])
-    # drop the zero pad channels of the 10-channel branches
     half = a.shape[3]
+    if padded_out:
+        idx = (list(range(half)) + list(range(half, half + q))
+               + list(range(half + qp, half + qp + q)))
+        return f, torch.tensor(idx, dtype=torch.long, device=f.device)
+    # drop the zero pad channels of the 10-channel branches
     f = torch.cat([f[..., :half], f[..., half:half + q], f[..., half + qp:half + qp + q]], -1)
     return f.contiguous()
 
@@ -790,23 +830,27 @@ def _head(m, feats, eca_names, nlm):
     ew = m.eca_fpn.conv.weight
     if gate == "beca":
         from .ops import BecaFn
-        feats_out = [ssh_train(ssh, BecaFn.apply(o, ew.reshape(-1)))
-                     for o, ssh in zip((o1, o2, o3), (m.ssh1, m.ssh2, m.ssh3))]
+        outs = [ssh_train(ssh, BecaFn.apply(o, ew.reshape(-1)), padded_out=True)
+                for o, ssh in zip((o1, o2, o3), (m.ssh1, m.ssh2, m.ssh3))]
     else:
-        feats_out = [ssh_train(ssh, o, ew)
-                     for o, ssh in zip((o1, o2, o3), (m.ssh1, m.ssh2, m.ssh3))]
+        outs = [ssh_train(ssh, o, ew, padded_out=True)
+                for o, ssh in zip((o1, o2, o3), (m.ssh1, m.ssh2, m.ssh3))]
     wb = []
     for i in range(3):
         for h in (m.BboxHead[i], m.ClassHead[i], m.LandmarkHead[i]):
             wb += [h.conv1x1.weight, h.conv1x1.bias]
-    return HeadsFn.apply(*feats_out, *wb)
+    return HeadsFn.apply(*[f for f, _ in outs], tuple(ci for _, ci in outs), *wb)
 
 
 def train_forward(model, kind, x):
     if model.mode != "train":
         raise NotImplementedError("training-mode forward returns logits (mode='train'); the "
                                   "reference's training scripts construct RetinaFace that way")
-    x = x.contiguous()
+    with _BatchCounts():
+        return _train_forward(model, kind, x.contiguous())
+
+
+def _train_forward(model, kind, x):
     if kind == "mnv3":
         body = model.body
         s = bn_act(conv(x, body.conv1, 2, 1, nchw_in=True), body.bn1, "hswish")

@@ -1,4 +1,5 @@
 """Weight packing into the MFMA fragment order (conv.hip header) — CPU."""
+import pytest
 import torch
 
 from jabd_amd import functional as F
@@ -41,3 +42,25 @@ def test_pack_tn_choices():
     for c in (112, 160, 480, 672, 960, 2048):
         tn = lib().jabd_conv_pack_tn(c)
         assert tn in (4, 5, 8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,transposed", [((64, 16, 1, 1), False), ((64, 16, 1, 1), True),
+                                               ((40, 40, 3, 3), False), ((40, 40, 3, 3), True),
+                                               ((12, 10, 3, 3), True), ((160, 960, 1, 1), False),
+                                               ((256, 64, 3, 3), True), ((16, 3, 3, 3), False),
+                                               ((10, 12, 3, 3), False)])
+def test_device_pack_matches_host_pack(cuda, shape, transposed):
+    """jabd_conv_pack_f32 (the training convs' per-step repack) writes exactly
+    the host PackedConv layouts, both the 16x16x4 and the 32x32x2 one."""
+    w = torch.randn(shape, generator=torch.Generator().manual_seed(sum(shape))).to(cuda)
+    wt = w.transpose(0, 1) if transposed else w
+    ref = F.PackedConv(F.conv_weight_2d(wt).contiguous(), None, shape[2], shape[3], wt.shape[1])
+    got = F.pack_weight_device(w, transposed)
+    for a in ("KH", "KW", "Cin", "Cout", "tn", "Ntiles", "Kc"):
+        assert getattr(got, a) == getattr(ref, a), a
+    assert torch.equal(got.w, ref.w)
+    assert (got.w32 is None) == (ref.w32 is None)
+    if ref.w32 is not None:
+        assert got.ntiles32 == ref.ntiles32 and got.tn32 == ref.tn32
+        assert torch.equal(got.w32, ref.w32)

@@ -210,7 +210,7 @@ def test_headsfn_grads(cuda, C):
     sum((o * d).sum() for o, d in zip(outs, dys)).backward()
     fg = [_nhwc(f).to(cuda).requires_grad_() for f in feats]
     wg = [torch.nn.Parameter(t.to(cuda)) for t in wb]
-    og = HeadsFn.apply(*fg, *wg)
+    og = HeadsFn.apply(*fg, (None, None, None), *wg)
     for o, r in zip(og, outs):
         assert rel_err(o.detach(), r.detach()) < TOL
     sum((o * d.float().to(cuda)).sum() for o, d in zip(og, dys)).backward()
