@@ -459,6 +459,15 @@ int jabd_bn_act_bwd_f32(const float* dy, int32_t lddy, int32_t dyc0, const float
                         const float* invstd, const float* gamma, const float* beta, int32_t act,
                         float slope, float* part, float* dgamma, float* dbeta, float* dx,
                         float* dres, jabd_stream_t stream);
+/* The same with the incoming gradient mapped per (image, channel) first:
+ * dy' = dy * dys[b][c] + dya[b][c], b = row / hw (dys NULL: no map) — the
+ * backward of an ECA gate that followed this BN (jabd_eca_bwd_terms_f32). */
+int jabd_bn_act_bwd_ex_f32(const float* dy, int32_t lddy, int32_t dyc0, const float* x,
+                           int32_t ldx, const float* res, int32_t ldr, int64_t M, int32_t C,
+                           const float* mean, const float* invstd, const float* gamma,
+                           const float* beta, int32_t act, float slope, const float* dys,
+                           const float* dya, int64_t hw, float* part, float* dgamma,
+                           float* dbeta, float* dx, float* dres, jabd_stream_t stream);
 /* Conv weight gradient (fp32 MFMA): x/geometry as the forward jabd_conv_args
  * with `y` pointing at dY; dw in torch layout [Cout][Cin][KH][KW]; part is
  * scratch of jabd_conv_wgrad_part_floats() floats.  The data gradient is
@@ -483,6 +492,12 @@ int jabd_eca_bwd_f32(const float* da, const float* x, int64_t B, int64_t HW, int
                      const float* scale, const float* mean, const float* w1d, int32_t k,
                      int32_t gate, float* part, int32_t nblk, float* dmean_ws, float* dw1d_ws,
                      float* dx, float* dw1d, jabd_stream_t stream);
+/* jabd_eca_bwd_f32 without the dx pass: dmean_ws [B][C] is the additive
+ * term, so dx = da * scale + dmean_ws (applied by the consumer). */
+int jabd_eca_bwd_terms_f32(const float* da, const float* x, int64_t B, int64_t HW, int32_t C,
+                           const float* scale, const float* mean, const float* w1d, int32_t k,
+                           int32_t gate, float* part, int32_t nblk, float* dmean_ws,
+                           float* dw1d_ws, float* dw1d, jabd_stream_t stream);
 /* dx = da * scale[b][c] and part[b][blk][c] = sum da * x (scale gradient). */
 int jabd_scale_bwd_f32(const float* da, const float* x, int64_t B, int64_t HW, int32_t C,
                        const float* scale, float* part, int32_t nblk, float* dx,

@@ -223,12 +223,26 @@ __global__ __launch_bounds__(kRedThreads) void bn_act_fwd_kernel(
 }
 
 // dz = dy * act'(z);  part[blk][0][c] = sum dz, part[blk][1][c] = sum dz * xhat
+// Optional per-(image, channel) affine map of the incoming gradient,
+// dy' = dy * dys[b][c] + dya[b][c] (b = row / hw): the backward of an ECA
+// gate applied after this BN (x * s[b][c], and the pooled-mean term of the
+// gate's own gradient), fused here instead of a separate pass over dy.
+__device__ __forceinline__ float4 dy_transform(float4 g, const float* __restrict__ dys,
+                                               const float* __restrict__ dya, int64_t b, int C,
+                                               int c) {
+  const float4 sc = *reinterpret_cast<const float4*>(dys + b * C + c);
+  const float4 ad = *reinterpret_cast<const float4*>(dya + b * C + c);
+  return make_float4(fmaf(g.x, sc.x, ad.x), fmaf(g.y, sc.y, ad.y), fmaf(g.z, sc.z, ad.z),
+                     fmaf(g.w, sc.w, ad.w));
+}
+
 __global__ __launch_bounds__(kRedThreads) void bn_bwd_part_kernel(
     const float* __restrict__ dy, int lddy, int dyc0, const float* __restrict__ x, int ldx,
     const float* __restrict__ res, int ldr, int64_t M, int C, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ gamma,
     const float* __restrict__ beta, int act, float slope, int64_t rows_per_blk,
-    float* __restrict__ part) {
+    float* __restrict__ part, const float* __restrict__ dys, const float* __restrict__ dya,
+    int64_t hw) {
   const int C4 = C >> 2;
   const int lanes = C4 < kRedThreads ? C4 : kRedThreads;
   const int rows_pass = kRedThreads / lanes;
@@ -249,7 +263,8 @@ __global__ __launch_bounds__(kRedThreads) void bn_bwd_part_kernel(
       const float4 bt = *reinterpret_cast<const float4*>(beta + c);
       for (int64_t m = m0 + r0; m < m1; m += rows_pass) {
         const float4 v = *reinterpret_cast<const float4*>(x + m * ldx + c);
-        const float4 g = *reinterpret_cast<const float4*>(dy + m * lddy + dyc0 + c);
+        float4 g = *reinterpret_cast<const float4*>(dy + m * lddy + dyc0 + c);
+        if (dys) g = dy_transform(g, dys, dya, m / hw, C, c);
         float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
         if (res) r = *reinterpret_cast<const float4*>(res + m * ldr + c);
         float xh[4] = {(v.x - mu.x) * is.x, (v.y - mu.y) * is.y, (v.z - mu.z) * is.z,
@@ -300,7 +315,8 @@ __global__ __launch_bounds__(kRedThreads) void bn_bwd_apply_kernel(
     const float* __restrict__ res, int ldr, int64_t M, int C, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ gamma,
     const float* __restrict__ beta, int act, float slope, const float* __restrict__ sdz,
-    const float* __restrict__ sdzx, float* __restrict__ dx, float* __restrict__ dres, int lanes) {
+    const float* __restrict__ sdzx, float* __restrict__ dx, float* __restrict__ dres, int lanes,
+    const float* __restrict__ dys, const float* __restrict__ dya, int64_t hw) {
   const EwMap e = ew_map(lanes, C >> 2);
   if (!e.ok) return;
   const int c = e.cg * 4;
@@ -320,7 +336,8 @@ __global__ __launch_bounds__(kRedThreads) void bn_bwd_apply_kernel(
     const int64_t m = e.m0 + (int64_t)k * e.rows_pass;
     if (m >= M) break;
     const float4 v = *reinterpret_cast<const float4*>(x + m * ldx + c);
-    const float4 g = *reinterpret_cast<const float4*>(dy + m * lddy + dyc0 + c);
+    float4 g = *reinterpret_cast<const float4*>(dy + m * lddy + dyc0 + c);
+    if (dys) g = dy_transform(g, dys, dya, m / hw, C, c);
     float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
     if (res) r = *reinterpret_cast<const float4*>(res + m * ldr + c);
     const float vv[4] = {v.x, v.y, v.z, v.w}, gg[4] = {g.x, g.y, g.z, g.w},
@@ -1321,14 +1338,28 @@ extern "C" int jabd_bn_act_bwd_f32(const float* dy, int32_t lddy, int32_t dyc0, 
                                    const float* gamma, const float* beta, int32_t act,
                                    float slope, float* part, float* dgamma, float* dbeta,
                                    float* dx, float* dres, jabd_stream_t stream) {
+  return jabd_bn_act_bwd_ex_f32(dy, lddy, dyc0, x, ldx, res, ldr, M, C, mean, invstd, gamma,
+                                beta, act, slope, nullptr, nullptr, 0, part, dgamma, dbeta, dx,
+                                dres, stream);
+}
+
+extern "C" int jabd_bn_act_bwd_ex_f32(const float* dy, int32_t lddy, int32_t dyc0,
+                                      const float* x, int32_t ldx, const float* res, int32_t ldr,
+                                      int64_t M, int32_t C, const float* mean,
+                                      const float* invstd, const float* gamma, const float* beta,
+                                      int32_t act, float slope, const float* dys,
+                                      const float* dya, int64_t hw, float* part, float* dgamma,
+                                      float* dbeta, float* dx, float* dres,
+                                      jabd_stream_t stream) {
   JABD_REQUIRE(dy && x && mean && invstd && gamma && beta && part && dgamma && dbeta && dx &&
                    C % 4 == 0 && lddy % 4 == 0 && dyc0 % 4 == 0 && ldx % 4 == 0,
                "bn_act_bwd: bad args");
+  JABD_REQUIRE(!dys || (dya && hw > 0 && M % hw == 0), "bn_act_bwd: dy transform needs dya, hw");
   hipStream_t st = as_stream(stream);
   const int64_t per = bn_rows_per_blk(M, C), nblk = cdiv(M, per);
   bn_bwd_part_kernel<<<(unsigned)nblk, kRedThreads, 0, st>>>(dy, lddy, dyc0, x, ldx, res, ldr, M,
                                                             C, mean, invstd, gamma, beta, act,
-                                                            slope, per, part);
+                                                            slope, per, part, dys, dya, hw);
   if (int e = check_launch("bn_bwd_part")) return e;
   bn_bwd_final_kernel<<<(unsigned)cdiv(C, kFinLanes), kFinThreads, 0, st>>>(part, nblk, C,
                                                                             dbeta, dgamma);
@@ -1337,7 +1368,7 @@ extern "C" int jabd_bn_act_bwd_f32(const float* dy, int32_t lddy, int32_t dyc0, 
   const dim3 grid = ew_grid(M, C, lanes);
   bn_bwd_apply_kernel<<<grid, kRedThreads, 0, st>>>(dy, lddy, dyc0, x, ldx, res, ldr, M, C, mean,
                                                     invstd, gamma, beta, act, slope, dbeta,
-                                                    dgamma, dx, dres, lanes);
+                                                    dgamma, dx, dres, lanes, dys, dya, hw);
   return check_launch("bn_bwd_apply");
 }
 
@@ -1484,6 +1515,30 @@ extern "C" int jabd_eca_bwd_f32(const float* da, const float* x, int64_t B, int6
   scale_add_kernel<<<(unsigned)cdiv(total4, 256), 256, 0, st>>>(da, scale, dmean_ws, HW, C, total4,
                                                                 dx);
   if (int e = check_launch("eca_scale_add")) return e;
+  eca_w_reduce_kernel<<<1, 64, 0, st>>>(dw1d_ws, (int)B, k, dw1d);
+  return check_launch("eca_w_reduce");
+}
+
+// The ECA backward without its dx pass: the per-image partials of sum(da * x),
+// the gate backward (dmean term [B][C], the Conv1d weight gradient).  The
+// caller folds dx = da * scale + dmean_ws into the next consumer
+// (jabd_bn_act_bwd_ex_f32's dy transform).
+extern "C" int jabd_eca_bwd_terms_f32(const float* da, const float* x, int64_t B, int64_t HW,
+                                      int32_t C, const float* scale, const float* mean,
+                                      const float* w1d, int32_t k, int32_t gate, float* part,
+                                      int32_t nblk, float* dmean_ws, float* dw1d_ws, float* dw1d,
+                                      jabd_stream_t stream) {
+  JABD_REQUIRE(da && x && scale && mean && w1d && part && dmean_ws && dw1d_ws && dw1d &&
+                   C % 4 == 0 && nblk > 0,
+               "eca_bwd_terms: bad args");
+  hipStream_t st = as_stream(stream);
+  const int64_t per = cdiv(HW, nblk);
+  scale_bwd_kernel<<<dim3((unsigned)nblk, (unsigned)B), 256, 0, st>>>(da, x, scale, HW, C, per,
+                                                                      nblk, nullptr, part);
+  if (int e = check_launch("scale_bwd")) return e;
+  eca_gate_bwd_kernel<<<(unsigned)B, 256, 2 * C * sizeof(float), st>>>(
+      part, nblk, C, mean, scale, w1d, k, gate, 1.f / (float)HW, dmean_ws, dw1d_ws);
+  if (int e = check_launch("eca_gate_bwd")) return e;
   eca_w_reduce_kernel<<<1, 64, 0, st>>>(dw1d_ws, (int)B, k, dw1d);
   return check_launch("eca_w_reduce");
 }

@@ -173,6 +173,11 @@ SIGNATURES = {
     "jabd_eca_bwd_f32": [c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp,
                          c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
     "jabd_scale_bwd_f32": [c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp],
+    "jabd_eca_bwd_terms_f32": [c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32,
+                               c_vp, c_i32, c_vp, c_vp, c_vp, c_vp],
+    "jabd_bn_act_bwd_ex_f32": [c_vp, c_i32, c_i32, c_vp, c_i32, c_vp, c_i32, c_i64, c_i32, c_vp,
+                               c_vp, c_vp, c_vp, c_i32, c_f32, c_vp, c_vp, c_i64, c_vp, c_vp,
+                               c_vp, c_vp, c_vp, c_vp],
     "jabd_heads_gather_f32": [c_vp, c_vp, c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp],
     "jabd_nlm_bwd_attn_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp,
                               c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],

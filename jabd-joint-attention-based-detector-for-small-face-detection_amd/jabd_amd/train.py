@@ -31,6 +31,9 @@ from . import functional as F
 from ._lib import ConvArgs, call, lib
 
 ACT = F.ACT
+# MobileNetV3 Block_eca training as one autograd node (MNv3BlockFn);
+# JABD_FUSED_BLOCKS=0 selects the per-op graph (A/B measurement, tests).
+FUSED_BLOCKS = __import__("os").environ.get("JABD_FUSED_BLOCKS", "1") != "0"
 
 
 def _st():
@@ -654,10 +657,248 @@ def conv(x, m, stride=1, pad=0, nchw_in=False):
     return ConvFn.apply(x, m.weight, m.bias, stride, pad, nchw_in)
 
 
+# ----------------------------------------------------------------------------- fused block
+def _bn_fwd(x, bn, act, slope=0.0, res=None):
+    """Batch-stat BN (+res) + act of NHWC x; running buffers updated in place.
+    Returns (y, (gamma, beta, mean, invstd))."""
+    B, H, W, C = x.shape
+    M = B * H * W
+    nblk = int(lib().jabd_bn_nblk(M, C))
+    part = torch.empty((nblk, 2, C), dtype=torch.float32, device=x.device)
+    mean = torch.empty(C, dtype=torch.float32, device=x.device)
+    invstd = torch.empty_like(mean)
+    call("jabd_bn_stats_f32", x.data_ptr(), C, M, C, part.data_ptr(), mean.data_ptr(),
+         invstd.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+         float(bn.momentum), float(bn.eps), _st())
+    g = bn.weight.detach()
+    b = bn.bias.detach()
+    y = torch.empty_like(x)
+    call("jabd_bn_act_fwd_f32", x.data_ptr(), C, M, C, mean.data_ptr(), invstd.data_ptr(),
+         g.data_ptr(), b.data_ptr(), _p(res), C, ACT[act], float(slope), y.data_ptr(), C, 0,
+         _st())
+    _count_batch(bn)
+    return y, (g, b, mean, invstd)
+
+
+def _bn_bwd(dy, x, st, act, slope=0.0, res=None, want_dres=False, dys=None, dya=None):
+    """Backward of _bn_fwd: (dx, dgamma, dbeta, dres); dys/dya: the per-(image,
+    channel) map of dy (jabd_bn_act_bwd_ex_f32)."""
+    g, b, mean, invstd = st
+    B, H, W, C = x.shape
+    M = B * H * W
+    nblk = int(lib().jabd_bn_nblk(M, C))
+    part = torch.empty((nblk, 2, C), dtype=torch.float32, device=x.device)
+    dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
+    dbeta = torch.empty_like(dgamma)
+    dx = torch.empty_like(x)
+    dres = torch.empty_like(x) if want_dres else None
+    call("jabd_bn_act_bwd_ex_f32", dy.data_ptr(), C, 0, x.data_ptr(), C, _p(res), C, M, C,
+         mean.data_ptr(), invstd.data_ptr(), g.data_ptr(), b.data_ptr(), ACT[act], float(slope),
+         _p(dys), _p(dya), H * W if dys is not None else 0, part.data_ptr(), dgamma.data_ptr(),
+         dbeta.data_ptr(), dx.data_ptr(), _p(dres), _st())
+    return dx, dgamma, dbeta, dres
+
+
+def _conv_fwd(x, weight, bias=None, stride=1, pad=0, ascale=None):
+    pk = _packed(weight, transposed=False)
+    B, H, W, _ = x.shape
+    OH = (H + 2 * pad - pk.KH) // stride + 1
+    OW = (W + 2 * pad - pk.KW) // stride + 1
+    y = torch.empty((B, OH, OW, pk.Cout), dtype=torch.float32, device=x.device)
+    a = _conv_args(x, pk, y, stride, pad, ascale=ascale)
+    if bias is not None:
+        bb = bias.detach()
+        a.bias = bb.data_ptr()
+    call("jabd_conv2d_nhwc_f32", ctypes.byref(a), _st())
+    return y
+
+
+def _dgrad_1x1_res(dy, weight, res):
+    """dx = dgrad of a 1x1 / stride-1 conv, + res added in the GEMM epilogue."""
+    pk = _packed(weight, transposed=True)
+    B, H, W, _ = dy.shape
+    dx = torch.empty((B, H, W, pk.Cout), dtype=torch.float32, device=dy.device)
+    a = _conv_args(dy, pk, dx, 1, 0)
+    if res is not None:
+        a.res, a.res_bs, a.res_ps, a.res_c0 = res.data_ptr(), res.stride(0), res.shape[3], 0
+    call("jabd_conv2d_nhwc_f32", ctypes.byref(a), _st())
+    return dx
+
+
+def _dw_fwd(x, weight, stride):
+    C, _, k, _ = weight.shape
+    wt = weight.detach().reshape(C, k * k).t().contiguous()
+    y, _ = F.dwconv(x, wt, None, k, stride)
+    return y, wt
+
+
+def _dw_bwd(dy, x, wt, k, stride, want_dx=True):
+    B, H, W, C = x.shape
+    OH, OW = dy.shape[1], dy.shape[2]
+    pad = k // 2
+    dx = None
+    if want_dx:
+        dx = torch.empty_like(x)
+        call("jabd_dw_dgrad_f32", dy.data_ptr(), wt.data_ptr(), B, H, W, C, OH, OW, k, stride,
+             pad, dx.data_ptr(), _st())
+    nparts = int(lib().jabd_dw_wgrad_part_floats(B * OH * OW, C, k))
+    part = torch.empty(nparts, dtype=torch.float32, device=x.device)
+    dw = torch.empty((C, 1, k, k), dtype=torch.float32, device=x.device)
+    call("jabd_dw_wgrad_f32", x.data_ptr(), dy.data_ptr(), B, H, W, C, OH, OW, k, stride, pad,
+         part.data_ptr(), dw.data_ptr(), _st())
+    return dx, dw
+
+
+class MNv3BlockFn(torch.autograd.Function):
+    """One Block_eca (nets/mobilenetV3.py:94-150) forward and backward as a
+    single autograd node, so the backward can fuse what per-op nodes cannot:
+
+      * the ECA gate's backward: the consumer conv's data gradient da, the
+        per-image partials sum(da * d) and the gate backward give
+        dd = da * scale + dmean/HW, which is applied inside BN2's backward
+        as its dy map (jabd_bn_act_bwd_ex_f32) — no dx pass over d;
+      * the residual: the skip branch's input gradient is added in the
+        epilogue of conv1's data-gradient GEMM — no autograd add pass.
+
+    Inputs: the block (config + buffers), s, then the parameters in the
+    order of _block_params(blk)."""
+
+    @staticmethod
+    def forward(ctx, blk, s, *params):
+        act = blk.act_name
+        k, stride = blk.kernel_size, blk.stride
+        e_pre = _conv_fwd(s, blk.conv1.weight)
+        e, st1 = _bn_fwd(e_pre, blk.bn1, act)
+        d_pre, wt2 = _dw_fwd(e, blk.conv2.weight, stride)
+        d, st2 = _bn_fwd(d_pre, blk.bn2, act)
+        B, OH, OW, E = d.shape
+        w1 = blk.eca.conv.weight.detach().reshape(-1).float().contiguous()
+        scale, mean = F.eca_gate(F.channel_sums(d), OH * OW, w1, "hsigmoid", return_mean=True)
+        p = _conv_fwd(d, blk.conv3.weight, ascale=scale)
+        sk = blk.skip
+        saved_skip = ()
+        if sk is None:
+            kind, res = "identity", s
+        elif stride == 1:
+            kind = "concat"
+            t_pre = _conv_fwd(s, sk[0].weight, sk[0].bias)
+            res, sts0 = _bn_fwd(t_pre, sk[1], "none")
+            saved_skip = (t_pre,)
+        elif len(sk) == 4:
+            kind = "dw_concat"
+            u_pre, wts = _dw_fwd(s, sk[0].weight, 2)
+            u, sts0 = _bn_fwd(u_pre, sk[1], "none")
+            t_pre = _conv_fwd(u, sk[2].weight, sk[2].bias)
+            res, sts2 = _bn_fwd(t_pre, sk[3], "none")
+            saved_skip = (u_pre, u, t_pre, wts)
+        else:
+            kind = "dw_residual"
+            u_pre, wts = _dw_fwd(s, sk[0].weight, 2)
+            res, sts0 = _bn_fwd(u_pre, sk[1], "none")
+            saved_skip = (u_pre, wts)
+        out, st3 = _bn_fwd(p, blk.bn3, act, res=res)
+        ctx.blk, ctx.kind = blk, kind
+        ctx.stats = [st1, st2, st3] + ([sts0] if kind != "identity" else []) + \
+            ([sts2] if kind == "dw_concat" else [])
+        ctx.save_for_backward(s, e_pre, e, d_pre, d, p, res, scale, mean, wt2, *saved_skip)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        blk, kind = ctx.blk, ctx.kind
+        act = blk.act_name
+        k, stride = blk.kernel_size, blk.stride
+        s, e_pre, e, d_pre, d, p, res, scale, mean, wt2, *sv = ctx.saved_tensors
+        st1, st2, st3 = ctx.stats[:3]
+        dout = dout.contiguous()
+        B, OH, OW, E = d.shape
+        # out = act(bn3(p) + res)
+        dp, dg3, db3, dres = _bn_bwd(dout, p, st3, act, res=res, want_dres=True)
+        # p = conv3(d * scale)
+        dW3 = _wgrad(d, dp, blk.conv3.weight, 1, 0, ascale=scale)
+        da = _dgrad(dp, blk.conv3.weight, 1, 0, OH, OW)
+        # ECA gate terms; BN2's backward applies dd = da * scale + dmean
+        w1 = blk.eca.conv.weight.detach().reshape(-1).float().contiguous()
+        kk = w1.numel()
+        HW = OH * OW
+        nblk = max(1, min(64, HW // 256))
+        part = torch.empty((B, nblk, E), dtype=torch.float32, device=d.device)
+        dmean = torch.empty((B, E), dtype=torch.float32, device=d.device)
+        dw1_img = torch.empty((B, kk), dtype=torch.float32, device=d.device)
+        dweca = torch.empty(kk, dtype=torch.float32, device=d.device)
+        call("jabd_eca_bwd_terms_f32", da.data_ptr(), d.data_ptr(), B, HW, E, scale.data_ptr(),
+             mean.data_ptr(), w1.data_ptr(), kk, ACT["hsigmoid"], part.data_ptr(), nblk,
+             dmean.data_ptr(), dw1_img.data_ptr(), dweca.data_ptr(), _st())
+        dd_pre, dg2, db2, _ = _bn_bwd(da, d_pre, st2, act, dys=scale, dya=dmean)
+        de, dW2 = _dw_bwd(dd_pre, e, wt2, k, stride)
+        de_pre, dg1, db1, _ = _bn_bwd(de, e_pre, st1, act)
+        dW1 = _wgrad(s, de_pre, blk.conv1.weight, 1, 0)
+        # skip branch -> its input gradient, then conv1's data gradient adds it
+        sk = blk.skip
+        skip_grads = ()
+        if kind == "identity":
+            ds_skip = dres
+        elif kind == "concat":
+            (t_pre,) = sv
+            sts0 = ctx.stats[3]
+            dt, dgs, dbs, _ = _bn_bwd(dres, t_pre, sts0, "none")
+            dWs = _wgrad(s, dt, sk[0].weight, 1, 0)
+            dbias = _chan_sum(dt) if sk[0].bias is not None else None
+            ds_skip = _dgrad_1x1_res(dt, sk[0].weight, None)
+            skip_grads = (dWs, dbias, dgs, dbs)
+        elif kind == "dw_concat":
+            u_pre, u, t_pre, wts = sv
+            sts0, sts2 = ctx.stats[3], ctx.stats[4]
+            dt, dg_s3, db_s3, _ = _bn_bwd(dres, t_pre, sts2, "none")
+            dWs2 = _wgrad(u, dt, sk[2].weight, 1, 0)
+            dbias2 = _chan_sum(dt) if sk[2].bias is not None else None
+            du = _dgrad(dt, sk[2].weight, 1, 0, u.shape[1], u.shape[2])
+            du_pre, dg_s1, db_s1, _ = _bn_bwd(du, u_pre, sts0, "none")
+            ds_skip, dWs0 = _dw_bwd(du_pre, s, wts, 3, 2)
+            skip_grads = (dWs0, dg_s1, db_s1, dWs2, dbias2, dg_s3, db_s3)
+        else:
+            u_pre, wts = sv
+            sts0 = ctx.stats[3]
+            du_pre, dg_s1, db_s1, _ = _bn_bwd(dres, u_pre, sts0, "none")
+            ds_skip, dWs0 = _dw_bwd(du_pre, s, wts, 3, 2)
+            skip_grads = (dWs0, dg_s1, db_s1)
+        ds = _dgrad_1x1_res(de_pre, blk.conv1.weight, ds_skip)
+        grads = (dW1, dg1, db1, dW2, dg2, db2, dweca.view_as(blk.eca.conv.weight), dW3, dg3,
+                 db3) + skip_grads
+        return (None, ds) + grads
+
+
+def _block_params(blk):
+    """Parameters of a Block_eca in MNv3BlockFn's gradient order."""
+    ps = [blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight,
+          blk.bn2.bias, blk.eca.conv.weight, blk.conv3.weight, blk.bn3.weight, blk.bn3.bias]
+    sk = blk.skip
+    if sk is None:
+        return ps
+    if blk.stride == 1:
+        return ps + [sk[0].weight, sk[0].bias, sk[1].weight, sk[1].bias]
+    if len(sk) == 4:
+        return ps + [sk[0].weight, sk[1].weight, sk[1].bias, sk[2].weight, sk[2].bias,
+                     sk[3].weight, sk[3].bias]
+    return ps + [sk[0].weight, sk[1].weight, sk[1].bias]
+
+
+def _fused_block_ok(blk, s):
+    if getattr(blk, "gate_kind", "eca") != "eca" or s.shape[3] % 4:
+        return False
+    bns = [blk.bn1, blk.bn2, blk.bn3] + ([m for m in blk.skip if isinstance(m, torch.nn.BatchNorm2d)]
+                                          if blk.skip is not None else [])
+    return all(bn.weight.shape[0] % 4 == 0 and bn.momentum is not None for bn in bns)
+
+
 def _mnv3_block(blk, s):
     """Training graph of Block_eca / Block / Block_eca_G (nets/mobilenetV3.py:
     :140-150, :81-91, :198-208): the gate is ECA on the project conv's load,
     SE or BECA applied explicitly, or none."""
+    if FUSED_BLOCKS and _fused_block_ok(blk, s):
+        ps = _block_params(blk)
+        # a parameter that is None (no conv bias) is passed as None
+        return MNv3BlockFn.apply(blk, s, *ps)
     act = blk.act_name
     e = bn_act(conv(s, blk.conv1), blk.bn1, act)
     d = bn_act(DwConvFn.apply(e, blk.conv2.weight, blk.stride), blk.bn2, act)
