@@ -34,6 +34,9 @@ enum {
 };
 
 const char* jabd_version(void);
+/* sizeof the argument structs (0: jabd_conv_args, 1: jabd_dw_args,
+ * 2: jabd_expdw_args; -1 otherwise) — for bindings to check their mirrors. */
+int64_t jabd_abi_struct_size(int32_t which);
 /* Copies the calling thread's last error message into buf (NUL-terminated). */
 int jabd_last_error(char* buf, size_t len);
 

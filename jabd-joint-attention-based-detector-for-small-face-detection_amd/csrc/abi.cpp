@@ -22,3 +22,13 @@ extern "C" int jabd_last_error(char* buf, size_t len) {
   buf[len - 1] = 0;
   return JABD_OK;
 }
+
+// Sizes of the argument structs, so bindings can check their mirrors.
+extern "C" int64_t jabd_abi_struct_size(int32_t which) {
+  switch (which) {
+    case 0: return (int64_t)sizeof(jabd_conv_args);
+    case 1: return (int64_t)sizeof(jabd_dw_args);
+    case 2: return (int64_t)sizeof(jabd_expdw_args);
+    default: return -1;
+  }
+}

@@ -86,6 +86,7 @@ class ExpDwArgs(ctypes.Structure):
 # name -> argtypes (every function returns int status unless listed in _RESTYPE)
 SIGNATURES = {
     "jabd_version": [],
+    "jabd_abi_struct_size": [c_i32],
     "jabd_last_error": [ctypes.c_char_p, c_size],
     "jabd_decode_f32": [c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_vp, c_vp],
     "jabd_decode_landm_f32": [c_vp, c_vp, c_i64, c_i64, c_f32, c_vp, c_vp],
@@ -211,7 +212,8 @@ _RESTYPE = {"jabd_version": ctypes.c_char_p, "jabd_dw_nblk": ctypes.c_int64,
             "jabd_bn_nblk": ctypes.c_int64, "jabd_conv_wgrad_part_floats": ctypes.c_int64,
             "jabd_dw_wgrad_part_floats": ctypes.c_int64,
             "jabd_adam_num_chunks": ctypes.c_int64, "jabd_beca_ws_floats": ctypes.c_int64,
-            "jabd_adaptive_pool_ws_floats": ctypes.c_int64}
+            "jabd_adaptive_pool_ws_floats": ctypes.c_int64,
+            "jabd_abi_struct_size": ctypes.c_int64}
 
 _lock = threading.Lock()
 _lib = None

@@ -40,3 +40,12 @@ def test_cpu_tensor_is_rejected():
     from jabd_amd import ops
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         ops.nms(torch.zeros(3, 4), torch.zeros(3), 0.3)
+
+
+def test_struct_mirrors_match_the_library():
+    """ctypes mirrors of the argument structs have the C sizes (a field added
+    on one side only would shift every later field)."""
+    import ctypes
+    from jabd_amd._lib import ConvArgs, DwArgs, ExpDwArgs, lib
+    for i, cls in enumerate((ConvArgs, DwArgs, ExpDwArgs)):
+        assert lib().jabd_abi_struct_size(i) == ctypes.sizeof(cls), cls.__name__

@@ -1,6 +1,6 @@
 """Run a few JABD training steps (for rocprofv3 --kernel-trace --stats).
 
-  python3 tools/train_steps.py --kind mnv3|r50 [--batch 32] [--steps 3]
+  python3 tools/train_steps.py --kind mnv3|beca|small|r50 [--batch 32] [--steps 3]
 """
 import argparse
 import os
