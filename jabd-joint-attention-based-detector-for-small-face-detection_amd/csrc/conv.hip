@@ -492,6 +492,190 @@ __global__ __launch_bounds__(256) void conv1x1_kernel(const ConvArgs p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// 3x3 / stride-1 / pad-1 convs with few input channels (Cin <= 64: the SSH
+// branches and FPN merges, Cin 40 / 12 at 128^2 and 64^2).  The generic
+// kernel re-reads every input pixel 9x per K chunk through L1; here a
+// workgroup stages its (8+2) x (16+2) x Cin input window once into LDS
+// (ECA gate applied while staging, zero padding written explicitly) and the
+// four waves — two output rows of 16 pixels each — take every A fragment
+// from LDS.  Same packed weights, MFMA mapping and vector epilogue (split
+// output for the fused SSH branches) as conv_gemm_kernel.
+// ---------------------------------------------------------------------------
+constexpr int k3Cols = 16, k3IC = k3Cols + 2;
+
+template <int TN, int TM>
+__global__ __launch_bounds__(256) void conv3x3_tile_kernel(const ConvArgs p, int tiles_w,
+                                                           int tiles_img) {
+  constexpr int k3Rows = 4 * TM, k3IR = k3Rows + 2;  // TM output rows per wave
+  extern __shared__ float c3_lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, j = lane & 15;
+  const int nblk_n = p.Ntiles / TN;
+  const int nb = blockIdx.x % nblk_n;
+  const int tile = blockIdx.x / nblk_n;
+  const int b = tile / tiles_img;
+  const int tr = tile - b * tiles_img;
+  const int oh0 = (tr / tiles_w) * k3Rows, ow0 = (tr % tiles_w) * k3Cols;
+  const int C4 = p.Cin >> 2;
+  const int PIT = p.Cin + 4;  // pixel pitch in LDS (floats)
+  // stage the input window: (k3IR x k3IC pixels) x Cin channels
+  {
+    const float* xb = p.x + (int64_t)b * p.x_bs + p.x_c0;
+    const float* sb = p.ascale ? p.ascale + (int64_t)b * p.ascale_bs : nullptr;
+    for (int i = threadIdx.x; i < k3IR * k3IC * C4; i += 256) {
+      const int px = i / C4, c4 = i - px * C4;
+      const int r = px / k3IC, c = px - r * k3IC;
+      const int ih = oh0 - 1 + r, iw = ow0 - 1 + c;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ih >= 0 && ih < p.H && iw >= 0 && iw < p.W) {
+        v = *reinterpret_cast<const float4*>(xb + ((int64_t)ih * p.W + iw) * p.x_ps + 4 * c4);
+        if (sb) {
+          const float4 s4 = *reinterpret_cast<const float4*>(sb + 4 * c4);
+          v.x *= s4.x; v.y *= s4.y; v.z *= s4.z; v.w *= s4.w;
+        }
+      }
+      *reinterpret_cast<float4*>(c3_lds + px * PIT + 4 * c4) = v;
+    }
+  }
+  __syncthreads();
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int u = 0; u < TN; ++u) acc[t][u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const float4* wbase = reinterpret_cast<const float4*>(p.w) + ((int64_t)nb * TN) * 64 + lane;
+  const int64_t wstride_k = (int64_t)p.Ntiles * 64;
+  const int Ktot = 9 * p.Cin;
+  // this lane's k4 = 16 kc + 4g walks (tap, channel) incrementally
+  int tci = 4 * g, tap = 0;
+  while (tci >= p.Cin) { tci -= p.Cin; ++tap; }
+  float4 b_cur[TN];
+#pragma unroll
+  for (int u = 0; u < TN; ++u) b_cur[u] = wbase[u * 64];
+  for (int kc = 0; kc < p.Kc; ++kc) {
+    float4 b_nxt[TN];
+    const bool more = kc + 1 < p.Kc;
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < TN; ++u) b_nxt[u] = wbase[(kc + 1) * wstride_k + u * 64];
+    }
+    float4 a[TM];
+    const bool kv = 16 * kc + 4 * g < Ktot;
+    const int kh = tap / 3, kw = tap - 3 * (tap / 3);
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      const int r = wave * TM + t + kh;  // window row
+      a[t] = kv ? *reinterpret_cast<const float4*>(c3_lds + (r * k3IC + j + kw) * PIT + tci)
+                : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u) {
+        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(b_cur[u].x, a[t].x, acc[t][u], 0, 0, 0);
+        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(b_cur[u].y, a[t].y, acc[t][u], 0, 0, 0);
+        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(b_cur[u].z, a[t].z, acc[t][u], 0, 0, 0);
+        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(b_cur[u].w, a[t].w, acc[t][u], 0, 0, 0);
+      }
+    tci += 16;
+    while (tci >= p.Cin) { tci -= p.Cin; ++tap; }
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < TN; ++u) b_cur[u] = b_nxt[u];
+    }
+  }
+  __syncthreads();  // the input window is dead: its LDS becomes the epilogue's
+
+  // epilogue: acc[t][u][r] = Y[pixel (oh0 + wave*TM + t, ow0 + j)][16(nb*TN+u) + 4g + r]
+  constexpr int LDW = 16 * TN + 4;
+  float* sm = c3_lds + wave * 16 * LDW;
+#pragma unroll
+  for (int t = 0; t < TM; ++t) {
+    const int oh = oh0 + wave * TM + t, ow = ow0 + j;
+    const bool pv = oh < p.OH && ow < p.OW;
+#pragma unroll
+    for (int u = 0; u < TN; ++u)
+      *reinterpret_cast<f32x4*>(sm + j * LDW + 16 * u + 4 * g) = acc[t][u];
+    const int64_t pix = (int64_t)oh * p.OW + ow;
+    const long long yoff = pv ? (long long)((int64_t)b * p.y_bs + pix * p.y_ps + p.y_c0) : -1;
+    const long long y2off = p.y2 ? (long long)((int64_t)b * p.y2_bs + pix * p.y2_ps + p.y2_c0) : 0;
+    wave_lds_sync();
+#pragma unroll
+    for (int f0 = 0; f0 < 16 * 4 * TN; f0 += 64) {
+      const int f = f0 + lane;
+      const int q = f / (4 * TN), c4 = f - q * (4 * TN);
+      const long long yo = __shfl(yoff, q);
+      const long long y2o = __shfl(y2off, q);
+      const int n0 = nb * TN * 16 + 4 * c4;
+      if (yo >= 0 && n0 < p.Cout) {
+        float4 v = *reinterpret_cast<const float4*>(sm + q * LDW + 4 * c4);
+        if (p.bias) {
+          const float4 bb = *reinterpret_cast<const float4*>(p.bias + n0);
+          v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
+        }
+        if (p.y2 && n0 >= p.nsplit) {
+          v.x = act_apply(v.x, p.act2, p.slope2);
+          v.y = act_apply(v.y, p.act2, p.slope2);
+          v.z = act_apply(v.z, p.act2, p.slope2);
+          v.w = act_apply(v.w, p.act2, p.slope2);
+          *reinterpret_cast<float4*>(p.y2 + y2o + (n0 - p.nsplit)) = v;
+        } else {
+          v.x = act_apply(v.x, p.act, p.slope);
+          v.y = act_apply(v.y, p.act, p.slope);
+          v.z = act_apply(v.z, p.act, p.slope);
+          v.w = act_apply(v.w, p.act, p.slope);
+          *reinterpret_cast<float4*>(p.y + yo + n0) = v;
+        }
+      }
+    }
+    wave_lds_sync();
+  }
+}
+
+// JABD_CONV3X3_TILE=0 disables the LDS-tiled 3x3 kernel (A/B).
+static bool conv3x3_tile_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("JABD_CONV3X3_TILE");
+    v = e && e[0] == '0' ? 0 : 1;
+  }
+  return v == 1;
+}
+
+static int conv3x3_rows_per_wave() {  // JABD_CONV3X3_TM=2|4 (A/B; 4 measured 5% slower)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("JABD_CONV3X3_TM");
+    v = e && e[0] == '4' ? 4 : 2;
+  }
+  return v;
+}
+
+static int launch_conv3x3_tile(const ConvArgs& a, hipStream_t st) {
+  const int tn = a.tn;
+  int tm = conv3x3_rows_per_wave();
+  if (tm == 4 && (int64_t)a.B * cdiv(a.OH, 16) * cdiv(a.OW, k3Cols) < 1024) tm = 2;
+  const int rows = 4 * tm;
+  const int tiles_w = (int)cdiv(a.OW, k3Cols), tiles_h = (int)cdiv(a.OH, rows);
+  const int tiles_img = tiles_w * tiles_h;
+  const int64_t grid = (int64_t)a.B * tiles_img * (a.Ntiles / tn);
+  JABD_REQUIRE(grid < (int64_t)0x7fffffff, "conv3x3: grid too large");
+  const size_t lds_in = (size_t)(rows + 2) * k3IC * (a.Cin + 4) * sizeof(float);
+  const size_t lds_epi = (size_t)4 * 16 * (16 * tn + 4) * sizeof(float);
+  const size_t lds = std::max(lds_in, lds_epi);
+  if (lds > 64 * 1024) return -1;
+#define C3_CASE(TN_, TM_)                                                                    \
+  if (tn == TN_ && tm == TM_) {                                                              \
+    conv3x3_tile_kernel<TN_, TM_><<<(unsigned)grid, 256, lds, st>>>(a, tiles_w, tiles_img);  \
+    return check_launch("conv3x3_tile");                                                     \
+  }
+  C3_CASE(1, 2) C3_CASE(2, 2) C3_CASE(3, 2) C3_CASE(1, 4) C3_CASE(2, 4) C3_CASE(3, 4)
+#undef C3_CASE
+  return -1;
+}
+
 template <int TM, int TN>
 static int launch_1x1(const ConvArgs& a, hipStream_t st) {
   const int64_t grid = cdiv(a.M, (int64_t)4 * 16 * TM) * (a.Ntiles / TN);
@@ -648,6 +832,12 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
       (!a.tconv || a.stride == 1 || (a.stride == 2 && !a.ascale)) && a.x_bs % 4 == 0 &&
       a.y_bs == OHW * a.y_ps && (!a.res || a.res_bs == OHW * a.res_ps) && use_conv32(a)) {
     const int r = conv1x1_m32_dispatch(a, st, true);
+    if (r >= 0) return r;
+  }
+  if (!is1x1 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && !a.tconv && !a.nchw_in &&
+      !a.x2 && !a.res && vec4 && (a.flags & 1) && a.Cin <= 64 && a.tn <= 3 &&
+      (!a.ascale || a.ascale_bs % 4 == 0) && conv3x3_tile_on()) {
+    const int r = launch_conv3x3_tile(a, st);
     if (r >= 0) return r;
   }
   // Pixel tiles per wave: 4 x 16 by default; small-M layers (the SSH / FPN

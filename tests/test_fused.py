@@ -82,3 +82,43 @@ def test_stem_parity(cuda, act, hw):
     got = y.permute(0, 3, 1, 2).cpu()
     assert got.shape == ref.shape
     assert rel_err(got, ref) < 2e-6, rel_err(got, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,split,hw,gate", [(40, 40, 0, (128, 96), False),
+                                                     (40, 32, 20, (37, 29), True),
+                                                     (12, 24, 12, (23, 50), False),
+                                                     (64, 48, 0, (9, 17), True),
+                                                     (12, 12, 0, (3, 5), False)])
+def test_conv3x3_tile_parity(cuda, cin, cout, split, hw, gate):
+    """The LDS-tiled 3x3 / stride-1 kernel (conv3x3_tile_kernel: SSH branches,
+    FPN merges) vs torch fp32 conv2d: ragged tiles, the ECA gate applied while
+    staging, and the split output of the fused SSH branches."""
+    from jabd_amd import functional as F
+    H, W = hw
+    g = torch.Generator().manual_seed(cin * 7 + cout + H)
+    B = 2
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (9 * cin) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    sc = torch.rand(B, cin, generator=g) if gate else None
+    xin = x * sc[:, :, None, None] if gate else x
+    ref = tF.conv2d(xin, w, b, padding=1)
+    conv = torch.nn.Conv2d(cin, cout, 3, padding=1)
+    with torch.no_grad():
+        conv.weight.copy_(w)
+        conv.bias.copy_(b)
+    pk = F.pack_conv(conv.to(cuda))
+    xg = x.permute(0, 2, 3, 1).contiguous().to(cuda)
+    asc = sc.to(cuda).contiguous() if gate else None
+    if split:
+        y = torch.empty((B, H, W, split), device=cuda)
+        y2 = torch.empty((B, H, W, cout - split), device=cuda)
+        F.conv(xg, pk, pad=1, act="relu", ascale=asc, out=y, y2=y2, nsplit=split,
+               act2="leaky", slope2=0.1)
+        got = torch.cat([y, y2], -1).permute(0, 3, 1, 2).cpu()
+        want = torch.cat([tF.relu(ref[:, :split]), tF.leaky_relu(ref[:, split:], 0.1)], 1)
+    else:
+        got = F.conv(xg, pk, pad=1, act="relu", ascale=asc).permute(0, 3, 1, 2).cpu()
+        want = tF.relu(ref)
+    assert rel_err(got, want) < 2e-5, rel_err(got, want)
