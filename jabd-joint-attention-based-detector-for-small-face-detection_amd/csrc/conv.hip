@@ -500,7 +500,8 @@ __global__ __launch_bounds__(256) void conv1x1_kernel(const ConvArgs p) {
 // (ECA gate applied while staging, zero padding written explicitly) and the
 // four waves — two output rows of 16 pixels each — take every A fragment
 // from LDS.  Same packed weights, MFMA mapping and vector epilogue (split
-// output for the fused SSH branches) as conv_gemm_kernel.
+// output for the fused SSH branches) as conv_gemm_kernel.  tconv = 1 (the
+// stride-1 data gradient, transposed weights) reads the window flipped.
 // ---------------------------------------------------------------------------
 constexpr int k3Cols = 16, k3IC = k3Cols + 2;
 
@@ -563,7 +564,13 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(const ConvArgs p, int
     }
     float4 a[TM];
     const bool kv = 16 * kc + 4 * g < Ktot;
-    const int kh = tap / 3, kw = tap - 3 * (tap / 3);
+    // forward: tap (kh, kw) reads window offset (kh, kw); the stride-1 data
+    // gradient (tconv) reads dy at (oh + 1 - kh, ow + 1 - kw): offset (2-kh, 2-kw)
+    int kh = tap / 3, kw = tap - 3 * (tap / 3);
+    if (p.tconv) {
+      kh = 2 - kh;
+      kw = 2 - kw;
+    }
 #pragma unroll
     for (int t = 0; t < TM; ++t) {
       const int r = wave * TM + t + kh;  // window row
@@ -634,14 +641,15 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(const ConvArgs p, int
   }
 }
 
-// JABD_CONV3X3_TILE=0 disables the LDS-tiled 3x3 kernel (A/B).
-static bool conv3x3_tile_on() {
+// JABD_CONV3X3_TILE=0 disables the LDS-tiled 3x3 kernel, =2 keeps it for
+// forward convs only (A/B).
+static bool conv3x3_tile_on(bool tconv) {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("JABD_CONV3X3_TILE");
-    v = e && e[0] == '0' ? 0 : 1;
+    v = e && e[0] == '0' ? 0 : (e && e[0] == '2' ? 2 : 1);
   }
-  return v == 1;
+  return v == 1 || (v == 2 && !tconv);
 }
 
 static int conv3x3_rows_per_wave() {  // JABD_CONV3X3_TM=2|4 (A/B; 4 measured 5% slower)
@@ -834,9 +842,9 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
     const int r = conv1x1_m32_dispatch(a, st, true);
     if (r >= 0) return r;
   }
-  if (!is1x1 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && !a.tconv && !a.nchw_in &&
+  if (!is1x1 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && !a.nchw_in &&
       !a.x2 && !a.res && vec4 && (a.flags & 1) && a.Cin <= 64 && a.tn <= 3 &&
-      (!a.ascale || a.ascale_bs % 4 == 0) && conv3x3_tile_on()) {
+      (!a.ascale || a.ascale_bs % 4 == 0) && conv3x3_tile_on(a.tconv)) {
     const int r = launch_conv3x3_tile(a, st);
     if (r >= 0) return r;
   }
