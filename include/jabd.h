@@ -383,6 +383,12 @@ typedef struct jabd_expdw_args {
   int32_t k, stride, act, nblk;
   float* y; int64_t y_bs; int32_t y_ps, OH, OW, reserved0;
   float* part;
+  /* optional (stride 2 only; sy NULL: none): the block's skip branch
+   * dw3x3/s2 + folded BN on the same input tile — sw [9][Cin] tap-major, sb
+   * [Cin] — written to sy [B][OH][OW][Cin] (pixel stride sy_ps, image stride
+   * sy_bs) by the first expanded-channel chunk's workgroups
+   * (nets/mobilenetV3.py:126-137, the K-concat source of the project GEMM). */
+  const float* sw; const float* sb; float* sy; int64_t sy_bs; int32_t sy_ps, reserved1;
 } jabd_expdw_args;
 int64_t jabd_expand_dw_nblk(int32_t OH, int32_t OW, int32_t k, int32_t stride);
 int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_t stream);

@@ -150,16 +150,25 @@ __device__ __forceinline__ void dw_lane(int l, int& c4, int& sl) {
     sl = 4 * (2 * h + par) + k;
   }
 }
-template <int K, int S, int TH, int TW, int EC, int ACT, int KP>
+template <int K, int S, int TH, int TW, int EC, int ACT, int KP, bool SKIP = false>
 __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p, const XdDivs dv,
                                                        int nitems) {
   using C = XdCfg<K, S, TH, TW, EC>;
   constexpr int NPF = (C::IPAD * 4 + 255) / 256;
   constexpr int NWD = (K * K + 1) * C::NC4;
+  constexpr int SKC = SKIP ? 160 : 4;  // skip-branch taps staged in LDS (Cin <= 160)
   __shared__ __attribute__((aligned(16))) float lds[C::LDS];
   __shared__ float4 wsh[K * K + 1][C::NC4];
+  __shared__ float4 sws[10][SKC / 4];  // 9 taps + bias of the skip dw, channel quads
   XdItem it;
   if (!xd_item<K, S, TH, TW, EC>(p, blockIdx.x, dv, nitems, it)) return;
+  const bool skip = SKIP && it.c0 == 0;
+  if (skip) {
+    for (int i = threadIdx.x; i < 10 * (p.Cin >> 2); i += 256) {
+      const int q = i / (p.Cin >> 2), c4 = i - q * (p.Cin >> 2);
+      sws[q][c4] = *reinterpret_cast<const float4*>((q < 9 ? p.sw + q * p.Cin : p.sb) + 4 * c4);
+    }
+  }
   // the whole input tile (halo included) inside the image: no per-pixel
   // bounds in the loads or the expanded-tile epilogue (most tiles)
   const bool interior =
@@ -234,6 +243,34 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
       asm volatile("" : "+v"(a));
       lds_barrier();
       if (kc + KP < p.Kc) load_stage(kc + KP, pf[s]);
+      // fused skip branch (stride 2, first chunk's workgroups): this stage's
+      // 16 channels for output pixel t & 63, channel quad t >> 6, taps from LDS
+      const int sc = 16 * kc + 4 * (t >> 6);
+      if (skip && sc < p.Cin) {
+        // output (orow, ocol) of the TH x TW tile reads tile pixels
+        // (2 orow + kh + PAD - 1, 2 ocol + kw + PAD - 1): the dw3x3/s2/p1 window
+        const int op = t & 63, orow = op / TW, ocol = op - orow * TW;
+        const int oh = it.oh0 + orow, ow = it.ow0 + ocol;
+        if (orow < TH && oh < p.OH && ow < p.OW) {
+          const int sq = sc >> 2;
+          float4 v = sws[9][sq];
+          const float* xq = lds + ((t >> 6) * C::IPAD) * 4;
+#pragma unroll 1
+          for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+              const int px = (2 * orow + kh + C::PAD - 1) * C::IW + 2 * ocol + kw + C::PAD - 1;
+              const float4 xv = *reinterpret_cast<const float4*>(xq + px * 4);
+              const float4 wv = sws[kh * 3 + kw][sq];
+              v.x = fmaf(xv.x, wv.x, v.x);
+              v.y = fmaf(xv.y, wv.y, v.y);
+              v.z = fmaf(xv.z, wv.z, v.z);
+              v.w = fmaf(xv.w, wv.w, v.w);
+            }
+          *reinterpret_cast<float4*>(p.sy + (int64_t)it.b * p.sy_bs +
+                                     ((int64_t)oh * p.OW + ow) * p.sy_ps + sc) = v;
+        }
+      }
       // a wave whose 16-channel tile lies past E skips its MFMAs (wave-uniform;
       // its accumulators are masked in the epilogue)
       if (ntv) {
@@ -426,6 +463,10 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
                "expand_dw: unsupported geometry");
   JABD_REQUIRE(a.act == ACT_NONE || a.act == ACT_RELU || a.act == ACT_HSWISH,
                "expand_dw: act %d", a.act);
+  JABD_REQUIRE(!a.sy || (a.stride == 2 && a.sw && a.sb && a.sy_ps % 4 == 0 && a.sy_ps >= a.Cin &&
+                         a.Cin <= 160),
+               "expand_dw: the fused skip branch needs stride 2, Cin <= 160, weights, bias and "
+               "sy_ps %% 4 == 0");
   const XdTile tl = xd_tile(a.k, a.stride);
   const int tiles_w = (int)cdiv(a.OW, tl.tw);
   const int tiles_img = (int)cdiv(a.OH, tl.th) * tiles_w;
@@ -450,7 +491,10 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
                "expand_dw: input must be < 4 GiB (buffer-descriptor offsets)");
 #define XD_LAUNCH(K_, S_, TH_, TW_, EC_, ACT_)                                                \
   do {                                                                                        \
-    if (a.Kc == 1 || xd_kp() == 1)                                                            \
+    if (S_ == 2 && a.sy)                                                                      \
+      expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1, true><<<(unsigned)nitems, 256, 0, st>>>( \
+          a, dv, (int)nitems);                                                                \
+    else if (a.Kc == 1 || xd_kp() == 1)                                                       \
       expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1><<<(unsigned)nitems, 256, 0, st>>>(       \
           a, dv, (int)nitems);                                                                \
     else if (a.Kc == 2 || xd_kp() == 2)                                                       \

@@ -80,6 +80,8 @@ class ExpDwArgs(ctypes.Structure):
         ("y", c_vp), ("y_bs", c_i64), ("y_ps", c_i32), ("OH", c_i32), ("OW", c_i32),
         ("reserved0", c_i32),
         ("part", c_vp),
+        ("sw", c_vp), ("sb", c_vp), ("sy", c_vp), ("sy_bs", c_i64), ("sy_ps", c_i32),
+        ("reserved1", c_i32),
     ]
 
 

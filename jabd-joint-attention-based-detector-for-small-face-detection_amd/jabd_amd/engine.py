@@ -31,6 +31,9 @@ NLM_SIZES_DEFAULT = (1, 4, 8, 12)
 # MNv3 blocks run expand 1x1 + depthwise as one kernel (csrc/expdw.hip);
 # JABD_FUSE_EXPAND_DW=0 selects the two-kernel path (A/B measurement, tests).
 FUSE_EXPAND_DW = os.environ.get("JABD_FUSE_EXPAND_DW", "1") != "0"
+# ... and the stride-2 blocks' dw3x3 skip branch into that kernel (it stages
+# the same input tile); JABD_FUSE_SKIP=0 runs it as its own dw launch.
+FUSE_SKIP = os.environ.get("JABD_FUSE_SKIP", "1") != "0"
 
 
 def _w1d(eca):
@@ -265,9 +268,15 @@ class _MNv3Block:
         return None
 
     def forward(self, x):
+        t = None
         if FUSE_EXPAND_DW:
-            d, part = F.expand_dw(x, self.expand, self.dw_w, self.dw_b, self.k, self.stride,
-                                  act=self.act, partials=self.gate == "eca")
+            fuse_skip = FUSE_SKIP and self.skip_dw is not None and self.stride == 2
+            r = F.expand_dw(x, self.expand, self.dw_w, self.dw_b, self.k, self.stride,
+                            act=self.act, partials=self.gate == "eca",
+                            skip=self.skip_dw if fuse_skip else None)
+            d, part = r[0], r[1]
+            if fuse_skip:
+                t = r[2]
         else:
             e = F.conv(x, self.expand, act=self.act)
             d, part = F.dwconv(e, self.dw_w, self.dw_b, self.k, self.stride, act=self.act,
@@ -277,7 +286,8 @@ class _MNv3Block:
             return F.conv(d, self.project, act=self.act, ascale=sc, res=x)
         if self.kind == "concat":
             return F.conv(d, self.project, act=self.act, ascale=sc, x2=x)
-        t, _ = F.dwconv(x, self.skip_dw[0], self.skip_dw[1], 3, 2)
+        if t is None:
+            t, _ = F.dwconv(x, self.skip_dw[0], self.skip_dw[1], 3, 2)
         if self.kind == "dw_concat":
             return F.conv(d, self.project, act=self.act, ascale=sc, x2=t)
         return F.conv(d, self.project, act=self.act, ascale=sc, res=t)

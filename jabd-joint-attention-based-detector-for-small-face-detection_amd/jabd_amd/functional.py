@@ -268,9 +268,11 @@ def dwconv(x, w, bias, k, stride, act="none", slope=0.0, partials=False):
 _XD_DBG = 0  # kernel-phase skip mask for tools/convbench.py timing experiments only
 
 
-def expand_dw(x, pk, w, bias, k, stride, act="none", partials=True):
+def expand_dw(x, pk, w, bias, k, stride, act="none", partials=True, skip=None):
     """Fused expand 1x1 (PackedConv pk, folded BN) + act -> depthwise k x k
-    (pad k//2, folded BN) + act; returns (y, ECA partials [B, nblk, E])."""
+    (pad k//2, folded BN) + act; returns (y, ECA partials [B, nblk, E]).
+    skip = (w [9][Cin], bias [Cin]) (stride 2): the block's dw3x3/s2 skip
+    branch computed from the same input tile; returns (y, partials, t)."""
     _check("expand_dw.x", x)
     B, H, W, C = x.shape
     if pk.KH != 1 or pk.KW != 1 or pk.Cin != C or pk.Cin2:
@@ -293,8 +295,13 @@ def expand_dw(x, pk, w, bias, k, stride, act="none", partials=True):
         nb = int(lib().jabd_expand_dw_nblk(OH, OW, k, stride))
         part = torch.empty((B, nb, E), dtype=torch.float32, device=x.device)
         a.nblk, a.part = nb, part.data_ptr()
+    t = None
+    if skip is not None:
+        t = torch.empty((B, OH, OW, C), dtype=torch.float32, device=x.device)
+        a.sw, a.sb = skip[0].data_ptr(), skip[1].data_ptr()
+        a.sy, a.sy_bs, a.sy_ps = t.data_ptr(), t.stride(0), C
     call("jabd_expand_dw_nhwc_f32", ctypes.byref(a), _stream())
-    return y, part
+    return (y, part, t) if skip is not None else (y, part)
 
 
 def channel_sums(x, nblk=None):

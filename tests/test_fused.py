@@ -56,6 +56,22 @@ def test_expand_dw_parity(cuda, spec, hw):
     # ECA pool partials: per-image channel sums of the activated output
     sums = part.sum(1).cpu().double()
     assert rel_err(sums, ref.double().sum((2, 3))) < 1e-5
+    if s == 2:  # the block's dw3x3/s2 + BN skip branch fused on the same input tile
+        sdw = torch.nn.Conv2d(cin, cin, 3, 2, 1, groups=cin, bias=False)
+        sbn = torch.nn.BatchNorm2d(cin)
+        with torch.no_grad():
+            sdw.weight.copy_(torch.randn(sdw.weight.shape, generator=g) / 3)
+            sbn.weight.copy_(1 + 0.2 * torch.randn(cin, generator=g))
+            sbn.bias.copy_(0.3 * torch.randn(cin, generator=g))
+            sbn.running_mean.copy_(0.1 * torch.randn(cin, generator=g))
+            sbn.running_var.copy_(0.5 + torch.rand(cin, generator=g))
+            sref = sbn.eval()(sdw(x))
+        skw, skb = F.pack_dw(sdw.to(cuda), sbn.to(cuda))
+        y3, part3, t = F.expand_dw(xg, pk, dw_w, dw_b, k, s, act=act, skip=(skw, skb))
+        assert torch.equal(y3, y)
+        assert rel_err(t.permute(0, 3, 1, 2).cpu(), sref) < 2e-5
+        t2, _ = F.dwconv(xg, skw, skb, 3, 2)
+        assert rel_err(t, t2) < 2e-6
     # the two-kernel path computes the same tensor
     e = F.conv(xg, pk, act=act)
     y2, part2 = F.dwconv(e, dw_w, dw_b, k, s, act=act, partials=True)
