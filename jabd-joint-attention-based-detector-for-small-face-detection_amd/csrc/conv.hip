@@ -758,6 +758,7 @@ static bool conv_generic_only() {
 
 namespace jabd {
 int conv1x1_m32_dispatch(const ConvArgs& a, hipStream_t st, bool kxk);
+int conv1x1_stream_dispatch(const ConvArgs& a, hipStream_t st);
 }
 
 // Which 1x1 kernel: the 32x32x2 LDS-weight kernel (conv32.hip) pays off when
@@ -833,6 +834,10 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
       (a.M + 64) * (maxps + 16) < ((int64_t)1 << 31) && !conv_generic_only();
   if (fast1x1 && use_conv32(a)) {
     const int r = conv1x1_m32_dispatch(a, st, false);
+    if (r >= 0) return r;
+  }
+  if (fast1x1 && !a.reserved1) {  // short-K / narrow-N: streaming kernel (conv_stream.hip)
+    const int r = conv1x1_stream_dispatch(a, st);
     if (r >= 0) return r;
   }
   // k x k implicit GEMM on the 32x32 kernel: 32-channel stages inside one tap
