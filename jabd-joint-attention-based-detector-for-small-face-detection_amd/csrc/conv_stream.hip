@@ -47,8 +47,18 @@ __device__ __forceinline__ float cs_act(float v, int act, float slope) {
 // KC >= p.Kc stages are compiled; stages past p.Kc issue a load of the last
 // real stage (an L1 hit, keeps the load sequence unpredicated) and skip their
 // MFMAs (wave-uniform branch).
+// Workgroup: 4 waves; 8 when the weights exceed 24 KiB (Kc x Ntiles > 24: the
+// Cout = 80 layers), so the one workgroup that fits a CU's LDS still gives
+// each SIMD two waves.
+template <int TN, int KC>
+struct CsCfg {
+  static constexpr int NW = KC * TN > 24 ? 8 : 4;
+};
+
 template <int TN, int KC, int X2, bool AS>
-__global__ __launch_bounds__(256) void conv1x1_stream_kernel(const ConvArgs p, int nblk, int ohw) {
+__global__ __launch_bounds__((CsCfg<TN, KC>::NW * 64)) void conv1x1_stream_kernel(const ConvArgs p,
+                                                                                int nblk, int ohw) {
+  constexpr int NW = CsCfg<TN, KC>::NW, NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   f32x4* wl = reinterpret_cast<f32x4*>(smem);
   float4* gl = reinterpret_cast<float4*>(smem + p.Kc * TN * 64 * 4);
@@ -57,18 +67,18 @@ __global__ __launch_bounds__(256) void conv1x1_stream_kernel(const ConvArgs p, i
   {
     const f32x4* ws = reinterpret_cast<const f32x4*>(p.w);
     const int nw = p.Kc * TN * 64;
-    for (int i = t; i < nw; i += 256) wl[i] = ws[i];
+    for (int i = t; i < nw; i += NT) wl[i] = ws[i];
     if (AS) {
       const int c4n = p.Cin >> 2;
-      for (int i = t; i < p.B * c4n; i += 256) {
+      for (int i = t; i < p.B * c4n; i += NT) {
         const int b = i / c4n, c = i - b * c4n;
         gl[i] = *reinterpret_cast<const float4*>(p.ascale + (int64_t)b * p.ascale_bs + 4 * c);
       }
     }
   }
   __syncthreads();
-  const int nwv = gridDim.x * 4;
-  int blk = blockIdx.x * 4 + wave;
+  const int nwv = gridDim.x * NW;
+  int blk = blockIdx.x * NW + wave;
   if (blk >= nblk) return;  // no barrier below
   const int M = (int)p.M, Cin = p.Cin, Ktot = p.Cin + (X2 ? p.Cin2 : 0);
   const int c4n = Cin >> 2;
@@ -181,18 +191,19 @@ static bool conv_stream_on() {
 }
 
 static int stream_kc(int kc) {
-  static const int ks[] = {1, 2, 3, 4, 5, 6, 8};
+  static const int ks[] = {1, 2, 3, 4, 5, 6, 8, 10, 12, 13, 16, 18};
   for (int k : ks)
     if (kc <= k) return k;
   return -1;
 }
 
 template <typename Kern>
-static int stream_grid(Kern kern, size_t lds, int64_t nwg) {
+static int stream_grid(Kern kern, int threads, size_t lds, int64_t nwg) {
   int dev = 0, ncu = 0, occ = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, lds) != hipSuccess || occ < 1)
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, threads, lds) != hipSuccess ||
+      occ < 1)
     return -1;
   const int64_t cap = (int64_t)ncu * occ;
   return (int)(nwg < cap ? nwg : cap);
@@ -204,12 +215,12 @@ static int stream_grid(Kern kern, size_t lds, int64_t nwg) {
 int conv1x1_stream_dispatch(const ConvArgs& a, hipStream_t st) {
   if (!conv_stream_on()) return -1;
   const int TN = a.Ntiles, KC = stream_kc(a.Kc);
-  if (TN < 1 || TN > 5 || KC < 0 || a.Kc * TN > 24) return -1;
+  if (TN < 1 || TN > 5 || KC < 0) return -1;
   if (a.x2 && a.x2_stride != 1) return -1;
   const int64_t ohw = (int64_t)a.OH * a.OW;
   if (a.ascale && (ohw % 16 || a.ascale_bs % 4)) return -1;
   const size_t lds = (size_t)a.Kc * TN * 1024 + (a.ascale ? (size_t)a.B * a.Cin * 4 : 0);
-  if (lds > 40 * 1024) return -1;
+  if (lds > (a.Kc * TN > 24 ? 150 : 40) * 1024) return -1;
   const int64_t nblk = cdiv(a.M, 16);
   if (nblk >= ((int64_t)1 << 27)) return -1;
   const int x2 = a.x2 ? 1 : 0;
@@ -217,9 +228,11 @@ int conv1x1_stream_dispatch(const ConvArgs& a, hipStream_t st) {
 #define CS_LAUNCH(TN_, KC_, X2_, AS_)                                                       \
   do {                                                                                      \
     auto kern = conv1x1_stream_kernel<TN_, KC_, X2_, AS_>;                                  \
-    const int grid = stream_grid(kern, lds, cdiv(nblk, 4));                                 \
+    constexpr int nw_ = CsCfg<TN_, KC_>::NW;                                                \
+    if ((a.Kc * TN > 24) != (nw_ == 8)) return -1;                                          \
+    const int grid = stream_grid(kern, nw_ * 64, lds, cdiv(nblk, nw_));                     \
     if (grid < 1) return -1;                                                                \
-    kern<<<grid, 256, lds, st>>>(a, (int)nblk, (int)ohw);                                   \
+    kern<<<grid, nw_ * 64, lds, st>>>(a, (int)nblk, (int)ohw);                              \
     return check_launch("conv1x1_stream");                                                  \
   } while (0)
 #define CS_FLAGS(TN_, KC_)                      \
@@ -232,9 +245,9 @@ int conv1x1_stream_dispatch(const ConvArgs& a, hipStream_t st) {
 #define CS_KC(TN_) \
   CS_FLAGS(TN_, 1) CS_FLAGS(TN_, 2) CS_FLAGS(TN_, 3) CS_FLAGS(TN_, 4) CS_FLAGS(TN_, 5) \
   CS_FLAGS(TN_, 6) CS_FLAGS(TN_, 8)
-  CS_KC(1) CS_KC(2) CS_KC(3)
-  CS_FLAGS(4, 1) CS_FLAGS(4, 2) CS_FLAGS(4, 3) CS_FLAGS(4, 4) CS_FLAGS(4, 5) CS_FLAGS(4, 6)
-  CS_FLAGS(5, 1) CS_FLAGS(5, 2) CS_FLAGS(5, 3) CS_FLAGS(5, 4)
+  CS_KC(1) CS_KC(2) CS_KC(3) CS_KC(4) CS_KC(5)
+  CS_FLAGS(2, 10) CS_FLAGS(3, 10) CS_FLAGS(3, 12)
+  CS_FLAGS(5, 10) CS_FLAGS(5, 12) CS_FLAGS(5, 13) CS_FLAGS(5, 16) CS_FLAGS(5, 18)
 #undef CS_KC
 #undef CS_FLAGS
 #undef CS_LAUNCH

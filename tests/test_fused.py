@@ -138,3 +138,51 @@ def test_conv3x3_tile_parity(cuda, cin, cout, split, hw, gate):
         got = F.conv(xg, pk, pad=1, act="relu", ascale=asc).permute(0, 3, 1, 2).cpu()
         want = tF.relu(ref)
     assert rel_err(got, want) < 2e-5, rel_err(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cin2,cout,gate,res,hw,act", [
+    (16, 0, 16, True, True, (33, 31), "relu"),      # KC 1, ragged last block
+    (64, 16, 24, True, False, (17, 23), "relu"),    # K-concat skip source (b2)
+    (72, 0, 24, True, True, (16, 16), "relu"),      # KC 5 with a half stage (b3)
+    (120, 0, 40, True, True, (8, 40), "hswish"),    # KC 8, TN 3 (b5)
+    (40, 0, 40, False, False, (31, 7), "leaky"),    # FPN lateral
+    (200, 0, 80, True, True, (12, 13), "hswish"),   # 8-wave workgroups (b8)
+    (240, 40, 80, True, False, (5, 9), "hswish"),   # KC 18 + K-concat (b7)
+])
+def test_conv1x1_stream_parity(cuda, cin, cin2, cout, gate, res, hw, act):
+    """The streaming 1x1 kernel (conv_stream.hip: persistent workgroups, LDS
+    weights + gates, next block's K stages in flight) vs torch fp32: ragged
+    pixel counts, half-filled K stages, the K-concatenated skip source, the
+    ECA gate on the first source only, residual and activation."""
+    from jabd_amd import functional as F
+    H, W = hw
+    B = 3
+    g = torch.Generator().manual_seed(cin * 5 + cout + H)
+    x = torch.randn(B, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    sc = torch.rand(B, cin, generator=g) if gate else None
+    ref = tF.conv2d(x * sc[:, :, None, None] if gate else x, w, b)
+    extra = None
+    if cin2:
+        x2 = torch.randn(B, cin2, H, W, generator=g)
+        w2 = torch.randn(cout, cin2, generator=g) / cin2 ** 0.5
+        t2 = torch.randn(cout, generator=g) * 0.1
+        ref = ref + tF.conv2d(x2, w2[:, :, None, None], t2)
+        extra = (w2.t().contiguous().to(cuda), t2.to(cuda))
+    r = torch.randn(B, cout, H, W, generator=g) if res else None
+    if res:
+        ref = ref + r
+    want = {"relu": tF.relu, "hswish": tF.hardswish,
+            "leaky": lambda v: tF.leaky_relu(v, 0.1)}[act](ref)
+    conv = torch.nn.Conv2d(cin, cout, 1)
+    with torch.no_grad():
+        conv.weight.copy_(w)
+        conv.bias.copy_(b)
+    pk = F.pack_conv(conv.to(cuda), extra=extra)
+    nhwc = lambda v: v.permute(0, 2, 3, 1).contiguous().to(cuda)  # noqa: E731
+    y = F.conv(nhwc(x), pk, act=act, slope=0.1, ascale=sc.to(cuda).contiguous() if gate else None,
+               x2=nhwc(x2) if cin2 else None, res=nhwc(r) if res else None)
+    got = y.permute(0, 3, 1, 2).cpu()
+    assert rel_err(got, want) < 2e-5, rel_err(got, want)
