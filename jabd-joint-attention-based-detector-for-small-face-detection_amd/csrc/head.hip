@@ -91,6 +91,79 @@ __global__ __launch_bounds__(256) void eca_gate_kernel(const float* __restrict__
   }
 }
 
+// Same result for C % 4 == 0 with the row reduction spread over the whole
+// workgroup: thread (row group rg, channel quad q) sums rows rg, rg + RG, ...
+// with float4 loads (8 in flight), the RG partial quads are summed in row-group
+// order through LDS (fixed order: deterministic), then the Conv1d + gate.  A
+// window covers channels [cs - 4, cs + 248 + 4) (k <= 9), cs = 248 * blockIdx.x.
+// The one-thread-per-channel form walks all nblk rows serially (up to 1024
+// dependent L2 round trips for the 512^2 gates).
+constexpr int kGateOC = 248;
+__global__ __launch_bounds__(256) void eca_gate4_kernel(const float* __restrict__ part,
+                                                        int nblk, int C, float inv_hw,
+                                                        const float* __restrict__ w1d, int k,
+                                                        int gate, float* __restrict__ scale,
+                                                        float* __restrict__ mean_out) {
+  __shared__ float4 red[256];
+  __shared__ float mean[kGateOC + 8];
+  const int b = blockIdx.y, t = threadIdx.x;
+  const int cs = blockIdx.x * kGateOC;
+  const int ce = min(C, cs + kGateOC);
+  const int nq = (ce - cs + 8) >> 2;  // quads of [cs - 4, ce + 4)
+  const int RG = 256 / nq;
+  const int rg = t / nq, q = t - rg * nq;
+  const int c = cs - 4 + 4 * q;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (rg < RG && c >= 0 && c < C) {
+    const float* pb = part + (int64_t)b * nblk * C + c;
+    float4 a[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    int r = rg;
+    for (; r + 7 * RG < nblk; r += 8 * RG) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float4 v = *reinterpret_cast<const float4*>(pb + (int64_t)(r + u * RG) * C);
+        a[u].x += v.x; a[u].y += v.y; a[u].z += v.z; a[u].w += v.w;
+      }
+    }
+    for (; r < nblk; r += RG) {
+      const float4 v = *reinterpret_cast<const float4*>(pb + (int64_t)r * C);
+      a[0].x += v.x; a[0].y += v.y; a[0].z += v.z; a[0].w += v.w;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      s.x += a[u].x; s.y += a[u].y; s.z += a[u].z; s.w += a[u].w;
+    }
+  }
+  red[t] = s;
+  __syncthreads();
+  if (t < nq) {
+    float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int g = 0; g < RG; ++g) {
+      const float4 v = red[g * nq + t];
+      m.x += v.x; m.y += v.y; m.z += v.z; m.w += v.w;
+    }
+    // zero outside [0, C): the Conv1d's zero padding
+    const bool in = c >= 0 && c < C;
+    mean[4 * t + 0] = in ? m.x * inv_hw : 0.f;
+    mean[4 * t + 1] = in ? m.y * inv_hw : 0.f;
+    mean[4 * t + 2] = in ? m.z * inv_hw : 0.f;
+    mean[4 * t + 3] = in ? m.w * inv_hw : 0.f;
+  }
+  __syncthreads();
+  const int h = (k - 1) / 2;
+  const int co = cs + t;
+  if (co < ce) {
+    float y = 0.f;
+    for (int j = 0; j < k; ++j) y = fmaf(w1d[j], mean[t + 4 - h + j], y);
+    const float g = gate == ACT_SIGMOID ? 1.f / (1.f + expf(-y))
+                                        : fminf(fmaxf(y + 3.f, 0.f), 6.f) * (1.f / 6.f);
+    scale[(int64_t)b * C + co] = g;
+    if (mean_out) mean_out[(int64_t)b * C + co] = mean[t + 4];
+  }
+}
+
 // First level of the ECA pool for many partial rows: block (s, b) sums rows
 // [s*R, min(nblk, (s+1)*R)) of part[b] in row order into out[b][s] — a
 // deterministic two-level sum that spreads the read of nblk x C partials over
@@ -461,6 +534,13 @@ extern "C" int jabd_eca_gate_f32(const float* part, int64_t nblk, int64_t B, int
   JABD_REQUIRE(gate == ACT_SIGMOID || gate == ACT_HSIGMOID, "eca_gate: gate must be (h)sigmoid");
   JABD_REQUIRE(C * sizeof(float) <= 64 * 1024, "eca_gate: C too large");
   JABD_REQUIRE(k <= 31, "eca_gate: k too large");
+  if (C % 4 == 0 && k <= 9 && nblk * C < ((int64_t)1 << 31) && B <= 65535) {
+    dim3 g4((unsigned)cdiv(C, kGateOC), (unsigned)B);
+    eca_gate4_kernel<<<g4, 256, 0, as_stream(stream)>>>(part, (int)nblk, (int)C,
+                                                       1.f / (float)hw, w1d, k, gate, scale,
+                                                       mean_out);
+    return check_launch("eca_gate");
+  }
   const int oc = 256 - 2 * ((k - 1) / 2);
   dim3 g((unsigned)cdiv(C, oc), (unsigned)B);
   eca_gate_kernel<<<g, 256, 0, as_stream(stream)>>>(part, nblk, (int)C, 1.f / (float)hw, w1d, k,

@@ -317,7 +317,9 @@ def channel_sums(x, nblk=None):
 
 def eca_gate(part, hw, w1d, gate, return_mean=False):
     B, nblk, C = part.shape
-    if nblk > 64:  # many tile partials: reduce them over many workgroups first
+    # many tile partials: reduce them over many workgroups first, unless the
+    # quad-vectorised gate kernel (C % 4 == 0, k <= 9) spreads the rows itself
+    if nblk > 64 and not (C % 4 == 0 and w1d.numel() <= 9 and nblk <= 4096):
         nsplit = min(64, (nblk + 7) // 8)
         red = torch.empty((B, nsplit, C), dtype=torch.float32, device=part.device)
         call("jabd_partial_reduce_f32", part.data_ptr(), nblk, B, C, nsplit, red.data_ptr(),

@@ -232,3 +232,25 @@ def test_maxpoolfn_grads(cuda):
     assert rel_err(_nchw(yg.detach()), y.detach()) < TOL
     (yg * _nhwc(dy.float()).to(cuda)).sum().backward()
     _check([_nchw(xg.grad)], [xr.grad], ["dx"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,C,nblk,k,gate", [(3, 16, 1024, 3, "hsigmoid"), (2, 72, 256, 3, "hsigmoid"),
+                                             (2, 672, 16, 5, "hsigmoid"), (2, 960, 4, 5, "sigmoid"),
+                                             (1, 40, 7, 3, "sigmoid"), (2, 250, 33, 5, "sigmoid")])
+def test_eca_gate_from_partials(cuda, B, C, nblk, k, gate):
+    """ECA gate from tile partial sums (AdaptiveAvgPool -> Conv1d(k, pad (k-1)/2,
+    no bias) -> (hard)sigmoid, nets/mobilenetV3.py:94-112) vs torch fp64: the
+    quad-vectorised kernel (C % 4 == 0, windows of 248 channels past C = 248)
+    and the per-channel fallback (C = 250)."""
+    from jabd_amd import functional as F
+    g = torch.Generator().manual_seed(C + nblk)
+    part = torch.randn(B, nblk, C, generator=g)
+    w = torch.randn(k, generator=g) * 0.5
+    hw = nblk * 64
+    mean = part.double().sum(1) / hw
+    y = torch.nn.functional.conv1d(mean[:, None, :], w.double()[None, None, :], padding=(k - 1) // 2)[:, 0]
+    want = torch.sigmoid(y) if gate == "sigmoid" else torch.nn.functional.hardsigmoid(y)
+    got, m = F.eca_gate(part.to(cuda), hw, w.to(cuda), gate, return_mean=True)
+    assert float((got.cpu().double() - want).abs().max()) < 1e-6
+    assert float((m.cpu().double() - mean).abs().max() / mean.abs().max()) < 1e-5
