@@ -507,6 +507,21 @@ int jabd_eca_bwd_terms_f32(const float* da, const float* x, int64_t B, int64_t H
                            const float* scale, const float* mean, const float* w1d, int32_t k,
                            int32_t gate, float* part, int32_t nblk, float* dmean_ws,
                            float* dw1d_ws, float* dw1d, jabd_stream_t stream);
+/* ECA-gated 1x1 project conv p = conv(x * scale[b][c]) (replaces, for
+ * nets/mobilenetV3.py:145-148's conv3 after eca_block :343-348, the
+ * backward pair jabd_conv_wgrad_f32 with ascale + the sum(da * x) pass of
+ * jabd_eca_bwd_terms_f32): args as jabd_conv_wgrad_f32 with the UNGATED x and
+ * ascale NULL; w the torch weight [Cout][Cin]; outputs dw [Cout][Cin] and
+ * ds[b][c] = sum_hw da * x with da the data gradient through w.  part is
+ * scratch of jabd_conv_wgrad_eca_part_floats() floats (0: shape unsupported). */
+int64_t jabd_conv_wgrad_eca_part_floats(const jabd_conv_args* args);
+int jabd_conv_wgrad_eca_f32(const jabd_conv_args* args, const float* scale, const float* w,
+                            float* part, float* dw, float* ds, jabd_stream_t stream);
+/* The gate half of jabd_eca_bwd_terms_f32 given part[b][blk][c] = sum da * x. */
+int jabd_eca_gate_bwd_f32(const float* part, int32_t nblk, int64_t B, int64_t HW, int32_t C,
+                          const float* scale, const float* mean, const float* w1d, int32_t k,
+                          int32_t gate, float* dmean_ws, float* dw1d_ws, float* dw1d,
+                          jabd_stream_t stream);
 /* dx = da * scale[b][c] and part[b][blk][c] = sum da * x (scale gradient). */
 int jabd_scale_bwd_f32(const float* da, const float* x, int64_t B, int64_t HW, int32_t C,
                        const float* scale, float* part, int32_t nblk, float* dx,

@@ -48,7 +48,6 @@ struct XdCfg {
   static constexpr int XP = 16;      // staged input: 4 quad planes of IPAD float4
   static constexpr int EP = EC + 4;  // expanded-tile pitch
   static constexpr int NPB = IPAD / 16, NNT = EC / 16, NBLK = NPB * NNT;
-  static constexpr int BPW = (NBLK + 3) / 4;  // MFMA blocks per wave
   static constexpr int LDS_X = IPAD * XP, LDS_E = IPAD * EP;
   static constexpr int LDS = LDS_X > LDS_E ? LDS_X : LDS_E;
   static constexpr int PW = S == 1 ? 4 : 2, NSTRIP = TW / PW, NC4 = EC / 4;
@@ -150,11 +149,14 @@ __device__ __forceinline__ void dw_lane(int l, int& c4, int& sl) {
     sl = 4 * (2 * h + par) + k;
   }
 }
-template <int K, int S, int TH, int TW, int EC, int ACT, int KP, bool SKIP = false>
-__global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p, const XdDivs dv,
+template <int K, int S, int TH, int TW, int EC, int ACT, int KP, bool SKIP = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_args p, const XdDivs dv,
                                                        int nitems) {
   using C = XdCfg<K, S, TH, TW, EC>;
-  constexpr int NPF = (C::IPAD * 4 + 255) / 256;
+  constexpr int T = 64 * NW;                  // threads
+  constexpr int NPF = (C::IPAD * 4 + T - 1) / T;
+  constexpr int BPW = (C::NBLK + NW - 1) / NW;  // MFMA blocks per wave
+  static_assert(NW % C::NNT == 0, "waves split evenly over the 16-channel tiles");
   constexpr int NWD = (K * K + 1) * C::NC4;
   constexpr int SKC = SKIP ? 160 : 4;  // skip-branch taps staged in LDS (Cin <= 160)
   __shared__ __attribute__((aligned(16))) float lds[C::LDS];
@@ -164,7 +166,7 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
   if (!xd_item<K, S, TH, TW, EC>(p, blockIdx.x, dv, nitems, it)) return;
   const bool skip = SKIP && it.c0 == 0;
   if (skip) {
-    for (int i = threadIdx.x; i < 10 * (p.Cin >> 2); i += 256) {
+    for (int i = threadIdx.x; i < 10 * (p.Cin >> 2); i += T) {
       const int q = i / (p.Cin >> 2), c4 = i - q * (p.Cin >> 2);
       sws[q][c4] = *reinterpret_cast<const float4*>((q < 9 ? p.sw + q * p.Cin : p.sb) + 4 * c4);
     }
@@ -194,7 +196,7 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
   // voffset 0xFFFFFFF0 and reads zeros (host: x < 4 GiB)
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(p.x), (short)0, (int)(uint32_t)((int64_t)p.B * p.x_bs * 4), 0x00020000);
-  // stage slot u of this thread: pixel u*64 + (t>>6)*16 + (t&15), channel quad (t>>4)&3
+  // stage slot u of this thread: pixel u*16*NW + (t>>6)*16 + (t&15), channel quad (t>>4)&3
   const int cq = ((t >> 4) & 3) * 4;
   const int spx0 = (t >> 6) * 16 + (t & 15);
   // KP-deep register ring of input stages: stage kc + KP is issued as soon
@@ -207,7 +209,7 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
     const bool cok = cofs < p.Cin;
 #pragma unroll
     for (int u = 0; u < NPF; ++u) {
-      const int px = u * 64 + spx0;
+      const int px = u * 16 * NW + spx0;
       const int r = px / C::IW, c = px - r * C::IW;
       const int ih = it.ih0 + r, iw = it.iw0 + c;
       const bool ok = px < C::IPX && cok &&
@@ -217,10 +219,10 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
     }
   };
   // accumulators start at the expand bias (no epilogue add)
-  f32x4 acc[C::BPW];
+  f32x4 acc[BPW];
   const f32x4 bias4 = (f32x4){pbi.x, pbi.y, pbi.z, pbi.w};
 #pragma unroll
-  for (int u = 0; u < C::BPW; ++u) acc[u] = bias4;
+  for (int u = 0; u < BPW; ++u) acc[u] = bias4;
 #pragma unroll
   for (int s = 0; s < KP; ++s)
     if (s < p.Kc) load_stage(s, pf[s]);
@@ -232,8 +234,8 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
       f32x4 a = wpk[(kc * p.Ntiles + ntc) * 64 + lane];
 #pragma unroll
       for (int u = 0; u < NPF; ++u) {
-        if (u * 64 + spx0 < C::IPAD)
-          *reinterpret_cast<float4*>(lds + (cq / 4 * C::IPAD + u * 64 + spx0) * 4) = pf[s][u];
+        if (u * 16 * NW + spx0 < C::IPAD)
+          *reinterpret_cast<float4*>(lds + (cq / 4 * C::IPAD + u * 16 * NW + spx0) * 4) = pf[s][u];
       }
       // retire the weight load here, before the next stage's loads are in
       // flight: the compiler's vmcnt tracking cannot count through the
@@ -244,9 +246,9 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
       lds_barrier();
       if (kc + KP < p.Kc) load_stage(kc + KP, pf[s]);
       // fused skip branch (stride 2, first chunk's workgroups): this stage's
-      // 16 channels for output pixel t & 63, channel quad t >> 6, taps from LDS
+      // 16 channels for output pixel t & 63, channel quad t >> 6 (waves 0-3), taps from LDS
       const int sc = 16 * kc + 4 * (t >> 6);
-      if (skip && sc < p.Cin) {
+      if (skip && wave < 4 && sc < p.Cin) {
         // output (orow, ocol) of the TH x TW tile reads tile pixels
         // (2 orow + kh + PAD - 1, 2 ocol + kw + PAD - 1): the dw3x3/s2/p1 window
         const int op = t & 63, orow = op / TW, ocol = op - orow * TW;
@@ -275,8 +277,8 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
       // its accumulators are masked in the epilogue)
       if (ntv) {
 #pragma unroll
-        for (int u = 0; u < C::BPW; ++u) {
-          const int blk = wave + 4 * u;
+        for (int u = 0; u < BPW; ++u) {
+          const int blk = wave + NW * u;
           if (blk < C::NBLK) {
             const int pb = blk / C::NNT;
             const f32x4 bv = *reinterpret_cast<const f32x4*>(lds + (g * C::IPAD + pb * 16 + j) * 4);
@@ -293,8 +295,8 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
   // expanded tile: act, zero outside the image / on padded channels
   if (interior) {
 #pragma unroll
-    for (int u = 0; u < C::BPW; ++u) {
-      const int blk = wave + 4 * u;
+    for (int u = 0; u < BPW; ++u) {
+      const int blk = wave + NW * u;
       if (blk < C::NBLK) {
         const int pb = blk / C::NNT;
         const int px = pb * 16 + j, ch = 16 * ntw + 4 * g;
@@ -309,8 +311,8 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
     }
   } else {
 #pragma unroll
-    for (int u = 0; u < C::BPW; ++u) {
-      const int blk = wave + 4 * u;
+    for (int u = 0; u < BPW; ++u) {
+      const int blk = wave + NW * u;
       if (blk < C::NBLK) {
         const int pb = blk / C::NNT;
         const int px = pb * 16 + j, ch = 16 * ntw + 4 * g;
@@ -341,8 +343,8 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
     const float4 bias2 = wsh[K * K][c4];
     float* yb = p.y + (int64_t)it.b * p.y_bs + it.c0 + chl;
 #pragma unroll 1
-    for (int pass = 0; pass * 256 < C::ITEMS; ++pass) {
-      const int strip = (pass * 4 + wave) * SPW + sl;
+    for (int pass = 0; pass * T < C::ITEMS; ++pass) {
+      const int strip = (pass * NW + wave) * SPW + sl;
       if (strip >= TH * C::NSTRIP) break;
       const int orow = strip / C::NSTRIP, st = strip - orow * C::NSTRIP;
       const int oh = it.oh0 + orow, owb = it.ow0 + st * C::PW;
@@ -404,13 +406,20 @@ __global__ __launch_bounds__(256, 2) void expdw1_kernel(const jabd_expdw_args p,
     if (lane < C::NC4) red[wave * C::NC4 + lane] = psum;
     __syncthreads();
     if (t < C::NC4 && it.c0 + 4 * t < p.E) {
-      const float4 a0 = red[t], a1 = red[C::NC4 + t], a2 = red[2 * C::NC4 + t],
-                   a3 = red[3 * C::NC4 + t];
-      float4 sm;
-      sm.x = (a0.x + a1.x) + (a2.x + a3.x);
-      sm.y = (a0.y + a1.y) + (a2.y + a3.y);
-      sm.z = (a0.z + a1.z) + (a2.z + a3.z);
-      sm.w = (a0.w + a1.w) + (a2.w + a3.w);
+      // pairwise over the waves in a fixed order
+      float4 v[NW];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) v[w] = red[w * C::NC4 + t];
+#pragma unroll
+      for (int h = NW / 2; h >= 1; h >>= 1)
+#pragma unroll
+        for (int w = 0; w < h; ++w) {
+          v[w].x += v[w + h].x;
+          v[w].y += v[w + h].y;
+          v[w].z += v[w + h].z;
+          v[w].w += v[w + h].w;
+        }
+      const float4 sm = v[0];
       *reinterpret_cast<float4*>(p.part + ((int64_t)it.b * (int)dv.tiles_img.d + it.t_in) * p.E +
                                  it.c0 + 4 * t) = sm;
     }
@@ -441,6 +450,22 @@ static int xd_kp() {
     kp = e && (e[0] == '2' || e[0] == '3') ? e[0] - '0' : 1;
   }
   return kp;
+}
+
+// Waves per workgroup.  The expanded tile's LDS caps resident workgroups
+// at 2-3 per CU, so 8-wave workgroups double the resident waves on the same
+// tile (half the accumulators and prefetch registers per wave).
+// JABD_EXPDW_NW=4|8 forces one form for A/B.
+static int xd_nw(const jabd_expdw_args& a, int EC) {
+  static int env = -1;
+  if (env < 0) {
+    const char* e = getenv("JABD_EXPDW_NW");
+    env = e && e[0] == '8' ? 8 : (e && e[0] == '4' ? 4 : 0);
+  }
+  (void)a;
+  (void)EC;
+  if (env) return env;
+  return 4;
 }
 
 extern "C" int64_t jabd_expand_dw_nblk(int32_t OH, int32_t OW, int32_t k, int32_t stride) {
@@ -484,6 +509,7 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
   const int64_t nitems = cdiv(ntiles, 8) * 8 * nch;
   JABD_REQUIRE(nitems < ((int64_t)1 << 31) && (int64_t)a.H * a.W * a.x_ps < ((int64_t)1 << 31),
                "expand_dw: problem too large for 32-bit item / pixel indexing");
+  const int nw = xd_nw(a, EC);
   hipStream_t st = as_stream(stream);
   const XdDivs dv{make_fastdiv((uint32_t)nch), make_fastdiv((uint32_t)tiles_img),
                   make_fastdiv((uint32_t)tiles_w)};
@@ -491,8 +517,14 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
                "expand_dw: input must be < 4 GiB (buffer-descriptor offsets)");
 #define XD_LAUNCH(K_, S_, TH_, TW_, EC_, ACT_)                                                \
   do {                                                                                        \
-    if (S_ == 2 && a.sy)                                                                      \
+    if (S_ == 2 && a.sy && nw == 8)                                                           \
+      expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1, true, 8><<<(unsigned)nitems, 512, 0, st>>>( \
+          a, dv, (int)nitems);                                                                \
+    else if (S_ == 2 && a.sy)                                                                 \
       expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1, true><<<(unsigned)nitems, 256, 0, st>>>( \
+          a, dv, (int)nitems);                                                                \
+    else if (nw == 8)                                                                         \
+      expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1, false, 8><<<(unsigned)nitems, 512, 0, st>>>( \
           a, dv, (int)nitems);                                                                \
     else if (a.Kc == 1 || xd_kp() == 1)                                                       \
       expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1><<<(unsigned)nitems, 256, 0, st>>>(       \

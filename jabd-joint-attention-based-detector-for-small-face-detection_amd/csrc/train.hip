@@ -1372,6 +1372,39 @@ extern "C" int jabd_bn_act_bwd_ex_f32(const float* dy, int32_t lddy, int32_t dyc
   return check_launch("bn_bwd_apply");
 }
 
+// The tiled weight-gradient kernels over chunks of `per` output pixels
+// (chunk c covers pixels [c*per, min((c+1)*per, M))), partials part[chunk][K][Cout].
+static void wgrad_launch_parts(const ConvArgs& a, int64_t per, int64_t nch, float* part,
+                               hipStream_t st) {
+  const int K = a.KH * a.KW * a.Cin;
+  if (wgrad_vec_ok(a) && wgrad32_ok(a)) {
+    const int tk = wg32_tile(K), tn = wg32_tile(a.Cout);
+    const int fast = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.H == a.OH &&
+                     a.W == a.OW;
+    dim3 g((unsigned)cdiv(K, tk), (unsigned)cdiv(a.Cout, tn), (unsigned)nch);
+#define W32_CASE(KT_, NT_)                                                        \
+  if (tk == KT_ && tn == NT_)                                                     \
+    conv_wgrad32_kernel<KT_, NT_><<<g, 256, 0, st>>>(a, (int)per, fast, part);
+    W32_CASE(64, 64) W32_CASE(64, 128) W32_CASE(128, 64) W32_CASE(128, 128)
+#undef W32_CASE
+  } else if (wgrad_vec_ok(a)) {
+    const int tk = wv_tile(K), tn = wv_tile(a.Cout);
+    const int fast = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.H == a.OH &&
+                     a.W == a.OW;
+    dim3 g((unsigned)cdiv(K, tk), (unsigned)cdiv(a.Cout, tn), (unsigned)nch);
+#define WV_CASE(KT_, NT_)                                                         \
+  if (tk == KT_ && tn == NT_)                                                     \
+    conv_wgrad_v_kernel<KT_, NT_><<<g, 256, 0, st>>>(a, (int)per, fast, part);
+    WV_CASE(16, 16) WV_CASE(16, 32) WV_CASE(16, 64)
+    WV_CASE(32, 16) WV_CASE(32, 32) WV_CASE(32, 64)
+    WV_CASE(64, 16) WV_CASE(64, 32) WV_CASE(64, 64)
+#undef WV_CASE
+  } else {
+    dim3 g((unsigned)cdiv(K, kWgT), (unsigned)cdiv(a.Cout, kWgT), (unsigned)nch);
+    conv_wgrad_kernel<<<g, 256, 0, st>>>(a, per, part);
+  }
+}
+
 extern "C" int64_t jabd_conv_wgrad_part_floats(const jabd_conv_args* args) {
   if (!args) return -1;
   ConvArgs a = *args;
@@ -1404,38 +1437,101 @@ extern "C" int jabd_conv_wgrad_f32(const jabd_conv_args* args, float* part, floa
                                                                   a.KH * a.KW, 16, dw);
     return check_launch("wgrad_reduce");
   }
-  if (wgrad_vec_ok(a) && wgrad32_ok(a)) {
-    const int tk = wg32_tile(K), tn = wg32_tile(a.Cout);
-    const int fast = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.H == a.OH &&
-                     a.W == a.OW;
-    dim3 g((unsigned)cdiv(K, tk), (unsigned)cdiv(a.Cout, tn), (unsigned)nch);
-#define W32_CASE(KT_, NT_)                                                        \
-  if (tk == KT_ && tn == NT_)                                                     \
-    conv_wgrad32_kernel<KT_, NT_><<<g, 256, 0, st>>>(a, (int)per, fast, part);
-    W32_CASE(64, 64) W32_CASE(64, 128) W32_CASE(128, 64) W32_CASE(128, 128)
-#undef W32_CASE
-  } else if (wgrad_vec_ok(a)) {
-    const int tk = wv_tile(K), tn = wv_tile(a.Cout);
-    const int fast = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.H == a.OH &&
-                     a.W == a.OW;
-    dim3 g((unsigned)cdiv(K, tk), (unsigned)cdiv(a.Cout, tn), (unsigned)nch);
-#define WV_CASE(KT_, NT_)                                                         \
-  if (tk == KT_ && tn == NT_)                                                     \
-    conv_wgrad_v_kernel<KT_, NT_><<<g, 256, 0, st>>>(a, (int)per, fast, part);
-    WV_CASE(16, 16) WV_CASE(16, 32) WV_CASE(16, 64)
-    WV_CASE(32, 16) WV_CASE(32, 32) WV_CASE(32, 64)
-    WV_CASE(64, 16) WV_CASE(64, 32) WV_CASE(64, 64)
-#undef WV_CASE
-  } else {
-    dim3 g((unsigned)cdiv(K, kWgT), (unsigned)cdiv(a.Cout, kWgT), (unsigned)nch);
-    conv_wgrad_kernel<<<g, 256, 0, st>>>(a, per, part);
-  }
+  wgrad_launch_parts(a, per, nch, part, st);
   if (int e = check_launch("conv_wgrad")) return e;
   const int64_t tot = (int64_t)K * a.Cout;
   const int lanes = tot >= 64 * 512 ? 64 : 16;
   wgrad_reduce2_kernel<<<(unsigned)cdiv(tot, lanes), 256, 0, st>>>(part, nch, K, a.Cout, a.Cin,
                                                                    a.KH * a.KW, lanes, dw);
   return check_launch("wgrad_reduce");
+}
+
+// ---------------------------------------------------------------------------
+// ECA-gated project conv (nets/mobilenetV3.py:343-348 then conv3 at :145):
+// p = conv3(d * s[b][c]).  Its weight gradient and the gate's input sum
+//   dW[n][c]  = sum_b s[b][c] G_b[c][n],
+//   ds[b][c]  = sum_hw da * d = sum_n W[n][c] G_b[c][n],   da = dgrad(dp),
+// with G_b[c][n] = sum over image b's pixels of d[c] dp[n], share one GEMM:
+// the weight-gradient kernels run on the ungated d over pixel chunks that
+// never straddle an image, and one reduction forms both.  This replaces the
+// separate sum(da * d) pass over two full tensors (scale_bwd).
+// ---------------------------------------------------------------------------
+// Workgroup per gated channel c: lane n sums image b's chunks in a fixed
+// order; the W-weighted terms are reduced per image from LDS in n order.
+__global__ __launch_bounds__(256) void wgrad_eca_reduce_kernel(
+    const float* __restrict__ part, int cpi, int B, int E, int Cout,
+    const float* __restrict__ scale, const float* __restrict__ w, float* __restrict__ dw,
+    float* __restrict__ ds) {
+  extern __shared__ float prod[];  // [B][Cout]
+  const int c = blockIdx.x, t = threadIdx.x;
+  const int64_t EN = (int64_t)E * Cout;
+  for (int n = t; n < Cout; n += blockDim.x) {
+    const float wn = w[(int64_t)n * E + c];
+    float acc = 0.f;
+    for (int b = 0; b < B; ++b) {
+      const float* pb = part + (int64_t)b * cpi * EN + (int64_t)c * Cout + n;
+      float g0 = 0.f, g1 = 0.f;
+      int j = 0;
+      for (; j + 1 < cpi; j += 2) {
+        g0 += pb[(int64_t)j * EN];
+        g1 += pb[(int64_t)(j + 1) * EN];
+      }
+      if (j < cpi) g0 += pb[(int64_t)j * EN];
+      const float g = g0 + g1;
+      acc = fmaf(scale[(int64_t)b * E + c], g, acc);
+      prod[b * Cout + n] = wn * g;
+    }
+    dw[(int64_t)n * E + c] = acc;
+  }
+  __syncthreads();
+  for (int b = t; b < B; b += blockDim.x) {
+    float sm = 0.f;
+    for (int n = 0; n < Cout; ++n) sm += prod[b * Cout + n];
+    ds[(int64_t)b * E + c] = sm;
+  }
+}
+
+// Image-aligned chunk length: the largest per = HW / 2^j (a multiple of the
+// kernels' 64-pixel stage) that is still >= the normal chunk length, or 0 if
+// the shape does not qualify (1x1 / stride 1, HW % 64, LDS for [B][Cout]).
+static int64_t wgrad_eca_per(const ConvArgs& a) {
+  const int64_t HW = (int64_t)a.OH * a.OW;
+  if (a.KH != 1 || a.KW != 1 || a.stride != 1 || a.pad != 0 || a.H != a.OH || a.W != a.OW ||
+      HW % kWgPx || (int64_t)a.B * a.Cout * 4 > 64 * 1024 || !wgrad_vec_ok(a) || a.ascale)
+    return 0;
+  const int64_t target = cdiv(a.M, wgrad_chunks(a));
+  int64_t per = HW;
+  while (per % (2 * kWgPx) == 0 && per / 2 >= target) per /= 2;
+  if (cdiv(a.M, per) * a.Cin * a.Cout > ((int64_t)64 << 20)) return 0;
+  return per;
+}
+
+extern "C" int64_t jabd_conv_wgrad_eca_part_floats(const jabd_conv_args* args) {
+  if (!args) return -1;
+  ConvArgs a = *args;
+  a.M = (int64_t)a.B * a.OH * a.OW;
+  const int64_t per = wgrad_eca_per(a);
+  return per ? cdiv(a.M, per) * a.Cin * a.Cout : 0;
+}
+
+extern "C" int jabd_conv_wgrad_eca_f32(const jabd_conv_args* args, const float* scale,
+                                       const float* w, float* part, float* dw, float* ds,
+                                       jabd_stream_t stream) {
+  JABD_REQUIRE(args && scale && w && part && dw && ds, "conv_wgrad_eca: null");
+  ConvArgs a = *args;
+  JABD_REQUIRE(a.x && a.y && !a.x2 && !a.tconv && !a.ascale, "conv_wgrad_eca: bad args");
+  a.M = (int64_t)a.B * a.OH * a.OW;
+  JABD_REQUIRE(a.M < (int64_t)0x7fffffff, "conv_wgrad_eca: M too large");
+  const int64_t per = wgrad_eca_per(a);
+  JABD_REQUIRE(per > 0, "conv_wgrad_eca: unsupported shape (jabd_conv_wgrad_eca_part_floats = 0)");
+  const int64_t nch = cdiv(a.M, per);
+  const int cpi = (int)(((int64_t)a.OH * a.OW) / per);
+  hipStream_t st = as_stream(stream);
+  wgrad_launch_parts(a, per, nch, part, st);
+  if (int e = check_launch("conv_wgrad")) return e;
+  wgrad_eca_reduce_kernel<<<(unsigned)a.Cin, 256, (size_t)a.B * a.Cout * sizeof(float), st>>>(
+      part, cpi, a.B, a.Cin, a.Cout, scale, w, dw, ds);
+  return check_launch("wgrad_eca_reduce");
 }
 
 extern "C" int jabd_dw_dgrad_f32(const float* dy, const float* w, int32_t B, int32_t H, int32_t W,
@@ -1536,6 +1632,22 @@ extern "C" int jabd_eca_bwd_terms_f32(const float* da, const float* x, int64_t B
   scale_bwd_kernel<<<dim3((unsigned)nblk, (unsigned)B), 256, 0, st>>>(da, x, scale, HW, C, per,
                                                                       nblk, nullptr, part);
   if (int e = check_launch("scale_bwd")) return e;
+  eca_gate_bwd_kernel<<<(unsigned)B, 256, 2 * C * sizeof(float), st>>>(
+      part, nblk, C, mean, scale, w1d, k, gate, 1.f / (float)HW, dmean_ws, dw1d_ws);
+  if (int e = check_launch("eca_gate_bwd")) return e;
+  eca_w_reduce_kernel<<<1, 64, 0, st>>>(dw1d_ws, (int)B, k, dw1d);
+  return check_launch("eca_w_reduce");
+}
+
+// The gate half of jabd_eca_bwd_terms_f32 from precomputed sums
+// part[b][blk][c] of da * x (e.g. jabd_conv_wgrad_eca_f32's ds, nblk = 1).
+extern "C" int jabd_eca_gate_bwd_f32(const float* part, int32_t nblk, int64_t B, int64_t HW,
+                                     int32_t C, const float* scale, const float* mean,
+                                     const float* w1d, int32_t k, int32_t gate, float* dmean_ws,
+                                     float* dw1d_ws, float* dw1d, jabd_stream_t stream) {
+  JABD_REQUIRE(part && scale && mean && w1d && dmean_ws && dw1d_ws && dw1d && nblk > 0 && HW > 0,
+               "eca_gate_bwd: bad args");
+  hipStream_t st = as_stream(stream);
   eca_gate_bwd_kernel<<<(unsigned)B, 256, 2 * C * sizeof(float), st>>>(
       part, nblk, C, mean, scale, w1d, k, gate, 1.f / (float)HW, dmean_ws, dw1d_ws);
   if (int e = check_launch("eca_gate_bwd")) return e;

@@ -34,6 +34,8 @@ ACT = F.ACT
 # MobileNetV3 Block_eca training as one autograd node (MNv3BlockFn);
 # JABD_FUSED_BLOCKS=0 selects the per-op graph (A/B measurement, tests).
 FUSED_BLOCKS = __import__("os").environ.get("JABD_FUSED_BLOCKS", "1") != "0"
+# JABD_ECA_WGRAD=0: the ECA block backward takes sum(da * d) from its own pass (A/B)
+ECA_WGRAD = __import__("os").environ.get("JABD_ECA_WGRAD", "1") != "0"
 
 
 def _st():
@@ -125,6 +127,31 @@ def _wgrad(x, dy, weight, stride, pad, nchw_in=False, ascale=None):
 def _chan_sum(t):
     """Per-channel sum of an NHWC tensor (kernel partials, tiny torch reduce)."""
     return F.channel_sums(t).sum(dim=(0, 1))
+
+
+def _wgrad_eca(x, dy, weight, scale):
+    """(dW, ds) of p = conv1x1(x * scale[b][c]) with ds[b][c] = sum_hw(da * x):
+    jabd_conv_wgrad_eca_f32, or None when the shape does not qualify."""
+    cout, cin = weight.shape[0], weight.shape[1]
+    B, H, W, ctot = x.shape
+    if ctot != cin or dy.shape[3] != cout:
+        return None
+    a = ConvArgs()
+    a.x, a.x_bs, a.x_ps = x.data_ptr(), H * W * cin, cin
+    a.B, a.H, a.W, a.Cin = B, H, W, cin
+    a.y, a.y_bs, a.y_ps, a.y_c0 = dy.data_ptr(), dy.stride(0), cout, 0
+    a.OH, a.OW, a.Cout = H, W, cout
+    a.KH, a.KW, a.stride, a.pad = 1, 1, 1, 0
+    nparts = int(lib().jabd_conv_wgrad_eca_part_floats(ctypes.byref(a)))
+    if nparts <= 0:
+        return None
+    part = torch.empty(nparts, dtype=torch.float32, device=dy.device)
+    dw = torch.empty_like(weight, dtype=torch.float32)
+    ds = torch.empty((B, cin), dtype=torch.float32, device=dy.device)
+    w = weight.detach().reshape(cout, cin).float().contiguous()
+    call("jabd_conv_wgrad_eca_f32", ctypes.byref(a), scale.data_ptr(), w.data_ptr(),
+         part.data_ptr(), dw.data_ptr(), ds.data_ptr(), _st())
+    return dw, ds
 
 
 def _dgrad(dy, weight, stride, pad, H, W):
@@ -815,20 +842,30 @@ class MNv3BlockFn(torch.autograd.Function):
         # out = act(bn3(p) + res)
         dp, dg3, db3, dres = _bn_bwd(dout, p, st3, act, res=res, want_dres=True)
         # p = conv3(d * scale)
-        dW3 = _wgrad(d, dp, blk.conv3.weight, 1, 0, ascale=scale)
-        da = _dgrad(dp, blk.conv3.weight, 1, 0, OH, OW)
-        # ECA gate terms; BN2's backward applies dd = da * scale + dmean
         w1 = blk.eca.conv.weight.detach().reshape(-1).float().contiguous()
         kk = w1.numel()
         HW = OH * OW
-        nblk = max(1, min(64, HW // 256))
-        part = torch.empty((B, nblk, E), dtype=torch.float32, device=d.device)
         dmean = torch.empty((B, E), dtype=torch.float32, device=d.device)
         dw1_img = torch.empty((B, kk), dtype=torch.float32, device=d.device)
         dweca = torch.empty(kk, dtype=torch.float32, device=d.device)
-        call("jabd_eca_bwd_terms_f32", da.data_ptr(), d.data_ptr(), B, HW, E, scale.data_ptr(),
-             mean.data_ptr(), w1.data_ptr(), kk, ACT["hsigmoid"], part.data_ptr(), nblk,
-             dmean.data_ptr(), dw1_img.data_ptr(), dweca.data_ptr(), _st())
+        ds = _wgrad_eca(d, dp, blk.conv3.weight, scale) if ECA_WGRAD else None
+        if ds is not None:
+            # dW3 and sum_hw(da * d) from one GEMM over image-aligned chunks
+            dW3, ds = ds
+            call("jabd_eca_gate_bwd_f32", ds.data_ptr(), 1, B, HW, E, scale.data_ptr(),
+                 mean.data_ptr(), w1.data_ptr(), kk, ACT["hsigmoid"], dmean.data_ptr(),
+                 dw1_img.data_ptr(), dweca.data_ptr(), _st())
+            da = _dgrad(dp, blk.conv3.weight, 1, 0, OH, OW)
+        else:
+            dW3 = _wgrad(d, dp, blk.conv3.weight, 1, 0, ascale=scale)
+            da = _dgrad(dp, blk.conv3.weight, 1, 0, OH, OW)
+            nblk = max(1, min(64, HW // 256))
+            part = torch.empty((B, nblk, E), dtype=torch.float32, device=d.device)
+            call("jabd_eca_bwd_terms_f32", da.data_ptr(), d.data_ptr(), B, HW, E,
+                 scale.data_ptr(), mean.data_ptr(), w1.data_ptr(), kk, ACT["hsigmoid"],
+                 part.data_ptr(), nblk, dmean.data_ptr(), dw1_img.data_ptr(), dweca.data_ptr(),
+                 _st())
+        # ECA gate terms; BN2's backward applies dd = da * scale + dmean
         dd_pre, dg2, db2, _ = _bn_bwd(da, d_pre, st2, act, dys=scale, dya=dmean)
         de, dW2 = _dw_bwd(dd_pre, e, wt2, k, stride)
         de_pre, dg1, db1, _ = _bn_bwd(de, e_pre, st1, act)

@@ -468,3 +468,33 @@ def test_dataparallel_replica_training_grads_reach_original(cuda):
         assert torch.equal(grads[0][k], grads[1][k]), k
     for k in set(grads[1]) - set(grads[0]):
         assert ".se." in k and float(grads[1][k].abs().max()) == 0.0, k
+
+
+@pytest.mark.parametrize("hw", [(32, 32)])
+@pytest.mark.parametrize("cls,spec,gate", [b for b in BLOCKS if b[0] == "Block_eca"])
+def test_mnv3_block_eca_wgrad_fused(cuda, cls, spec, gate, monkeypatch, hw):
+    """Block_eca training at map sizes whose HW is a multiple of 64, so the
+    project conv's weight gradient and the ECA gate's sum(da * d) come from
+    one GEMM over image-aligned chunks (jabd_conv_wgrad_eca_f32).  Sizes are
+    picked so that no BN output lies within fp32 rounding of an activation
+    kink: at 3x32x64 one BN2 output of the 120-channel block is 9.5e-8, its
+    ReLU mask differs from the float64 run in this and in the separate-pass
+    path alike, and the flipped element's gradient moves its whole channel
+    through the BN backward (tools/block_bisect.py)."""
+    import nets.mobilenetV3 as mv3
+    from jabd_amd import train as T
+    taken = []
+    orig = T._wgrad_eca
+
+    def spy(*a):
+        r = orig(*a)
+        taken.append(r is not None)
+        return r
+
+    monkeypatch.setattr(T, "_wgrad_eca", spy)
+    k, cin, exp, cout, act, se, stride = spec
+    act_cls = nn.ReLU if act == "relu" else nn.Hardswish
+    m = init_for_parity(getattr(mv3, cls)(k, cin, exp, cout, act_cls, se, stride), seed=cin)
+    _composite(cuda, m, lambda ctx, x: model_ref.block(ctx, x, "", spec, gate),
+               [_x((3, cin) + hw, cin)], True)
+    assert taken and all(taken)

@@ -254,3 +254,70 @@ def test_eca_gate_from_partials(cuda, B, C, nblk, k, gate):
     got, m = F.eca_gate(part.to(cuda), hw, w.to(cuda), gate, return_mean=True)
     assert float((got.cpu().double() - want).abs().max()) < 1e-6
     assert float((m.cpu().double() - mean).abs().max() / mean.abs().max()) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,h,w,E,cout", [(3, 32, 48, 64, 24), (3, 32, 48, 480, 112),
+                                          (2, 16, 16, 672, 160), (4, 8, 8, 120, 40)])
+def test_wgrad_eca(cuda, B, h, w, E, cout):
+    """jabd_conv_wgrad_eca_f32: dW of conv1x1(d * s) and ds = sum_hw(da * d),
+    da = dp W, from one GEMM over image-aligned chunks, vs float64."""
+    from jabd_amd.train import _wgrad_eca
+    g = torch.Generator().manual_seed(E)
+    d = torch.randn(B, h, w, E, generator=g, dtype=torch.float64)
+    dp = torch.randn(B, h, w, cout, generator=g, dtype=torch.float64)
+    s = torch.rand(B, E, generator=g, dtype=torch.float64)
+    W = torch.randn(cout, E, 1, 1, generator=g, dtype=torch.float64) / E ** 0.5
+    dw_ref = torch.einsum("bhwc,bhwn,bc->nc", d, dp, s)
+    ds_ref = torch.einsum("bhwn,nc,bhwc->bc", dp, W[:, :, 0, 0], d)
+    r = _wgrad_eca(d.float().to(cuda), dp.float().to(cuda), W.float().to(cuda),
+                   s.float().to(cuda))
+    assert r is not None
+    dw, ds = r
+    _check([dw[:, :, 0, 0], ds], [dw_ref, ds_ref], ["dw", "ds"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,k,h,w", [(480, 3, 32, 48), (120, 5, 32, 64), (120, 5, 32, 32),
+                                     (64, 3, 16, 64), (40, 5, 8, 72)])
+def test_dwconvfn_grads_wide(cuda, c, k, h, w):
+    """Depthwise backward on wider maps (several W strips per row)."""
+    from jabd_amd.train import DwConvFn
+    g = torch.Generator().manual_seed(c + k)
+    x = torch.randn(3, c, h, w, generator=g)
+    wt = torch.randn(c, 1, k, k, generator=g) / k
+    xr, wr = x.double().requires_grad_(), wt.double().requires_grad_()
+    y = tF.conv2d(xr, wr, None, 1, k // 2, 1, c)
+    dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(2), dtype=torch.float64)
+    (y * dy).sum().backward()
+    xg = _nhwc(x).to(cuda).requires_grad_()
+    wg = torch.nn.Parameter(wt.to(cuda))
+    yg = DwConvFn.apply(xg, wg, 1)
+    assert rel_err(_nchw(yg.detach()), y.detach()) < TOL
+    (yg * _nhwc(dy.float()).to(cuda)).sum().backward()
+    _check([_nchw(xg.grad), wg.grad], [xr.grad, wr.grad], ["dx", "dw"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,act,h,w", [(480, "hswish", 32, 48), (120, "relu", 32, 64),
+                                       (120, "relu", 32, 32)])
+def test_bnactfn_grads_wide(cuda, c, act, h, w):
+    from jabd_amd.train import BnActFn
+    g = torch.Generator().manual_seed(c)
+    x = torch.randn(3, c, h, w, generator=g) * 2 + 1
+    gam = 1 + 0.2 * torch.randn(c, generator=g)
+    bet = 0.1 * torch.randn(c, generator=g)
+    xr, gr, br = (t.double().requires_grad_() for t in (x, gam, bet))
+    rm, rv = torch.zeros(c, dtype=torch.float64), torch.ones(c, dtype=torch.float64)
+    z = tF.batch_norm(xr, rm, rv, gr, br, True, 0.1, 1e-5)
+    y = {"relu": tF.relu, "hswish": tF.hardswish}[act](z)
+    dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(4), dtype=torch.float64)
+    (y * dy).sum().backward()
+    xg = _nhwc(x).to(cuda).requires_grad_()
+    gg, bg = (torch.nn.Parameter(t.to(cuda)) for t in (gam, bet))
+    rmg, rvg = torch.zeros(c, device=cuda), torch.ones(c, device=cuda)
+    yg = BnActFn.apply(xg, gg, bg, None, rmg, rvg, act, 0.1, 0.1, 1e-5)
+    assert rel_err(_nchw(yg.detach()), y.detach()) < TOL
+    (yg * _nhwc(dy.float()).to(cuda)).sum().backward()
+    _check([_nchw(xg.grad), gg.grad, bg.grad], [xr.grad, gr.grad, br.grad],
+           ["dx", "dgamma", "dbeta"])

@@ -38,6 +38,20 @@ MNV3 = [
     ("ssh1.c3", 32, 128, 128, 40, 20, 3, 1, 0, 1, 0, "relu"),
     ("merge1", 32, 128, 128, 40, 40, 3, 1, 0, 0, 0, "leaky"),
 ]
+# training-pass 1x1 data gradients (transposed weights, no act) at C4 shapes
+TR = [
+    ("b1.proj", 32, 512, 512, 16, 16, 1, 1, 0, 1, 1, "relu"),
+    ("b1e.dg", 32, 512, 512, 64, 16, 1, 1, 0, 0, 0, "none"),
+    ("b3e.dg", 32, 256, 256, 72, 24, 1, 1, 0, 0, 0, "none"),
+    ("b5e.dg", 32, 128, 128, 120, 40, 1, 1, 0, 0, 0, "none"),
+    ("b1p.dg", 32, 512, 512, 16, 16, 1, 1, 0, 0, 0, "none"),
+    ("b3p.dg", 32, 256, 256, 24, 72, 1, 1, 0, 0, 0, "none"),
+    ("t.480a", 3, 32, 48, 112, 480, 1, 1, 0, 0, 0, "none"),
+    ("t.480b", 3, 20, 24, 112, 480, 1, 1, 0, 0, 0, "none"),
+    ("t.480c", 2, 32, 32, 112, 480, 1, 1, 0, 0, 0, "none"),
+    ("t.480d", 3, 32, 48, 480, 112, 1, 1, 0, 0, 0, "none"),
+    ("t.480e", 3, 32, 48, 112, 480, 1, 1, 0, 1, 0, "none"),
+]
 R50 = [
     ("l1.c1", 16, 256, 256, 64, 64, 1, 1, 0, 0, 0, "relu"),
     ("l1.c2", 16, 256, 256, 64, 64, 3, 1, 0, 0, 0, "relu"),
@@ -194,7 +208,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="")
     args = ap.parse_args()
-    shapes = {"mnv3": MNV3, "r50": R50, "all": MNV3 + R50, "xd": XD}[args.set]
+    shapes = {"tr": TR, "mnv3": MNV3, "r50": R50, "all": MNV3 + R50, "xd": XD}[args.set]
     if args.only:
         shapes = [s for s in shapes if s[0] in args.only.split(",")]
     print("# JABD_CONV32=%s JABD_CONV_GENERIC=%s" % (os.environ.get("JABD_CONV32"),

@@ -18,7 +18,7 @@ import glob
 import json
 import sys
 
-KERNELS = ("conv_gemm_kernel", "conv1x1_kernel", "conv1x1_m32_kernel", "expdw_kernel", "expdw1_kernel")  # the conv stack
+KERNELS = ("conv_gemm_kernel", "conv1x1_kernel", "conv1x1_m32_kernel", "conv1x1_stream_kernel", "conv3x3_tile_kernel", "expdw_kernel", "expdw1_kernel")  # the conv stack
 
 
 def _sum(d, counter):
