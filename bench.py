@@ -92,8 +92,12 @@ def conv_roofline(model, x, steps):
     (F.expand_dw).  Events are recorded on torch's current stream, which is the
     stream every libjabd launch uses."""
     from jabd_amd import functional as F
+    from jabd_amd import engine as E
     recs = []
     orig, orig_xd = F.conv, F.expand_dw
+    # per-kernel durations in isolation: one stream (the timed C2 loop splits
+    # the batch over EVAL_STREAMS streams, where launches overlap)
+    streams, E.EVAL_STREAMS = E.EVAL_STREAMS, 1
 
     def timed_conv(xx, pk, stride=1, pad=0, **kw):
         s = torch.cuda.Event(enable_timing=True)
@@ -128,6 +132,7 @@ def conv_roofline(model, x, steps):
         torch.cuda.synchronize()
     finally:
         F.conv, F.expand_dw = orig, orig_xd
+        E.EVAL_STREAMS = streams
     t_ms = sum(r[0].elapsed_time(r[1]) for r in recs)
     flops = sum(r[2] for r in recs)
     nbytes = sum(r[3] for r in recs)
@@ -555,6 +560,10 @@ def main():
     model = build_model(device)
     x = synth.images(args.batch, args.size, seed=1234 + rank, device=device)
     if args.pmc_forward_only:
+        # one stream, as conv_roofline times the kernels (rocprof durations of
+        # overlapping launches would include each other's contention)
+        from jabd_amd import engine as E
+        E.EVAL_STREAMS = 1
         with torch.no_grad():
             for _ in range(args.steps):
                 model(x)

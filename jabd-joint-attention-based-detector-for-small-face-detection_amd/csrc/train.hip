@@ -1457,7 +1457,8 @@ extern "C" int jabd_conv_wgrad_f32(const jabd_conv_args* args, float* part, floa
 // separate sum(da * d) pass over two full tensors (scale_bwd).
 // ---------------------------------------------------------------------------
 // Workgroup per gated channel c: lane n sums image b's chunks in a fixed
-// order; the W-weighted terms are reduced per image from LDS in n order.
+// order (cpi = 1 after wgrad_img_reduce_kernel); the W-weighted terms are
+// reduced per image from LDS in n order.
 __global__ __launch_bounds__(256) void wgrad_eca_reduce_kernel(
     const float* __restrict__ part, int cpi, int B, int E, int Cout,
     const float* __restrict__ scale, const float* __restrict__ w, float* __restrict__ dw,
@@ -1491,18 +1492,48 @@ __global__ __launch_bounds__(256) void wgrad_eca_reduce_kernel(
   }
 }
 
+// G[b][i] = sum_j part[b * cpi + j][i] (i < EN, EN % 4 == 0): the per-image
+// sum of the chunk partials, float4 per thread, j in order (deterministic).
+__global__ __launch_bounds__(256) void wgrad_img_reduce_kernel(const float* __restrict__ part,
+                                                               int cpi, int64_t EN,
+                                                               float* __restrict__ G) {
+  const int64_t i4 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int b = blockIdx.y;
+  if (i4 * 4 >= EN) return;
+  const float4* pb = reinterpret_cast<const float4*>(part + (int64_t)b * cpi * EN) + i4;
+  const int64_t st = EN / 4;
+  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0, a3 = a0;
+  int j = 0;
+  for (; j + 3 < cpi; j += 4) {
+    const float4 v0 = pb[j * st], v1 = pb[(j + 1) * st], v2 = pb[(j + 2) * st],
+                 v3 = pb[(j + 3) * st];
+    a0.x += v0.x; a0.y += v0.y; a0.z += v0.z; a0.w += v0.w;
+    a1.x += v1.x; a1.y += v1.y; a1.z += v1.z; a1.w += v1.w;
+    a2.x += v2.x; a2.y += v2.y; a2.z += v2.z; a2.w += v2.w;
+    a3.x += v3.x; a3.y += v3.y; a3.z += v3.z; a3.w += v3.w;
+  }
+  for (; j < cpi; ++j) {
+    const float4 v = pb[j * st];
+    a0.x += v.x; a0.y += v.y; a0.z += v.z; a0.w += v.w;
+  }
+  reinterpret_cast<float4*>(G + (int64_t)b * EN)[i4] =
+      make_float4((a0.x + a1.x) + (a2.x + a3.x), (a0.y + a1.y) + (a2.y + a3.y),
+                  (a0.z + a1.z) + (a2.z + a3.z), (a0.w + a1.w) + (a2.w + a3.w));
+}
+
 // Image-aligned chunk length: the largest per = HW / 2^j (a multiple of the
 // kernels' 64-pixel stage) that is still >= the normal chunk length, or 0 if
 // the shape does not qualify (1x1 / stride 1, HW % 64, LDS for [B][Cout]).
 static int64_t wgrad_eca_per(const ConvArgs& a) {
   const int64_t HW = (int64_t)a.OH * a.OW;
   if (a.KH != 1 || a.KW != 1 || a.stride != 1 || a.pad != 0 || a.H != a.OH || a.W != a.OW ||
-      HW % kWgPx || (int64_t)a.B * a.Cout * 4 > 64 * 1024 || !wgrad_vec_ok(a) || a.ascale)
+      HW % kWgPx || (int64_t)a.B * a.Cout * 4 > 64 * 1024 || !wgrad_vec_ok(a) || a.ascale ||
+      ((int64_t)a.Cin * a.Cout) % 4)
     return 0;
   const int64_t target = cdiv(a.M, wgrad_chunks(a));
   int64_t per = HW;
   while (per % (2 * kWgPx) == 0 && per / 2 >= target) per /= 2;
-  if (cdiv(a.M, per) * a.Cin * a.Cout > ((int64_t)64 << 20)) return 0;
+  if ((cdiv(a.M, per) + a.B) * a.Cin * a.Cout > ((int64_t)64 << 20)) return 0;
   return per;
 }
 
@@ -1511,7 +1542,7 @@ extern "C" int64_t jabd_conv_wgrad_eca_part_floats(const jabd_conv_args* args) {
   ConvArgs a = *args;
   a.M = (int64_t)a.B * a.OH * a.OW;
   const int64_t per = wgrad_eca_per(a);
-  return per ? cdiv(a.M, per) * a.Cin * a.Cout : 0;
+  return per ? (cdiv(a.M, per) + a.B) * a.Cin * a.Cout : 0;  // chunk partials + per-image sums
 }
 
 extern "C" int jabd_conv_wgrad_eca_f32(const jabd_conv_args* args, const float* scale,
@@ -1529,8 +1560,13 @@ extern "C" int jabd_conv_wgrad_eca_f32(const jabd_conv_args* args, const float* 
   hipStream_t st = as_stream(stream);
   wgrad_launch_parts(a, per, nch, part, st);
   if (int e = check_launch("conv_wgrad")) return e;
+  const int64_t EN = (int64_t)a.Cin * a.Cout;
+  float* G = part + nch * EN;
+  wgrad_img_reduce_kernel<<<dim3((unsigned)cdiv(EN / 4, 256), (unsigned)a.B), 256, 0, st>>>(
+      part, cpi, EN, G);
+  if (int e = check_launch("wgrad_img_reduce")) return e;
   wgrad_eca_reduce_kernel<<<(unsigned)a.Cin, 256, (size_t)a.B * a.Cout * sizeof(float), st>>>(
-      part, cpi, a.B, a.Cin, a.Cout, scale, w, dw, ds);
+      G, 1, a.B, a.Cin, a.Cout, scale, w, dw, ds);
   return check_launch("wgrad_eca_reduce");
 }
 

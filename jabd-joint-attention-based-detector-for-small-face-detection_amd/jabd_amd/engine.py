@@ -34,6 +34,10 @@ FUSE_EXPAND_DW = os.environ.get("JABD_FUSE_EXPAND_DW", "1") != "0"
 # ... and the stride-2 blocks' dw3x3 skip branch into that kernel (it stages
 # the same input tile); JABD_FUSE_SKIP=0 runs it as its own dw launch.
 FUSE_SKIP = os.environ.get("JABD_FUSE_SKIP", "1") != "0"
+# Eval batches of EVAL_SPLIT_MIN+ images run as EVAL_STREAMS image groups on
+# their own HIP streams (Engine.run); JABD_EVAL_STREAMS=1 runs one stream (A/B).
+EVAL_STREAMS = int(os.environ.get("JABD_EVAL_STREAMS", "2"))
+EVAL_SPLIT_MIN = int(os.environ.get("JABD_EVAL_SPLIT_MIN", "8"))
 
 
 def _w1d(eca):
@@ -201,15 +205,20 @@ class _Head:
             return M.beca_gate(f, w1d)
         return F.eca_gate(F.channel_sums(f), f.shape[1] * f.shape[2], w1d, "sigmoid")
 
-    def forward(self, feats, softmax):
+    def forward(self, feats, softmax, out=None):
         B = feats[0].shape[0]
         scales = [self._gate(f, w1d) for f, w1d in zip(feats, self.eca_in)]
         levels = self.fpn.forward(feats, scales)
         A = sum(2 * o.shape[1] * o.shape[2] for o in levels)
         dev = levels[0].device
-        loc = torch.empty((B, A, 4), dtype=torch.float32, device=dev)
-        conf = torch.empty((B, A, 2), dtype=torch.float32, device=dev)
-        landm = torch.empty((B, A, 10), dtype=torch.float32, device=dev)
+        if out is not None:  # batch slices of the caller's outputs
+            loc, conf, landm = out
+            if loc.shape[1] != A:
+                raise RuntimeError(f"engine: anchor count {loc.shape[1]} != {A} of the levels")
+        else:
+            loc = torch.empty((B, A, 4), dtype=torch.float32, device=dev)
+            conf = torch.empty((B, A, 2), dtype=torch.float32, device=dev)
+            landm = torch.empty((B, A, 10), dtype=torch.float32, device=dev)
         a_off = 0
         for i, o in enumerate(levels):
             _, h, w, C = o.shape
@@ -338,13 +347,68 @@ class Engine:
                            for stage in mnv3_stages(m.body)]
             self.head = _Head(m, getattr(m, "eca_names", ("eca_40", "eca_80", "eca_160")), "nlm",
                               dev, gate=getattr(m, "head_gate", "sigmoid"))
+            # the JABD-MNv3 detector (ECA blocks, mean-pool ECA head): 2 streams
+            # +1.5% at bs32 1024^2; MobileNetV3_Small (SE gates, 4 ms/step of
+            # small launches) loses 28% and the BECA head is neutral, so they
+            # keep one stream
+            self.split_ok = (self.head.gate == "sigmoid" and
+                             all(b.gate == "eca" for layer in self.layers for b in layer))
         else:
             self.stem = F.pack_conv(m.body.conv1, m.body.bn1)
             self.layers = [[b._jabd_cached(dev, lambda b=b: _R50Block(b))
                             for b in getattr(m.body, f"layer{i}")] for i in (1, 2, 3, 4)]
             self.head = _Head(m, ("eca_64", "eca_128", "eca_256"), "Nlm", dev)
+            self.split_ok = False  # compute-bound convs; not measured split
 
     def run(self, x, softmax):
+        """Forward of a batch.  From EVAL_SPLIT_MIN images up, the batch is
+        split into EVAL_STREAMS image groups, each run on its own HIP stream
+        (every op is per image, so the groups are independent): the small
+        launches of one group (ECA gates, pools, the 32x32 / 64x64 head convs,
+        NLM, heads) run beside the large convs of the other instead of leaving
+        most of the CUs idle.  The heads write straight into batch slices of
+        one set of outputs."""
+        B = x.shape[0]
+        n = min(EVAL_STREAMS, B) if B >= EVAL_SPLIT_MIN and self.split_ok else 1
+        if n <= 1:
+            return self._run(x, softmax)
+        cur = torch.cuda.current_stream(x.device)
+        if getattr(self, "_streams", None) is None or len(self._streams) < n:
+            self._streams = [torch.cuda.Stream(device=x.device) for _ in range(n)]
+        bounds = [B * i // n for i in range(n + 1)]
+        with torch.no_grad():
+            H, W = x.shape[2], x.shape[3]
+            A = self.anchors(H, W)
+            dev = x.device
+            out = (torch.empty((B, A, 4), dtype=torch.float32, device=dev),
+                   torch.empty((B, A, 2), dtype=torch.float32, device=dev),
+                   torch.empty((B, A, 10), dtype=torch.float32, device=dev))
+            for i in range(n):
+                st = self._streams[i]
+                st.wait_stream(cur)
+                b0, b1 = bounds[i], bounds[i + 1]
+                with torch.cuda.stream(st):
+                    self._run(x[b0:b1], softmax, out=tuple(o[b0:b1] for o in out))
+            for i in range(n):
+                cur.wait_stream(self._streams[i])
+        return out
+
+    def anchors(self, H, W):
+        """Anchor count of an H x W input: 2 per cell of the stride-8/16/32 maps
+        (the detector's own conv arithmetic, pad 1, kernel 3, stride 2)."""
+        def down(v, times):
+            for _ in range(times):
+                v = (v + 2 - 3) // 2 + 1
+            return v
+        if self.kind == "mnv3":
+            sizes = [(down(H, t), down(W, t)) for t in (3, 4, 5)]
+        else:  # R50: 7x7/s2 stem, 3x3/s2 max-pool, then /2 per stage
+            h, w = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+            h, w = down(h, 1), down(w, 1)
+            sizes = [(down(h, t), down(w, t)) for t in (1, 2, 3)]
+        return sum(2 * a * b for a, b in sizes)
+
+    def _run(self, x, softmax, out=None):
         with torch.no_grad():
             if self.kind == "mnv3":
                 s = F.stem(x, self.stem[0], self.stem[1], "hswish")
@@ -362,7 +426,7 @@ class Engine:
                         s = blk.forward(s)
                     if li >= 1:
                         feats.append(s)
-            return self.head.forward(feats, softmax=softmax)
+            return self.head.forward(feats, softmax=softmax, out=out)
 
 
 def _check_input(x):

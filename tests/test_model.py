@@ -109,3 +109,31 @@ def test_r50_forward_parity_full_size(cuda):
     from jabd_amd import synth
     x = synth.images(1, 1024, seed=4321)
     _compare(_r50(), model_ref.retinaface_r50, x, cuda, "eval", elem_tol=1e-2)
+
+
+@pytest.mark.gpu
+def test_mnv3_eval_stream_split(cuda):
+    """Engine.run splits a batch of >= EVAL_SPLIT_MIN images over EVAL_STREAMS
+    HIP streams: the outputs equal the one-stream forward's, image by image
+    (every op is per image), and the oracle's."""
+    from jabd_amd import engine as E
+    m = _mnv3().to(cuda)
+    x = torch.randn(9, 3, 96, 128, generator=torch.Generator().manual_seed(3)) * 60
+    xg = x.to(cuda)
+    assert E.EVAL_STREAMS >= 2 and x.shape[0] >= E.EVAL_SPLIT_MIN
+    with torch.no_grad():
+        split = [t.clone() for t in m(xg)]
+        saved = E.EVAL_STREAMS
+        E.EVAL_STREAMS = 1
+        try:
+            one = m(xg)
+        finally:
+            E.EVAL_STREAMS = saved
+    eng = m._jabd_cached(xg.device, None, tag="engine")
+    assert eng.split_ok
+    for a, b in zip(split, one):
+        assert a.shape == b.shape
+        assert torch.equal(a, b)
+    ref = model_ref.retinaface_mnv3({k: v.cpu() for k, v in m.state_dict().items()}, x)
+    for a, r in zip(split, ref):
+        assert rel_err(a.cpu(), r) < 1e-3
