@@ -468,6 +468,16 @@ int jabd_bn_act_bwd_f32(const float* dy, int32_t lddy, int32_t dyc0, const float
                         const float* invstd, const float* gamma, const float* beta, int32_t act,
                         float slope, float* part, float* dgamma, float* dbeta, float* dx,
                         float* dres, jabd_stream_t stream);
+/* jabd_bn_act_fwd_f32 (contiguous x / y, no residual) that also writes the
+ * channel sums of y per block of rows, part[B][nblk][C] with nblk =
+ * jabd_bn_sum_nblk(hw, C) (0: hw not a multiple of the block; use
+ * jabd_channel_sum_f32) — the ECA pool input of a MobileNetV3 Block_eca
+ * (nets/mobilenetV3.py:141-148, 343-348) without a pass over y. */
+int64_t jabd_bn_sum_nblk(int64_t hw, int32_t C);
+int jabd_bn_act_fwd_sum_f32(const float* x, int64_t M, int32_t C, const float* mean,
+                            const float* invstd, const float* gamma, const float* beta,
+                            int32_t act, float slope, float* y, int64_t hw, float* part,
+                            jabd_stream_t stream);
 /* The same with the incoming gradient mapped per (image, channel) first:
  * dy' = dy * dys[b][c] + dya[b][c], b = row / hw (dys NULL: no map) — the
  * backward of an ECA gate that followed this BN (jabd_eca_bwd_terms_f32). */

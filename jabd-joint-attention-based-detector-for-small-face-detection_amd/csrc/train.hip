@@ -222,6 +222,55 @@ __global__ __launch_bounds__(kRedThreads) void bn_act_fwd_kernel(
   }
 }
 
+// y = act((x - mean) * invstd * gamma + beta) and, for the ECA gate that
+// follows BN2 in a MobileNetV3 block (nets/mobilenetV3.py:141-148), the
+// channel sums of y per block of RB = rp * kEwIters rows (rp a power of two
+// dividing H*W / kEwIters, so no block straddles an image): part[blk][c],
+// i.e. [B][HW / RB][C] — the pass over y that F.channel_sums would make.
+__global__ __launch_bounds__(kRedThreads) void bn_act_fwd_sum_kernel(
+    const float* __restrict__ x, int64_t M, int C, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ beta, int act, float slope, float* __restrict__ y, int lanes,
+    int rp, float* __restrict__ part) {
+  __shared__ float4 red[kRedThreads];
+  const int t = threadIdx.x, r0 = t / lanes, cl = t - r0 * lanes;
+  const int C4 = C >> 2;
+  const int cg = blockIdx.y * lanes + cl;
+  const bool ok = r0 < rp && cg < C4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (ok) {
+    const int c = cg * 4;
+    const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+    const float4 is = *reinterpret_cast<const float4*>(invstd + c);
+    const float4 gm = *reinterpret_cast<const float4*>(gamma + c);
+    const float4 bt = *reinterpret_cast<const float4*>(beta + c);
+    const int64_t m0 = (int64_t)blockIdx.x * rp * kEwIters + r0;
+#pragma unroll 2
+    for (int k = 0; k < kEwIters; ++k) {
+      const int64_t m = m0 + (int64_t)k * rp;
+      if (m >= M) break;
+      const float4 v = *reinterpret_cast<const float4*>(x + m * C + c);
+      float4 o;
+      o.x = act_f((v.x - mu.x) * is.x * gm.x + bt.x, act, slope);
+      o.y = act_f((v.y - mu.y) * is.y * gm.y + bt.y, act, slope);
+      o.z = act_f((v.z - mu.z) * is.z * gm.z + bt.z, act, slope);
+      o.w = act_f((v.w - mu.w) * is.w * gm.w + bt.w, act, slope);
+      *reinterpret_cast<float4*>(y + m * C + c) = o;
+      acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+    }
+  }
+  red[t] = acc;
+  __syncthreads();
+  if (r0 == 0 && cg < C4) {
+    float4 S = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = 0; r < rp; ++r) {
+      const float4 a = red[r * lanes + cl];
+      S.x += a.x; S.y += a.y; S.z += a.z; S.w += a.w;
+    }
+    reinterpret_cast<float4*>(part + (int64_t)blockIdx.x * C)[cg] = S;
+  }
+}
+
 // dz = dy * act'(z);  part[blk][0][c] = sum dz, part[blk][1][c] = sum dz * xhat
 // Optional per-(image, channel) affine map of the incoming gradient,
 // dy' = dy * dys[b][c] + dya[b][c] (b = row / hw): the backward of an ECA
@@ -1330,6 +1379,38 @@ extern "C" int jabd_bn_act_fwd_f32(const float* x, int32_t ldx, int64_t M, int32
   bn_act_fwd_kernel<<<grid, kRedThreads, 0, as_stream(stream)>>>(
       x, ldx, M, C, mean, invstd, gamma, beta, res, ldr, act, slope, y, ldy, yc0, lanes);
   return check_launch("bn_act_fwd");
+}
+
+// Rows per channel-sum block of jabd_bn_act_fwd_sum_f32 for C channels:
+// rp (a power of two, rp * lanes <= 256) times kEwIters.
+static int bn_sum_rp(int C) {
+  const int C4 = C / 4, lanes = C4 < 64 ? C4 : 64;
+  int rp = 1;
+  while (rp * 2 * lanes <= kRedThreads) rp *= 2;
+  return rp;
+}
+
+extern "C" int64_t jabd_bn_sum_nblk(int64_t hw, int32_t C) {
+  if (hw <= 0 || C <= 0 || C % 4) return 0;
+  const int64_t rb = (int64_t)bn_sum_rp(C) * kEwIters;
+  return hw % rb ? 0 : hw / rb;
+}
+
+extern "C" int jabd_bn_act_fwd_sum_f32(const float* x, int64_t M, int32_t C, const float* mean,
+                                       const float* invstd, const float* gamma,
+                                       const float* beta, int32_t act, float slope, float* y,
+                                       int64_t hw, float* part, jabd_stream_t stream) {
+  JABD_REQUIRE(x && mean && invstd && gamma && beta && y && part && C % 4 == 0 && hw > 0 &&
+                   M % hw == 0,
+               "bn_act_fwd_sum: bad args");
+  JABD_REQUIRE(jabd_bn_sum_nblk(hw, C) > 0, "bn_act_fwd_sum: hw %lld not a multiple of the %d-row "
+               "block (jabd_bn_sum_nblk = 0)", (long long)hw, bn_sum_rp(C) * kEwIters);
+  if (M == 0) return JABD_OK;
+  const int C4 = C / 4, lanes = C4 < 64 ? C4 : 64, rp = bn_sum_rp(C);
+  const dim3 grid((unsigned)(M / ((int64_t)rp * kEwIters)), (unsigned)cdiv(C4, lanes), 1);
+  bn_act_fwd_sum_kernel<<<grid, kRedThreads, 0, as_stream(stream)>>>(
+      x, M, C, mean, invstd, gamma, beta, act, slope, y, lanes, rp, part);
+  return check_launch("bn_act_fwd_sum");
 }
 
 extern "C" int jabd_bn_act_bwd_f32(const float* dy, int32_t lddy, int32_t dyc0, const float* x,

@@ -168,6 +168,9 @@ SIGNATURES = {
                             c_vp, c_vp, c_vp, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "jabd_conv_wgrad_part_floats": [ctypes.POINTER(ConvArgs)],
     "jabd_conv_wgrad_f32": [ctypes.POINTER(ConvArgs), c_vp, c_vp, c_vp],
+    "jabd_bn_sum_nblk": [c_i64, c_i32],
+    "jabd_bn_act_fwd_sum_f32": [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_f32, c_vp,
+                                c_i64, c_vp, c_vp],
     "jabd_conv_wgrad_eca_part_floats": [ctypes.POINTER(ConvArgs)],
     "jabd_conv_wgrad_eca_f32": [ctypes.POINTER(ConvArgs), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "jabd_eca_gate_bwd_f32": [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32,
@@ -216,7 +219,7 @@ SIGNATURES = {
 _RESTYPE = {"jabd_version": ctypes.c_char_p, "jabd_dw_nblk": ctypes.c_int64,
             "jabd_expand_dw_nblk": ctypes.c_int64,
             "jabd_bn_nblk": ctypes.c_int64, "jabd_conv_wgrad_part_floats": ctypes.c_int64,
-            "jabd_conv_wgrad_eca_part_floats": ctypes.c_int64,
+            "jabd_conv_wgrad_eca_part_floats": ctypes.c_int64, "jabd_bn_sum_nblk": ctypes.c_int64,
             "jabd_dw_wgrad_part_floats": ctypes.c_int64,
             "jabd_adam_num_chunks": ctypes.c_int64, "jabd_beca_ws_floats": ctypes.c_int64,
             "jabd_adaptive_pool_ws_floats": ctypes.c_int64,

@@ -34,9 +34,12 @@ FUSE_EXPAND_DW = os.environ.get("JABD_FUSE_EXPAND_DW", "1") != "0"
 # ... and the stride-2 blocks' dw3x3 skip branch into that kernel (it stages
 # the same input tile); JABD_FUSE_SKIP=0 runs it as its own dw launch.
 FUSE_SKIP = os.environ.get("JABD_FUSE_SKIP", "1") != "0"
-# Eval batches of EVAL_SPLIT_MIN+ images run as EVAL_STREAMS image groups on
-# their own HIP streams (Engine.run); JABD_EVAL_STREAMS=1 runs one stream (A/B).
-EVAL_STREAMS = int(os.environ.get("JABD_EVAL_STREAMS", "2"))
+# JABD_EVAL_STREAMS=2: eval batches of EVAL_SPLIT_MIN+ images run as image
+# groups on their own HIP streams (Engine.run).  Off by default: at bs32
+# 1024^2 two streams are +1.7% with weights_init's near-zero activations but
+# -15% with O(1) activations (4540 -> 3840 img/s, same box): the overlapped
+# launches cost more clock than the filled CUs gain once the data is real.
+EVAL_STREAMS = int(os.environ.get("JABD_EVAL_STREAMS", "1"))
 EVAL_SPLIT_MIN = int(os.environ.get("JABD_EVAL_SPLIT_MIN", "8"))
 
 
@@ -347,10 +350,9 @@ class Engine:
                            for stage in mnv3_stages(m.body)]
             self.head = _Head(m, getattr(m, "eca_names", ("eca_40", "eca_80", "eca_160")), "nlm",
                               dev, gate=getattr(m, "head_gate", "sigmoid"))
-            # the JABD-MNv3 detector (ECA blocks, mean-pool ECA head): 2 streams
-            # +1.5% at bs32 1024^2; MobileNetV3_Small (SE gates, 4 ms/step of
-            # small launches) loses 28% and the BECA head is neutral, so they
-            # keep one stream
+            # the split is offered for the JABD-MNv3 detector (ECA blocks,
+            # mean-pool ECA head) only; MobileNetV3_Small (SE gates, 4 ms/step
+            # of small launches) loses 28% with it and the BECA head is neutral
             self.split_ok = (self.head.gate == "sigmoid" and
                              all(b.gate == "eca" for layer in self.layers for b in layer))
         else:

@@ -36,6 +36,8 @@ ACT = F.ACT
 FUSED_BLOCKS = __import__("os").environ.get("JABD_FUSED_BLOCKS", "1") != "0"
 # JABD_ECA_WGRAD=0: the ECA block backward takes sum(da * d) from its own pass (A/B)
 ECA_WGRAD = __import__("os").environ.get("JABD_ECA_WGRAD", "1") != "0"
+# JABD_ECA_SUMS=0: the ECA pool of a block reads d in its own pass (A/B)
+ECA_SUMS = __import__("os").environ.get("JABD_ECA_SUMS", "1") != "0"
 
 
 def _st():
@@ -685,9 +687,11 @@ def conv(x, m, stride=1, pad=0, nchw_in=False):
 
 
 # ----------------------------------------------------------------------------- fused block
-def _bn_fwd(x, bn, act, slope=0.0, res=None):
+def _bn_fwd(x, bn, act, slope=0.0, res=None, sums=False):
     """Batch-stat BN (+res) + act of NHWC x; running buffers updated in place.
-    Returns (y, (gamma, beta, mean, invstd))."""
+    Returns (y, (gamma, beta, mean, invstd)); sums=True adds the per-image
+    channel-sum partials of y ([B, nblk, C], written by the apply pass) or
+    None when the map size does not fit its row blocks."""
     B, H, W, C = x.shape
     M = B * H * W
     nblk = int(lib().jabd_bn_nblk(M, C))
@@ -700,10 +704,21 @@ def _bn_fwd(x, bn, act, slope=0.0, res=None):
     g = bn.weight.detach()
     b = bn.bias.detach()
     y = torch.empty_like(x)
-    call("jabd_bn_act_fwd_f32", x.data_ptr(), C, M, C, mean.data_ptr(), invstd.data_ptr(),
-         g.data_ptr(), b.data_ptr(), _p(res), C, ACT[act], float(slope), y.data_ptr(), C, 0,
-         _st())
+    nsum = int(lib().jabd_bn_sum_nblk(H * W, C)) if sums and ECA_SUMS and res is None and \
+        x.is_contiguous() else 0
+    if nsum:
+        psum = torch.empty((B, nsum, C), dtype=torch.float32, device=x.device)
+        call("jabd_bn_act_fwd_sum_f32", x.data_ptr(), M, C, mean.data_ptr(), invstd.data_ptr(),
+             g.data_ptr(), b.data_ptr(), ACT[act], float(slope), y.data_ptr(), H * W,
+             psum.data_ptr(), _st())
+    else:
+        psum = None
+        call("jabd_bn_act_fwd_f32", x.data_ptr(), C, M, C, mean.data_ptr(), invstd.data_ptr(),
+             g.data_ptr(), b.data_ptr(), _p(res), C, ACT[act], float(slope), y.data_ptr(), C, 0,
+             _st())
     _count_batch(bn)
+    if sums:
+        return y, (g, b, mean, invstd), psum
     return y, (g, b, mean, invstd)
 
 
@@ -797,10 +812,12 @@ class MNv3BlockFn(torch.autograd.Function):
         e_pre = _conv_fwd(s, blk.conv1.weight)
         e, st1 = _bn_fwd(e_pre, blk.bn1, act)
         d_pre, wt2 = _dw_fwd(e, blk.conv2.weight, stride)
-        d, st2 = _bn_fwd(d_pre, blk.bn2, act)
+        d, st2, psum = _bn_fwd(d_pre, blk.bn2, act, sums=True)
         B, OH, OW, E = d.shape
         w1 = blk.eca.conv.weight.detach().reshape(-1).float().contiguous()
-        scale, mean = F.eca_gate(F.channel_sums(d), OH * OW, w1, "hsigmoid", return_mean=True)
+        if psum is None:
+            psum = F.channel_sums(d)
+        scale, mean = F.eca_gate(psum, OH * OW, w1, "hsigmoid", return_mean=True)
         p = _conv_fwd(d, blk.conv3.weight, ascale=scale)
         sk = blk.skip
         saved_skip = ()

@@ -113,19 +113,20 @@ def test_r50_forward_parity_full_size(cuda):
 
 @pytest.mark.gpu
 def test_mnv3_eval_stream_split(cuda):
-    """Engine.run splits a batch of >= EVAL_SPLIT_MIN images over EVAL_STREAMS
-    HIP streams: the outputs equal the one-stream forward's, image by image
-    (every op is per image), and the oracle's."""
+    """Engine.run with EVAL_STREAMS = 2 splits a batch of >= EVAL_SPLIT_MIN
+    images over two HIP streams: the outputs equal the one-stream forward's,
+    image by image (every op is per image), and the oracle's."""
     from jabd_amd import engine as E
     m = _mnv3().to(cuda)
     x = torch.randn(9, 3, 96, 128, generator=torch.Generator().manual_seed(3)) * 60
     xg = x.to(cuda)
-    assert E.EVAL_STREAMS >= 2 and x.shape[0] >= E.EVAL_SPLIT_MIN
+    assert x.shape[0] >= E.EVAL_SPLIT_MIN
+    saved = E.EVAL_STREAMS
     with torch.no_grad():
-        split = [t.clone() for t in m(xg)]
-        saved = E.EVAL_STREAMS
-        E.EVAL_STREAMS = 1
         try:
+            E.EVAL_STREAMS = 2
+            split = [t.clone() for t in m(xg)]
+            E.EVAL_STREAMS = 1
             one = m(xg)
         finally:
             E.EVAL_STREAMS = saved
