@@ -49,6 +49,7 @@ __device__ __forceinline__ float act32(float v, int act, float slope) {
 
 constexpr int kBK = 32;          // K channels per stage
 constexpr int kG = kBK / 8;      // 8-channel groups per stage
+constexpr int kGateLds = 1024;   // ECA gate channels staged in LDS
 
 // Workgroup = 4 waves stacked along M (BM = 128*TM pixels) x BN = 32*TN
 // channels.  Tiles never straddle an image when `per_img` (ECA gate folded
@@ -56,7 +57,8 @@ constexpr int kG = kBK / 8;      // 8-channel groups per stage
 // KXK: k x k implicit GEMM (tap-major K; every 32-channel stage lies inside
 // one tap, host guarantees Cin % 32 == 0, no K-concat source); stride-1
 // transposed form (tconv) for the data gradient.
-template <int TM, int TN, bool KXK>
+template <int TM, int TN, bool KXK, bool AS>
+// AS: the ECA gate (ascale) is set — staged in LDS, applied at the weight store.
 // phase >= 0 (KXK, stride-2 tconv): this launch covers only the output
 // pixels (2i + ph, 2j + pw), phase = 2 ph + pw, and only the taps that reach
 // them — the sub-pixel decomposition of a strided data gradient (the other
@@ -67,6 +69,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
   constexpr int NB4 = kG * TN * 64;            // float4 of one weight stage
   constexpr int NBT = (NB4 + 255) / 256;       // ... per thread
   __shared__ float4 sB[2][NB4];
+  __shared__ __attribute__((aligned(16))) float sGate[AS ? kGateLds : 4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 5, j = lane & 31;
   const int nblk_n = p.Ntiles / TN;  // Ntiles counts 32-channel tiles here
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
   const int cps = p.Cin / kBK;  // KXK: stages per tap
   const int x2_pix = (p.x2 && p.x2_stride != 1) ? (int)(p.x2_bs / p.x2_ps) : 0;
   const float4* wg = reinterpret_cast<const float4*>(p.w);
-  const float* sc = p.ascale ? p.ascale + (int64_t)img * p.ascale_bs : nullptr;
+  const float* sc = AS ? p.ascale + (int64_t)img * p.ascale_bs : nullptr;
 
   auto load_a = [&](int s, float4 (&a)[TM][kG]) {
     if constexpr (KXK) {
@@ -167,7 +170,13 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
         a[t][q] = r;
       }
   };
-  // weight stage s -> registers (ECA gate applied to the rows k < Cin)
+  // ECA gate of this workgroup's image staged in LDS once (Cin <= kGateLds):
+  // store_b applies it on the way to LDS.  Applied in load_b (from global) the
+  // multiply makes the wave wait for the weight and gate loads before the
+  // stage's MFMAs instead of behind them (b12 project 312 -> see DESIGN).
+  const bool gate_lds = AS && p.Cin <= kGateLds;
+  // weight stage s -> registers (ECA gate applied to the rows k < Cin when it
+  // is not staged in LDS)
   auto load_b = [&](int s, float4 (&b)[NBT]) {
     // phase mode: local stage -> the global tap's weight stage
     if (KXK && phase >= 0) {
@@ -184,7 +193,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
         const int u = rem >> 6, l = rem & 63;
         const int k8 = s * kG + g;
         v = wg[((int64_t)k8 * p.Ntiles + nb * TN + u) * 64 + l];
-        if (sc) {
+        if (sc && !gate_lds) {
           int k0 = 8 * k8 + 4 * (l >> 5);
           if (KXK) k0 -= (s / cps) * p.Cin;  // channel within the stage's tap
           if (k0 < p.Cin) {
@@ -196,11 +205,28 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
       b[i] = v;
     }
   };
-  auto store_b = [&](int buf, const float4 (&b)[NBT]) {
+  auto store_b = [&](int buf, int s, const float4 (&b)[NBT]) {
+    if (KXK && phase >= 0) {  // as load_b: the global tap's weight stage
+      const int tl = s / cps, khi = tl / nkw;
+      const int tap = (kh0 + 2 * khi) * p.KW + kw0 + 2 * (tl - khi * nkw);
+      s = tap * cps + (s - tl * cps);
+    }
 #pragma unroll
     for (int i = 0; i < NBT; ++i) {
       const int f = i * 256 + threadIdx.x;
-      if (f < NB4) sB[buf][f] = b[i];
+      if (f < NB4) {
+        float4 v = b[i];
+        if (gate_lds) {
+          const int g = f / (TN * 64), l = f & 63;
+          int k0 = 8 * (s * kG + g) + 4 * (l >> 5);
+          if (KXK) k0 -= (s / cps) * p.Cin;
+          if (k0 < p.Cin) {
+            const float4 s4 = *reinterpret_cast<const float4*>(sGate + k0);
+            v.x *= s4.x; v.y *= s4.y; v.z *= s4.z; v.w *= s4.w;
+          }
+        }
+        sB[buf][f] = v;
+      }
     }
   };
 
@@ -213,10 +239,14 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
       for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
 
   float4 a_cur[TM][kG], a_nxt[TM][kG], b_nxt[NBT];
+  if (gate_lds) {
+    for (int i = threadIdx.x; i < p.Cin; i += 256) sGate[i] = sc[i];
+    __syncthreads();
+  }
   if (S > 0) {  // (a phase of a 1x1 stride-2 data gradient has no taps: zeros)
     load_a(0, a_cur);
     load_b(0, b_nxt);
-    store_b(0, b_nxt);
+    store_b(0, 0, b_nxt);
   }
   __syncthreads();
   for (int s = 0; s < S; ++s) {
@@ -253,7 +283,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
           acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(bw[u].w, a_cur[t][q].w, acc[t][u], 0, 0, 0);
     }
     if (more) {
-      store_b((s + 1) & 1, b_nxt);
+      store_b((s + 1) & 1, s + 1, b_nxt);
 #pragma unroll
       for (int t = 0; t < TM; ++t)
 #pragma unroll
@@ -294,8 +324,17 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
   }
 }
 
+template <int TM, int TN, bool KXK, bool AS>
+static int launch_m32_as(const ConvArgs& a, hipStream_t st);
+
 template <int TM, int TN, bool KXK>
 static int launch_m32(const ConvArgs& a, hipStream_t st) {
+  if (a.ascale) return launch_m32_as<TM, TN, KXK, true>(a, st);
+  return launch_m32_as<TM, TN, KXK, false>(a, st);
+}
+
+template <int TM, int TN, bool KXK, bool AS>
+static int launch_m32_as(const ConvArgs& a, hipStream_t st) {
   constexpr int BM = 4 * 32 * TM;
   const int64_t OHW = (int64_t)a.OH * a.OW;
   const int per_img = a.ascale != nullptr;
@@ -308,7 +347,7 @@ static int launch_m32(const ConvArgs& a, hipStream_t st) {
         if (Mp <= 0) continue;
         const int64_t grid = cdiv(Mp, BM) * (a.Ntiles / TN);
         JABD_REQUIRE(grid < (int64_t)0x7fffffff, "conv32: grid too large");
-        conv1x1_m32_kernel<TM, TN, KXK><<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, 0,
+        conv1x1_m32_kernel<TM, TN, KXK, AS><<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, 0,
                                                                         2 * ph + pw);
         if (int e = check_launch("conv1x1_m32")) return e;
       }
@@ -317,7 +356,7 @@ static int launch_m32(const ConvArgs& a, hipStream_t st) {
   const int64_t mtiles = per_img ? mt_img * a.B : cdiv(a.M, BM);
   const int64_t grid = mtiles * (a.Ntiles / TN);
   JABD_REQUIRE(grid < (int64_t)0x7fffffff, "conv32: grid too large");
-  conv1x1_m32_kernel<TM, TN, KXK><<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, per_img, -1);
+  conv1x1_m32_kernel<TM, TN, KXK, AS><<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, per_img, -1);
   return check_launch("conv1x1_m32");
 }
 

@@ -46,6 +46,12 @@ TR = [
     ("b5e.dg", 32, 128, 128, 120, 40, 1, 1, 0, 0, 0, "none"),
     ("b1p.dg", 32, 512, 512, 16, 16, 1, 1, 0, 0, 0, "none"),
     ("b3p.dg", 32, 256, 256, 24, 72, 1, 1, 0, 0, 0, "none"),
+    ("b12.p.asc", 32, 64, 64, 672, 112, 1, 1, 0, 1, 1, "hswish"),
+    ("b12.p.noasc", 32, 64, 64, 672, 112, 1, 1, 0, 0, 1, "hswish"),
+    ("b11.p.asc", 32, 64, 64, 480, 112, 1, 1, 80, 1, 0, "hswish"),
+    ("b11.p.noasc", 32, 64, 64, 480, 112, 1, 1, 80, 0, 0, "hswish"),
+    ("b15.p.asc", 32, 32, 32, 960, 160, 1, 1, 0, 1, 1, "hswish"),
+    ("b15.p.noasc", 32, 32, 32, 960, 160, 1, 1, 0, 0, 1, "hswish"),
     ("t.480a", 3, 32, 48, 112, 480, 1, 1, 0, 0, 0, "none"),
     ("t.480b", 3, 20, 24, 112, 480, 1, 1, 0, 0, 0, "none"),
     ("t.480c", 2, 32, 32, 112, 480, 1, 1, 0, 0, 0, "none"),
