@@ -3,6 +3,8 @@
 // fused with the FPN's nearest up-sample and lateral add, and the three
 // detection heads written straight into the anchor-major output layout.
 // All HBM/latency-bound: one pass over each activation, fixed-order sums.
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "common.h"
@@ -310,13 +312,15 @@ __global__ __launch_bounds__(256) void nlm_pool_kernel(const float* __restrict__
 // and combined by butterfly), and writes every 4th float4 channel group of
 // the output.  One lane per pixel ran the 225-bin chain serially at two waves
 // per SIMD (latency-bound, ~10% of its HBM floor).
-template <int CH>
+template <int CH, int PX>
 __global__ __launch_bounds__(256) void nlm_apply_kernel(
     const float* __restrict__ src, int64_t src_bs, int src_ps, int hs, int ws, int C, int h,
     int w, const float* __restrict__ wq, const float* __restrict__ bq,
     const float* __restrict__ kpool, const float* __restrict__ vpool, int S,
     const float* __restrict__ wW, const float* __restrict__ bW, const float* __restrict__ lateral,
     float* __restrict__ out, float* __restrict__ q_out, float* __restrict__ ctx_out) {
+  // PX pixels per quad: every K / V bin read from LDS serves PX pixels (the
+  // bin loops were LDS-read bound at one pixel per quad).
   static_assert(CH == 4, "one q channel per quad lane");
   extern __shared__ float sm[];  // K [S][CH], V [S][CH], wq [CH][C], wW [C][CH], bW [C]
   const int b = blockIdx.y;
@@ -336,82 +340,111 @@ __global__ __launch_bounds__(256) void nlm_apply_kernel(
   for (int t = threadIdx.x; t < C; t += blockDim.x) sbW[t] = bW[t];
   __syncthreads();
   const int r = threadIdx.x & 3;
-  const int pix = blockIdx.x * (blockDim.x >> 2) + (threadIdx.x >> 2);
-  const bool pv = pix < h * w;
-  const int pc = pv ? pix : 0;  // the quad stays whole for the shuffles
-  const int i = pc / w, jx = pc - (pc / w) * w;
-  const float* xp = src + (int64_t)b * src_bs +
-                    ((int64_t)nearest_src(i, hs, h) * ws + nearest_src(jx, ws, w)) * src_ps;
-  float qr = bq[r];
-  for (int c = 0; c < C; c += 4) {
-    const float4 x = *reinterpret_cast<const float4*>(xp + c);
-    const float* wr = sWq + r * C + c;
-    qr = fmaf(wr[0], x.x, qr);
-    qr = fmaf(wr[1], x.y, qr);
-    qr = fmaf(wr[2], x.z, qr);
-    qr = fmaf(wr[3], x.w, qr);
-  }
   const int qb = threadIdx.x & ~3;  // quad base lane
-  float q[CH];
+  // quad's pixels: pix0 + i * 64 (consecutive quads -> consecutive pixels)
+  const int pix0 = blockIdx.x * (blockDim.x >> 2) * PX + (threadIdx.x >> 2);
+  int pix[PX];
+  bool pv[PX];
+  const float* xp[PX];
+  float q[PX][CH];
 #pragma unroll
-  for (int o = 0; o < CH; ++o) q[o] = __shfl(qr, (qb + o) & 63);
+  for (int i = 0; i < PX; ++i) {
+    pix[i] = pix0 + i * (blockDim.x >> 2);
+    pv[i] = pix[i] < h * w;
+    const int pc = pv[i] ? pix[i] : 0;  // the quad stays whole for the shuffles
+    const int yy = pc / w, xx = pc - yy * w;
+    xp[i] = src + (int64_t)b * src_bs +
+            ((int64_t)nearest_src(yy, hs, h) * ws + nearest_src(xx, ws, w)) * src_ps;
+    float qr = bq[r];
+    for (int c = 0; c < C; c += 4) {
+      const float4 x = *reinterpret_cast<const float4*>(xp[i] + c);
+      const float* wr = sWq + r * C + c;
+      qr = fmaf(wr[0], x.x, qr);
+      qr = fmaf(wr[1], x.y, qr);
+      qr = fmaf(wr[2], x.z, qr);
+      qr = fmaf(wr[3], x.w, qr);
+    }
+#pragma unroll
+    for (int o = 0; o < CH; ++o) q[i][o] = __shfl(qr, (qb + o) & 63);
+  }
   const float4* K4 = reinterpret_cast<const float4*>(sK);
   const float4* V4 = reinterpret_cast<const float4*>(sV);
-  float mx = -INFINITY;
+  float mx[PX];
+#pragma unroll
+  for (int i = 0; i < PX; ++i) mx[i] = -INFINITY;
 #pragma unroll 4
   for (int s = r; s < S; s += 4) {
     const float4 k = K4[s];
-    mx = fmaxf(mx, fmaf(q[0], k.x, fmaf(q[1], k.y, fmaf(q[2], k.z, q[3] * k.w))));
+#pragma unroll
+    for (int i = 0; i < PX; ++i)
+      mx[i] = fmaxf(mx[i], fmaf(q[i][0], k.x, fmaf(q[i][1], k.y, fmaf(q[i][2], k.z, q[i][3] * k.w))));
   }
-  float den = 0.f, cx[CH] = {0.f, 0.f, 0.f, 0.f};
+  float den[PX], cx[PX][CH];
+#pragma unroll
+  for (int i = 0; i < PX; ++i) {
+    den[i] = 0.f;
+#pragma unroll
+    for (int o = 0; o < CH; ++o) cx[i][o] = 0.f;
+  }
 #pragma unroll 4
   for (int s = r; s < S; s += 4) {
     const float4 k = K4[s], v = V4[s];
-    const float e = __expf(fmaf(q[0], k.x, fmaf(q[1], k.y, fmaf(q[2], k.z, q[3] * k.w))) - mx);
-    den += e;
-    cx[0] = fmaf(e, v.x, cx[0]);
-    cx[1] = fmaf(e, v.y, cx[1]);
-    cx[2] = fmaf(e, v.z, cx[2]);
-    cx[3] = fmaf(e, v.w, cx[3]);
-  }
-  // combine the quad's partials at the quad max (fixed butterfly order)
-  float M = fmaxf(mx, __shfl_xor(mx, 1));
-  M = fmaxf(M, __shfl_xor(M, 2));
-  const float sc = mx == -INFINITY ? 0.f : __expf(mx - M);  // lane with no bins (S < 4)
-  den *= sc;
 #pragma unroll
-  for (int o = 0; o < CH; ++o) cx[o] *= sc;
-#pragma unroll
-  for (int m = 1; m <= 2; m <<= 1) {
-    den += __shfl_xor(den, m);
-#pragma unroll
-    for (int o = 0; o < CH; ++o) cx[o] += __shfl_xor(cx[o], m);
-  }
-  if (!pv) return;
-  const float inv = 1.f / den;
-#pragma unroll
-  for (int o = 0; o < CH; ++o) cx[o] *= inv;
-  if (q_out && r == 0) {  // training: saved for the backward
-    const int64_t mq = ((int64_t)b * h * w + pix) * CH;
-    *reinterpret_cast<float4*>(q_out + mq) = make_float4(q[0], q[1], q[2], q[3]);
-    *reinterpret_cast<float4*>(ctx_out + mq) = make_float4(cx[0], cx[1], cx[2], cx[3]);
-  }
-  const int64_t opix = ((int64_t)b * h * w + pix) * C;
-  for (int c = 4 * r; c < C; c += 16) {
-    const float4 x = *reinterpret_cast<const float4*>(xp + c);
-    const float4 lt = lateral ? *reinterpret_cast<const float4*>(lateral + opix + c)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);  // standalone NLM
-    float v[4] = {x.x, x.y, x.z, x.w};
-    float lv[4] = {lt.x, lt.y, lt.z, lt.w};
-    float rr[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float a = sbW[c + e];
-#pragma unroll
-      for (int o = 0; o < CH; ++o) a = fmaf(sWW[(c + e) * CH + o], cx[o], a);
-      rr[e] = lv[e] + (a + v[e]);
+    for (int i = 0; i < PX; ++i) {
+      const float e = __expf(
+          fmaf(q[i][0], k.x, fmaf(q[i][1], k.y, fmaf(q[i][2], k.z, q[i][3] * k.w))) - mx[i]);
+      den[i] += e;
+      cx[i][0] = fmaf(e, v.x, cx[i][0]);
+      cx[i][1] = fmaf(e, v.y, cx[i][1]);
+      cx[i][2] = fmaf(e, v.z, cx[i][2]);
+      cx[i][3] = fmaf(e, v.w, cx[i][3]);
     }
-    *reinterpret_cast<float4*>(out + opix + c) = make_float4(rr[0], rr[1], rr[2], rr[3]);
+  }
+#pragma unroll
+  for (int i = 0; i < PX; ++i) {
+    // combine the quad's partials at the quad max (fixed butterfly order)
+    float M = fmaxf(mx[i], __shfl_xor(mx[i], 1));
+    M = fmaxf(M, __shfl_xor(M, 2));
+    const float sc = mx[i] == -INFINITY ? 0.f : __expf(mx[i] - M);  // lane with no bins (S < 4)
+    den[i] *= sc;
+#pragma unroll
+    for (int o = 0; o < CH; ++o) cx[i][o] *= sc;
+#pragma unroll
+    for (int m = 1; m <= 2; m <<= 1) {
+      den[i] += __shfl_xor(den[i], m);
+#pragma unroll
+      for (int o = 0; o < CH; ++o) cx[i][o] += __shfl_xor(cx[i][o], m);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PX; ++i) {
+    if (!pv[i]) continue;
+    const float inv = 1.f / den[i];
+    float c4[CH];
+#pragma unroll
+    for (int o = 0; o < CH; ++o) c4[o] = cx[i][o] * inv;
+    if (q_out && r == 0) {  // training: saved for the backward
+      const int64_t mq = ((int64_t)b * h * w + pix[i]) * CH;
+      *reinterpret_cast<float4*>(q_out + mq) = make_float4(q[i][0], q[i][1], q[i][2], q[i][3]);
+      *reinterpret_cast<float4*>(ctx_out + mq) = make_float4(c4[0], c4[1], c4[2], c4[3]);
+    }
+    const int64_t opix = ((int64_t)b * h * w + pix[i]) * C;
+    for (int c = 4 * r; c < C; c += 16) {
+      const float4 x = *reinterpret_cast<const float4*>(xp[i] + c);
+      const float4 lt = lateral ? *reinterpret_cast<const float4*>(lateral + opix + c)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);  // standalone NLM
+      float v[4] = {x.x, x.y, x.z, x.w};
+      float lv[4] = {lt.x, lt.y, lt.z, lt.w};
+      float rr[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float a = sbW[c + e];
+#pragma unroll
+        for (int o = 0; o < CH; ++o) a = fmaf(sWW[(c + e) * CH + o], c4[o], a);
+        rr[e] = lv[e] + (a + v[e]);
+      }
+      *reinterpret_cast<float4*>(out + opix + c) = make_float4(rr[0], rr[1], rr[2], rr[3]);
+    }
   }
 }
 
@@ -439,19 +472,33 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* __restrict__ x,
   float o[kHeadOut];
 #pragma unroll
   for (int n = 0; n < kHeadOut; ++n) o[n] = bias[n];
+  // the pixel's channels in chunks of kHeadChunk float4, all loads of a chunk
+  // issued before its FMAs: one HBM round trip per 32 channels instead of one
+  // per 4 (a 40-channel pixel was 10 dependent load -> FMA steps)
+  constexpr int kHeadChunk = 8;
 #pragma unroll 1
-  for (int c = 0; c < C; c += 4) {
-    const float4 v = *reinterpret_cast<const float4*>(xp + c);
+  for (int c0 = 0; c0 < C; c0 += 4 * kHeadChunk) {
+    float4 xv[kHeadChunk];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      asm volatile("" ::: "memory");
+    for (int q = 0; q < kHeadChunk; ++q)
+      xv[q] = c0 + 4 * q < C ? *reinterpret_cast<const float4*>(xp + c0 + 4 * q)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int n = 16 * h; n < 16 * h + 16; ++n) {
-        const float4 wr = *reinterpret_cast<const float4*>(wt + n * C + c);
-        o[n] = fmaf(wr.x, v.x, o[n]);
-        o[n] = fmaf(wr.y, v.y, o[n]);
-        o[n] = fmaf(wr.z, v.z, o[n]);
-        o[n] = fmaf(wr.w, v.w, o[n]);
+    for (int q = 0; q < kHeadChunk; ++q) {
+      const int c = c0 + 4 * q;
+      if (c >= C) break;  // wave-uniform
+      const float4 v = xv[q];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int n = 16 * h; n < 16 * h + 16; ++n) {
+          const float4 wr = *reinterpret_cast<const float4*>(wt + n * C + c);
+          o[n] = fmaf(wr.x, v.x, o[n]);
+          o[n] = fmaf(wr.y, v.y, o[n]);
+          o[n] = fmaf(wr.z, v.z, o[n]);
+          o[n] = fmaf(wr.w, v.w, o[n]);
+        }
       }
     }
   }
@@ -591,10 +638,23 @@ extern "C" int jabd_nlm_apply_f32(const float* src, int64_t src_bs, int32_t src_
   JABD_REQUIRE(C > 0 && C % 4 == 0 && src_ps % 4 == 0 && S > 0, "nlm_apply: bad sizes");
   const size_t smem = (2 * (size_t)S * ch + 2 * (size_t)ch * C + C) * sizeof(float);
   JABD_REQUIRE(smem <= 64 * 1024, "nlm_apply: LDS %zu > 64KiB", smem);
-  dim3 g((unsigned)cdiv((int64_t)h * w, 64), (unsigned)B);  // a quad of lanes per pixel
-  nlm_apply_kernel<4><<<g, 256, smem, as_stream(stream)>>>(src, src_bs, src_ps, hs, ws, C, h, w,
-                                                           wq, bq, kpool, vpool, S, wW, bW,
-                                                           lateral, out, q_out, ctx_out);
+  // JABD_NLM_PX=1: one pixel per quad (A/B)
+  static int px = -1;
+  if (px < 0) {
+    const char* e = getenv("JABD_NLM_PX");
+    px = e && e[0] == '1' ? 1 : 2;
+  }
+  if (px == 2) {
+    dim3 g((unsigned)cdiv((int64_t)h * w, 128), (unsigned)B);  // a quad of lanes per 2 pixels
+    nlm_apply_kernel<4, 2><<<g, 256, smem, as_stream(stream)>>>(src, src_bs, src_ps, hs, ws, C, h,
+                                                                w, wq, bq, kpool, vpool, S, wW, bW,
+                                                                lateral, out, q_out, ctx_out);
+  } else {
+    dim3 g((unsigned)cdiv((int64_t)h * w, 64), (unsigned)B);  // a quad of lanes per pixel
+    nlm_apply_kernel<4, 1><<<g, 256, smem, as_stream(stream)>>>(src, src_bs, src_ps, hs, ws, C, h,
+                                                                w, wq, bq, kpool, vpool, S, wW, bW,
+                                                                lateral, out, q_out, ctx_out);
+  }
   return check_launch("nlm_apply");
 }
 
