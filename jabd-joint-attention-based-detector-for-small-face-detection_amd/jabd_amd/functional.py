@@ -304,11 +304,17 @@ def expand_dw(x, pk, w, bias, k, stride, act="none", partials=True, skip=None):
     return (y, part, t) if skip is not None else (y, part)
 
 
+# pixels per channel-sum block: 64 gives the 64x64 / 32x32 maps 64 / 16 blocks
+# per image instead of 16 / 4 (the 32x32 sums ran as 128 workgroups);
+# JABD_CSUM_PX=256 restores the old split (A/B)
+_CSUM_PX = int(__import__("os").environ.get("JABD_CSUM_PX", "64"))
+
+
 def channel_sums(x, nblk=None):
     B, H, W, C = x.shape
     HW = H * W
     if nblk is None:
-        nblk = max(1, min(64, HW // 256))
+        nblk = max(1, min(64, HW // _CSUM_PX))
     part = torch.empty((B, nblk, C), dtype=torch.float32, device=x.device)
     call("jabd_channel_sum_f32", x.data_ptr(), x.stride(0), C, B, HW, C, nblk, part.data_ptr(),
          _stream())
