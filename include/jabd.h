@@ -487,6 +487,18 @@ int jabd_bn_act_bwd_ex_f32(const float* dy, int32_t lddy, int32_t dyc0, const fl
                            const float* beta, int32_t act, float slope, const float* dys,
                            const float* dya, int64_t hw, float* part, float* dgamma,
                            float* dbeta, float* dx, float* dres, jabd_stream_t stream);
+/* n <= 4 ECA pools + gates in two launches (the head's per-level gates,
+ * nets/retinaface_r.py:208-224): host arrays of n entries; tensor i is NHWC
+ * with B images at x[i] (+ b * x_bs[i], pixel stride x_ps[i]), HW[i] pixels,
+ * C[i] % 4 == 0 channels; part[i] is scratch of B * nblk[i] * C[i] floats;
+ * w1d[i] the Conv1d weight (k[i] <= 9 taps); scale[i] [B][C[i]] receives the
+ * gate (SIGMOID / HSIGMOID).  Same result as jabd_channel_sum_f32 +
+ * jabd_eca_gate_f32 per tensor. */
+int jabd_eca_pool_gate_multi_f32(int32_t n, int64_t B, const float* const* x, const int64_t* x_bs,
+                                 const int32_t* x_ps, const int64_t* HW, const int32_t* C,
+                                 const int64_t* nblk, float* const* part, const float* const* w1d,
+                                 const int32_t* k, int32_t gate, float* const* scale,
+                                 jabd_stream_t stream);
 /* Conv weight gradient (fp32 MFMA): x/geometry as the forward jabd_conv_args
  * with `y` pointing at dY; dw in torch layout [Cout][Cin][KH][KW]; part is
  * scratch of jabd_conv_wgrad_part_floats() floats.  The data gradient is

@@ -16,14 +16,14 @@ namespace jabd {
 constexpr int kSumThreads = 256;
 
 // part[b][blk][c] = sum over this block's pixels of x[b, pix, c]
-__global__ __launch_bounds__(kSumThreads) void channel_sum_kernel(
-    const float* __restrict__ x, int64_t x_bs, int x_ps, int64_t HW, int C, int64_t per_blk,
-    int64_t nblk, float* __restrict__ part) {
+__device__ __forceinline__ void channel_sum_body(const float* __restrict__ x, int64_t x_bs,
+                                                 int x_ps, int64_t HW, int C, int64_t per_blk,
+                                                 int64_t nblk, float* __restrict__ part,
+                                                 float* red) {
   const int b = blockIdx.y;
   const int64_t p0 = blockIdx.x * per_blk;
   const int64_t p1 = min(p0 + per_blk, HW);
   const float* xb = x + (int64_t)b * x_bs;
-  extern __shared__ float red[];  // [rows][C]
   const int rows = kSumThreads / C > 0 ? kSumThreads / C : 1;
   for (int c0 = 0; c0 < C; c0 += kSumThreads) {
     const int c = c0 + (threadIdx.x % min(C, kSumThreads));
@@ -50,6 +50,29 @@ __global__ __launch_bounds__(kSumThreads) void channel_sum_kernel(
     }
     __syncthreads();
   }
+}
+
+__global__ __launch_bounds__(kSumThreads) void channel_sum_kernel(
+    const float* __restrict__ x, int64_t x_bs, int x_ps, int64_t HW, int C, int64_t per_blk,
+    int64_t nblk, float* __restrict__ part) {
+  __shared__ float red[kSumThreads];  // [rows][min(C, kSumThreads)]
+  channel_sum_body(x, x_bs, x_ps, HW, C, per_blk, nblk, part, red);
+}
+
+// Several independent channel sums in one launch (blockIdx.z picks the
+// tensor): the head's ECA pools of the three pyramid levels.
+struct CsumMulti {
+  const float* x[4];
+  int64_t x_bs[4], HW[4], per[4], nblk[4];
+  int x_ps[4], C[4];
+  float* part[4];
+};
+__global__ __launch_bounds__(kSumThreads) void channel_sum_multi_kernel(const CsumMulti d) {
+  __shared__ float red[kSumThreads];
+  const int z = blockIdx.z;
+  if (blockIdx.x >= d.nblk[z]) return;  // whole workgroup
+  channel_sum_body(d.x[z], d.x_bs[z], d.x_ps[z], d.HW[z], d.C[z], d.per[z], d.nblk[z], d.part[z],
+                   red);
 }
 
 // scale[b][c] = gate( sum_t w[t] * mean[b][c + t - (k-1)/2] )   (zero padded)
@@ -101,13 +124,11 @@ __global__ __launch_bounds__(256) void eca_gate_kernel(const float* __restrict__
 // The one-thread-per-channel form walks all nblk rows serially (up to 1024
 // dependent L2 round trips for the 512^2 gates).
 constexpr int kGateOC = 248;
-__global__ __launch_bounds__(256) void eca_gate4_kernel(const float* __restrict__ part,
-                                                        int nblk, int C, float inv_hw,
-                                                        const float* __restrict__ w1d, int k,
-                                                        int gate, float* __restrict__ scale,
-                                                        float* __restrict__ mean_out) {
-  __shared__ float4 red[256];
-  __shared__ float mean[kGateOC + 8];
+__device__ __forceinline__ void eca_gate4_body(const float* __restrict__ part, int nblk, int C,
+                                               float inv_hw, const float* __restrict__ w1d,
+                                               int k, int gate, float* __restrict__ scale,
+                                               float* __restrict__ mean_out, float4* red,
+                                               float* mean) {
   const int b = blockIdx.y, t = threadIdx.x;
   const int cs = blockIdx.x * kGateOC;
   const int ce = min(C, cs + kGateOC);
@@ -164,6 +185,34 @@ __global__ __launch_bounds__(256) void eca_gate4_kernel(const float* __restrict_
     scale[(int64_t)b * C + co] = g;
     if (mean_out) mean_out[(int64_t)b * C + co] = mean[t + 4];
   }
+}
+
+__global__ __launch_bounds__(256) void eca_gate4_kernel(const float* __restrict__ part,
+                                                        int nblk, int C, float inv_hw,
+                                                        const float* __restrict__ w1d, int k,
+                                                        int gate, float* __restrict__ scale,
+                                                        float* __restrict__ mean_out) {
+  __shared__ float4 red[256];
+  __shared__ float mean[kGateOC + 8];
+  eca_gate4_body(part, nblk, C, inv_hw, w1d, k, gate, scale, mean_out, red, mean);
+}
+
+// Several gates in one launch (blockIdx.z picks the tensor).
+struct GateMulti {
+  const float* part[4];
+  const float* w1d[4];
+  float* scale[4];
+  int nblk[4], C[4], k[4];
+  float inv_hw[4];
+  int gate;
+};
+__global__ __launch_bounds__(256) void eca_gate4_multi_kernel(const GateMulti d) {
+  __shared__ float4 red[256];
+  __shared__ float mean[kGateOC + 8];
+  const int z = blockIdx.z;
+  if ((int)blockIdx.x * kGateOC >= d.C[z]) return;  // whole workgroup
+  eca_gate4_body(d.part[z], d.nblk[z], d.C[z], d.inv_hw[z], d.w1d[z], d.k[z], d.gate,
+                 d.scale[z], nullptr, red, mean);
 }
 
 // First level of the ECA pool for many partial rows: block (s, b) sums rows
@@ -555,9 +604,62 @@ extern "C" int jabd_channel_sum_f32(const float* x, int64_t x_bs, int32_t x_ps, 
   const int cw = (int)(C < kSumThreads ? C : kSumThreads);
   const int rows = C >= kSumThreads ? 1 : kSumThreads / (int)C;
   dim3 g((unsigned)nblk, (unsigned)B);
-  channel_sum_kernel<<<g, kSumThreads, rows * cw * sizeof(float), as_stream(stream)>>>(
-      x, x_bs, x_ps, HW, (int)C, per, nblk, part);
+  (void)rows;
+  (void)cw;
+  channel_sum_kernel<<<g, kSumThreads, 0, as_stream(stream)>>>(x, x_bs, x_ps, HW, (int)C, per,
+                                                               nblk, part);
   return check_launch("channel_sum");
+}
+
+// Up to 4 channel sums and their ECA gates in two launches (the head's
+// per-level pools: nets/retinaface_r.py:219-224 applied to the three FPN
+// inputs, or to the three SSH inputs).  Arrays of n entries; every tensor
+// has B images, C % 4 == 0, k <= 9; part[i] holds B x nblk[i] x C[i] floats.
+extern "C" int jabd_eca_pool_gate_multi_f32(int32_t n, int64_t B, const float* const* x,
+                                            const int64_t* x_bs, const int32_t* x_ps,
+                                            const int64_t* HW, const int32_t* C,
+                                            const int64_t* nblk, float* const* part,
+                                            const float* const* w1d, const int32_t* k,
+                                            int32_t gate, float* const* scale,
+                                            jabd_stream_t stream) {
+  JABD_REQUIRE(n >= 1 && n <= 4 && B > 0 && B <= 65535 && x && x_bs && x_ps && HW && C && nblk &&
+                   part && w1d && k && scale,
+               "eca_pool_gate_multi: bad args");
+  JABD_REQUIRE(gate == ACT_SIGMOID || gate == ACT_HSIGMOID, "eca_pool_gate_multi: gate");
+  CsumMulti cs{};
+  GateMulti gm{};
+  int64_t maxblk = 1, maxc = 1;
+  for (int i = 0; i < n; ++i) {
+    JABD_REQUIRE(x[i] && part[i] && w1d[i] && scale[i] && C[i] > 0 && C[i] % 4 == 0 &&
+                     HW[i] > 0 && nblk[i] > 0 && k[i] > 0 && k[i] <= 9 && (k[i] & 1) &&
+                     nblk[i] * C[i] < ((int64_t)1 << 31),
+                 "eca_pool_gate_multi: bad entry %d", i);
+    cs.x[i] = x[i];
+    cs.x_bs[i] = x_bs[i];
+    cs.x_ps[i] = x_ps[i];
+    cs.HW[i] = HW[i];
+    cs.C[i] = C[i];
+    cs.nblk[i] = nblk[i];
+    cs.per[i] = cdiv(HW[i], nblk[i]);
+    cs.part[i] = part[i];
+    gm.part[i] = part[i];
+    gm.w1d[i] = w1d[i];
+    gm.scale[i] = scale[i];
+    gm.nblk[i] = (int)nblk[i];
+    gm.C[i] = C[i];
+    gm.k[i] = k[i];
+    gm.inv_hw[i] = 1.f / (float)HW[i];
+    maxblk = std::max<int64_t>(maxblk, nblk[i]);
+    maxc = std::max<int64_t>(maxc, C[i]);
+  }
+  gm.gate = gate;
+  hipStream_t st = as_stream(stream);
+  channel_sum_multi_kernel<<<dim3((unsigned)maxblk, (unsigned)B, (unsigned)n), kSumThreads, 0,
+                             st>>>(cs);
+  if (int e = check_launch("channel_sum_multi")) return e;
+  eca_gate4_multi_kernel<<<dim3((unsigned)cdiv(maxc, kGateOC), (unsigned)B, (unsigned)n), 256, 0,
+                           st>>>(gm);
+  return check_launch("eca_gate_multi");
 }
 
 extern "C" int jabd_partial_reduce_f32(const float* part, int64_t nblk, int64_t B, int64_t C,

@@ -168,6 +168,8 @@ SIGNATURES = {
                             c_vp, c_vp, c_vp, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "jabd_conv_wgrad_part_floats": [ctypes.POINTER(ConvArgs)],
     "jabd_conv_wgrad_f32": [ctypes.POINTER(ConvArgs), c_vp, c_vp, c_vp],
+    "jabd_eca_pool_gate_multi_f32": [c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                     c_vp, c_i32, c_vp, c_vp],
     "jabd_bn_sum_nblk": [c_i64, c_i32],
     "jabd_bn_act_fwd_sum_f32": [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_f32, c_vp,
                                 c_i64, c_vp, c_vp],

@@ -41,6 +41,9 @@ FUSE_SKIP = os.environ.get("JABD_FUSE_SKIP", "1") != "0"
 # launches cost more clock than the filled CUs gain once the data is real.
 EVAL_STREAMS = int(os.environ.get("JABD_EVAL_STREAMS", "1"))
 EVAL_SPLIT_MIN = int(os.environ.get("JABD_EVAL_SPLIT_MIN", "8"))
+# The head's three per-level ECA gates as one pool + gate launch pair
+# (F.eca_gates_multi); JABD_GATES_MULTI=0 launches them level by level (A/B).
+GATES_MULTI = os.environ.get("JABD_GATES_MULTI", "1") != "0"
 
 
 def _w1d(eca):
@@ -208,9 +211,18 @@ class _Head:
             return M.beca_gate(f, w1d)
         return F.eca_gate(F.channel_sums(f), f.shape[1] * f.shape[2], w1d, "sigmoid")
 
+    def _gates(self, fs, w1ds):
+        """The gates of the three levels; mean-pool ECA as one multi-tensor
+        pool + gate pair of launches (F.eca_gates_multi)."""
+        if GATES_MULTI and self.gate == "sigmoid" and all(f.stride(3) == 1 for f in fs):
+            sc = F.eca_gates_multi(list(fs), list(w1ds), "sigmoid")
+            if sc is not None:
+                return sc
+        return [self._gate(f, w1d) for f, w1d in zip(fs, w1ds)]
+
     def forward(self, feats, softmax, out=None):
         B = feats[0].shape[0]
-        scales = [self._gate(f, w1d) for f, w1d in zip(feats, self.eca_in)]
+        scales = self._gates(feats, self.eca_in)
         levels = self.fpn.forward(feats, scales)
         A = sum(2 * o.shape[1] * o.shape[2] for o in levels)
         dev = levels[0].device
@@ -223,10 +235,10 @@ class _Head:
             conf = torch.empty((B, A, 2), dtype=torch.float32, device=dev)
             landm = torch.empty((B, A, 10), dtype=torch.float32, device=dev)
         a_off = 0
+        scs = self._gates(levels, [self.eca_fpn] * len(levels))
         for i, o in enumerate(levels):
             _, h, w, C = o.shape
-            sc = self._gate(o, self.eca_fpn)
-            feat = self.ssh[i].forward(o, sc)
+            feat = self.ssh[i].forward(o, scs[i])
             wt, bs = self.heads[i]
             F.heads(feat, wt, bs, loc, conf, landm, a_off, softmax)
             a_off += 2 * h * w

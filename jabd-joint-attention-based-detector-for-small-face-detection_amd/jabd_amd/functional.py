@@ -321,6 +321,31 @@ def channel_sums(x, nblk=None):
     return part
 
 
+def eca_gates_multi(xs, w1ds, gate):
+    """ECA gates ([B, C] each) of up to 4 NHWC tensors in two launches
+    (jabd_eca_pool_gate_multi_f32); the same as eca_gate(channel_sums(x), ...)
+    per tensor.  None when a tensor does not qualify (k > 9, C % 4)."""
+    n = len(xs)
+    if n == 0 or n > 4 or any(w.numel() > 9 or x.shape[3] % 4 for x, w in zip(xs, w1ds)):
+        return None
+    B = xs[0].shape[0]
+    dev = xs[0].device
+    A64, A32, AP = ctypes.c_int64 * n, ctypes.c_int32 * n, ctypes.c_void_p * n
+    nblk = [max(1, min(64, (x.shape[1] * x.shape[2]) // _CSUM_PX)) for x in xs]
+    parts = [torch.empty((B, nb, x.shape[3]), dtype=torch.float32, device=dev)
+             for x, nb in zip(xs, nblk)]
+    scales = [torch.empty((B, x.shape[3]), dtype=torch.float32, device=dev) for x in xs]
+    arrs = (AP(*[x.data_ptr() for x in xs]), A64(*[x.stride(0) for x in xs]),
+            A32(*[x.stride(2) for x in xs]), A64(*[x.shape[1] * x.shape[2] for x in xs]),
+            A32(*[x.shape[3] for x in xs]), A64(*nblk), AP(*[p.data_ptr() for p in parts]),
+            AP(*[w.data_ptr() for w in w1ds]), A32(*[w.numel() for w in w1ds]),
+            AP(*[s.data_ptr() for s in scales]))
+    a = [ctypes.addressof(t) for t in arrs]
+    call("jabd_eca_pool_gate_multi_f32", n, B, a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7],
+         a[8], ACT[gate], a[9], _stream())
+    return scales
+
+
 def eca_gate(part, hw, w1d, gate, return_mean=False):
     B, nblk, C = part.shape
     # many tile partials: reduce them over many workgroups first, unless the

@@ -186,3 +186,23 @@ def test_conv1x1_stream_parity(cuda, cin, cin2, cout, gate, res, hw, act):
                x2=nhwc(x2) if cin2 else None, res=nhwc(r) if res else None)
     got = y.permute(0, 3, 1, 2).cpu()
     assert rel_err(got, want) < 2e-5, rel_err(got, want)
+
+
+@pytest.mark.gpu
+def test_eca_gates_multi_equal_per_tensor(cuda):
+    """The head's three ECA gates in one pool + gate launch pair
+    (jabd_eca_pool_gate_multi_f32) equal the per-tensor pool + gate, bit for
+    bit, on the pyramid shapes (40/80/160 channels, 32/16/8 maps) and on a
+    channel-offset view (pixel stride > C)."""
+    from jabd_amd import functional as F
+    g = torch.Generator().manual_seed(5)
+    xs = [torch.randn(3, s, s, c, generator=g).to(cuda) for s, c in ((32, 40), (16, 80), (8, 160))]
+    wide = torch.randn(3, 12, 12, 48, generator=g).to(cuda)
+    xs.append(wide[..., 8:48])  # 40 channels at pixel stride 48
+    ws = [torch.randn(k, generator=g).to(cuda) for k in (3, 3, 5, 3)]
+    got = F.eca_gates_multi(xs, ws, "sigmoid")
+    assert got is not None
+    for x, w, s in zip(xs, ws, got):
+        xc = x.contiguous()
+        ref = F.eca_gate(F.channel_sums(xc), xc.shape[1] * xc.shape[2], w, "sigmoid")
+        assert torch.equal(s, ref)
