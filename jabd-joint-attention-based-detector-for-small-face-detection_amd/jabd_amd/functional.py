@@ -13,6 +13,19 @@ from ._lib import ConvArgs, DwArgs, ExpDwArgs, call, lib
 
 ACT = {"none": 0, "relu": 1, "leaky": 2, "hswish": 3, "hsigmoid": 4, "sigmoid": 5}
 
+# Test hook (tests/_kinks.py), None in use: when set, the training forward
+# hands it the operands from which each backward kernel derives the region
+# of a piecewise activation (ReLU / LeakyReLU / Hardswish / Hardsigmoid) or a
+# max-pool argmax, so the float64 oracle can be run with this path's own
+# masks.  tap(kind, *operands); kinds: "bn", "eca", "beca", "act", "ssh",
+# "maxpool".
+KINK_TAP = None
+
+
+def tap(kind, *operands):
+    if KINK_TAP is not None:
+        KINK_TAP(kind, *operands)
+
 
 def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)

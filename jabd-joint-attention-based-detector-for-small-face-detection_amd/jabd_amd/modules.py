@@ -96,6 +96,8 @@ class ActFn(torch.autograd.Function):
         x = _dense(x)
         y = torch.empty_like(x)
         call("jabd_act_f32", x.data_ptr(), x.numel(), ACT[act], float(slope), y.data_ptr(), _st())
+        if act in ("relu", "leaky", "hswish", "hsigmoid"):
+            F.tap("act", act, slope, x)
         ctx.save_for_backward(x)
         ctx.cfg = (act, slope)
         return y

@@ -394,6 +394,8 @@ class BecaFn(torch.autograd.Function):
         part = beca_part(B, H * W, C, x.device)
         call("jabd_beca_fwd_f32", _p(x), B, H * W, C, _p(w), w.numel(), _p(y), _p(stats),
              _p(part), part.numel(), _stream())
+        from .functional import tap
+        tap("beca", stats[2].view(B, C))
         ctx.save_for_backward(x, w, stats)
         return y
 

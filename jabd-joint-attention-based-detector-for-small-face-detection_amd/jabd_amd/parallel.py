@@ -16,7 +16,9 @@ replica and:
     sized for xGMI ring all-reduce.  Buckets are launched from gradient hooks
     while backward is still running (overlap), in one fixed order on every
     rank; parameters that never get a gradient (the reference's built-but-
-    unused SeModule weights) are found on the first step and left out;
+    unused SeModule weights) are found on the first step and left out, and
+    the buckets are planned again whenever the set of parameters with
+    gradients changes (freezing / unfreezing the backbone);
   * broadcast_buffers copies rank 0's BN running buffers to every rank.
 
 Collectives run on torch.distributed ("nccl" = RCCL on ROCm, or "gloo").
@@ -34,12 +36,21 @@ def _world(group):
 class GradAllReduce:
     """SUM all-reduce of every gradient after backward.
 
-    overlap=True: after a first synchronous step (which finds the parameters
-    that receive gradients), buckets are filled by post-accumulate-grad hooks
-    and their all-reduces launched asynchronously during backward — bucket i
-    only after buckets 0..i-1, so every rank issues the same collective
-    sequence.  Call the object after loss.backward() to wait for the
-    collectives and write the sums back into .grad."""
+    overlap=True: buckets are filled by post-accumulate-grad hooks and their
+    all-reduces launched asynchronously during backward — bucket i only after
+    buckets 0..i-1, so every rank issues the same collective sequence.  Call
+    the object after loss.backward() to wait for the collectives and write
+    the sums back into .grad.
+
+    The plan (which parameters, in which buckets) is made from the
+    parameters that actually received a gradient in a synchronous step, and
+    is made again whenever that set changes: when the requires_grad flags
+    change (the reference's Freeze_Train schedule, train_mobilenetV3_ecagai.py:
+    576-610, freezes the backbone and later unfreezes it on the same model),
+    when a parameter outside the plan gets a gradient, or when a planned
+    bucket stays incomplete.  Such a step waits for (and discards) the
+    collectives already launched and all-reduces synchronously instead; every
+    rank runs the same graph, so every rank takes the same branch."""
 
     def __init__(self, model, group=None, bucket_bytes=BUCKET_BYTES, overlap=True):
         self.model = model
@@ -47,6 +58,7 @@ class GradAllReduce:
         self.bucket_bytes = bucket_bytes
         self.overlap = overlap
         self.buckets = None      # [[param, ...], ...] in launch order
+        self.plan_key = None     # requires_grad flags the plan was made under
         self.hooks = []
         self._reset()
 
@@ -71,21 +83,33 @@ class GradAllReduce:
         self.flat = {}
         self.works = {}
         self.next_launch = 0
+        self.unplanned = False
+
+    def _key(self):
+        return tuple(p.requires_grad for p in self.model.parameters())
 
     def _install(self, params):
+        """Hooks on every parameter that can receive a gradient: the planned
+        ones fill buckets, any other one marks the step as unplanned."""
+        self.remove()
         self.buckets = self._plan(params)
+        self.plan_key = self._key()
         self.where = {}
         for bi, b in enumerate(self.buckets):
             for p in b:
                 self.where[p] = bi
-        for p in params:
-            self.hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        for p in self.model.parameters():
+            if p.requires_grad:
+                self.hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
 
     def _on_grad(self, p):
-        bi = self.where[p]
+        bi = self.where.get(p)
+        if bi is None:
+            self.unplanned = True
+            return
         left = self.pending.get(bi, len(self.buckets[bi])) - 1
         self.pending[bi] = left
-        if left == 0:
+        if left == 0 and not self.unplanned:
             b = self.buckets[bi]
             self.flat[bi] = torch.cat([q.grad.reshape(-1) for q in b])
             while self.next_launch in self.flat and self.next_launch not in self.works:
@@ -93,6 +117,9 @@ class GradAllReduce:
                 self.works[i] = dist.all_reduce(self.flat[i], op=dist.ReduceOp.SUM,
                                                 group=self.group, async_op=True)
                 self.next_launch += 1
+
+    def _with_grad(self):
+        return [p for p in self.model.parameters() if p.requires_grad and p.grad is not None]
 
     def _sync_all(self, params):
         for b in self._plan(params):
@@ -113,27 +140,25 @@ class GradAllReduce:
         if not _world(self.group):
             self._reset()
             return
-        if self.buckets is None:
-            # first step: the parameters with a gradient define the buckets
-            # (identical on every rank: same model, same graph)
-            params = [p for p in self.model.parameters() if p.grad is not None]
-            self._sync_all(params)
-            if self.overlap:
-                self._install(params)
-            else:
-                self.buckets = []
-                self.static = params
+        if not self.overlap:
+            self._sync_all(self._with_grad())
+            return
+        ok = (self.buckets is not None and not self.unplanned and self.plan_key == self._key()
+              and len(self.works) == len(self.buckets))
+        if ok:
+            for i, b in enumerate(self.buckets):
+                self.works[i].wait()
+                self._scatter(b, self.flat[i])
             self._reset()
             return
-        if not self.overlap:
-            self._sync_all(self.static)
-            return
-        if len(self.works) != len(self.buckets):
-            raise RuntimeError("GradAllReduce: not every bucket received its gradients this "
-                               "step (the set of parameters with gradients changed)")
-        for i, b in enumerate(self.buckets):
-            self.works[i].wait()
-            self._scatter(b, self.flat[i])
+        # first step, or the set of parameters with gradients changed: drain
+        # what was launched (those sums went to flat copies, .grad is intact),
+        # all-reduce this step synchronously and plan again from it
+        for w in self.works.values():
+            w.wait()
+        params = self._with_grad()
+        self._sync_all(params)
+        self._install(params)
         self._reset()
 
     def remove(self):

@@ -23,6 +23,7 @@ Torch is used only for allocation, views and a few tiny reductions of
 kernel partials.  There is no CPU path.
 """
 import ctypes
+import threading
 import weakref
 
 import torch
@@ -223,6 +224,8 @@ class EcaConvFn(torch.autograd.Function):
         B, H, W, C = x.shape
         w1 = w1d.detach().reshape(-1).float().contiguous()
         scale, mean = F.eca_gate(F.channel_sums(x), H * W, w1, gate, return_mean=True)
+        if gate == "hsigmoid":
+            F.tap("eca", gate, mean, w1)
         pk = _packed(weight, transposed=False)
         OH = (H + 2 * pad - pk.KH) // stride + 1
         OW = (W + 2 * pad - pk.KW) // stride + 1
@@ -275,6 +278,8 @@ class BnActFn(torch.autograd.Function):
         call("jabd_bn_act_fwd_f32", x.data_ptr(), C, M, C, mean.data_ptr(), invstd.data_ptr(),
              g.data_ptr(), b.data_ptr(), _p(res), C, ACT[act], float(slope), y.data_ptr(), C, 0,
              _st())
+        if act != "none":
+            F.tap("bn", act, slope, x, mean, invstd, g, b, res)
         ctx.save_for_backward(x, g, b, res if res is not None else None, mean, invstd)
         ctx.cfg = (act, slope, res is not None)
         return y
@@ -511,6 +516,7 @@ class SshTailFn(torch.autograd.Function):
             saved += [x, gg, bb_, mean, invstd]
             outs.append(c0)
             c0 += C
+        F.tap("ssh", [saved[5 * i:5 * i + 5] for i in range(3)])
         ctx.save_for_backward(*saved)
         ctx.offs = outs
         return y
@@ -607,6 +613,7 @@ class MaxPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
         y = F.maxpool(x, 3, 2, 1)
+        F.tap("maxpool", x)
         ctx.save_for_backward(x)
         return y
 
@@ -648,26 +655,35 @@ def bn_act(x, bn, act="none", slope=0.0, res=None):
 
 
 # num_batches_tracked increments of one train_forward, applied as one
-# multi-tensor add at its end (75 one-element kernels otherwise)
-_NBT = []
+# multi-tensor add at its end (75 one-element kernels otherwise).  Per thread:
+# nn.DataParallel runs the replicas' forwards on concurrent threads.
+_NBT = threading.local()
+
+
+def _nbt_stack():
+    st = getattr(_NBT, "stack", None)
+    if st is None:
+        st = _NBT.stack = []
+    return st
 
 
 def _count_batch(bn):
     t = bn.num_batches_tracked
     if t is None:
         return
-    if _NBT:
-        _NBT[-1].append(t)
+    st = _nbt_stack()
+    if st:
+        st[-1].append(t)
     else:
         t.add_(1)
 
 
 class _BatchCounts:
     def __enter__(self):
-        _NBT.append([])
+        _nbt_stack().append([])
 
     def __exit__(self, *exc):
-        ts = _NBT.pop()
+        ts = _nbt_stack().pop()
         if ts and exc[0] is None:
             torch._foreach_add_(ts, 1)
 
@@ -717,6 +733,8 @@ def _bn_fwd(x, bn, act, slope=0.0, res=None, sums=False):
              g.data_ptr(), b.data_ptr(), _p(res), C, ACT[act], float(slope), y.data_ptr(), C, 0,
              _st())
     _count_batch(bn)
+    if act != "none":
+        F.tap("bn", act, slope, x, mean, invstd, g, b, res)
     if sums:
         return y, (g, b, mean, invstd), psum
     return y, (g, b, mean, invstd)
@@ -818,6 +836,7 @@ class MNv3BlockFn(torch.autograd.Function):
         if psum is None:
             psum = F.channel_sums(d)
         scale, mean = F.eca_gate(psum, OH * OW, w1, "hsigmoid", return_mean=True)
+        F.tap("eca", "hsigmoid", mean, w1)
         p = _conv_fwd(d, blk.conv3.weight, ascale=scale)
         sk = blk.skip
         saved_skip = ()

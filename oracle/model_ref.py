@@ -41,11 +41,72 @@ def eca_kernel_size(channel, b=1, gamma=2):
     return k if k % 2 else k + 1
 
 
+# ----------------------------------------------------------------------------- kinks
+# Every activation whose derivative jumps (ReLU, LeakyReLU, Hardswish,
+# Hardsigmoid) and the max-pool argmax go through kink() / maxpool().  By
+# default they are the plain torch ops.  With REPLAY set (tests/_kinks.py) a
+# call asks REPLAY.match(kind, z) for the HIP forward's own pre-activation of
+# the same tensor; the forward value stays this run's, and the backward takes
+# the derivative's region (which side of each kink) from the HIP tensor.  An
+# element within fp32 rounding of a kink then has the same mask in both runs,
+# so a gradient comparison measures the kernels, not the mask flips.
+REPLAY = None
+
+_ACT_FN = {
+    "relu": lambda z, s: F.relu(z),
+    "leaky": lambda z, s: F.leaky_relu(z, s),
+    "hswish": lambda z, s: F.hardswish(z),
+    "hsigmoid": lambda z, s: F.hardsigmoid(z),
+}
+
+
+class _KinkFn(torch.autograd.Function):
+    """act(z) whose backward uses the region of zr (PyTorch's *_backward
+    conventions: relu/leaky z > 0; hardswish z < -3 -> 0, z <= 3 -> z/3 + 1/2,
+    else 1; hardsigmoid 1/6 on (-3, 3))."""
+
+    @staticmethod
+    def forward(ctx, z, zr, kind, slope):
+        ctx.save_for_backward(z, zr)
+        ctx.cfg = (kind, slope)
+        return _ACT_FN[kind](z, slope)
+
+    @staticmethod
+    def backward(ctx, g):
+        z, zr = ctx.saved_tensors
+        kind, slope = ctx.cfg
+        one, zero = torch.ones_like(z), torch.zeros_like(z)
+        if kind in ("relu", "leaky"):
+            d = torch.where(zr > 0, one, zero + (slope if kind == "leaky" else 0.0))
+        elif kind == "hswish":
+            d = torch.where(zr < -3, zero, torch.where(zr <= 3, z / 3 + 0.5, one))
+        else:
+            d = torch.where((zr > -3) & (zr < 3), one / 6, zero)
+        return g * d, None, None, None
+
+
+def kink(z, kind, slope=0.0):
+    if REPLAY is not None:
+        zr = REPLAY.match(kind, z)
+        if zr is not None:
+            return _KinkFn.apply(z, zr.to(z.dtype), kind, slope)
+    return _ACT_FN[kind](z, slope)
+
+
+def maxpool(x, k=3, s=2, p=1):
+    """F.max_pool2d(x, 3, 2, 1); under REPLAY the argmax of each window is the
+    HIP input's (first maximum in scan order, as torch's and the kernel's)."""
+    if REPLAY is not None:
+        xr = REPLAY.match("maxpool", x)
+        if xr is not None:
+            _, idx = F.max_pool2d(xr.double(), k, s, p, return_indices=True)
+            return x.flatten(2).gather(2, idx.flatten(2)).view(idx.shape)
+    return F.max_pool2d(x, k, s, p)
+
+
 def _act(x, kind):
-    if kind == "relu":
-        return F.relu(x)
-    if kind == "hswish":
-        return F.hardswish(x)
+    if kind in ("relu", "hswish"):
+        return kink(x, kind)
     if kind is None:
         return x
     raise ValueError(kind)
@@ -74,7 +135,7 @@ def eca(ctx, x, name, gate):
     k = w.shape[-1]
     y = x.mean(dim=(2, 3))                                # AdaptiveAvgPool2d(1)
     y = F.conv1d(y.unsqueeze(1), w, padding=(k - 1) // 2).squeeze(1)
-    y = torch.sigmoid(y) if gate == "sigmoid" else F.hardsigmoid(y)
+    y = torch.sigmoid(y) if gate == "sigmoid" else kink(y, "hsigmoid")
     return x * y[:, :, None, None]
 
 
@@ -98,7 +159,7 @@ def block_eca(ctx, x, pre, spec):
 
 def mnv3_body(ctx, x):
     """MobileNetV3_Large_eca stem + layer1..3 -> (C3, C4, C5)."""
-    x = F.hardswish(ctx.bn(ctx.conv(x, "body.conv1", 2, 1), "body.bn1"))
+    x = kink(ctx.bn(ctx.conv(x, "body.conv1", 2, 1), "body.bn1"), "hswish")
     feats = []
     for li, layer in enumerate(MNV3_LAYERS):
         for bi, spec in enumerate(layer):
@@ -109,20 +170,20 @@ def mnv3_body(ctx, x):
 
 def r50_body(ctx, x):
     """torchvision resnet50 stem + layer1..4, returning layer2/3/4."""
-    x = F.relu(ctx.bn(ctx.conv(x, "body.conv1", 2, 3), "body.bn1"))
-    x = F.max_pool2d(x, 3, 2, 1)
+    x = kink(ctx.bn(ctx.conv(x, "body.conv1", 2, 3), "body.bn1"), "relu")
+    x = maxpool(x)
     feats = []
     for li, (w, n, s) in enumerate(R50_LAYERS):
         for bi in range(n):
             pre = f"body.layer{li + 1}.{bi}."
             st = s if bi == 0 else 1
-            out = F.relu(ctx.bn(ctx.conv(x, pre + "conv1"), pre + "bn1"))
-            out = F.relu(ctx.bn(ctx.conv(out, pre + "conv2", st, 1), pre + "bn2"))
+            out = kink(ctx.bn(ctx.conv(x, pre + "conv1"), pre + "bn1"), "relu")
+            out = kink(ctx.bn(ctx.conv(out, pre + "conv2", st, 1), pre + "bn2"), "relu")
             out = ctx.bn(ctx.conv(out, pre + "conv3"), pre + "bn3")
             idn = x
             if bi == 0:
                 idn = ctx.bn(ctx.conv(x, pre + "downsample.0", st), pre + "downsample.1")
-            x = F.relu(out + idn)
+            x = kink(out + idn, "relu")
         if li >= 1:
             feats.append(x)
     return feats
@@ -149,7 +210,7 @@ def nlm(ctx, x, pre, sizes=(1, 4, 8, 12)):
 
 def conv_bn_act(ctx, x, pre, leaky, padding=0, act=True):
     y = ctx.bn(ctx.conv(x, pre + ".0", 1, padding), pre + ".1")
-    return F.leaky_relu(y, leaky) if act else y
+    return kink(y, "leaky", leaky) if act else y
 
 
 def _up(x, ref, mode):
@@ -184,7 +245,7 @@ def ssh(ctx, x, pre, leaky):
     b = conv_bn_act(ctx, b1, pre + "conv5X5_2", leaky, 1, act=False)
     c1 = conv_bn_act(ctx, b1, pre + "conv7X7_2", leaky, 1)
     c = conv_bn_act(ctx, c1, pre + "conv7x7_3", leaky, 1, act=False)
-    return F.relu(torch.cat([a, b, c], 1))
+    return kink(torch.cat([a, b, c], 1), "relu")
 
 
 def heads(ctx, feats, mode):
@@ -257,7 +318,7 @@ def retinaface_mnv3_small(P, x, mode="eval", train_bn=False):
     210-229) tapped after bneck[2], [7], [10], under the JABD head of
     nets/retinaface_r.py:304-343 (eca_24/48/96)."""
     ctx = Ctx(P, train_bn)
-    x = F.hardswish(ctx.bn(ctx.conv(x, "body.conv1", 2, 1), "body.bn1"))
+    x = kink(ctx.bn(ctx.conv(x, "body.conv1", 2, 1), "body.bn1"), "hswish")
     feats = []
     i = 0
     for layer in MNV3_SMALL_LAYERS:
@@ -276,8 +337,8 @@ def retinaface_mnv3_small(P, x, mode="eval", train_bn=False):
 def se(ctx, x, pre):
     """SeModule.forward (nets/mobilenetV3.py:18-32): x * hsigmoid(conv(relu(bn(conv(GAP(x))))))."""
     y = F.adaptive_avg_pool2d(x, 1)
-    y = F.relu(ctx.bn(ctx.conv(y, pre + "se.1"), pre + "se.2"))
-    y = F.hardsigmoid(ctx.conv(y, pre + "se.4"))
+    y = kink(ctx.bn(ctx.conv(y, pre + "se.1"), pre + "se.2"), "relu")
+    y = kink(ctx.conv(y, pre + "se.4"), "hsigmoid")
     return x * y
 
 
@@ -290,7 +351,7 @@ def stdv_eca(ctx, x, pre):
     var = (x - mean).pow(2).sum(3, keepdim=True).sum(2, keepdim=True) / (x.shape[2] * x.shape[3])
     y = var.pow(0.5)
     y = F.conv1d(y.squeeze(-1).transpose(-1, -2), w, padding=(k - 1) // 2)
-    y = F.hardsigmoid(y.transpose(-1, -2).unsqueeze(-1))
+    y = kink(y.transpose(-1, -2).unsqueeze(-1), "hsigmoid")
     return x * y
 
 
@@ -329,13 +390,13 @@ def mobilenetv3(P, x, stages, train_bn=False):
     510-522): stem, stages = [(prefix, [(spec, gate), ...]), ...], conv2+bn2+hs,
     GAP, linear3+bn3+hs (dropout: identity in eval), linear4."""
     ctx = Ctx(P, train_bn)
-    x = F.hardswish(ctx.bn(ctx.conv(x, "conv1", 2, 1), "bn1"))
+    x = kink(ctx.bn(ctx.conv(x, "conv1", 2, 1), "bn1"), "hswish")
     for pre, blocks in stages:
         for bi, (spec, gate) in enumerate(blocks):
             x = block(ctx, x, f"{pre}.{bi}.", spec, gate)
-    x = F.hardswish(ctx.bn(ctx.conv(x, "conv2"), "bn2"))
+    x = kink(ctx.bn(ctx.conv(x, "conv2"), "bn2"), "hswish")
     x = F.adaptive_avg_pool2d(x, 1).flatten(1)
-    x = F.hardswish(bn1d(ctx, F.linear(x, P["linear3.weight"]), "bn3"))
+    x = kink(bn1d(ctx, F.linear(x, P["linear3.weight"]), "bn3"), "hswish")
     return F.linear(x, P["linear4.weight"], P["linear4.bias"])
 
 
@@ -345,10 +406,10 @@ def mobilenetv1_stage(ctx, x, pre, specs):
     for i, (kind, cin, cout, stride) in enumerate(specs):
         p = f"{pre}.{i}."
         if kind == "bn":
-            x = F.leaky_relu(ctx.bn(ctx.conv(x, p + "0", stride, 1), p + "1"), 0.1)
+            x = kink(ctx.bn(ctx.conv(x, p + "0", stride, 1), p + "1"), "leaky", 0.1)
         else:
-            x = F.leaky_relu(ctx.bn(ctx.conv(x, p + "0", stride, 1, cin), p + "1"), 0.1)
-            x = F.leaky_relu(ctx.bn(ctx.conv(x, p + "3"), p + "4"), 0.1)
+            x = kink(ctx.bn(ctx.conv(x, p + "0", stride, 1, cin), p + "1"), "leaky", 0.1)
+            x = kink(ctx.bn(ctx.conv(x, p + "3"), p + "4"), "leaky", 0.1)
     return x
 
 

@@ -138,3 +138,34 @@ def test_mnv3_eval_stream_split(cuda):
     ref = model_ref.retinaface_mnv3({k: v.cpu() for k, v in m.state_dict().items()}, x)
     for a, r in zip(split, ref):
         assert rel_err(a.cpu(), r) < 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,B", [("mnv3", 32), ("r50", 64)])
+def test_benchmarked_batch_last_image(cuda, kind, B):
+    """The benchmarked batches at 1024x1024 (C2: JABD-MobileNetV3 bs32; C3's
+    model: R50 RetinaFace bs64, whose layer1 activations are [64,256,256,256]
+    = 1.07e9 elements): images 0 and B-1 of the full batch equal bs1 runs of
+    the same images (per-image batch strides, no cross-image mixing), and
+    image B-1 matches the oracle (nets/retinaface_r.py:304-343,
+    nets/retinaface_eca_nonlocal.py:314-359)."""
+    model, fn = (_mnv3(), model_ref.retinaface_mnv3) if kind == "mnv3" else \
+        (_r50(), model_ref.retinaface_r50)
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    mg = model.to(cuda)
+    gen = torch.Generator(device=cuda).manual_seed(77)
+    x = torch.rand((B, 3, 1024, 1024), generator=gen, device=cuda) * 255.0 - 117.0
+    with torch.no_grad():
+        full = [t.clone() for t in mg(x)]
+        for i in (0, B - 1):
+            one = mg(x[i:i + 1].contiguous())
+            for f, o, name in zip(full, one, ("loc", "conf", "landm")):
+                e = rel_err(f[i:i + 1], o)
+                print(f"{kind} image {i}: {name} bs{B} vs bs1 rel {e:.2e} "
+                      f"identical={torch.equal(f[i:i + 1], o)}")
+                assert e <= 1e-6, (i, name, e)
+        ref = fn(sd, x[B - 1:B].cpu(), "eval")
+    for f, r, name in zip(full, ref, ("loc", "conf", "landm")):
+        e = rel_err(f[B - 1:B], r)
+        print(f"{kind} image {B - 1} vs oracle: {name} rel {e:.2e}")
+        assert e < TOL, (name, e)

@@ -15,6 +15,7 @@ import pytest
 import torch
 import torch.nn as nn
 
+from _kinks import Kinks
 from _util import init_for_parity, rel_err
 from oracle import model_ref
 
@@ -147,28 +148,40 @@ def _composite(cuda, module, ref_fn, inputs, train, fwd_tol=1e-4, grad_tol=2e-3,
     """module(*inputs) (or module(list) with as_list) on the GPU vs
     ref_fn(ctx, *inputs) through the oracle, whose parameters are the
     module's state_dict keys under `prefix`.  Training: every input and
-    parameter gradient against a float64 oracle run, relative error within
-    max(grad_tol, 4x the float32 oracle's own error) — hard-sigmoid / hswish
-    kinks make some gradients move by percent under fp32 rounding alone."""
+    parameter gradient against a float64 oracle run whose activation masks
+    are the HIP forward's own (tests/_kinks.py; every oracle kink must find
+    its HIP tensor), relative error within max(grad_tol, 4x the error of the
+    equally mask-matched float32 oracle run)."""
+    snap = {prefix + k: v.detach().cpu().clone() for k, v in module.state_dict().items()}
+
     def run_ref(dtype):
-        P = {prefix + k: v for k, v in _P(module, dtype, grad=train).items()}
+        P = {k: (v.clone().to(dtype).requires_grad_(train)
+                 if v.is_floating_point() and "running" not in k
+                 else (v.clone().to(dtype) if v.is_floating_point() else v.clone()))
+             for k, v in snap.items()}
         ctx = model_ref.Ctx(P, train)
         xr = [t.to(dtype).requires_grad_(train) for t in inputs]
         ref = ref_fn(ctx, *xr)
         refs = list(ref) if isinstance(ref, (list, tuple)) else [ref]
         return P, xr, refs
 
-    P, xr, refs = run_ref(torch.float64)
+    kk = Kinks()
     m = module.to(cuda).train(train)
     xg = [_cl(t.to(cuda)).requires_grad_(train) for t in inputs]
-    out = m(xg) if as_list else m(*xg)
+    with kk.record():
+        out = m(xg) if as_list else m(*xg)
     outs = list(out) if isinstance(out, (list, tuple)) else [out]
+    with kk.replay():
+        P, xr, refs = run_ref(torch.float64)
     for o, r in zip(outs, refs):
         assert o.shape == r.shape
         assert rel_err(o.detach(), r.detach()) < fwd_tol, rel_err(o.detach(), r.detach())
     if not train:
         return
-    P32, xr32, refs32 = run_ref(torch.float32)
+    assert not kk.unmatched, kk.unmatched
+    with kk.replay():
+        P32, xr32, refs32 = run_ref(torch.float32)
+    assert not kk.unmatched, kk.unmatched
     g = torch.Generator().manual_seed(12)
     wts = [torch.randn(r.shape, generator=g, dtype=torch.float64) for r in refs]
     sum((r * w).sum() for r, w in zip(refs, wts)).backward()
@@ -470,17 +483,16 @@ def test_dataparallel_replica_training_grads_reach_original(cuda):
         assert ".se." in k and float(grads[1][k].abs().max()) == 0.0, k
 
 
-@pytest.mark.parametrize("hw", [(32, 32)])
+@pytest.mark.parametrize("hw", [(32, 48), (20, 24), (16, 16), (32, 32), (8, 8), (16, 24), (40, 40),
+                                (32, 64)])
 @pytest.mark.parametrize("cls,spec,gate", [b for b in BLOCKS if b[0] == "Block_eca"])
 def test_mnv3_block_eca_wgrad_fused(cuda, cls, spec, gate, monkeypatch, hw):
-    """Block_eca training at map sizes whose HW is a multiple of 64, so the
-    project conv's weight gradient and the ECA gate's sum(da * d) come from
-    one GEMM over image-aligned chunks (jabd_conv_wgrad_eca_f32).  Sizes are
-    picked so that no BN output lies within fp32 rounding of an activation
-    kink: at 3x32x64 one BN2 output of the 120-channel block is 9.5e-8, its
-    ReLU mask differs from the float64 run in this and in the separate-pass
-    path alike, and the flipped element's gradient moves its whole channel
-    through the BN backward (tools/block_bisect.py)."""
+    """Block_eca training (the fused MNv3BlockFn node) over eight map sizes
+    (3x40x32x64 is where the 120-channel block has a BN2 output of 9.5e-8):
+    the project conv's weight gradient and the ECA gate's sum(da * d) come
+    from one GEMM over image-aligned pixel chunks (jabd_conv_wgrad_eca_f32,
+    asserted below); every gradient against the mask-matched float64 oracle
+    (_composite)."""
     import nets.mobilenetV3 as mv3
     from jabd_amd import train as T
     taken = []

@@ -78,7 +78,7 @@ def _overlap_worker(rank, world, port, q):
         unused = torch.nn.Linear(3, 3)  # parameters that never get a gradient
         m.add_module("unused", unused)
         red = GradAllReduce(m, bucket_bytes=4096)  # several buckets
-        ok = True
+        ok = red.hooks == []                  # nothing installed before the first step
         for step in range(3):
             x = torch.randn(5, 8, generator=torch.Generator().manual_seed(10 * step + rank))
             m.zero_grad()
@@ -94,7 +94,8 @@ def _overlap_worker(rank, world, port, q):
             ok &= len(got) == 6 and all(torch.allclose(g, a, rtol=1e-6, atol=1e-6)
                                          for g, a in zip(got, allg))
             ok &= unused.weight.grad is None
-            ok &= (red.hooks != []) == (step >= 0)
+            ok &= red.hooks != [] and len(red.buckets) > 1   # planned after step 1
+            ok &= red.works == {} and red.pending == {}
         q.put((rank, ok))
     finally:
         dist.destroy_process_group()
@@ -105,6 +106,70 @@ def test_grad_allreduce_overlap_hooks_gloo():
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_overlap_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}
+
+
+def _freeze_worker(rank, world, port, q):
+    """The reference's Freeze_Train schedule (train_mobilenetV3_ecagai.py:
+    576-610) on one model: the first part frozen for two steps, then
+    unfrozen.  After unfreezing, its gradients must be SUM-reduced too (the
+    reducer plans again), and every step equals the explicit sum of both
+    ranks' gradients; a parameter that stops receiving a gradient also
+    triggers a re-plan instead of an error."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from jabd_amd.parallel import GradAllReduce
+        torch.manual_seed(0)
+        body = torch.nn.Sequential(torch.nn.Linear(8, 32), torch.nn.ReLU())
+        head = torch.nn.Sequential(torch.nn.Linear(32, 32), torch.nn.ReLU(),
+                                   torch.nn.Linear(32, 2))
+        m = torch.nn.Sequential(body, head)
+        red = GradAllReduce(m, bucket_bytes=1024)
+        ok = True
+        plan = {}
+        for step in range(7):
+            frozen = step < 2
+            for p in body.parameters():
+                p.requires_grad_(not frozen)
+            skip_last = step == 5          # the last layer unused for one step
+            x = torch.randn(4, 8, generator=torch.Generator().manual_seed(100 * step + rank))
+            m.zero_grad()
+            h = head[1](head[0](body(x)))
+            out = h.sum() if skip_last else head[2](h).square().sum()
+            out.backward()
+            mine = [(n, p.grad.clone()) for n, p in m.named_parameters() if p.grad is not None]
+            want = {}
+            for n, t in mine:
+                lst = [torch.zeros_like(t) for _ in range(world)]
+                dist.all_gather(lst, t)
+                want[n] = sum(lst)
+            red()
+            got = {n: p.grad for n, p in m.named_parameters() if p.grad is not None}
+            ok &= set(got) == set(want)
+            ok &= all(torch.allclose(got[n], want[n], rtol=1e-6, atol=1e-6) for n in want)
+            ok &= any(n.startswith("0.") for n in got) == (not frozen)
+            plan[step] = sum(len(b) for b in red.buckets)
+        # planned sizes: head only (4 tensors), then head + body (6), then the
+        # step without the last layer (4), then all 6 again
+        ok &= plan[0] == 4 and plan[1] == 4 and plan[2] == 6 and plan[4] == 6
+        ok &= plan[5] == 4 and plan[6] == 6
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_freeze_unfreeze_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_freeze_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)
