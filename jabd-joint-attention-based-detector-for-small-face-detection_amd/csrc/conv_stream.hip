@@ -26,6 +26,8 @@
 // output channel, so A is read from HBM exactly once).
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "common.h"
 #include "conv_args.h"
 
@@ -223,6 +225,13 @@ int conv1x1_stream_dispatch(const ConvArgs& a, hipStream_t st) {
   if (lds > (a.Kc * TN > 24 ? 150 : 40) * 1024) return -1;
   const int64_t nblk = cdiv(a.M, 16);
   if (nblk >= ((int64_t)1 << 27)) return -1;
+  // the kernel forms pixel offsets m * ps in 32-bit ints (the caller's fast1x1
+  // condition already bounds (M + 64) * (max ps + 16) < 2^31; kept here so the
+  // kernel never relies on a caller's check)
+  const int64_t maxps = std::max<int64_t>(std::max<int64_t>(a.x_ps, a.y_ps),
+                                          std::max<int64_t>(a.res ? a.res_ps : 0,
+                                                            a.x2 ? a.x2_ps : 0));
+  if ((a.M + 16) * (maxps + 16) >= ((int64_t)1 << 31)) return -1;
   const int x2 = a.x2 ? 1 : 0;
   const bool as = a.ascale != nullptr;
 #define CS_LAUNCH(TN_, KC_, X2_, AS_)                                                       \

@@ -509,6 +509,11 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
   const int64_t nitems = cdiv(ntiles, 8) * 8 * nch;
   JABD_REQUIRE(nitems < ((int64_t)1 << 31) && (int64_t)a.H * a.W * a.x_ps < ((int64_t)1 << 31),
                "expand_dw: problem too large for 32-bit item / pixel indexing");
+  // the input is read through a buffer descriptor with 32-bit byte offsets:
+  // a larger x would be truncated to zeros, so refuse it (the caller splits
+  // the batch, engine.py)
+  JABD_REQUIRE((int64_t)a.B * a.x_bs * 4 < ((int64_t)1 << 32),
+               "expand_dw: input must be < 4 GiB (split the batch)");
   const int nw = xd_nw(a, EC);
   hipStream_t st = as_stream(stream);
   const XdDivs dv{make_fastdiv((uint32_t)nch), make_fastdiv((uint32_t)tiles_img),

@@ -41,6 +41,8 @@ FUSE_SKIP = os.environ.get("JABD_FUSE_SKIP", "1") != "0"
 # launches cost more clock than the filled CUs gain once the data is real.
 EVAL_STREAMS = int(os.environ.get("JABD_EVAL_STREAMS", "1"))
 EVAL_SPLIT_MIN = int(os.environ.get("JABD_EVAL_SPLIT_MIN", "8"))
+# Engine.run: activation elements one chunk of a batch may reach (32-bit offsets)
+CHUNK_ELEMS = (1 << 31) - 1
 # The head's three per-level ECA gates as one pool + gate launch pair
 # (F.eca_gates_multi); JABD_GATES_MULTI=0 launches them level by level (A/B).
 GATES_MULTI = os.environ.get("JABD_GATES_MULTI", "1") != "0"
@@ -383,6 +385,20 @@ class Engine:
         most of the CUs idle.  The heads write straight into batch slices of
         one set of outputs."""
         B = x.shape[0]
+        # the kernels index a batch's activations with 32-bit element offsets
+        # (and expand_dw reads its input through a < 4 GiB buffer descriptor):
+        # the largest stored activation is <= 16*H*W elements per image (R50
+        # layer1: 256 channels at H/4 x W/4), so larger batches run in chunks
+        per_img = 16 * x.shape[2] * x.shape[3]
+        chunk = max(1, CHUNK_ELEMS // per_img)
+        if B > chunk:
+            A = self.anchors(x.shape[2], x.shape[3])
+            out = tuple(torch.empty((B, A, k), dtype=torch.float32, device=x.device)
+                        for k in (4, 2, 10))
+            for b0 in range(0, B, chunk):
+                b1 = min(B, b0 + chunk)
+                self._run(x[b0:b1], softmax, out=tuple(o[b0:b1] for o in out))
+            return out
         n = min(EVAL_STREAMS, B) if B >= EVAL_SPLIT_MIN and self.split_ok else 1
         if n <= 1:
             return self._run(x, softmax)

@@ -148,6 +148,8 @@ class EcaScaleFn(torch.autograd.Function):
         B, H, W, C = x.shape
         w1 = w1d.detach().reshape(-1).float().contiguous()
         scale, mean = F.eca_gate(F.channel_sums(x), H * W, w1, gate, return_mean=True)
+        if gate == "hsigmoid":
+            F.tap("eca", gate, mean, w1)
         y = torch.empty_like(x)
         call("jabd_channel_scale_f32", x.data_ptr(), B, H * W, C, scale.data_ptr(), y.data_ptr(),
              _st())

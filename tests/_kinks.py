@@ -21,7 +21,9 @@ kernel being wrong — or a real kernel error could be excused as a flip.
   * `with kk.replay():` installs it as oracle.model_ref.REPLAY.  Each oracle
     kink()/maxpool() call is paired with the recorded tensor of the same
     family and shape that is closest to it (max-abs difference relative to
-    the oracle tensor's max, which must be < 1e-3), and the oracle's backward
+    the oracle tensor's max, which must be < 1e-2: distinct tensors differ by
+    O(1), and a batch-statistics BN over two 1x1 samples — the SE gate —
+    amplifies fp32 error to ~1e-3), and the oracle's backward
     takes its region from it.
 
 Both oracle runs (float64 and float32) are replayed, so the float32 run's
@@ -62,7 +64,7 @@ def _nchw(z):
 
 
 class Kinks:
-    def __init__(self, tol=1e-3):
+    def __init__(self, tol=1e-2):
         self.rec = []            # (family, [candidate float64 tensors])
         self.tol = tol
         self.used = set()
@@ -123,7 +125,8 @@ class Kinks:
                 return []
             a, b, c = (_nchw(t) for t in (a, b, c))
             q = (shape[1] - a.shape[1]) // 2
-            if q <= 0 or q > b.shape[1]:
+            if q <= 0 or q > b.shape[1] or a.shape[0] != shape[0] or \
+                    tuple(a.shape[2:]) != tuple(shape[2:]):
                 return []
             return [torch.cat([a, b[:, :q], c[:, :q]], 1)]
         out = []
