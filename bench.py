@@ -18,8 +18,13 @@ Extra fields on the one JSON line:
                (csrc/adam.hip) wd 5e-4 as train_mobilenetV3_ecagai.py:564) on every rank ->
                whole-job images/sec, data-parallel weak scaling; at N=1 also
                C3 (configs[2]): R50 RetinaFace training step at bs64 1024x1024.
+  predict_fps_bs1  the reference's own perf path: predict.py get_FPS (bs1,
+               100 iterations of forward + decode + filter + NMS + host copy)
+               at 640^2 and 1024^2 for the R50 and MNv3 detectors.
+  c5_e2e       C5 end to end: bs8 2048^2 forward + decode + NMS.
   cpu_baseline the oracle's PyTorch-CPU restatement of the same forward at
-               1024x1024, bs1, on this host (rank 0, N=1 only).
+               1024x1024, bs1, on this host (rank 0, N=1 only), plus legs
+               (C1, C2/C3 forwards, C3/C4 training steps at bs1/bs4, C5 NMS).
 """
 import argparse
 import json
@@ -48,6 +53,7 @@ def parse():
     ap.add_argument("--size", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-nms", action="store_true")
+    ap.add_argument("--no-predict", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-train", action="store_true")
     ap.add_argument("--train-steps", type=int, default=10)
@@ -292,6 +298,120 @@ def augment_bench(device, reps=20):
             "algorithmic_bytes": nbytes, "achieved_gbs": nbytes / (ms * 1e-3) / 1e9}
 
 
+def _weights_init_model(kind, mode="eval"):
+    import contextlib
+    import io
+    from nets.retinaface_training import weights_init
+    RetinaFace, cfg = detector(kind)
+    torch.manual_seed(0)
+    m = RetinaFace(cfg=cfg, mode=mode)
+    with contextlib.redirect_stdout(io.StringIO()):
+        weights_init(m)
+    return m, cfg
+
+
+def predict_fps(device, iters=100, warmup=10):
+    """The reference's own performance path, predict.py mode 'fps'
+    (get_FPS, predict.py:253-333, test_interval=100 at :522-526): bs1, the
+    letterboxed network input prepared once, then per iteration the forward,
+    decode, conf[:, 1:2], decode_landm, cat and non_max_suppression (score
+    >= 0.5, NMS 0.3) with the kept rows handed back to the host — here the
+    eval forward + jabd_detect_f32 + one device-to-host copy of the kept
+    rows.  `detect_image_fps` is the whole detect_image per call (host image
+    upload, letterbox + preprocess, forward, detect, correct_boxes, host
+    copy).  R50 is the detector predict.py loads (nets/retinaface_eca_nonlocal,
+    predict.py:15,101); JABD-MobileNetV3 beside it.  Weights: weights_init."""
+    import numpy as np
+    from jabd_amd import ops
+    from jabd_amd.predict import detect_image
+    from utils.anchors import Anchors
+    out = {}
+    for kind in ("r50", "mnv3"):
+        net, cfg = _weights_init_model(kind)
+        net = net.eval().to(device)
+        for size in (640, 1024):
+            img = np.random.default_rng(size).integers(0, 256, (size * 3 // 4, size, 3)) \
+                .astype(np.float32)
+            x = ops.letterbox(torch.from_numpy(img).to(device), (size, size),
+                              mean=(104.0, 117.0, 123.0))
+            pri = Anchors(cfg, image_size=(size, size)).get_anchors().to(device).float()
+            var = cfg["variance"]
+
+            def step():
+                with torch.no_grad():
+                    loc, conf, landm = net(x)
+                    rows, nk = ops.detect(loc, conf, landm, pri, var, 0.5, 0.3)
+                    k = int(nk[0].item())
+                    return rows[0, :k].cpu().numpy()
+            for _ in range(warmup):
+                step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                kept = step()
+            el = time.perf_counter() - t0
+            for _ in range(3):
+                detect_image(net, img, (size, size), cfg, 0.5, 0.3)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(iters // 2):
+                detect_image(net, img, (size, size), cfg, 0.5, 0.3)
+            el2 = time.perf_counter() - t1
+            with torch.no_grad():
+                cand = int((net(x)[1][0, :, 1] >= 0.5).sum())
+            out[f"{kind}_{size}"] = {
+                "fps": iters / el, "ms_per_image": el / iters * 1e3,
+                "detect_image_fps": (iters // 2) / el2, "iters": iters,
+                "anchors": int(pri.shape[0]), "candidates_ge_0.5": cand,
+                "kept": int(kept.shape[0])}
+        del net
+        torch.cuda.empty_cache()
+    out["note"] = ("bs1 wall clock per iteration (host-side launch/ctypes/n_keep sync costs "
+                   "included), as get_FPS; weights_init weights put ~half the anchors at a "
+                   "conf of ~0.5, so NMS runs over thousands of candidates")
+    return out
+
+
+def c5_e2e(device, batch=8, size=2048, steps=5, warmup=2):
+    """C5 end to end (BASELINE configs[4]): JABD-MobileNetV3 eval forward on a
+    bs8 2048x2048 batch + jabd_detect_f32 (decode, >= 0.5 filter, NMS 0.3)
+    over its 172,032 anchors per image, timed between synchronisations."""
+    from jabd_amd import ops, synth
+    from utils.anchors import Anchors
+    net, cfg = _weights_init_model("mnv3")
+    net = net.eval().to(device)
+    x = synth.images(batch, size, seed=99, device=device)
+    pri = Anchors(cfg, image_size=(size, size)).get_anchors().to(device).float()
+    var = cfg["variance"]
+    with torch.no_grad():
+        for _ in range(warmup):
+            rows, nk = ops.detect(*net(x), pri, var, 0.5, 0.3)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            rows, nk = ops.detect(*net(x), pri, var, 0.5, 0.3)
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / steps
+        loc, conf, landm = net(x)
+        cand = (conf[:, :, 1] >= 0.5).sum(1)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(steps):
+            ops.detect(loc, conf, landm, pri, var, 0.5, 0.3)
+        torch.cuda.synchronize()
+        el_det = (time.perf_counter() - t1) / steps
+    del net
+    torch.cuda.empty_cache()
+    A = int(pri.shape[0])
+    return {"config": f"C5: JABD-MobileNetV3 eval forward bs{batch} {size}x{size} + decode + "
+                      f">=0.5 filter + NMS 0.3 (jabd_detect_f32), weights_init weights",
+            "images_per_sec": batch / el, "ms_per_batch": el * 1e3,
+            "detect_ms_per_batch": el_det * 1e3, "anchors_per_image": A,
+            "boxes_per_sec": batch * A / el,
+            "nms_candidates_per_image": [int(v) for v in cand],
+            "kept_per_image": [int(v) for v in nk]}
+
+
 def detector(kind):
     """(RetinaFace class, cfg) of a detector kind: mnv3 (JABD-MobileNetV3),
     beca (JABD-MobileNetV3-BECA), small (MobileNetV3_Small + ECA head), r50."""
@@ -461,7 +581,12 @@ def pmc_traffic():
 
 
 def host_cores():
-    """(threads this process may use, physical cores per lscpu)."""
+    """CPU budget of the CPU baseline: BASELINE.md asks for
+    torch.set_num_threads(<physical cores>); the threads used are
+    min(physical cores, CPUs in this process's affinity mask, the cgroup CPU
+    quota) — on the GPU box the job's share of the host is a quota, not the
+    affinity mask.  Returns (threads, info dict)."""
+    import math
     import subprocess
     phys = None
     try:
@@ -470,11 +595,36 @@ def host_cores():
         phys = int(kv["Core(s) per socket"].strip()) * int(kv["Socket(s)"].strip())
     except Exception:
         pass
-    return torch.get_num_threads(), phys
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = os.cpu_count()
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except Exception:
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0:
+                quota = q / per
+        except Exception:
+            pass
+    cands = [v for v in (phys, aff, math.floor(quota) if quota else None) if v]
+    threads = max(1, min(cands)) if cands else torch.get_num_threads()
+    return threads, {"host_physical_cores": phys, "affinity_cpus": aff,
+                     "cgroup_cpu_quota": quota,
+                     "threads_rule": "min(physical cores, affinity CPUs, cgroup CPU quota)"}
 
 
-def _time_bounded(fn, seconds, min_iters=1):
-    fn()  # warm-up
+def _time_bounded(fn, seconds, min_iters=1, warm=True):
+    if warm:
+        fn()  # warm-up
     n, t0 = 0, time.perf_counter()
     while n < min_iters or time.perf_counter() - t0 < seconds:
         fn()
@@ -482,13 +632,38 @@ def _time_bounded(fn, seconds, min_iters=1):
     return n, time.perf_counter() - t0
 
 
+def _cpu_train_step(fn, sd, cfg, size, batch, seed):
+    """One training step of the oracle on the CPU (train_mobilenetV3_ecagai.py:
+    518-533): batch-stat forward, match + MultiBoxLoss (oracle/box_ref.py),
+    loss = 2 * loss_l + loss_c + loss_landm, autograd backward, Adam (lr 1e-3,
+    weight_decay 5e-4, as :564) over the parameters."""
+    from jabd_amd import synth
+    from oracle import box_ref
+    P = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and "running" not in k
+             else v.clone()) for k, v in sd.items()}
+    params = [v for v in P.values() if isinstance(v, torch.Tensor) and v.requires_grad]
+    opt = torch.optim.Adam(params, 1e-3, weight_decay=5e-4)
+    pri = box_ref.anchors(cfg, (size, size))
+    x = synth.images(batch, size, seed=seed)
+    tg = [torch.from_numpy(t) for t in synth.targets(batch, size, seed=seed)]
+
+    def step():
+        opt.zero_grad()
+        loc, conf, landm = fn(P, x, "train", train_bn=True)
+        lt, ct, lmt = box_ref.match_batch(tg, pri)
+        rl, rc, rlm, _ = box_ref.multibox_loss(loc, conf, landm, lt, ct, lmt)
+        (2.0 * rl + rc + rlm).backward()
+        opt.step()
+    return step
+
+
 def cpu_baseline(size, seconds):
     """The oracle's PyTorch-CPU restatement timed on this host (rank 0, N=1):
     headline leg C2 (MNv3 eval forward, bs1 1024^2) plus the legs BASELINE.md
     plans — C1 end to end (640^2 bs1: preprocess, forward, decode, score
-    filter, torchvision-CPU NMS), C2/C3 forwards at bs4, C3 (R50) at bs1, and
-    C5's NMS over one 100k-box image (oracle/nms_ref.c) — each a bounded
-    sample of a few seconds."""
+    filter, torchvision-CPU NMS), C2/C3 forwards at bs4, C3 (R50) at bs1, the
+    C3 (R50) and C4 (MNv3) training steps at bs1 and bs4, and C5's NMS over
+    one 100k-box image (oracle/nms_ref.c) — each a bounded sample."""
     from oracle import box_ref, model_ref, prep_ref
     from nets.retinaface_r import RetinaFace
     from nets.retinaface_eca_nonlocal import RetinaFace as R50
@@ -498,7 +673,9 @@ def cpu_baseline(size, seconds):
     import contextlib
     import io
     import numpy as np
-    threads, phys = host_cores()
+    threads, info = host_cores()
+    saved_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
     torch.manual_seed(0)
     with contextlib.redirect_stdout(io.StringIO()):
         m = RetinaFace(cfg=cfg_mnet, mode="eval")
@@ -508,39 +685,55 @@ def cpu_baseline(size, seconds):
     sd = {k: v.float() for k, v in m.eval().state_dict().items()}
     sdr = {k: v.float() for k, v in r.eval().state_dict().items()}
     legs = {}
-    with torch.no_grad():
-        x1 = synth.images(1, size, seed=1234)
-        n, dt = _time_bounded(lambda: model_ref.retinaface_mnv3(sd, x1), seconds)
-        head = {"value": n / dt, "unit": "images/sec", "cores": threads,
-                "host_physical_cores": phys, "kind": "port",
-                "sample": f"{n} images, bs1 {size}x{size}, oracle model_ref.retinaface_mnv3 "
-                          "(PyTorch-CPU fp32 restatement)"}
-        x4 = synth.images(4, size, seed=1234)
-        n, dt = _time_bounded(lambda: model_ref.retinaface_mnv3(sd, x4), 3.0)
-        legs["C2_mnv3_bs4"] = {"images_per_sec": 4 * n / dt, "batches": n}
-        n, dt = _time_bounded(lambda: model_ref.retinaface_r50(sdr, x1), 3.0)
-        legs["C3_r50_bs1"] = {"images_per_sec": n / dt, "batches": n}
-        n, dt = _time_bounded(lambda: model_ref.retinaface_r50(sdr, x4), 3.0)
-        legs["C3_r50_bs4"] = {"images_per_sec": 4 * n / dt, "batches": n}
-        img = np.random.default_rng(640).integers(0, 256, (480, 640, 3)).astype(np.float32)
-        pri = box_ref.anchors(cfg_mnet, (640, 640))
+    try:
+        with torch.no_grad():
+            x1 = synth.images(1, size, seed=1234)
+            n, dt = _time_bounded(lambda: model_ref.retinaface_mnv3(sd, x1), seconds)
+            head = {"value": n / dt, "unit": "images/sec", "cores": threads, **info,
+                    "kind": "port",
+                    "sample": f"{n} images, bs1 {size}x{size}, oracle model_ref.retinaface_mnv3 "
+                              "(PyTorch-CPU fp32 restatement)"}
+            x4 = synth.images(4, size, seed=1234)
+            n, dt = _time_bounded(lambda: model_ref.retinaface_mnv3(sd, x4), 3.0)
+            legs["C2_mnv3_bs4"] = {"images_per_sec": 4 * n / dt, "batches": n}
+            n, dt = _time_bounded(lambda: model_ref.retinaface_r50(sdr, x1), 3.0)
+            legs["C3_r50_bs1"] = {"images_per_sec": n / dt, "batches": n}
+            n, dt = _time_bounded(lambda: model_ref.retinaface_r50(sdr, x4), 3.0)
+            legs["C3_r50_bs4"] = {"images_per_sec": 4 * n / dt, "batches": n}
+            img = np.random.default_rng(640).integers(0, 256, (480, 640, 3)).astype(np.float32)
+            pri = box_ref.anchors(cfg_mnet, (640, 640))
 
-        def c1():
-            xx = torch.from_numpy(prep_ref.preprocess(img, (640, 640)))[None]
-            loc, conf, landm = model_ref.retinaface_mnv3(sd, xx, "eval")
-            det = torch.cat([box_ref.decode(loc[0], pri, cfg_mnet["variance"]), conf[0][:, 1:2],
-                             box_ref.decode_landm(landm[0], pri, cfg_mnet["variance"])], -1)
-            rows = box_ref.non_max_suppression(det, 0.5, 0.3)
-            if len(rows):
-                prep_ref.correct_rows(np.asarray(rows, np.float32), (640, 640), (480, 640))
-        n, dt = _time_bounded(c1, 3.0)
-        legs["C1_detect_image_640"] = {"images_per_sec": n / dt, "images": n,
-                                       "stages": "letterbox+preprocess, forward, decode, "
-                                                 ">=0.5 filter, NMS 0.3, correct_boxes"}
-    bx, sc = synth.nms_boxes(1, 100_000, seed=99)
-    n, dt = _time_bounded(lambda: box_ref.nms(bx[0], sc[0], 0.3), 1.0)
-    legs["C5_nms_100k"] = {"boxes_per_sec": 100_000 * n / dt, "images": n,
-                           "kind": "oracle/nms_ref.c (torchvision-CPU NMS restated in C), 1 thread"}
+            def c1():
+                xx = torch.from_numpy(prep_ref.preprocess(img, (640, 640)))[None]
+                loc, conf, landm = model_ref.retinaface_mnv3(sd, xx, "eval")
+                det = torch.cat([box_ref.decode(loc[0], pri, cfg_mnet["variance"]),
+                                 conf[0][:, 1:2],
+                                 box_ref.decode_landm(landm[0], pri, cfg_mnet["variance"])], -1)
+                rows = box_ref.non_max_suppression(det, 0.5, 0.3)
+                if len(rows):
+                    prep_ref.correct_rows(np.asarray(rows, np.float32), (640, 640), (480, 640))
+            n, dt = _time_bounded(c1, 3.0)
+            legs["C1_detect_image_640"] = {"images_per_sec": n / dt, "images": n,
+                                           "stages": "letterbox+preprocess, forward, decode, "
+                                                     ">=0.5 filter, NMS 0.3, correct_boxes"}
+        # training steps ("the training step for C3", bs 1 and 4)
+        for name, fn, sdd, cfg in (("C4_mnv3_train", model_ref.retinaface_mnv3, sd, cfg_mnet),
+                                   ("C3_r50_train", model_ref.retinaface_r50, sdr, cfg_re50)):
+            for bs in (1, 4):
+                step = _cpu_train_step(fn, sdd, cfg, size, bs, 4321)
+                # seconds per step already: no separate warm-up step
+                n, dt = _time_bounded(step, 3.0, warm=False)
+                legs[f"{name}_bs{bs}"] = {
+                    "images_per_sec": bs * n / dt, "steps": n,
+                    "step": "batch-stat forward, match + MultiBoxLoss (OHEM 7:1), backward, "
+                            "Adam wd 5e-4 (train_mobilenetV3_ecagai.py:518-533)"}
+        bx, sc = synth.nms_boxes(1, 100_000, seed=99)
+        n, dt = _time_bounded(lambda: box_ref.nms(bx[0], sc[0], 0.3), 1.0)
+        legs["C5_nms_100k"] = {"boxes_per_sec": 100_000 * n / dt, "images": n,
+                               "kind": "oracle/nms_ref.c (torchvision-CPU NMS restated in C), "
+                                       "1 thread"}
+    finally:
+        torch.set_num_threads(saved_threads)
     head["legs"] = legs
     return head
 
@@ -635,6 +828,9 @@ def main():
         if not args.no_nms:
             extra["nms"] = nms_bench(device)
             extra["augment"] = augment_bench(device)
+        if world == 1 and not args.no_predict:
+            extra["predict_fps_bs1"] = predict_fps(device)
+            extra["c5_e2e"] = c5_e2e(device)
         if world == 1 and not args.no_cpu_baseline:
             extra["cpu_baseline"] = cpu_baseline(args.size, args.cpu_seconds)
         line = {

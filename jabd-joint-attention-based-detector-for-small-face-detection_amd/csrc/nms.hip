@@ -16,9 +16,11 @@
 //                    (grid_* kernels below);  dense (NaN boxes, thr < 0, or
 //                    more candidate pairs than the workspace holds): every
 //                    pair in 64x64 tiles (nms_mask).
-//   5. nms_scan      one workgroup per image walks the row blocks on the
-//                    device (suppressed-set bitset in LDS, next block's lists
-//                    prefetched), writes kept rows + count.
+//   5. scan          grid images: nms_scan_pull, one wave per image pulls
+//                    each row block's incoming pairs against the kept bitset
+//                    in LDS (lists of the next blocks in flight); dense
+//                    images: nms_scan (push of per-row lists).  Both write
+//                    the kept rows + count.
 // Compile with -ffp-contract=off: IoU must round exactly like the CPU kernel
 // (no FMA in (x2-x1)*(y2-y1) or inter/(a+b-inter)).
 #include <hipcub/hipcub.hpp>
@@ -300,21 +302,39 @@ __device__ __forceinline__ uint64_t grid_key(int b, int cw, int ch, int y, int x
          ((uint64_t)(y + kCellOff) << 18) | (uint64_t)(x + kCellOff);
 }
 
-// ext[b][0][cw] = largest width of width class cw, ext[b][1][ch] = largest height
-__global__ void grid_ext(const float4* __restrict__ sbox, const float* __restrict__ sarea,
-                         const int* __restrict__ counts, const int* __restrict__ nanflag,
-                         int64_t n, float inv_w, unsigned* __restrict__ ext,
-                         int* __restrict__ dense) {
-  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+// ext[b][0][cw] = largest width of width class cw, ext[b][1][ch] = largest
+// height.  The classes one image occupies are few (tens), so per-box global
+// atomics would serialise on a handful of L2 addresses: each workgroup takes
+// kExtPer boxes per thread into LDS maxima first and flushes the classes it
+// touched with one global atomic each.
+static constexpr int kExtPer = 16;
+__global__ __launch_bounds__(256) void grid_ext(const float4* __restrict__ sbox,
+                                                const float* __restrict__ sarea,
+                                                const int* __restrict__ counts,
+                                                const int* __restrict__ nanflag, int64_t n,
+                                                float inv_w, unsigned* __restrict__ ext,
+                                                int* __restrict__ dense) {
+  __shared__ unsigned le[2 * kNC];
+  const int t = threadIdx.x;
   const int b = blockIdx.y;
-  if (r == 0 && nanflag[b]) atomicOr(&dense[b], 1);
-  if (r >= counts[b]) return;
-  const float4 bx = sbox[(int64_t)b * n + r];
-  const float a = sarea[(int64_t)b * n + r];
-  if (!grid_active(bx, a)) return;
-  const float w = bx.z - bx.x, h = bx.w - bx.y;
-  atomicMax(&ext[(int64_t)b * 2 * kNC + grid_class(w, inv_w)], __float_as_uint(w));
-  atomicMax(&ext[(int64_t)b * 2 * kNC + kNC + grid_class(h, inv_w)], __float_as_uint(h));
+  for (int i = t; i < 2 * kNC; i += 256) le[i] = 0u;
+  if (blockIdx.x == 0 && t == 0 && nanflag[b]) atomicOr(&dense[b], 1);
+  __syncthreads();
+  const int cnt = counts[b];
+  const int64_t base = (int64_t)blockIdx.x * 256 * kExtPer;
+  for (int k = 0; k < kExtPer; ++k) {
+    const int64_t r = base + (int64_t)k * 256 + t;
+    if (r >= cnt) break;
+    const float4 bx = sbox[(int64_t)b * n + r];
+    const float a = sarea[(int64_t)b * n + r];
+    if (!grid_active(bx, a)) continue;
+    const float w = bx.z - bx.x, h = bx.w - bx.y;
+    atomicMax(&le[grid_class(w, inv_w)], __float_as_uint(w));
+    atomicMax(&le[kNC + grid_class(h, inv_w)], __float_as_uint(h));
+  }
+  __syncthreads();
+  for (int i = t; i < 2 * kNC; i += 256)
+    if (le[i]) atomicMax(&ext[(int64_t)b * 2 * kNC + i], le[i]);
 }
 
 __global__ void grid_keys(const float4* __restrict__ sbox, const float* __restrict__ sarea,
@@ -423,7 +443,7 @@ __global__ __launch_bounds__(256) void grid_pairs(
     int ps[kBuf];
 #pragma unroll
     for (int q = 0; q < kBuf; ++q)
-      if (q < np && base + q < cap) ps[q] = atomicAdd(&rowcnt[(int64_t)b * n + pr[q]], 1);
+      if (q < np && base + q < cap) ps[q] = atomicAdd(&rowcnt[(int64_t)b * n + pc[q]], 1);
 #pragma unroll
     for (int q = 0; q < kBuf; ++q) {
       if (q < np) {
@@ -493,7 +513,10 @@ __global__ __launch_bounds__(256) void grid_pairs(
   if (ntest) atomicAdd(&tested[(int64_t)b * 64 + lane], (unsigned long long)ntest);
 }
 
-// CSR of each row's off-block columns: csr[rowoff[row] + slot] = col.
+// CSR by destination row: each off-block pair (row suppresses col, row
+// ranked earlier, in an earlier 64-row block) is stored in col's list as
+// (row << 6) | (col & 63): csr[rowoff[col] + slot].  A row block's incoming
+// pairs are then one contiguous range (rows of a block are contiguous).
 __global__ void grid_scatter(const int* __restrict__ npairs, const int* __restrict__ dense,
                              int64_t cap, int64_t n, const int* __restrict__ prow,
                              const int* __restrict__ pcol, const int* __restrict__ pslot,
@@ -502,36 +525,317 @@ __global__ void grid_scatter(const int* __restrict__ npairs, const int* __restri
   const int b = blockIdx.y;
   if (dense[b] || s >= cap || s >= npairs[b]) return;
   const int64_t o = (int64_t)b * cap + s;
-  csr[rowoff[(int64_t)b * n + prow[o]] + pslot[o]] = pcol[o];
+  const int col = pcol[o];
+  csr[rowoff[(int64_t)b * n + col] + pslot[o]] = (prow[o] << 6) | (col & 63);
 }
 
-// One workgroup per image walks the row blocks in rank order.  Block c's
+// ---------------------------------------------------------------------------
+// Greedy scan of a grid image as a pull over row blocks.  Block c's kept rows
+// are the valid rows not removed by (a) a kept row of an earlier block with a
+// pair into it — block c's incoming list, looked up in the kept bitset of the
+// earlier blocks — nor (b) an earlier kept row of the same block (diag words,
+// resolved in rank order).  Nothing a block reads from HBM depends on the
+// scan state, so it can be staged ahead of the scan:
+//   * one workgroup per image: wave 0 scans, waves 1..15 are loaders, each
+//     staging every 15th row block (diag words, original row ids, incoming
+//     pairs) into LDS rings and publishing it with a ready flag;
+//   * the scan wave never touches HBM except for its output stores: per block
+//     it waits for the flag (LDS), looks the pairs up in the kept bitset (LDS),
+//     ORs the removed bits across the wave (DPP), resolves the block and
+//     publishes how far it got, which frees ring space for the loaders.
+// The incoming pairs of consecutive blocks are consecutive in the CSR, so
+// the pair ring is indexed by CSR position modulo its size; a block whose
+// list alone exceeds the ring is read by the scan wave from HBM instead.
+// Every wait is bounded (kSpinMax): a broken hand-off ends the kernel with
+// *err set instead of hanging the device.
+// ---------------------------------------------------------------------------
+static constexpr int kPullLoaders = 15;
+static constexpr int kMetaRing = 32;        // row blocks staged ahead
+static constexpr int kEntRing = 8192;       // incoming pairs staged ahead (power of two)
+static constexpr unsigned kSpinMax = 1u << 22;
+static constexpr int kPullStaticLds = kEntRing * 4 + kMetaRing * 64 * 12 + kMetaRing * 24 + 16;
+
+__device__ __forceinline__ uint32_t wave_or32(uint32_t v) {
+  // inclusive OR-scan inside each 16-lane row, then across rows (gfx9 DPP)
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return __builtin_amdgcn_readlane(v, 63);
+}
+
+__device__ __forceinline__ int lds_acquire(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_release(int* p, int v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's data writes have landed
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__global__ __launch_bounds__(64 * (kPullLoaders + 1)) void nms_scan_pull(
+    const uint64_t* __restrict__ diag, const int* __restrict__ dense,
+    const int* __restrict__ rowcnt, const int* __restrict__ rowoff,
+    const uint32_t* __restrict__ csr, const int* __restrict__ sidx,
+    const int* __restrict__ counts, int64_t n, int img0, int64_t* __restrict__ keep,
+    int64_t keep_bstride, int64_t* __restrict__ n_keep, int* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ uint32_t ents[kEntRing];
+  __shared__ uint64_t mdiag[kMetaRing][64];
+  __shared__ int msid[kMetaRing][64];
+  __shared__ int mready[kMetaRing], me0[kMetaRing], mne[kMetaRing], mend[kMetaRing];
+  __shared__ uint64_t mpre[kMetaRing];
+  __shared__ int s_done, s_done_e;
+  const int b = blockIdx.x;
+  if (dense[b]) return;  // workgroup-uniform: the dense-list scan owns this image
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cnt = counts[b];
+  const int nbv = (cnt + 63) >> 6;
+  uint64_t* kb = reinterpret_cast<uint64_t*>(smem);  // kept bits per block
+  const int64_t rb0 = (int64_t)b * n;
+  if (tid < kMetaRing) mready[tid] = -1;
+  if (tid == 0) {
+    s_done = 0;
+    s_done_e = 0;
+  }
+  __syncthreads();
+  if (cnt == 0) {
+    if (tid == 0) n_keep[b + img0] = 0;
+    return;
+  }
+  const int E0 = rowoff[rb0];  // CSR position of this image's first pair
+
+  if (wave > 0) {  // ------------------------------------------------ loaders
+#ifdef JABD_NMS_TRACE
+    uint64_t l_start = __builtin_readcyclecounter(), l_space = 0, l_load = 0;
+#endif
+    for (int c = wave - 1; c < nbv; c += kPullLoaders) {
+#ifdef JABD_NMS_TRACE
+      const uint64_t tl0 = __builtin_readcyclecounter();
+#endif
+      const int slot = c % kMetaRing;
+      const int last = min(64 * c + 64, cnt) - 1;
+      const int e0 = rowoff[rb0 + 64 * c];
+      const int e1 = rowoff[rb0 + last] + rowcnt[rb0 + last];
+      const int ne = e1 - e0;
+      const bool fits = ne <= kEntRing;
+      const int r = 64 * c + lane;
+      const int rr = r < cnt ? r : 0;
+      const uint64_t dg = r < cnt ? diag[rb0 + rr] : 0ull;
+      const int sd = sidx[rb0 + rr];
+      uint32_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int q = lane + 64 * k;
+        v[k] = (fits && q < ne) ? csr[e0 + q] : 0u;
+      }
+#ifdef JABD_NMS_TRACE
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint64_t tl1 = __builtin_readcyclecounter();
+      l_load += tl1 - tl0;
+#endif
+      unsigned spin = 0;
+      while (!(lds_acquire(&s_done) > c - kMetaRing &&
+               (!fits || lds_acquire(&s_done_e) >= e1 - E0 - kEntRing))) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spin > kSpinMax) {
+          if (lane == 0) atomicOr(err, 1);
+          return;
+        }
+      }
+#ifdef JABD_NMS_TRACE
+      l_space += __builtin_readcyclecounter() - tl1;
+#endif
+      // pairs whose source block is already final (< D) are resolved here
+      // against the kept bitset; only the rest (sources in the last few
+      // blocks) are compacted into the ring for the scan wave
+      const int D = lds_acquire(&s_done);
+      uint32_t plo = 0, phi = 0;
+      int nu = 0;  // wave-uniform
+      auto stage = [&](const uint32_t (&vv)[8], int q0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int q = q0 + lane + 64 * k;
+          const bool ok = q < ne;
+          const int sb = (int)(vv[k] >> 12);  // source block
+          const bool res = ok && sb < D;
+          const uint64_t w = kb[res ? sb : 0];
+          const bool hit = res && ((w >> ((vv[k] >> 6) & 63)) & 1);
+          const uint32_t bit = vv[k] & 63;
+          plo |= (hit && bit < 32) ? 1u << (bit & 31) : 0u;
+          phi |= (hit && bit >= 32) ? 1u << (bit & 31) : 0u;
+          const bool un = ok && !res;
+          const uint64_t um = __ballot(un);
+          if (un) {
+            const int pos = nu + __popcll(um & ((1ull << lane) - 1));
+            ents[(e0 - E0 + pos) & (kEntRing - 1)] = vv[k];
+          }
+          nu += __popcll(um);
+        }
+      };
+      if (fits) {
+        stage(v, 0);
+        for (int q0 = 512; q0 < ne; q0 += 512) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int q = q0 + lane + 64 * k;
+            v[k] = q < ne ? csr[e0 + q] : 0u;
+          }
+          stage(v, q0);
+        }
+      }
+      const uint32_t rlo = wave_or32(plo), rhi = wave_or32(phi);
+      mdiag[slot][lane] = dg;
+      msid[slot][lane] = sd;
+      if (lane == 0) {
+        me0[slot] = e0;
+        mne[slot] = fits ? nu : -ne - 1;
+        mpre[slot] = fits ? ((uint64_t)rhi << 32) | rlo : 0ull;
+        mend[slot] = e1 - E0;
+      }
+      if (lane == 0) lds_release(&mready[slot], c);
+    }
+#ifdef JABD_NMS_TRACE
+    if (lane == 0 && b == 0)
+      printf("loader %d img 0: %llu cycles, %llu loading, %llu waiting for space\n", wave,
+             (unsigned long long)(__builtin_readcyclecounter() - l_start),
+             (unsigned long long)l_load, (unsigned long long)l_space);
+#endif
+    return;
+  }
+
+  // -------------------------------------------------------------- scan wave
+  int64_t* kout = keep + (int64_t)(b + img0) * keep_bstride;
+  int nkeep = 0;
+#ifdef JABD_NMS_TRACE
+  uint64_t t_start = __builtin_readcyclecounter(), t_spin = 0, n_spin = 0;
+#endif
+  for (int c = 0; c < nbv; ++c) {
+    const int slot = c % kMetaRing;
+    unsigned spin = 0;
+#ifdef JABD_NMS_TRACE
+    const uint64_t ts = __builtin_readcyclecounter();
+    if (lds_acquire(&mready[slot]) != c) ++n_spin;
+#endif
+    while (lds_acquire(&mready[slot]) != c) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spin > kSpinMax) {
+        if (lane == 0) {
+          atomicOr(err, 2);
+          n_keep[b + img0] = nkeep;
+        }
+        return;
+      }
+    }
+#ifdef JABD_NMS_TRACE
+    t_spin += __builtin_readcyclecounter() - ts;
+#endif
+    const int e0 = me0[slot];
+    int ne = mne[slot];  // unresolved pairs left by the loader (or -total - 1: read from HBM)
+    const bool fits = ne >= 0;
+    if (!fits) ne = -ne - 1;
+    const uint64_t pre = mpre[slot];
+    const int e_end = mend[slot];
+    const uint64_t dg = mdiag[slot][lane];
+    const int sd = msid[slot][lane];
+    uint32_t mlo = 0, mhi = 0;
+    auto pass = [&](const uint32_t (&v)[8], int q0) {
+      uint64_t w[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) w[k] = kb[v[k] >> 12];  // src block = (v >> 6) >> 6
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const bool hit = q0 + lane + 64 * k < ne && ((w[k] >> ((v[k] >> 6) & 63)) & 1);
+        const uint32_t bit = v[k] & 63;
+        mlo |= (hit && bit < 32) ? 1u << (bit & 31) : 0u;
+        mhi |= (hit && bit >= 32) ? 1u << (bit & 31) : 0u;
+      }
+    };
+    if (fits) {
+      for (int q0 = 0; q0 < ne; q0 += 64) {  // usually one short pass
+        const int q = q0 + lane;
+        const uint32_t v = q < ne ? ents[(e0 - E0 + q) & (kEntRing - 1)] : 0u;
+        const uint64_t w = kb[v >> 12];
+        const bool hit = q < ne && ((w >> ((v >> 6) & 63)) & 1);
+        const uint32_t bit = v & 63;
+        mlo |= (hit && bit < 32) ? 1u << (bit & 31) : 0u;
+        mhi |= (hit && bit >= 32) ? 1u << (bit & 31) : 0u;
+      }
+    } else {
+      // a list larger than the ring: the loader left it whole; read it from HBM
+      // in its own branch (a global load pending where the paths join would
+      // make the compiler wait vmcnt(0) there, i.e. for this wave's stores)
+      for (int q0 = 0; q0 < ne; q0 += 512) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int q = q0 + lane + 64 * k;
+          v[k] = csr[e0 + (q < ne ? q : 0)];
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        pass(v, q0);
+      }
+    }
+    uint64_t rem = pre;
+    if (ne > 0) rem |= ((uint64_t)wave_or32(mhi) << 32) | wave_or32(mlo);
+    const int lim = cnt - 64 * c < 64 ? cnt - 64 * c : 64;
+    const uint64_t valid = lim == 64 ? ~0ull : ((1ull << lim) - 1);
+    uint64_t todo = __ballot(dg != 0) & valid;
+    const uint32_t dlo = (uint32_t)dg, dhi = (uint32_t)(dg >> 32);
+    while (todo) {  // rows with in-block suppressions, in rank order
+      const int t = __ffsll((unsigned long long)todo) - 1;
+      todo &= todo - 1;
+      if (!((rem >> t) & 1)) {
+        const uint32_t lo = __builtin_amdgcn_readlane(dlo, t);
+        const uint32_t hi = __builtin_amdgcn_readlane(dhi, t);
+        rem |= ((uint64_t)hi << 32) | lo;
+      }
+    }
+    const uint64_t kept = valid & ~rem;
+    if ((kept >> lane) & 1) kout[nkeep + __popcll(kept & ((1ull << lane) - 1))] = sd;
+    nkeep += __popcll(kept);
+    if (lane == 0) {
+      kb[c] = kept;
+      s_done_e = e_end;  // ordered before s_done by the release below
+      lds_release(&s_done, c + 1);
+    }
+  }
+  if (lane == 0) n_keep[b + img0] = nkeep;
+#ifdef JABD_NMS_TRACE
+  if (lane == 0)
+    printf("nms_scan_pull img %d: %d blocks, %llu cycles, %llu spinning, %llu blocks waited\n", b,
+           nbv, (unsigned long long)(__builtin_readcyclecounter() - t_start),
+           (unsigned long long)t_spin, (unsigned long long)n_spin);
+#endif
+}
+
+// Dense-list images (NaN boxes, thr < 0, or a grid overflow: dense[b] != 0):
+// one workgroup per image walks the row blocks in rank order.  Block c's
 // suppressed-set word comes from LDS; wave 0 resolves the block (only rows
 // with in-block suppressions need the ordered pass); then every kept row
-// ORs its sparse list into the LDS bitset.  The next block's row data is
-// prefetched into registers while the current one resolves.
+// ORs its (column block, bits) list into the LDS bitset.  The next block's
+// row data is prefetched into registers while the current one resolves.
 static constexpr int kPrefetchEnt = 4;  // list entries per row prefetched (256 threads / 64 rows)
 
 __global__ __launch_bounds__(256) void nms_scan(
     const uint64_t* __restrict__ diag, const int* __restrict__ nzcnt,
     const int* __restrict__ ent_cb, const uint64_t* __restrict__ ent_bits,
-    const int* __restrict__ dense, const int* __restrict__ rowcnt, const int* __restrict__ rowoff,
-    const int* __restrict__ csr,
-    const int* __restrict__ sidx, const int* __restrict__ counts, int64_t n, int64_t nb, int img0,
-    int64_t* __restrict__ keep, int64_t keep_bstride, int64_t* __restrict__ n_keep) {
+    const int* __restrict__ dense, const int* __restrict__ sidx, const int* __restrict__ counts,
+    int64_t n, int64_t nb, int img0, int64_t* __restrict__ keep, int64_t keep_bstride,
+    int64_t* __restrict__ n_keep) {
   extern __shared__ unsigned long long removed[];
   __shared__ uint64_t s_kept;
   __shared__ int s_nkeep;
   const int b = blockIdx.x;
+  if (!dense[b]) return;  // grid images: nms_scan_pull
   const int cnt = counts[b];
   const int64_t nbv = (cnt + 63) / 64;
   const int tid = threadIdx.x, lane = tid & 63, e = tid >> 6;
   for (int64_t w = tid; w < nbv; w += blockDim.x) removed[w] = 0;
   if (tid == 0) s_nkeep = 0;
   const uint64_t* dimg = diag + (int64_t)b * n;
-  const bool dn = dense[b] != 0;  // mask lists: dense (cb, bits) entries or grid CSR columns
-  const int* cimg = (dn ? nzcnt : rowcnt) + (int64_t)b * n;
-  const int* oimg = rowoff + (int64_t)b * n;
+  const int* cimg = nzcnt + (int64_t)b * n;
   const int64_t ebase = (int64_t)b * ent_base(nb, nb);
   const int* sid = sidx + (int64_t)b * n;
   int64_t* kout = keep + (int64_t)(b + img0) * keep_bstride;
@@ -544,15 +848,9 @@ __global__ __launch_bounds__(256) void nms_scan(
       pcnt = cimg[r];
       if (e == 0) pdiag = dimg[r];
       if (e < pcnt) {
-        if (dn) {
-          const int64_t off = ebase + ent_base(c, nb) + (int64_t)lane * (nb - c - 1) + e;
-          pcb = ent_cb[off];
-          pbits = ent_bits[off];
-        } else {
-          const int col = csr[oimg[r] + e];
-          pcb = col >> 6;
-          pbits = (uint64_t)1 << (col & 63);
-        }
+        const int64_t off = ebase + ent_base(c, nb) + (int64_t)lane * (nb - c - 1) + e;
+        pcb = ent_cb[off];
+        pbits = ent_bits[off];
       }
     }
   };
@@ -594,17 +892,9 @@ __global__ __launch_bounds__(256) void nms_scan(
     if ((kept >> lane) & 1) {
       if (e < pcnt) atomicOr(&removed[pcb], (unsigned long long)pbits);
       if (pcnt > kPrefetchEnt) {  // long lists: the row's 4 threads share the rest
-        if (dn) {
-          const int64_t off = ebase + ent_base(c, nb) + (int64_t)lane * (nb - c - 1);
-          for (int q = kPrefetchEnt + e; q < pcnt; q += kPrefetchEnt)
-            atomicOr(&removed[ent_cb[off + q]], (unsigned long long)ent_bits[off + q]);
-        } else {
-          const int* lst = csr + oimg[c * 64 + lane];
-          for (int q = kPrefetchEnt + e; q < pcnt; q += kPrefetchEnt) {
-            const int col = lst[q];
-            atomicOr(&removed[col >> 6], 1ull << (col & 63));
-          }
-        }
+        const int64_t off = ebase + ent_base(c, nb) + (int64_t)lane * (nb - c - 1);
+        for (int q = kPrefetchEnt + e; q < pcnt; q += kPrefetchEnt)
+          atomicOr(&removed[ent_cb[off + q]], (unsigned long long)ent_bits[off + q]);
       }
     }
     prefetch(c + 1, pdiag, pcnt, pcb, pbits);
@@ -634,7 +924,7 @@ struct NmsWs {
   size_t tmp_bytes;
   float4* sbox;
   float* sarea;
-  int *sidx, *counts, *nanflag;
+  int *sidx, *counts, *nanflag, *err;
   uint64_t* diag;
   int* nzcnt;
   int* ent_cb;
@@ -668,6 +958,7 @@ static void carve_nms(A& a, int64_t batch, int64_t n, NmsWs* w) {
   T(int, bc * n, sidx);
   T(int, bc, counts);
   T(int, bc, nanflag);
+  T(int, 1, err);
   T(uint64_t, bc * n, diag);
   T(int, bc * n, nzcnt);
   T(int, ents, ent_cb);
@@ -709,7 +1000,8 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
   JABD_REQUIRE(n < kMaxRows, "nms: n=%lld exceeds %lld rows per image", (long long)n,
                (long long)kMaxRows);
   const int64_t nb = cdiv(n, 64);
-  JABD_REQUIRE(nb * 8 <= 160 * 1024, "nms: n=%lld too large for the LDS scan", (long long)n);
+  JABD_REQUIRE(nb * 12 + 4 <= 160 * 1024, "nms: n=%lld too large for the LDS scan",
+               (long long)n);
   if (batch == 0) return JABD_OK;
   if (n == 0) {
     JABD_HIP(hipMemsetAsync(n_keep, 0, sizeof(int64_t) * batch, st));
@@ -720,7 +1012,9 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
   const int filter = score_thr > -INFINITY ? 1 : 0;
   const int64_t per_pass = images_per_pass(batch, n);
   // log-area class width W' >= 1.01 * -ln(thr) (wider is always safe)
-  const bool grid = iou_thr >= 0.0 && !nms_dense_only();
+  // the pull scan keeps one kept word per row block in LDS next to its rings
+  const bool grid = iou_thr >= 0.0 && !nms_dense_only() &&
+                    nb * 8 + kPullStaticLds <= 160 * 1024;
   double wcls = iou_thr > 0.0 ? 1.01 * -std::log(iou_thr) : INFINITY;
   if (wcls < 0.2) wcls = 0.2;  // wider classes are always safe; keeps ln-range / W' < kNC
   wcls /= kK;
@@ -739,6 +1033,7 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
     }
     JABD_HIP(hipMemsetAsync(w.counts, 0, sizeof(int) * bc, st));
     JABD_HIP(hipMemsetAsync(w.nanflag, 0, sizeof(int) * bc, st));
+    JABD_HIP(hipMemsetAsync(w.err, 0, sizeof(int), st));
     JABD_HIP(hipMemsetAsync(w.nzcnt, 0, sizeof(int) * bc * n, st));
     dim3 g1((unsigned)cdiv(n, 256), bc);
     nms_keys<<<g1, 256, 0, st>>>(scores, score_stride, score_bstride, n_valid, n, bc,
@@ -758,7 +1053,8 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
       JABD_HIP(hipMemsetAsync(w.ext, 0, sizeof(unsigned) * bc * 2 * kNC, st));
       JABD_HIP(hipMemsetAsync(w.diag, 0, sizeof(uint64_t) * bc * n, st));
       JABD_HIP(hipMemsetAsync(w.rowcnt, 0, sizeof(int) * bc * n, st));
-      grid_ext<<<g1, 256, 0, st>>>(w.sbox, w.sarea, w.counts, w.nanflag, n, inv_w, w.ext, w.dense);
+      dim3 ge((unsigned)cdiv(n, 256 * kExtPer), bc);
+      grid_ext<<<ge, 256, 0, st>>>(w.sbox, w.sarea, w.counts, w.nanflag, n, inv_w, w.ext, w.dense);
       if (int e = check_launch("grid_ext")) return e;
       grid_keys<<<g1, 256, 0, st>>>(w.sbox, w.sarea, w.counts, n, inv_w, fcell, w.ext, w.kin,
                                      w.gval_in, w.nact, w.dense);
@@ -790,10 +1086,22 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
       JABD_HIP(hipFuncSetAttribute((const void*)nms_scan,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     }
-    nms_scan<<<bc, 256, nb * sizeof(uint64_t), st>>>(
-        w.diag, w.nzcnt, w.ent_cb, w.ent_bits, w.dense, w.rowcnt, w.rowoff, w.csr, w.sidx,
-        w.counts, n, nb, (int)img0, keep, n, n_keep);
+    nms_scan<<<bc, 256, nb * sizeof(uint64_t), st>>>(w.diag, w.nzcnt, w.ent_cb, w.ent_bits,
+                                                      w.dense, w.sidx, w.counts, n, nb,
+                                                      (int)img0, keep, n, n_keep);
     if (int e = check_launch("nms_scan")) return e;
+    if (grid) {
+      const size_t lds = (size_t)nb * 8;
+      if (lds + kPullStaticLds > 64 * 1024) {
+        JABD_HIP(hipFuncSetAttribute((const void*)nms_scan_pull,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     160 * 1024 - kPullStaticLds));
+      }
+      nms_scan_pull<<<bc, 64 * (kPullLoaders + 1), lds, st>>>(
+          w.diag, w.dense, w.rowcnt, w.rowoff, reinterpret_cast<const uint32_t*>(w.csr), w.sidx,
+          w.counts, n, (int)img0, keep, n, n_keep, w.err);
+      if (int e = check_launch("nms_scan_pull")) return e;
+    }
   }
   return JABD_OK;
 }
@@ -843,7 +1151,10 @@ extern "C" int jabd_nms_pair_stats(const void* ws, size_t ws_bytes, int64_t batc
                           hipMemcpyDeviceToHost, st));
   JABD_HIP(hipMemcpyAsync(hits, w.npairs, sizeof(int32_t) * batch, hipMemcpyDeviceToHost, st));
   JABD_HIP(hipMemcpyAsync(dense, w.dense, sizeof(int32_t) * batch, hipMemcpyDeviceToHost, st));
+  int err = 0;
+  JABD_HIP(hipMemcpyAsync(&err, w.err, sizeof(int), hipMemcpyDeviceToHost, st));
   JABD_HIP(hipStreamSynchronize(st));
+  JABD_REQUIRE(err == 0, "nms: the pull scan's staging hand-off timed out (flags %d)", err);
   for (int64_t b = 0; b < batch; ++b) {
     unsigned long long t = 0;
     for (int l = 0; l < 64; ++l) t += slots[(size_t)b * 64 + l];

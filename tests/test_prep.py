@@ -160,3 +160,40 @@ def test_detect_image_c1_640(cuda):
     assert got.shape == ref_final.shape
     # decode's exp() may differ by an ulp between HIP and the CPU library
     np.testing.assert_allclose(got, ref_final, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_detect_c5_2048(cuda):
+    """C5 end to end (BASELINE configs[4]: 2048x2048, 172,032 anchors per
+    image): the eval forward at 2048^2 feeds jabd_detect_f32 (decode, the
+    >= 0.5 score filter, NMS 0.3 — utils/utils_bbox.py:29-46,260-296), whose
+    kept rows equal the host oracle's decode + non_max_suppression
+    (torchvision-CPU NMS, oracle/nms_ref.c) on the same forward output: same
+    count, same NMS order; decode's exp may differ by an ulp."""
+    from _util import init_for_parity
+    from jabd_amd import ops, synth
+    from nets.retinaface_r import RetinaFace
+    from oracle import box_ref
+    from utils.anchors import Anchors
+    from utils.config import cfg_mnet
+    net = init_for_parity(RetinaFace(cfg=cfg_mnet, mode="eval"), seed=5).eval().to(cuda)
+    x = synth.images(1, 2048, seed=99, device=cuda)
+    pri_dev = Anchors(cfg_mnet, image_size=(2048, 2048)).get_anchors().to(cuda).float()
+    assert pri_dev.shape[0] == 172032
+    with torch.no_grad():
+        loc, conf, landm = net(x)
+        rows, nk = ops.detect(loc, conf, landm, pri_dev, cfg_mnet["variance"], 0.5, 0.3)
+    k = int(nk[0])
+    pri = box_ref.anchors(cfg_mnet, (2048, 2048))
+    var = cfg_mnet["variance"]
+    lo, cf, lm = (t[0].cpu() for t in (loc, conf, landm))
+    cand = int((cf[:, 1] >= 0.5).sum())
+    det = torch.cat([box_ref.decode(lo, pri, var), cf[:, 1:2], box_ref.decode_landm(lm, pri, var)],
+                    -1)
+    ref = np.asarray(box_ref.non_max_suppression(det, 0.5, 0.3), np.float32)
+    print(f"C5 2048^2: {cand} candidates >= 0.5, {k} kept")
+    assert cand > 10000, "the input must exercise NMS at scale"
+    assert k == ref.shape[0]
+    got = rows[0, :k].cpu().numpy()
+    np.testing.assert_array_equal(got[:, 4], ref[:, 4])        # scores: the same rows, in order
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-4)
