@@ -66,26 +66,33 @@ __device__ __forceinline__ uint32_t score_key_desc(float s) {
   return ~u;                                                 // descending
 }
 
-__global__ void nms_keys(const float* __restrict__ scores, int64_t score_stride,
-                         int64_t score_bstride, const int64_t* __restrict__ n_valid,
-                         int64_t n, int batch, float thr, int filter, int img0,
-                         uint64_t* __restrict__ keys, int* __restrict__ counts) {
-  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  int b = blockIdx.y;
-  if (i >= n || b >= batch) return;
-  float s = scores[(int64_t)(b + img0) * score_bstride + i * score_stride];
-  int64_t nv = n_valid ? n_valid[b + img0] : n;
-  bool valid = i < nv;
-  if (filter) valid = valid && (s >= thr);
-  uint64_t img = valid ? (uint64_t)b : 255u;
-  keys[(int64_t)b * n + i] = (img << 56) | ((uint64_t)score_key_desc(s) << kRowBits) | (uint64_t)i;
-  if (valid) {
-    // one atomic per wave: count valid lanes with a ballot
-    uint64_t m = __ballot(1);
-    int lane = threadIdx.x & 63;
-    int leader = __ffsll((unsigned long long)m) - 1;
-    if (lane == leader) atomicAdd(&counts[b], __popcll(m));
+__global__ __launch_bounds__(256) void nms_keys(const float* __restrict__ scores,
+                                                int64_t score_stride, int64_t score_bstride,
+                                                const int64_t* __restrict__ n_valid, int64_t n,
+                                                int batch, float thr, int filter, int img0,
+                                                uint64_t* __restrict__ keys,
+                                                int* __restrict__ counts) {
+  __shared__ int wg_count;
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (threadIdx.x == 0) wg_count = 0;
+  __syncthreads();
+  bool valid = false;
+  if (i < n && b < batch) {
+    const float s = scores[(int64_t)(b + img0) * score_bstride + i * score_stride];
+    const int64_t nv = n_valid ? n_valid[b + img0] : n;
+    valid = i < nv;
+    if (filter) valid = valid && (s >= thr);
+    const uint64_t img = valid ? (uint64_t)b : 255u;
+    keys[(int64_t)b * n + i] =
+        (img << 56) | ((uint64_t)score_key_desc(s) << kRowBits) | (uint64_t)i;
   }
+  // one LDS atomic per wave, one global atomic per workgroup (all the
+  // workgroups of an image add into one counter)
+  const uint64_t m = __ballot(valid);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(&wg_count, __popcll(m));
+  __syncthreads();
+  if (threadIdx.x == 0 && wg_count) atomicAdd(&counts[b], wg_count);
 }
 
 __global__ void nms_gather(const uint64_t* __restrict__ sorted, int64_t total,
@@ -153,21 +160,35 @@ __device__ __forceinline__ bool iou_gt(float ix1, float iy1, float ix2, float iy
   return (double)ovr > thr;
 }
 
+// Dense-image tiles (64 rows x kColBlocksPerWG column blocks) as a grid-
+// stride loop over a fixed grid: with no dense image in the batch (the
+// common case) every workgroup leaves after one look at dense[].
 __global__ __launch_bounds__(256) void nms_mask(
     const float4* __restrict__ sbox, const float* __restrict__ sarea,
-    const int* __restrict__ counts, int64_t n, int64_t nb, double thr,
+    const int* __restrict__ counts, int64_t n, int64_t nb, int bc, double thr,
     const int* __restrict__ nanflag, const int* __restrict__ dense, uint64_t* __restrict__ diag,
     int* __restrict__ nzcnt, int* __restrict__ ent_cb, uint64_t* __restrict__ ent_bits) {
-  const int b = blockIdx.z;
-  if (!dense[b]) return;  // this image's mask came from the grid path
-  const int64_t rb = blockIdx.y;
-  const int64_t cbg = (int64_t)blockIdx.x * kColBlocksPerWG;
-  const int cnt = counts[b];
-  const int64_t nbv = (cnt + 63) / 64;
-  if (rb >= nbv || cbg + kColBlocksPerWG <= rb || cbg >= nbv) return;
-
+  __shared__ int any_dense;
+  if (threadIdx.x == 0) {
+    int a = 0;
+    for (int q = 0; q < bc; ++q) a |= dense[q];
+    any_dense = a;
+  }
+  __syncthreads();
+  if (!any_dense) return;
   __shared__ float4 cbox[kColBlocksPerWG * 64];
   __shared__ float carea[kColBlocksPerWG * 64];
+  const int64_t ncbg = (nb + kColBlocksPerWG - 1) / kColBlocksPerWG;
+  const int64_t ntiles = ncbg * nb * bc;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  const int b = (int)(tile / (ncbg * nb));
+  const int64_t rb = (tile / ncbg) % nb;
+  const int64_t cbg = (tile % ncbg) * kColBlocksPerWG;
+  if (!dense[b]) continue;  // this image's mask came from the grid path
+  const int cnt = counts[b];
+  const int64_t nbv = (cnt + 63) / 64;
+  if (rb >= nbv || cbg + kColBlocksPerWG <= rb || cbg >= nbv) continue;
+
   const float4* ib = sbox + (int64_t)b * n;
   const float* ia = sarea + (int64_t)b * n;
   for (int t = threadIdx.x; t < kColBlocksPerWG * 64; t += blockDim.x) {
@@ -249,6 +270,8 @@ __global__ __launch_bounds__(256) void nms_mask(
       }
     }
   }
+  __syncthreads();  // cbox is refilled by the next tile
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -303,9 +326,11 @@ __device__ __forceinline__ uint64_t grid_key(int b, int cw, int ch, int y, int x
 }
 
 // ext[b][0][cw] = largest width of width class cw, ext[b][1][ch] = largest
-// height.  The classes one image occupies are few (tens), so per-box global
-// atomics would serialise on a handful of L2 addresses: each workgroup takes
-// kExtPer boxes per thread into LDS maxima first and flushes the classes it
+// height; ext[b][2] / ext[b][3] = the smallest width / height, stored
+// complemented (~bits) so one atomicMax over a zeroed array serves both.
+// The classes one image occupies are few (tens), so per-box global atomics
+// would serialise on a handful of L2 addresses: each workgroup takes kExtPer
+// boxes per thread into LDS extremes first and flushes the classes it
 // touched with one global atomic each.
 static constexpr int kExtPer = 16;
 __global__ __launch_bounds__(256) void grid_ext(const float4* __restrict__ sbox,
@@ -314,10 +339,10 @@ __global__ __launch_bounds__(256) void grid_ext(const float4* __restrict__ sbox,
                                                 const int* __restrict__ nanflag, int64_t n,
                                                 float inv_w, unsigned* __restrict__ ext,
                                                 int* __restrict__ dense) {
-  __shared__ unsigned le[2 * kNC];
+  __shared__ unsigned le[4 * kNC];
   const int t = threadIdx.x;
   const int b = blockIdx.y;
-  for (int i = t; i < 2 * kNC; i += 256) le[i] = 0u;
+  for (int i = t; i < 4 * kNC; i += 256) le[i] = 0u;
   if (blockIdx.x == 0 && t == 0 && nanflag[b]) atomicOr(&dense[b], 1);
   __syncthreads();
   const int cnt = counts[b];
@@ -329,18 +354,21 @@ __global__ __launch_bounds__(256) void grid_ext(const float4* __restrict__ sbox,
     const float a = sarea[(int64_t)b * n + r];
     if (!grid_active(bx, a)) continue;
     const float w = bx.z - bx.x, h = bx.w - bx.y;
-    atomicMax(&le[grid_class(w, inv_w)], __float_as_uint(w));
-    atomicMax(&le[kNC + grid_class(h, inv_w)], __float_as_uint(h));
+    const int cw = grid_class(w, inv_w), ch = grid_class(h, inv_w);
+    atomicMax(&le[cw], __float_as_uint(w));
+    atomicMax(&le[kNC + ch], __float_as_uint(h));
+    atomicMax(&le[2 * kNC + cw], ~__float_as_uint(w));
+    atomicMax(&le[3 * kNC + ch], ~__float_as_uint(h));
   }
   __syncthreads();
-  for (int i = t; i < 2 * kNC; i += 256)
-    if (le[i]) atomicMax(&ext[(int64_t)b * 2 * kNC + i], le[i]);
+  for (int i = t; i < 4 * kNC; i += 256)
+    if (le[i]) atomicMax(&ext[(int64_t)b * 4 * kNC + i], le[i]);
 }
 
 __global__ void grid_keys(const float4* __restrict__ sbox, const float* __restrict__ sarea,
                           const int* __restrict__ counts, int64_t n, float inv_w, float fcell,
                           const unsigned* __restrict__ ext, uint64_t* __restrict__ key,
-                          int* __restrict__ val, int* __restrict__ nact, int* __restrict__ dense) {
+                          int* __restrict__ val, int* __restrict__ dense) {
   const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int b = blockIdx.y;
   if (r >= n) return;
@@ -351,12 +379,11 @@ __global__ void grid_keys(const float4* __restrict__ sbox, const float* __restri
     const float a = sarea[o];
     if (grid_active(bx, a)) {
       const int cw = grid_class(bx.z - bx.x, inv_w), ch = grid_class(bx.w - bx.y, inv_w);
-      const unsigned* e = ext + (int64_t)b * 2 * kNC;
+      const unsigned* e = ext + (int64_t)b * 4 * kNC;
       const float sx = grid_cell_size(e, cw, fcell), sy = grid_cell_size(e + kNC, ch, fcell);
       const float fx = floorf((bx.x + bx.z) * 0.5f / sx), fy = floorf((bx.y + bx.w) * 0.5f / sy);
       if (fabsf(fx) < (float)kCellLim && fabsf(fy) < (float)kCellLim) {
         k = grid_key(b, cw, ch, (int)fy, (int)fx);
-        atomicAdd(&nact[b], 1);
       } else {
         atomicOr(&dense[b], 2);
       }
@@ -380,20 +407,73 @@ __global__ void grid_gather(const uint64_t* __restrict__ skey, const int* __rest
   garea[q] = sarea[o];
 }
 
-__device__ __forceinline__ int64_t lower_bound_u64(const uint64_t* a, int64_t lo, int64_t hi,
-                                                   uint64_t v) {
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (a[mid] < v) lo = mid + 1;
-    else hi = mid;
+// Cell runs: after the sort, the boxes of one (image, classes, cell) key are
+// a contiguous run [lo, hi) of the key order.  An open-addressing table maps
+// each run's key to its bounds, so a box finds a neighbour cell with one or
+// two 16-byte loads instead of a binary search over the image's keys.
+struct CellRun {
+  unsigned long long key;  // ~0: empty slot
+  int lo, hi;
+};
+static constexpr unsigned long long kEmptyKey = ~0ull;
+
+__device__ __forceinline__ uint32_t run_hash(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return (uint32_t)k;
+}
+
+__global__ void grid_runs_insert(const uint64_t* __restrict__ skey, int64_t total,
+                                 CellRun* __restrict__ tab, uint32_t mask) {
+  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (p >= total) return;
+  const uint64_t k = skey[p];
+  if (k == kEmptyKey || (p > 0 && skey[p - 1] == k)) return;  // not a run start
+  uint32_t h = run_hash(k) & mask;
+  for (;;) {
+    const unsigned long long prev = atomicCAS(&tab[h].key, kEmptyKey, (unsigned long long)k);
+    if (prev == kEmptyKey || prev == k) {
+      tab[h].lo = (int)p;
+      return;
+    }
+    h = (h + 1) & mask;
   }
-  return lo;
+}
+
+__device__ __forceinline__ int run_find(const CellRun* __restrict__ tab, uint32_t mask, uint64_t k,
+                                        int& lo) {
+  uint32_t h = run_hash(k) & mask;
+  for (;;) {
+    const uint4 e = *reinterpret_cast<const uint4*>(&tab[h]);
+    const uint64_t kk = ((uint64_t)e.y << 32) | e.x;
+    if (kk == k) {
+      lo = (int)e.z;
+      return (int)e.w;
+    }
+    if (kk == kEmptyKey) return -1;
+    h = (h + 1) & mask;
+  }
+}
+
+__global__ void grid_runs_end(const uint64_t* __restrict__ skey, int64_t total,
+                              CellRun* __restrict__ tab, uint32_t mask) {
+  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (p >= total) return;
+  const uint64_t k = skey[p];
+  if (k == kEmptyKey || (p + 1 < total && skey[p + 1] == k)) return;  // not a run end
+  uint32_t h = run_hash(k) & mask;
+  while (tab[h].key != k) h = (h + 1) & mask;
+  tab[h].hi = (int)(p + 1);
 }
 
 __global__ __launch_bounds__(256) void grid_pairs(
     const uint64_t* __restrict__ skey, const int* __restrict__ sval, int64_t total,
     const float4* __restrict__ gbox, const float* __restrict__ garea, int64_t n, int bc,
-    float inv_w, float fcell, const unsigned* __restrict__ ext, const int* __restrict__ nact,
+    float inv_w, float fcell, const unsigned* __restrict__ ext,
+    const CellRun* __restrict__ tab, uint32_t tmask,
     double thr, int64_t cap, int* __restrict__ dense, uint64_t* __restrict__ diag,
     int* __restrict__ npairs, int* __restrict__ rowcnt, int* __restrict__ prow,
     int* __restrict__ pcol, int* __restrict__ pslot, unsigned long long* __restrict__ tested) {
@@ -404,15 +484,19 @@ __global__ __launch_bounds__(256) void grid_pairs(
   if (k == ~0ull) return;
   const int b = (int)(k >> 56);
   if (dense[b] & 3) return;
-  int64_t seg0 = 0;
-  for (int q = 0; q < b; ++q) seg0 += nact[q];
-  const int64_t seg1 = seg0 + nact[b];
   const int i = sval[p];
   const float4 bi = gbox[p];
   const float ai = garea[p];
   const int cw = (int)((k >> 46) & (kNC - 1)), ch = (int)((k >> 36) & (kNC - 1));
-  const unsigned* ew = ext + (int64_t)b * 2 * kNC;
+  const unsigned* ew = ext + (int64_t)b * 4 * kNC;
   const unsigned* eh = ew + kNC;
+  const unsigned* ewn = ew + 2 * kNC;  // complemented minima
+  const unsigned* ehn = ew + 3 * kNC;
+  const float wi = bi.z - bi.x, hi_ = bi.w - bi.y;
+  // IoU <= min(w_i, w_j) / max(w_i, w_j) (heights alike): a class whose
+  // extents cannot reach a ratio above thr holds no partner (1% margin)
+  const bool ratio = thr > 0.0;
+  const float rlo = (float)thr * 0.99f, rhi = ratio ? 1.01f / (float)thr : 0.f;
   const float cx = (bi.x + bi.z) * 0.5f, cy = (bi.y + bi.w) * 0.5f;
   const float thrf = (float)thr;
   const uint64_t lt = (1ull << lane) - 1;
@@ -475,35 +559,59 @@ __global__ __launch_bounds__(256) void grid_pairs(
       ch2 = ch - kK + q2 % (2 * kK + 1);
     }
     if (cw2 >= kNC || ch2 < 0 || ch2 >= kNC || ew[cw2] == 0u || eh[ch2] == 0u) continue;
+    const float wmax2 = __uint_as_float(ew[cw2]), hmax2 = __uint_as_float(eh[ch2]);
+    if (ratio && (wmax2 < wi * rlo || __uint_as_float(~ewn[cw2]) > wi * rhi ||
+                  hmax2 < hi_ * rlo || __uint_as_float(~ehn[ch2]) > hi_ * rhi))
+      continue;
+    // a partner j of this class has |dcx| < f (w_i + w_j) / 2 <= f (w_i + wmax2) / 2
+    // (fcell = 1.05 f: rounding margin), and its cell is floor(cx_j / sx)
+    // with the cell size sx its own key was built with (<= 3 cells per axis)
     const float sx = grid_cell_size(ew, cw2, fcell), sy = grid_cell_size(eh, ch2, fcell);
-    const float fx = floorf(cx / sx), fy = floorf(cy / sy);
-    if (fabsf(fx) > (float)(kCellLim + 1) || fabsf(fy) > (float)(kCellLim + 1)) continue;
-    const int X = (int)fx, Y = (int)fy;
-    for (int dy = -1; dy <= 1; ++dy) {
-      const uint64_t lo = grid_key(b, cw2, ch2, Y + dy, X - 1);
-      const uint64_t hi = grid_key(b, cw2, ch2, Y + dy, X + 1);
-      for (int64_t q = lower_bound_u64(skey, seg0, seg1, lo); q < seg1 && skey[q] <= hi; ++q) {
-        const int j = sval[q];
-        // same class: each pair once, from the lower rank
-        bool hit = !(nbr == 0 && j <= i);
-        ntest += hit;
-        if (hit) hit = iou_gt(bi.x, bi.y, bi.z, bi.w, ai, gbox[q], garea[q], thr, thrf, true);
-        if (hit) {
-          const int row = i < j ? i : j, col = i < j ? j : i;
-          if ((row >> 6) == (col >> 6)) {
-            atomicOr((unsigned long long*)&diag[(int64_t)b * n + row],
-                     (unsigned long long)1 << (col & 63));
-          } else {
+    const float rx = 0.5f * fcell * (wi + wmax2), ry = 0.5f * fcell * (hi_ + hmax2);
+    const float lim = (float)(kCellLim + 1);
+    const int X0 = (int)fmaxf(floorf((cx - rx) / sx), -lim), X1 = (int)fminf(floorf((cx + rx) / sx), lim);
+    const int Y0 = (int)fmaxf(floorf((cy - ry) / sy), -lim), Y1 = (int)fminf(floorf((cy + ry) / sy), lim);
+    for (int Y = Y0; Y <= Y1; ++Y) {
+      for (int X = X0; X <= X1; ++X) {
+        int q = 0;
+        const int qe = run_find(tab, tmask, grid_key(b, cw2, ch2, Y, X), q);
+        // candidates four at a time: their loads are in flight together
+        for (; q < qe; q += 4) {
+          if (__ballot(np > kBuf - 4)) flush();
+          int jj[4];
+          float4 bb[4];
+          float aa[4];
 #pragma unroll
-            for (int t2 = 0; t2 < kBuf; ++t2)
-              if (t2 == np) {
-                pr[t2] = row;
-                pc[t2] = col;
+          for (int u = 0; u < 4; ++u) {
+            const int qq = q + u < qe ? q + u : q;
+            jj[u] = sval[qq];
+            bb[u] = gbox[qq];
+            aa[u] = garea[qq];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int j = jj[u];
+            // same class: each pair once, from the lower rank
+            bool hit = q + u < qe && !(nbr == 0 && j <= i);
+            ntest += hit;
+            if (hit) hit = iou_gt(bi.x, bi.y, bi.z, bi.w, ai, bb[u], aa[u], thr, thrf, true);
+            if (hit) {
+              const int row = i < j ? i : j, col = i < j ? j : i;
+              if ((row >> 6) == (col >> 6)) {
+                atomicOr((unsigned long long*)&diag[(int64_t)b * n + row],
+                         (unsigned long long)1 << (col & 63));
+              } else {
+#pragma unroll
+                for (int t2 = 0; t2 < kBuf; ++t2)
+                  if (t2 == np) {
+                    pr[t2] = row;
+                    pc[t2] = col;
+                  }
+                ++np;
               }
-            ++np;
+            }
           }
         }
-        if (__ballot(np == kBuf)) flush();
       }
     }
   }
@@ -521,12 +629,15 @@ __global__ void grid_scatter(const int* __restrict__ npairs, const int* __restri
                              int64_t cap, int64_t n, const int* __restrict__ prow,
                              const int* __restrict__ pcol, const int* __restrict__ pslot,
                              const int* __restrict__ rowoff, int* __restrict__ csr) {
-  const int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int b = blockIdx.y;
-  if (dense[b] || s >= cap || s >= npairs[b]) return;
-  const int64_t o = (int64_t)b * cap + s;
-  const int col = pcol[o];
-  csr[rowoff[(int64_t)b * n + col] + pslot[o]] = (prow[o] << 6) | (col & 63);
+  if (dense[b]) return;
+  const int64_t np = min((int64_t)npairs[b], cap);
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < np;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t o = (int64_t)b * cap + s;
+    const int col = pcol[o];
+    csr[rowoff[(int64_t)b * n + col] + pslot[o]] = (prow[o] << 6) | (col & 63);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -931,8 +1042,10 @@ struct NmsWs {
   uint64_t* ent_bits;
   // grid path
   unsigned* ext;
-  int *dense, *nact, *npairs, *gval_in, *gval_out, *rowcnt, *rowoff, *prow, *pcol, *pslot, *csr;
+  int *dense, *npairs, *gval_in, *gval_out, *rowcnt, *rowoff, *prow, *pcol, *pslot, *csr;
   unsigned long long* tested;  // grid candidates IoU-tested per image (measurement)
+  CellRun* runs;               // cell-run hash table (power-of-two slots)
+  uint32_t run_mask;
   float4* gbox;
   float* garea;
   int64_t cap;
@@ -963,9 +1076,8 @@ static void carve_nms(A& a, int64_t batch, int64_t n, NmsWs* w) {
   T(int, bc * n, nzcnt);
   T(int, ents, ent_cb);
   T(uint64_t, ents, ent_bits);
-  T(unsigned, bc * 2 * kNC, ext);
+  T(unsigned, bc * 4 * kNC, ext);
   T(int, bc, dense);
-  T(int, bc, nact);
   T(int, bc, npairs);
   T(unsigned long long, bc * 64, tested);
   T(int, bc * n, gval_in);
@@ -978,7 +1090,11 @@ static void carve_nms(A& a, int64_t batch, int64_t n, NmsWs* w) {
   T(int, bc * cap, csr);
   T(float4, bc * n, gbox);
   T(float, bc * n, garea);
+  int64_t slots = 1024;
+  while (slots < 2 * bc * n) slots <<= 1;  // load factor <= 1/2
+  T(CellRun, slots, runs);
 #undef T
+  if (w) w->run_mask = (uint32_t)(slots - 1);
   if (w) {
     w->tmp_bytes = tb;
     w->cap = cap;
@@ -1047,39 +1163,43 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
     if (int e = check_launch("nms_gather")) return e;
     if (grid) {
       JABD_HIP(hipMemsetAsync(w.dense, 0, sizeof(int) * bc, st));
-      JABD_HIP(hipMemsetAsync(w.nact, 0, sizeof(int) * bc, st));
       JABD_HIP(hipMemsetAsync(w.npairs, 0, sizeof(int) * bc, st));
       JABD_HIP(hipMemsetAsync(w.tested, 0, sizeof(unsigned long long) * bc * 64, st));
-      JABD_HIP(hipMemsetAsync(w.ext, 0, sizeof(unsigned) * bc * 2 * kNC, st));
+      JABD_HIP(hipMemsetAsync(w.ext, 0, sizeof(unsigned) * bc * 4 * kNC, st));
+      JABD_HIP(hipMemsetAsync(w.runs, 0xFF, sizeof(CellRun) * ((size_t)w.run_mask + 1), st));
       JABD_HIP(hipMemsetAsync(w.diag, 0, sizeof(uint64_t) * bc * n, st));
       JABD_HIP(hipMemsetAsync(w.rowcnt, 0, sizeof(int) * bc * n, st));
       dim3 ge((unsigned)cdiv(n, 256 * kExtPer), bc);
       grid_ext<<<ge, 256, 0, st>>>(w.sbox, w.sarea, w.counts, w.nanflag, n, inv_w, w.ext, w.dense);
       if (int e = check_launch("grid_ext")) return e;
       grid_keys<<<g1, 256, 0, st>>>(w.sbox, w.sarea, w.counts, n, inv_w, fcell, w.ext, w.kin,
-                                     w.gval_in, w.nact, w.dense);
+                                     w.gval_in, w.dense);
       if (int e = check_launch("grid_keys")) return e;
       JABD_HIP(hipcub::DeviceRadixSort::SortPairs(w.tmp, w.tmp_bytes, w.kin, w.kout, w.gval_in,
                                                   w.gval_out, (int)(bc * n), 0, 64, st));
       grid_gather<<<(unsigned)cdiv((int64_t)bc * n, 256), 256, 0, st>>>(
           w.kout, w.gval_out, (int64_t)bc * n, w.sbox, w.sarea, n, w.gbox, w.garea);
       if (int e = check_launch("grid_gather")) return e;
-      grid_pairs<<<(unsigned)cdiv((int64_t)bc * n, 256), 256, 0, st>>>(
-          w.kout, w.gval_out, (int64_t)bc * n, w.gbox, w.garea, n, bc, inv_w, fcell, w.ext, w.nact,
-          iou_thr, w.cap, w.dense, w.diag, w.npairs, w.rowcnt, w.prow, w.pcol, w.pslot,
-          w.tested);
+      const unsigned gt = (unsigned)cdiv((int64_t)bc * n, 256);
+      grid_runs_insert<<<gt, 256, 0, st>>>(w.kout, (int64_t)bc * n, w.runs, w.run_mask);
+      if (int e = check_launch("grid_runs_insert")) return e;
+      grid_runs_end<<<gt, 256, 0, st>>>(w.kout, (int64_t)bc * n, w.runs, w.run_mask);
+      if (int e = check_launch("grid_runs_end")) return e;
+      grid_pairs<<<gt, 256, 0, st>>>(
+          w.kout, w.gval_out, (int64_t)bc * n, w.gbox, w.garea, n, bc, inv_w, fcell, w.ext,
+          w.runs, w.run_mask, iou_thr, w.cap, w.dense, w.diag, w.npairs, w.rowcnt, w.prow, w.pcol,
+          w.pslot, w.tested);
       if (int e = check_launch("grid_pairs")) return e;
       JABD_HIP(hipcub::DeviceScan::ExclusiveSum(w.tmp, w.tmp_bytes, w.rowcnt, w.rowoff,
                                                 (int)(bc * n), st));
-      dim3 gs((unsigned)cdiv(w.cap, 256), bc);
+      dim3 gs((unsigned)std::min<int64_t>(cdiv(w.cap, 256), 512), bc);
       grid_scatter<<<gs, 256, 0, st>>>(w.npairs, w.dense, w.cap, n, w.prow, w.pcol, w.pslot,
                                        w.rowoff, w.csr);
       if (int e = check_launch("grid_scatter")) return e;
     } else {
       JABD_HIP(hipMemsetD32Async((hipDeviceptr_t)w.dense, 1, bc, st));
     }
-    dim3 g2((unsigned)cdiv(nb, kColBlocksPerWG), (unsigned)nb, (unsigned)bc);
-    nms_mask<<<g2, 256, 0, st>>>(w.sbox, w.sarea, w.counts, n, nb, iou_thr, w.nanflag, w.dense,
+    nms_mask<<<2048, 256, 0, st>>>(w.sbox, w.sarea, w.counts, n, nb, bc, iou_thr, w.nanflag, w.dense,
                                  w.diag, w.nzcnt, w.ent_cb, w.ent_bits);
     if (int e = check_launch("nms_mask")) return e;
     if (nb * sizeof(uint64_t) > 64 * 1024) {
