@@ -300,6 +300,7 @@ static constexpr int kCellOff = 1 << 17;  // 18-bit biased cell coordinates
 static constexpr int kCellLim = 1 << 14;
 static constexpr int64_t kPairsPerBox = 128;  // off-block pair capacity per box
 static constexpr int kK = 2;                  // class sub-division (neighbour range)
+static constexpr int kGridNbr = 1 + kK + kK * (2 * kK + 1);  // class pairs searched per box
 
 __device__ __forceinline__ bool grid_active(float4 bx, float a) {
   return bx.z > bx.x && bx.w > bx.y && a < INFINITY;
@@ -477,7 +478,13 @@ __global__ __launch_bounds__(256) void grid_pairs(
     double thr, int64_t cap, int* __restrict__ dense, uint64_t* __restrict__ diag,
     int* __restrict__ npairs, int* __restrict__ rowcnt, int* __restrict__ prow,
     int* __restrict__ pcol, int* __restrict__ pslot, unsigned long long* __restrict__ tested) {
-  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  // XCD-aware block order: hardware block id g runs on XCD g % 8; give each
+  // XCD one contiguous eighth of the key order (= one image when the batch
+  // holds 8), so an image's candidate arrays stay in one XCD's L2
+  // (host: gridDim.x is a multiple of 8, so the map is a permutation)
+  const int64_t g = blockIdx.x, per = gridDim.x / 8;
+  const int64_t lb = (g % 8) * per + g / 8;
+  const int64_t p = lb * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
   if (p >= total) return;
   const uint64_t k = skey[p];
@@ -546,9 +553,8 @@ __global__ __launch_bounds__(256) void grid_pairs(
 
   // own class, then the forward half of the neighbour classes:
   // (0, 1..kK) and (1..kK, -kK..kK)
-  constexpr int NNB = kK + kK * (2 * kK + 1);
   unsigned ntest = 0;
-  for (int nbr = 0; nbr <= NNB; ++nbr) {
+  for (int nbr = 0; nbr < kGridNbr; ++nbr) {
     int cw2, ch2;
     if (nbr <= kK) {
       cw2 = cw;
@@ -1185,7 +1191,7 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
       if (int e = check_launch("grid_runs_insert")) return e;
       grid_runs_end<<<gt, 256, 0, st>>>(w.kout, (int64_t)bc * n, w.runs, w.run_mask);
       if (int e = check_launch("grid_runs_end")) return e;
-      grid_pairs<<<gt, 256, 0, st>>>(
+      grid_pairs<<<(gt + 7) / 8 * 8, 256, 0, st>>>(
           w.kout, w.gval_out, (int64_t)bc * n, w.gbox, w.garea, n, bc, inv_w, fcell, w.ext,
           w.runs, w.run_mask, iou_thr, w.cap, w.dense, w.diag, w.npairs, w.rowcnt, w.prow, w.pcol,
           w.pslot, w.tested);
