@@ -202,6 +202,17 @@ int jabd_nlm_attn_bwd_f32(const float* q, const float* kp, const float* vp, cons
                           const float* lse, const float* dctx, int32_t B, int32_t P, int32_t S,
                           int32_t ch, float* dq, float* pmat, float* dsmat,
                           jabd_stream_t stream);
+/* dK = dsmat . q and dV = pmat . dctx ([B, S, P] x [B, P, ch] -> [B, S, ch],
+ * replacing the reference autograd's two batched matmul gradients of
+ * train_mobilenetV3_ecagai.py:220,226) on the fp32 MFMA: P is cut into chunks
+ * of 2048 pixels whose partial products land in ws (ws_floats >=
+ * jabd_nlm_attn_dkv_ws_floats(B, P, S, ch)) and are then summed in chunk
+ * order, so the result is deterministic.  ch <= 64. */
+int64_t jabd_nlm_attn_dkv_ws_floats(int32_t B, int32_t P, int32_t S, int32_t ch);
+int jabd_nlm_attn_dkv_f32(const float* dsmat, const float* pmat, const float* q,
+                          const float* dctx, int32_t B, int32_t P, int32_t S, int32_t ch,
+                          float* ws, int64_t ws_floats, float* dk, float* dv,
+                          jabd_stream_t stream);
 /* y = a + b (+ c if non-NULL), n floats (n % 4 == 0, 16-byte aligned): the
  * NLM residual + FPN lateral add of the bicubic variant
  * (train_mobilenetV3_ecagai.py:233, 271). */
@@ -331,7 +342,15 @@ typedef struct jabd_conv_args {
    * convolutions of one input fused along N, e.g. the SSH branches that read
    * the same tensor).  nsplit % 4 == 0; served by the generic kernel. */
   float* y2; int64_t y2_bs; int32_t y2_ps, y2_c0, nsplit, act2; float slope2; int32_t reserved2;
+  /* optional workspace (nullable): with ws_bytes >= jabd_conv_workspace_size(args)
+   * the library may split the K reduction of a k x k conv whose output grid
+   * is too small to fill the device (bs1 inference of the R50 detector:
+   * predict.py:253-333) over several workgroups — partial sums in ws, then a
+   * fixed-order reduction (deterministic).  NULL: no split. */
+  void* ws; int64_t ws_bytes;
 } jabd_conv_args;
+/* Workspace bytes jabd_conv2d_nhwc_f32 can use for args (0: it would not split). */
+int64_t jabd_conv_workspace_size(const jabd_conv_args* args);
 /* N-tiles (16 output channels each) grouped per workgroup for a Cout. */
 int jabd_conv_pack_tn(int cout);
 /* 32-channel N-tiles per workgroup of the 32x32x2 1x1 kernel for a Cout. */

@@ -63,8 +63,12 @@ template <int TM, int TN, bool KXK, bool AS>
 // pixels (2i + ph, 2j + pw), phase = 2 ph + pw, and only the taps that reach
 // them — the sub-pixel decomposition of a strided data gradient (the other
 // 3/4 of a naive transposed conv's taps read structural zeros).
+// ks > 1 (split K): blockIdx.y takes K stages [y * ceil(S/ks), ...) and writes
+// its raw sums to part[y][m][n] (n < Ntiles32 * 32); m32_ksplit_reduce adds
+// the ks partials in order and applies the epilogue.
 __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, int mtiles_img,
-                                                             int per_img, int phase) {
+                                                             int per_img, int phase, int ks,
+                                                             float* __restrict__ part) {
   constexpr int BM = 4 * 32 * TM;
   constexpr int NB4 = kG * TN * 64;            // float4 of one weight stage
   constexpr int NBT = (NB4 + 255) / 256;       // ... per thread
@@ -100,7 +104,10 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
     pm[t] = m < m_hi ? m : -1;
   }
   const int Kt = KXK ? nkh * nkw * p.Cin : p.Cin + (p.x2 ? p.Cin2 : 0);
-  const int S = (Kt + kBK - 1) / kBK;
+  const int S_all = (Kt + kBK - 1) / kBK;
+  const int kchunk = (S_all + ks - 1) / ks;
+  const int s_beg = ks > 1 ? (int)blockIdx.y * kchunk : 0;
+  const int S = ks > 1 ? min(S_all, s_beg + kchunk) : S_all;  // stages [s_beg, S)
   // KXK: per-lane output coordinates (oh, ow), image base of each pixel tile,
   // and the flat output pixel om (differs from m in phase mode)
   int poh[TM], pow_[TM], om[TM];
@@ -243,13 +250,13 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
     for (int i = threadIdx.x; i < p.Cin; i += 256) sGate[i] = sc[i];
     __syncthreads();
   }
-  if (S > 0) {  // (a phase of a 1x1 stride-2 data gradient has no taps: zeros)
-    load_a(0, a_cur);
-    load_b(0, b_nxt);
-    store_b(0, 0, b_nxt);
+  if (S > s_beg) {  // (a phase of a 1x1 stride-2 data gradient has no taps: zeros)
+    load_a(s_beg, a_cur);
+    load_b(s_beg, b_nxt);
+    store_b(s_beg & 1, s_beg, b_nxt);
   }
   __syncthreads();
-  for (int s = 0; s < S; ++s) {
+  for (int s = s_beg; s < S; ++s) {
     const bool more = s + 1 < S;
     if (more) {
       load_a(s + 1, a_nxt);
@@ -292,6 +299,24 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
     __syncthreads();
   }
 
+  if (ks > 1) {  // raw partial sums of this K range
+    const int npad = p.Ntiles * 32;
+    float* pb = part + (int64_t)blockIdx.y * p.M * npad;
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      if (pm[t] < 0) continue;
+      float* prow = pb + (int64_t)om[t] * npad;
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int n = (nb * TN + u) * 32 + 8 * c + 4 * h;
+          *reinterpret_cast<float4*>(prow + n) = make_float4(
+              acc[t][u][4 * c], acc[t][u][4 * c + 1], acc[t][u][4 * c + 2], acc[t][u][4 * c + 3]);
+        }
+    }
+    return;
+  }
   // epilogue: acc[t][u][4c + e] = Y[pixel pm[t]][nb*BN + 32u + 8c + 4h + e]
 #pragma unroll
   for (int t = 0; t < TM; ++t) {
@@ -324,6 +349,49 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
   }
 }
 
+// Y[m][n] = act(sum_y part[y][m][n] + bias[n] (+ R[m][n])), partials added in
+// y order (deterministic); one thread per (pixel, 4 channels).
+__global__ __launch_bounds__(256) void m32_ksplit_reduce(const ConvArgs p, int ks,
+                                                         const float* __restrict__ part) {
+  const int npad = p.Ntiles * 32, c4n = (p.Cout + 3) >> 2;
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= p.M * c4n) return;
+  const int64_t m = i / c4n;
+  const int n = (int)(i - m * c4n) * 4;
+  float4 v = *reinterpret_cast<const float4*>(part + m * npad + n);
+  for (int y = 1; y < ks; ++y) {
+    const float4 q = *reinterpret_cast<const float4*>(part + ((int64_t)y * p.M + m) * npad + n);
+    v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
+  }
+  if (p.bias) {
+    const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
+    v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
+  }
+  if (p.res) {
+    const float4 rr = *reinterpret_cast<const float4*>(p.res + m * p.res_ps + p.res_c0 + n);
+    v.x += rr.x; v.y += rr.y; v.z += rr.z; v.w += rr.w;
+  }
+  v.x = act32(v.x, p.act, p.slope);
+  v.y = act32(v.y, p.act, p.slope);
+  v.z = act32(v.z, p.act, p.slope);
+  v.w = act32(v.w, p.act, p.slope);
+  *reinterpret_cast<float4*>(p.y + m * p.y_ps + p.y_c0 + n) = v;
+}
+
+// K split of a forward k x k launch whose grid (`grid` workgroups) cannot fill
+// the device: enough splits for ~512 workgroups, each keeping >= 8 stages of
+// 32 channels; 1 = no split.  Needs a caller workspace (args.ws).
+static int m32_ksplit(const ConvArgs& a, bool kxk, int64_t grid) {
+  if (!kxk || a.tconv || a.Cout % 4 || grid >= 256) return 1;
+  const int S = (a.KH * a.KW * a.Cin + kBK - 1) / kBK;
+  int ks = (int)std::min<int64_t>(8, (512 + grid - 1) / grid);
+  ks = std::min(ks, S / 8);
+  return ks >= 2 ? ks : 1;
+}
+static int64_t m32_ksplit_bytes(const ConvArgs& a, int ks) {
+  return ks > 1 ? (int64_t)ks * a.B * a.OH * a.OW * a.ntiles32 * 32 * (int64_t)sizeof(float) : 0;
+}
+
 template <int TM, int TN, bool KXK, bool AS>
 static int launch_m32_as(const ConvArgs& a, hipStream_t st);
 
@@ -348,7 +416,7 @@ static int launch_m32_as(const ConvArgs& a, hipStream_t st) {
         const int64_t grid = cdiv(Mp, BM) * (a.Ntiles / TN);
         JABD_REQUIRE(grid < (int64_t)0x7fffffff, "conv32: grid too large");
         conv1x1_m32_kernel<TM, TN, KXK, AS><<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, 0,
-                                                                        2 * ph + pw);
+                                                                        2 * ph + pw, 1, nullptr);
         if (int e = check_launch("conv1x1_m32")) return e;
       }
     return JABD_OK;
@@ -356,7 +424,18 @@ static int launch_m32_as(const ConvArgs& a, hipStream_t st) {
   const int64_t mtiles = per_img ? mt_img * a.B : cdiv(a.M, BM);
   const int64_t grid = mtiles * (a.Ntiles / TN);
   JABD_REQUIRE(grid < (int64_t)0x7fffffff, "conv32: grid too large");
-  conv1x1_m32_kernel<TM, TN, KXK, AS><<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, per_img, -1);
+  const int ks = a.ws ? m32_ksplit(a, KXK, grid) : 1;
+  if (ks > 1 && a.ws_bytes >= m32_ksplit_bytes(a, ks)) {
+    float* part = static_cast<float*>(a.ws);
+    conv1x1_m32_kernel<TM, TN, KXK, AS><<<dim3((unsigned)grid, (unsigned)ks), 256, 0, st>>>(
+        a, (int)mt_img, per_img, -1, ks, part);
+    if (int e = check_launch("conv1x1_m32 (split K)")) return e;
+    const int64_t n4 = a.M * ((a.Cout + 3) / 4);
+    m32_ksplit_reduce<<<(unsigned)cdiv(n4, 256), 256, 0, st>>>(a, ks, part);
+    return check_launch("m32_ksplit_reduce");
+  }
+  conv1x1_m32_kernel<TM, TN, KXK, AS><<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, per_img, -1,
+                                                                     1, nullptr);
   return check_launch("conv1x1_m32");
 }
 
@@ -366,6 +445,18 @@ using namespace jabd;
 
 // N-tiles (32 output channels each) per workgroup for the 32x32 kernel.
 // Prefers a 64x128 wave tile (TM=2, TN<=4), else the exact-fit wide tile.
+extern "C" int64_t jabd_conv_workspace_size(const jabd_conv_args* args) {
+  if (!args) return 0;
+  const ConvArgs& a = *args;
+  if (!a.w32 || a.KH * a.KW == 1 || a.Cin % 32 || a.tconv || a.nchw_in || a.tn32 <= 0) return 0;
+  const int TM = a.tn32 <= 4 ? 2 : 1;
+  const int64_t BM = 4 * 32 * TM;
+  const int64_t OHW = (int64_t)a.OH * a.OW;
+  const int64_t mtiles = a.ascale ? cdiv(OHW, BM) * a.B : cdiv((int64_t)a.B * OHW, BM);
+  const int64_t grid = mtiles * (a.ntiles32 / a.tn32);
+  return m32_ksplit_bytes(a, m32_ksplit(a, true, grid));
+}
+
 extern "C" int jabd_conv_pack_tn32(int cout) {
   const int nt = (cout + 31) / 32;
   if (nt <= 4) return nt;

@@ -251,6 +251,118 @@ extern "C" int jabd_nlm_attn_bwd_f32(const float* q, const float* kp, const floa
   return check_launch("nlm_attn_bwd");
 }
 
+// dK = dS . q and dV = P . dctx per image: out[b][s][c] = sum_p A[b][s][p] X[b][p][c]
+// (A = dsmat / pmat [B, S, P], X = q / dctx [B, P, ch]) on the 16x16x4 fp32
+// MFMA: a workgroup takes 16 rows s x all ch columns x one chunk of kDkvChunk
+// pixels (its 4 waves a quarter each, summed in LDS), writes the chunk's
+// partial sums, and dkv_sum_kernel adds the chunks in order (deterministic).
+// Four consecutive pixels per lane and MFMA group: A as one float4 load when
+// P % 4 == 0 (rows 16-byte aligned), else four scalar loads.
+constexpr int kDkvChunk = 2048;
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+template <int NT>  // 16-column tiles covering ch
+__global__ __launch_bounds__(256) void dkv_part_kernel(const float* __restrict__ dsm,
+                                                       const float* __restrict__ pm,
+                                                       const float* __restrict__ q,
+                                                       const float* __restrict__ dctx, int P,
+                                                       int S, int ch, int nchunk,
+                                                       float* __restrict__ part) {
+  __shared__ float red[4][16][NT * 16];
+  const int which = blockIdx.z;  // 0: dK (dsm, q), 1: dV (pm, dctx)
+  const float* A = which ? pm : dsm;
+  const float* X = which ? dctx : q;
+  const int b = blockIdx.y / nchunk, chunk = blockIdx.y - b * nchunk;
+  const int s0 = blockIdx.x * 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i = lane & 15, k = lane >> 4;
+  const int srow = s0 + i < S ? s0 + i : S - 1;
+  const float* Ab = A + ((int64_t)b * S + srow) * P;
+  const float* Xb = X + (int64_t)b * P * ch;
+  const bool vec = (P & 3) == 0;  // rows 16-byte aligned
+  const int p_beg = chunk * kDkvChunk + wave * (kDkvChunk / 4);
+  const int p_end = min(P, p_beg + kDkvChunk / 4);
+  f32x4v acc[NT];
+#pragma unroll
+  for (int u = 0; u < NT; ++u) acc[u] = (f32x4v){0.f, 0.f, 0.f, 0.f};
+  for (int p = p_beg; p < p_end; p += 16) {
+    const int pa = p + 4 * k;  // this lane's four pixels pa .. pa + 3
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (vec && pa + 3 < p_end) a = *reinterpret_cast<const float4*>(Ab + pa);
+    else {
+      if (pa < p_end) a.x = Ab[pa];
+      if (pa + 1 < p_end) a.y = Ab[pa + 1];
+      if (pa + 2 < p_end) a.z = Ab[pa + 2];
+      if (pa + 3 < p_end) a.w = Ab[pa + 3];
+    }
+    const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+      const int c = 16 * u + i;
+      float xv[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        xv[t] = (c < ch && pa + t < p_end) ? Xb[(int64_t)(pa + t) * ch + c] : 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], xv[t], acc[u], 0, 0, 0);
+    }
+  }
+  // acc[u][r] = out[s0 + 4k + r][16u + i]
+#pragma unroll
+  for (int u = 0; u < NT; ++u)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave][4 * k + r][16 * u + i] = acc[u][r];
+  __syncthreads();
+  for (int e = threadIdx.x; e < 16 * NT * 16; e += 256) {
+    const int r = e / (NT * 16), c = e - r * (NT * 16);
+    const float v = ((red[0][r][c] + red[1][r][c]) + red[2][r][c]) + red[3][r][c];
+    if (s0 + r < S && c < ch)
+      part[(((int64_t)which * gridDim.y + blockIdx.y) * S + s0 + r) * ch + c] = v;
+  }
+}
+
+// out[which][b][s][c] = sum over the image's chunks, in order
+__global__ void dkv_sum_kernel(const float* __restrict__ part, int B, int S, int ch, int nchunk,
+                               float* __restrict__ dk, float* __restrict__ dv) {
+  const int64_t n = (int64_t)B * S * ch;
+  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int which = blockIdx.y;
+  if (e >= n) return;
+  const int64_t b = e / ((int64_t)S * ch), r = e - b * S * ch;
+  const float* src = part + ((int64_t)which * B * nchunk + b * nchunk) * S * ch + r;
+  float v = 0.f;
+  for (int c = 0; c < nchunk; ++c) v += src[(int64_t)c * S * ch];
+  (which ? dv : dk)[e] = v;
+}
+
+extern "C" int64_t jabd_nlm_attn_dkv_ws_floats(int32_t B, int32_t P, int32_t S, int32_t ch) {
+  if (B <= 0 || P <= 0 || S <= 0 || ch <= 0) return 0;
+  return 2 * (int64_t)B * cdiv(P, kDkvChunk) * S * ch;
+}
+
+extern "C" int jabd_nlm_attn_dkv_f32(const float* dsmat, const float* pmat, const float* q,
+                                     const float* dctx, int32_t B, int32_t P, int32_t S,
+                                     int32_t ch, float* ws, int64_t ws_floats, float* dk,
+                                     float* dv, jabd_stream_t stream) {
+  JABD_REQUIRE(dsmat && pmat && q && dctx && ws && dk && dv, "nlm_attn_dkv: null pointer");
+  JABD_REQUIRE(B > 0 && P > 0 && S > 0 && ch > 0 && ch <= 64,
+               "nlm_attn_dkv: bad shape B=%d P=%d S=%d ch=%d (ch <= 64)", B, P, S, ch);
+  JABD_REQUIRE(ws_floats >= jabd_nlm_attn_dkv_ws_floats(B, P, S, ch),
+               "nlm_attn_dkv: workspace too small");
+  hipStream_t st = as_stream(stream);
+  const int nchunk = (int)cdiv(P, kDkvChunk);
+  const dim3 g((unsigned)cdiv(S, 16), (unsigned)(B * nchunk), 2);
+  const int nt = (ch + 15) / 16;
+  if (nt == 1) dkv_part_kernel<1><<<g, 256, 0, st>>>(dsmat, pmat, q, dctx, P, S, ch, nchunk, ws);
+  else if (nt == 2) dkv_part_kernel<2><<<g, 256, 0, st>>>(dsmat, pmat, q, dctx, P, S, ch, nchunk, ws);
+  else if (nt == 3) dkv_part_kernel<3><<<g, 256, 0, st>>>(dsmat, pmat, q, dctx, P, S, ch, nchunk, ws);
+  else dkv_part_kernel<4><<<g, 256, 0, st>>>(dsmat, pmat, q, dctx, P, S, ch, nchunk, ws);
+  if (int e = check_launch("nlm_attn_dkv_part")) return e;
+  const int64_t n = (int64_t)B * S * ch;
+  dkv_sum_kernel<<<dim3((unsigned)cdiv(n, 256), 2), 256, 0, st>>>(ws, B, S, ch, nchunk, dk, dv);
+  return check_launch("nlm_attn_dkv_sum");
+}
+
 extern "C" int jabd_add3_f32(const float* a, const float* b, const float* c, int64_t n, float* y,
                              jabd_stream_t stream) {
   JABD_REQUIRE(a && b && y && n >= 0 && n % 4 == 0, "add3: bad args (n %% 4 == 0 required)");

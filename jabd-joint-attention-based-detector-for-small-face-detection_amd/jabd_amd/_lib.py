@@ -52,6 +52,7 @@ class ConvArgs(ctypes.Structure):
         ("w32", c_vp), ("ntiles32", c_i32), ("tn32", c_i32),
         ("y2", c_vp), ("y2_bs", c_i64), ("y2_ps", c_i32), ("y2_c0", c_i32), ("nsplit", c_i32),
         ("act2", c_i32), ("slope2", c_f32), ("reserved2", c_i32),
+        ("ws", c_vp), ("ws_bytes", c_i64),
     ]
 
 
@@ -123,6 +124,9 @@ SIGNATURES = {
     "jabd_nlm_attn_fwd_f32": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],
     "jabd_nlm_attn_bwd_f32": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32,
                               c_vp, c_vp, c_vp, c_vp],
+    "jabd_nlm_attn_dkv_ws_floats": [c_i32, c_i32, c_i32, c_i32],
+    "jabd_nlm_attn_dkv_f32": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_i64,
+                              c_vp, c_vp, c_vp],
     "jabd_add3_f32": [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
     "jabd_beca_ws_floats": [c_i64, c_i64, c_int],
     "jabd_conv_pack_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32,
@@ -140,6 +144,7 @@ SIGNATURES = {
     "jabd_conv_pack_tn": [c_int],
     "jabd_conv_pack_tn32": [c_int],
     "jabd_conv2d_nhwc_f32": [ctypes.POINTER(ConvArgs), c_vp],
+    "jabd_conv_workspace_size": [ctypes.POINTER(ConvArgs)],
     "jabd_stem_nchw_f32": [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp],
     "jabd_dw_nblk": [c_i64, c_i64, c_i64, c_i64],
     "jabd_dwconv_nhwc_f32": [ctypes.POINTER(DwArgs), c_vp],
@@ -225,7 +230,8 @@ _RESTYPE = {"jabd_version": ctypes.c_char_p, "jabd_dw_nblk": ctypes.c_int64,
             "jabd_dw_wgrad_part_floats": ctypes.c_int64,
             "jabd_adam_num_chunks": ctypes.c_int64, "jabd_beca_ws_floats": ctypes.c_int64,
             "jabd_adaptive_pool_ws_floats": ctypes.c_int64,
-            "jabd_abi_struct_size": ctypes.c_int64}
+            "jabd_abi_struct_size": ctypes.c_int64, "jabd_conv_workspace_size": ctypes.c_int64,
+            "jabd_nlm_attn_dkv_ws_floats": ctypes.c_int64}
 
 _lock = threading.Lock()
 _lib = None

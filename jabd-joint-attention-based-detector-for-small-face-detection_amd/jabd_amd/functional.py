@@ -21,6 +21,11 @@ ACT = {"none": 0, "relu": 1, "leaky": 2, "hswish": 3, "hsigmoid": 4, "sigmoid": 
 # "maxpool".
 KINK_TAP = None
 
+# Split-K for small-grid k x k convs (conv32.hip m32_ksplit).  It regroups
+# the fp32 K sum, so an image's outputs then depend (in rounding only) on the
+# batch it was run in; set False for batch-invariant results.
+CONV_KSPLIT = True
+
 
 def tap(kind, *operands):
     if KINK_TAP is not None:
@@ -231,6 +236,14 @@ def conv(x, pk, stride=1, pad=0, act="none", slope=0.0, ascale=None, x2=None, x2
     a.act, a.slope = ACT[act], float(slope)
     a.nchw_in = 1 if nchw_in else 0
     a.reserved1 = _CONV_DBG
+    ws = None
+    if CONV_KSPLIT and pk.KH * pk.KW > 1 and pk.w32 is not None and not nchw_in and y2 is None:
+        # a k x k conv whose output grid cannot fill the device (bs1) may split
+        # its K reduction over workgroups: give it the workspace it asks for
+        nbytes = int(lib().jabd_conv_workspace_size(ctypes.byref(a)))
+        if nbytes > 0:
+            ws = torch.empty(nbytes // 4, dtype=torch.float32, device=x.device)
+            a.ws, a.ws_bytes = ws.data_ptr(), nbytes
     if y2 is not None:
         _check("conv.y2", y2)
         a.y2, a.y2_bs, a.y2_ps, a.y2_c0 = y2.data_ptr(), y2.stride(0), y2.shape[3], y2_c0

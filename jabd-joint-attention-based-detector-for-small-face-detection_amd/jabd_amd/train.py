@@ -460,7 +460,7 @@ class Add3Fn(torch.autograd.Function):
 class NlmAttnFn(torch.autograd.Function):
     """softmax(q . kp^T) . vp (train_mobilenetV3_ecagai.py:216-226) for NLM
     widths other than 4: HIP forward (online softmax) and backward (dq in the
-    kernel; dK = dS . q and dV = P . dctx as per-image batched GEMMs)."""
+    kernel; dK = dS . q and dV = P . dctx in nlm_attn.hip dkv_part_kernel)."""
 
     @staticmethod
     def forward(ctx, q, kp, vp):
@@ -483,9 +483,13 @@ class NlmAttnFn(torch.autograd.Function):
         call("jabd_nlm_attn_bwd_f32", q.data_ptr(), kp.data_ptr(), vp.data_ptr(), out.data_ptr(),
              lse.data_ptr(), dctx.data_ptr(), B, P, S, ch, dq.data_ptr(), pm.data_ptr(),
              dsm.data_ptr(), _st())
-        # [S x P] . [P x ch] per image: plain batched GEMMs (hipBLASLt)
-        dk = torch.bmm(dsm, q.view(B, P, ch))
-        dv = torch.bmm(pm, dctx.view(B, P, ch))
+        # [S x P] . [P x ch] per image on the MFMA, chunks over P summed in order
+        dk = torch.empty_like(kp)
+        dv = torch.empty_like(vp)
+        nws = int(lib().jabd_nlm_attn_dkv_ws_floats(B, P, S, ch))
+        ws = torch.empty(nws, dtype=torch.float32, device=dev)
+        call("jabd_nlm_attn_dkv_f32", dsm.data_ptr(), pm.data_ptr(), q.data_ptr(),
+             dctx.data_ptr(), B, P, S, ch, ws.data_ptr(), nws, dk.data_ptr(), dv.data_ptr(), _st())
         return dq, dk, dv
 
 

@@ -43,7 +43,7 @@ def test_beca_state_dict_layout():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(2, 40, 16, 16), (3, 40, 23, 17)])
+@pytest.mark.parametrize("shape", [(2, 40, 16, 16), (3, 40, 23, 17), (1, 40, 48, 50)])
 def test_nlm40_forward_and_gradients(cuda, shape):
     """NLM(40).forward alone (eval: fused pack; training: NlmAttnFn graph) vs the
     oracle's NLM (nets/retinaface_r.py:124-152 = script :208-234)."""
@@ -78,6 +78,34 @@ def test_nlm40_forward_and_gradients(cuda, shape):
             continue
         e = rel_err(named[k].grad, p.grad)
         assert e < 1e-4, (k, e)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,P,S,ch", [(1, 1, 1, 8), (2, 391, 110, 40), (3, 2048, 110, 40),
+                                      (2, 5001, 17, 64), (1, 4097, 33, 20), (4, 64, 110, 12)])
+def test_nlm_attn_dkv_kernel(cuda, B, P, S, ch):
+    """dK = dS . q, dV = P . dctx (nlm_attn.hip dkv kernels) vs fp64 bmm: chunk
+    boundaries (P over 2048), ragged P, S not a multiple of 16, ch tiles."""
+    import ctypes
+    from jabd_amd._lib import call, lib
+    g = torch.Generator().manual_seed(P + S + ch)
+    dsm, pm = torch.randn(B, S, P, generator=g), torch.rand(B, S, P, generator=g)
+    q, dctx = torch.randn(B, P, ch, generator=g), torch.randn(B, P, ch, generator=g)
+    ref_k, ref_v = (torch.bmm(a.double(), x.double()) for a, x in ((dsm, q), (pm, dctx)))
+    nws = int(lib().jabd_nlm_attn_dkv_ws_floats(B, P, S, ch))
+    t = [v.to(cuda).contiguous() for v in (dsm, pm, q, dctx)]
+    ws = torch.empty(nws, device=cuda)
+    dk = torch.full((B, S, ch), float("nan"), device=cuda)
+    dv = torch.full((B, S, ch), float("nan"), device=cuda)
+    call("jabd_nlm_attn_dkv_f32", *(v.data_ptr() for v in t), B, P, S, ch, ws.data_ptr(), nws,
+         dk.data_ptr(), dv.data_ptr(), None)
+    torch.cuda.synchronize()
+    # fp32 accumulation over P terms: |err| <= ~P * eps * sum|a x|, bar 1e-5 of max
+    assert rel_err(dk, ref_k) < 1e-5, rel_err(dk, ref_k)
+    assert rel_err(dv, ref_v) < 1e-5, rel_err(dv, ref_v)
+    with pytest.raises(RuntimeError):
+        call("jabd_nlm_attn_dkv_f32", *(v.data_ptr() for v in t), B, P, S, ch, ws.data_ptr(),
+             nws - 1, dk.data_ptr(), dv.data_ptr(), None)
 
 
 @pytest.mark.gpu
