@@ -464,6 +464,59 @@ int jabd_heads_f32(const float* x, int64_t x_bs, int32_t x_ps, int32_t B, int32_
                    jabd_stream_t stream);
 
 /* ======================================================================== *
+ * Training-graph glue (no PyTorch kernels in a training step)
+ * ======================================================================== */
+/* Windowed copy: dst [d0][d1][d2] (dense) = scale * src[i0][i1][i2 + off2]
+ * of src [s0][s1][s2] where that index lies inside the source dims, else
+ * fill.  Pads (d >= s) or crops (d <= s) each dim, off2 starts the window
+ * inside dim 2; up to JABD_WINDOW_MAX tensors per launch.  Replaces the
+ * torch.cat / slice / stack glue of a training step: the zero-padding of the
+ * SSH 10-channel branches (nets/layers.py:37-68 with out_channel 40:
+ * conv5X5_1 / conv7X7_2 widths 10) and the crops back, column splits, the
+ * loss-gradient vector. */
+#define JABD_WINDOW_MAX 32
+typedef struct jabd_window_copy {
+  const float* src;
+  float* dst;
+  int32_t s0, s1, s2;
+  int32_t d0, d1, d2;
+  int32_t off2;
+  float fill;
+  float scale;
+  int32_t reserved;
+} jabd_window_copy;
+int jabd_window_copy_multi_f32(int32_t n, const jabd_window_copy* descs, jabd_stream_t stream);
+/* dst [cols][rows] = src [rows][cols]^T (depthwise weights [C][k*k] -> tap-major). */
+int jabd_transpose_f32(const float* src, int32_t rows, int32_t cols, float* dst,
+                       jabd_stream_t stream);
+/* out[c] = sum_r part[r][c], rows in order (bias gradients from the per-block
+ * channel sums of jabd_channel_sum_f32). */
+int jabd_colsum_f32(const float* part, int64_t rows, int32_t C, float* out,
+                    jabd_stream_t stream);
+/* out[e] = in[0][e] + in[1][e] + ... (left to right), n elements, up to
+ * JABD_SUM_MAX inputs: the gradient of a tensor consumed n_in times (the FPN
+ * features, the SSH inputs, the head ECA weight; nets/retinaface_r.py:287-343). */
+#define JABD_SUM_MAX 8
+int jabd_sum_multi_f32(int32_t n_in, const float* const* in, int64_t n, float* out,
+                       jabd_stream_t stream);
+/* out[0] = wa * a[0] + b[0] + c[0]: the total MultiBoxLoss of a training step,
+ * loss = loc_weight * loss_l + loss_c + loss_landm (train_mobilenetV3_ecagai.py:529). */
+int jabd_weighted_sum3_f32(const float* a, const float* b, const float* c, float wa, float* out,
+                           jabd_stream_t stream);
+/* out [cout_is_rows ? K x Cout] = conv weight [Cout][Cin][KH][KW] as the
+ * tap-major [(kh*KW + kw)*Cin + ci][co] matrix (the stem kernel's layout). */
+int jabd_conv_w2d_f32(const float* w, int32_t cout, int32_t cin, int32_t taps, float* out,
+                      jabd_stream_t stream);
+/* The Bbox / Class / Landmark heads of one level (nets/retinaface_r.py:19-58:
+ * 1x1 convs, 8 / 4 / 20 outputs over C channels) as one [32][Cf] matrix wt
+ * and bias [32] (dir 0), or wt unpacked into the three gradients (dir 1).
+ * Feature channel j sits at column j < half + q ? j : j + qp - q (SSH output
+ * with its two q-channel branches padded to qp); q == qp: Cf == C. */
+int jabd_heads_wpack_f32(float* wb, float* wc, float* wl, const float* bb, const float* bc,
+                         const float* bl, int32_t C, int32_t half, int32_t q, int32_t qp,
+                         float* wt, int32_t Cf, float* bias, int32_t dir, jabd_stream_t stream);
+
+/* ======================================================================== *
  * A11 training (loss.backward() of train_*.py:532) — fp32 NHWC, row-major
  * [M = B*H*W rows][C], ld = row stride in floats.  BatchNorm2d in training
  * mode (batch statistics, momentum update of the running buffers).

@@ -29,6 +29,7 @@ extern "C" int64_t jabd_abi_struct_size(int32_t which) {
     case 0: return (int64_t)sizeof(jabd_conv_args);
     case 1: return (int64_t)sizeof(jabd_dw_args);
     case 2: return (int64_t)sizeof(jabd_expdw_args);
+    case 3: return (int64_t)sizeof(jabd_window_copy);
     default: return -1;
   }
 }

@@ -29,6 +29,13 @@ namespace jabd {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Phase-skip mask for timing experiments only (tools/xd_variant.sh builds
+// libraries with -DXD_SKIP=n; results are wrong): 1 expand MFMAs, 2 expanded-
+// tile LDS writes, 4 depthwise phase, 8 ECA reduce, 16 input loads.
+#ifndef XD_SKIP
+#define XD_SKIP 0
+#endif
+
 // Activation fixed at compile time (no per-element branch).  Hardswish
 // multiplies by 1/6 instead of dividing (<= 1 ulp from x*relu6(x+3)/6; an
 // IEEE divide is ~10 VALU instructions per element here).
@@ -215,7 +222,8 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
       const bool ok = px < C::IPX && cok &&
                       (interior || ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W));
       const uint32_t off = ok ? (base + (uint32_t)((ih * p.W + iw) * p.x_ps)) * 4u : 0xFFFFFFF0u;
-      dst[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+      if (XD_SKIP & 16) dst[u] = make_float4(0.f, 0.f, 0.f, (float)off);
+      else dst[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
     }
   };
   // accumulators start at the expand bias (no epilogue add)
@@ -275,7 +283,7 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
       }
       // a wave whose 16-channel tile lies past E skips its MFMAs (wave-uniform;
       // its accumulators are masked in the epilogue)
-      if (ntv) {
+      if (ntv && !(XD_SKIP & 1)) {
 #pragma unroll
         for (int u = 0; u < BPW; ++u) {
           const int blk = wave + NW * u;
@@ -293,7 +301,8 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
     }
   }
   // expanded tile: act, zero outside the image / on padded channels
-  if (interior) {
+  if (XD_SKIP & 2) {
+  } else if (interior) {
 #pragma unroll
     for (int u = 0; u < BPW; ++u) {
       const int blk = wave + NW * u;
@@ -339,7 +348,7 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
   const bool chv = it.c0 + chl < p.E;
   constexpr int SPW = 64 / C::NC4;  // strips per wave per pass
   float4 psum = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (chv) {
+  if (chv && !(XD_SKIP & 4)) {
     const float4 bias2 = wsh[K * K][c4];
     float* yb = p.y + (int64_t)it.b * p.y_bs + it.c0 + chl;
 #pragma unroll 1
@@ -386,7 +395,7 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
       }
     }
   }
-  if (p.part) {
+  if (p.part && !(XD_SKIP & 8)) {
     // sum the lanes holding the same channel quad (dw_lane): EC = 32 -> lane
     // xor 12, 20 (the even-popcount quad permutations) and 32; EC = 16 ->
     // xor 4, 8, 16, 32.  Fixed order: deterministic.  Lanes 0..NC4-1 then

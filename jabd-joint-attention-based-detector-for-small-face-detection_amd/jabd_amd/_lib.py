@@ -86,6 +86,19 @@ class ExpDwArgs(ctypes.Structure):
     ]
 
 
+class WindowCopy(ctypes.Structure):
+    """Mirror of `jabd_window_copy` (include/jabd.h)."""
+    _fields_ = [
+        ("src", c_vp), ("dst", c_vp),
+        ("s0", c_i32), ("s1", c_i32), ("s2", c_i32),
+        ("d0", c_i32), ("d1", c_i32), ("d2", c_i32),
+        ("off2", c_i32), ("fill", c_f32), ("scale", c_f32), ("reserved", c_i32),
+    ]
+
+
+WINDOW_MAX = 32  # JABD_WINDOW_MAX
+
+
 # name -> argtypes (every function returns int status unless listed in _RESTYPE)
 SIGNATURES = {
     "jabd_version": [],
@@ -124,6 +137,14 @@ SIGNATURES = {
     "jabd_nlm_attn_fwd_f32": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],
     "jabd_nlm_attn_bwd_f32": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32,
                               c_vp, c_vp, c_vp, c_vp],
+    "jabd_window_copy_multi_f32": [c_i32, ctypes.POINTER(WindowCopy), c_vp],
+    "jabd_transpose_f32": [c_vp, c_i32, c_i32, c_vp, c_vp],
+    "jabd_colsum_f32": [c_vp, c_i64, c_i32, c_vp, c_vp],
+    "jabd_sum_multi_f32": [c_i32, ctypes.POINTER(c_vp), c_i64, c_vp, c_vp],
+    "jabd_weighted_sum3_f32": [c_vp, c_vp, c_vp, c_f32, c_vp, c_vp],
+    "jabd_conv_w2d_f32": [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp],
+    "jabd_heads_wpack_f32": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32,
+                             c_vp, c_i32, c_vp, c_i32, c_vp],
     "jabd_nlm_attn_dkv_ws_floats": [c_i32, c_i32, c_i32, c_i32],
     "jabd_nlm_attn_dkv_f32": [c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_i64,
                               c_vp, c_vp, c_vp],

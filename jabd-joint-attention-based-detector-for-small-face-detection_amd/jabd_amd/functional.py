@@ -347,6 +347,66 @@ def channel_sums(x, nblk=None):
     return part
 
 
+def dims3(shape):
+    """A tensor shape as the (d0, d1, d2) of jabd_window_copy: conv weights
+    [Cout][Cin][KH][KW] -> (Cout, Cin, KH*KW); vectors [C] -> (1, C, 1)."""
+    shape = tuple(shape)
+    if len(shape) == 0:
+        return (1, 1, 1)
+    if len(shape) == 1:
+        return (1, shape[0], 1)
+    if len(shape) == 2:
+        return (shape[0], shape[1], 1)
+    n2 = 1
+    for d in shape[2:]:
+        n2 *= d
+    return (shape[0], shape[1], n2)
+
+
+def window_copies(items):
+    """[(src, dst, fill[, off2[, scale]])] -> dst (dense) = scale * src's
+    window starting at off2 along dim 2, fill outside
+    (jabd_window_copy_multi_f32; src None = fill only).  Both tensors are
+    read as dims3() boxes, so a pad or a crop along dims 0 / 1 of a conv
+    weight or a BN vector, or a column range of a [rows][cols] matrix, is
+    one descriptor; up to 32 per launch."""
+    from ._lib import WINDOW_MAX, WindowCopy
+    for i in range(0, len(items), WINDOW_MAX):
+        chunk = items[i:i + WINDOW_MAX]
+        arr = (WindowCopy * len(chunk))()
+        for d, it in zip(arr, chunk):
+            src, dst, fill = it[:3]
+            if not dst.is_contiguous() or (src is not None and not src.is_contiguous()):
+                raise RuntimeError("window_copies: tensors must be contiguous")
+            d.src = src.data_ptr() if src is not None else None
+            d.dst = dst.data_ptr()
+            d.s0, d.s1, d.s2 = dims3(src.shape) if src is not None else (0, 0, 0)
+            d.d0, d.d1, d.d2 = dims3(dst.shape)
+            d.off2 = int(it[3]) if len(it) > 3 else 0
+            d.fill = float(fill)
+            d.scale = float(it[4]) if len(it) > 4 else 1.0
+        call("jabd_window_copy_multi_f32", len(chunk), arr, _stream())
+
+
+def transpose(src, out=None):
+    """[rows][cols] -> [cols][rows] on the device (jabd_transpose_f32)."""
+    rows, cols = src.shape
+    out = torch.empty((cols, rows), dtype=torch.float32, device=src.device) if out is None else out
+    call("jabd_transpose_f32", src.data_ptr(), rows, cols, out.data_ptr(), _stream())
+    return out
+
+
+def channel_total(x):
+    """Per-channel sum of an NHWC tensor: block partials (jabd_channel_sum_f32)
+    summed in a fixed order (jabd_colsum_f32)."""
+    part = channel_sums(x)
+    C = x.shape[3]
+    out = torch.empty(C, dtype=torch.float32, device=x.device)
+    call("jabd_colsum_f32", part.data_ptr(), part.shape[0] * part.shape[1], C, out.data_ptr(),
+         _stream())
+    return out
+
+
 def eca_gates_multi(xs, w1ds, gate):
     """ECA gates ([B, C] each) of up to 4 NHWC tensors in two launches
     (jabd_eca_pool_gate_multi_f32); the same as eca_gate(channel_sums(x), ...)

@@ -175,7 +175,18 @@ def match_encode(targets, priors, threshold, variances, raw_loc=False):
     counts = [int(t.shape[0]) for t in targets]
     if any(c == 0 for c in counts):
         raise ValueError("match: an image has no targets (the reference's match() fails too)")
-    flat = _dev("match.targets", torch.cat([t.reshape(-1, 15) for t in targets], 0))
+    for t in targets:
+        _dev("match.targets", t)
+    if len(targets) == 1:
+        flat = targets[0].reshape(-1, 15).contiguous()
+    else:  # the images' rows back to back, one launch
+        flat = torch.empty((sum(counts), 15), dtype=torch.float32, device=dev)
+        items, o = [], 0
+        for t, c in zip(targets, counts):
+            items.append((t.reshape(-1, 15).contiguous(), flat[o:o + c], 0.0))
+            o += c
+        from .functional import window_copies
+        window_copies(items)
     offs = [0]
     for c in counts:
         offs.append(offs[-1] + c)

@@ -191,6 +191,40 @@ def shard(batch_images, batch_targets, rank, world):
     return batch_images[lo:hi], batch_targets[lo:hi]
 
 
+class _WeightedLossFn(torch.autograd.Function):
+    """loss = w * loss_l + loss_c + loss_landm (train_mobilenetV3_ecagai.py:529)
+    in one launch; the backward hands (w * g, g, g) to MultiBoxLoss."""
+
+    @staticmethod
+    def forward(ctx, r, c, lm, w):
+        out = torch.empty((), dtype=torch.float32, device=r.device)
+        from ._lib import call
+        from .functional import _stream
+        call("jabd_weighted_sum3_f32", r.data_ptr(), c.data_ptr(), lm.data_ptr(), w,
+             out.data_ptr(), _stream())
+        ctx.w = w
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from .functional import window_copies
+        g = g.contiguous()
+        gr = torch.empty((), dtype=torch.float32, device=g.device)
+        window_copies([(g, gr, 0.0, 0, ctx.w)])
+        return gr, g, g, None
+
+
+_ONE = {}
+
+
+def _one(dev):
+    """The backward seed d(loss)/d(loss) = 1, allocated once per device."""
+    t = _ONE.get(str(dev))
+    if t is None:
+        t = _ONE[str(dev)] = torch.ones((), dtype=torch.float32, device=dev)
+    return t
+
+
 def train_step(model, criterion, optimizer, images, targets, priors, loc_weight=2.0,
                reducer=None):
     """One fit_one_epoch iteration (train_mobilenetV3_ecagai.py:518-533) on
@@ -202,8 +236,8 @@ def train_step(model, criterion, optimizer, images, targets, priors, loc_weight=
     out = model(images)
     with criterion.global_counts(reducer is not None and _world(group), group):
         r_loss, c_loss, landm_loss = criterion(out, priors, targets)
-    loss = loc_weight * r_loss + c_loss + landm_loss
-    loss.backward()
+    loss = _WeightedLossFn.apply(r_loss, c_loss, landm_loss, float(loc_weight))
+    torch.autograd.backward(loss, _one(loss.device))
     if reducer is not None:
         reducer()
     optimizer.step()

@@ -41,6 +41,19 @@ ECA_WGRAD = __import__("os").environ.get("JABD_ECA_WGRAD", "1") != "0"
 ECA_SUMS = __import__("os").environ.get("JABD_ECA_SUMS", "1") != "0"
 
 
+_ZEROS = {}
+
+
+def _zeros(n, dev):
+    """A read-only zero vector of >= n floats per device (allocated once)."""
+    key = str(dev)
+    t = _ZEROS.get(key)
+    if t is None or t.numel() < n:
+        t = torch.zeros(max(n, 64), dtype=torch.float32, device=dev)
+        _ZEROS[key] = t
+    return t
+
+
 def _st():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
@@ -128,8 +141,8 @@ def _wgrad(x, dy, weight, stride, pad, nchw_in=False, ascale=None):
 
 
 def _chan_sum(t):
-    """Per-channel sum of an NHWC tensor (kernel partials, tiny torch reduce)."""
-    return F.channel_sums(t).sum(dim=(0, 1))
+    """Per-channel sum of an NHWC tensor (bias gradients)."""
+    return F.channel_total(t)
 
 
 def _wgrad_eca(x, dy, weight, scale):
@@ -185,8 +198,10 @@ class ConvFn(torch.autograd.Function):
         y = torch.empty((B, OH, OW, pk.Cout), dtype=torch.float32, device=x.device)
         if (nchw_in and pk.KH == 3 and stride == 2 and pad == 1 and pk.Cin == 3
                 and pk.Cout == 16):
-            wt = F.conv_weight_2d(weight.detach().float()).contiguous()
-            zb = torch.zeros(16, dtype=torch.float32, device=x.device)
+            wd = weight.detach()
+            wt = torch.empty((27, 16), dtype=torch.float32, device=x.device)
+            call("jabd_conv_w2d_f32", wd.data_ptr(), 16, 3, 9, wt.data_ptr(), _st())
+            zb = _zeros(16, x.device)
             call("jabd_stem_nchw_f32", x.data_ptr(), B, H, W, wt.data_ptr(), zb.data_ptr(),
                  ACT["none"], y.data_ptr(), _st())
         else:
@@ -391,8 +406,11 @@ class NlmFn(torch.autograd.Function):
         ctxv = cx.view(B, h, w, ch)
         dWW = _wgrad(ctxv, dout, torch.empty((C, ch, 1, 1), device=dev), 1, 0)
         dWq = _wgrad(xup, dq, torch.empty((ch, C, 1, 1), device=dev), 1, 0)
-        dk_only = dkv[..., :ch].contiguous()
-        dv_only = dkv[..., ch:].contiguous()
+        dk_only = torch.empty(dkv.shape[:-1] + (ch,), dtype=torch.float32, device=dev)
+        dv_only = torch.empty_like(dk_only)
+        kv = dkv.contiguous().view(1, -1, 2 * ch)  # columns are dim 2 of the window
+        F.window_copies([(kv, dk_only.view(1, -1, ch), 0.0, 0),
+                         (kv, dv_only.view(1, -1, ch), 0.0, ch)])
         dWk = _wgrad(xup, dk_only, torch.empty((ch, C, 1, 1), device=dev), 1, 0)
         dWv = _wgrad(xup, dv_only, torch.empty((ch, C, 1, 1), device=dev), 1, 0)
         g = (dWq, _chan_sum(dq), dWk, _chan_sum(dk_only), dWv, _chan_sum(dv_only), dWW,
@@ -554,8 +572,9 @@ class HeadsFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, f1, f2, f3, cidx, *wb):
-        """cidx: per level None, or the channel index of each real feature
-        channel in a zero-padded feature tensor (ssh_train(padded_out=True))."""
+        """cidx: per level None, or the (half, q, qp) layout of a feature
+        tensor whose two q-channel branches are zero-padded to qp channels
+        (ssh_train(padded_out=True))."""
         feats = (f1, f2, f3)
         B = f1.shape[0]
         A = sum(2 * f.shape[1] * f.shape[2] for f in feats)
@@ -566,21 +585,21 @@ class HeadsFn(torch.autograd.Function):
         a_off = 0
         cat = []
         for i, f in enumerate(feats):
-            ws = wb[6 * i:6 * i + 6]  # Wb, bb, Wc, bc, Wl, bl
+            ws = [t.detach() for t in wb[6 * i:6 * i + 6]]  # Wb, bb, Wc, bc, Wl, bl
             C = ws[0].shape[1]
-            wt = torch.cat([ws[0].detach().reshape(8, C), ws[2].detach().reshape(4, C),
-                            ws[4].detach().reshape(20, C)]).float()
-            if cidx[i] is not None:  # zero columns at the feature's pad channels
-                wp = wt.new_zeros((32, f.shape[3]))
-                wp[:, cidx[i]] = wt
-                wt = wp
-            wt = wt.contiguous()
-            bs = torch.cat([ws[1].detach(), ws[3].detach(), ws[5].detach()]).float().contiguous()
+            Cf = f.shape[3]
+            half, q, qp = cidx[i] if cidx[i] is not None else (C, 0, 0)
+            wt = torch.empty((32, Cf), dtype=torch.float32, device=dev)
+            bs = torch.empty(32, dtype=torch.float32, device=dev)
+            call("jabd_heads_wpack_f32", ws[0].data_ptr(), ws[2].data_ptr(), ws[4].data_ptr(),
+                 ws[1].data_ptr(), ws[3].data_ptr(), ws[5].data_ptr(), C, half, q, qp,
+                 wt.data_ptr(), Cf, bs.data_ptr(), 0, _st())
             F.heads(f, wt, bs, loc, conf, landm, a_off, softmax=False)
             cat.append(wt)
             a_off += 2 * f.shape[1] * f.shape[2]
         ctx.save_for_backward(f1, f2, f3, *cat)
         ctx.cidx = cidx
+        ctx.cs = [wb[6 * i].shape[1] for i in range(3)]
         return loc, conf, landm
 
     @staticmethod
@@ -588,27 +607,31 @@ class HeadsFn(torch.autograd.Function):
         f1, f2, f3, w1, w2, w3 = ctx.saved_tensors
         dev = f1.device
         B = f1.shape[0]
-        A = gl.shape[1]
-        gl = gl.contiguous() if gl is not None else torch.zeros((B, A, 4), device=dev)
-        gc = gc.contiguous() if gc is not None else torch.zeros((B, A, 2), device=dev)
-        glm = glm.contiguous() if glm is not None else torch.zeros((B, A, 10), device=dev)
+        A = sum(2 * f.shape[1] * f.shape[2] for f in (f1, f2, f3))
+        zero = None
+        if gl is None or gc is None or glm is None:
+            zero = torch.empty((B, A, 10), dtype=torch.float32, device=dev)
+            F.window_copies([(None, zero, 0.0)])
+        gl = gl.contiguous() if gl is not None else zero[..., :4].contiguous()
+        gc = gc.contiguous() if gc is not None else zero[..., :2].contiguous()
+        glm = glm.contiguous() if glm is not None else zero
         a_off = 0
         dfs, dws = [], []
-        for f, wt in zip((f1, f2, f3), (w1, w2, w3)):
-            _, h, w, C = f.shape
+        for i, (f, wt) in enumerate(zip((f1, f2, f3), (w1, w2, w3))):
+            _, h, w, Cf = f.shape
             dout = torch.empty((B, h, w, 32), dtype=torch.float32, device=dev)
             call("jabd_heads_gather_f32", gl.data_ptr(), gc.data_ptr(), glm.data_ptr(), B, A,
                  a_off, h * w, dout.data_ptr(), _st())
-            wconv = wt.view(32, C, 1, 1)
+            wconv = wt.view(32, Cf, 1, 1)
             dfs.append(_dgrad(dout, wconv, 1, 0, h, w))
-            dW = _wgrad(f, dout, wconv, 1, 0).view(32, C)
-            ci = ctx.cidx[len(dfs) - 1]
-            if ci is not None:
-                dW = dW[:, ci]
-                C = dW.shape[1]
+            dW = _wgrad(f, dout, wconv, 1, 0).view(32, Cf)
+            C = ctx.cs[i]
+            half, q, qp = ctx.cidx[i] if ctx.cidx[i] is not None else (C, 0, 0)
+            g3 = [torch.empty((r, C, 1, 1), dtype=torch.float32, device=dev) for r in (8, 4, 20)]
+            call("jabd_heads_wpack_f32", g3[0].data_ptr(), g3[1].data_ptr(), g3[2].data_ptr(),
+                 None, None, None, C, half, q, qp, dW.data_ptr(), Cf, None, 1, _st())
             db = _chan_sum(dout)
-            dws += [dW[:8].reshape(8, C, 1, 1), db[:8], dW[8:12].reshape(4, C, 1, 1), db[8:12],
-                    dW[12:].reshape(20, C, 1, 1), db[12:]]
+            dws += [g3[0], db[:8], g3[1], db[8:12], g3[2], db[12:]]
             a_off += 2 * h * w
         return tuple(dfs) + (None,) + tuple(dws)
 
@@ -643,15 +666,11 @@ def bn_act(x, bn, act="none", slope=0.0, res=None):
     g, b = bn.weight, bn.bias
     rm, rv = bn.running_mean, bn.running_var
     if C != g.shape[0]:  # zero-padded channels (10 -> 12): pad params/buffers
-        pad = C - g.shape[0]
-        g = torch.cat([g, g.new_zeros(pad)])
-        b = torch.cat([b, b.new_zeros(pad)])
-        rm_p = torch.cat([rm, rm.new_zeros(pad)])
-        rv_p = torch.cat([rv, rv.new_ones(pad)])
+        g, b, rm_p, rv_p = _padded([(g, (C,), 0.0), (b, (C,), 0.0), (rm, (C,), 0.0),
+                                    (rv, (C,), 1.0)])
         y = BnActFn.apply(x, g, b, res, rm_p, rv_p, act, slope, bn.momentum, bn.eps)
         with torch.no_grad():
-            rm.copy_(rm_p[: rm.shape[0]])
-            rv.copy_(rv_p[: rv.shape[0]])
+            F.window_copies([(rm_p, rm, 0.0), (rv_p, rv, 0.0)])
     else:
         y = BnActFn.apply(x, g, b, res, rm, rv, act, slope, bn.momentum, bn.eps)
     _count_batch(bn)
@@ -692,14 +711,87 @@ class _BatchCounts:
             torch._foreach_add_(ts, 1)
 
 
+class PadFn(torch.autograd.Function):
+    """Zero-pad several tensors along dims 0 / 1 in one launch (conv weights
+    [Cout][Cin][..] and BN vectors [C] of the 10-channel SSH branches ->
+    12 channels); the backward crops the gradients back in one launch.
+    spec: per tensor (padded shape, fill)."""
+
+    @staticmethod
+    def forward(ctx, spec, *ts):
+        ctx.set_materialize_grads(False)
+        outs, items = [], []
+        for t, (shape, fill) in zip(ts, spec):
+            t = t.detach()
+            if not t.is_contiguous():
+                t = t.contiguous()
+            o = torch.empty(shape, dtype=torch.float32, device=t.device)
+            items.append((t, o, fill))
+            outs.append(o)
+        F.window_copies(items)
+        ctx.shapes = [tuple(t.shape) for t in ts]
+        nd = [o for t, o in zip(ts, outs) if not t.requires_grad]
+        if nd:
+            ctx.mark_non_differentiable(*nd)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        items, res = [], []
+        for g, shape in zip(gs, ctx.shapes):
+            if g is None:
+                res.append(None)
+                continue
+            o = torch.empty(shape, dtype=torch.float32, device=g.device)
+            items.append((g if g.is_contiguous() else g.contiguous(), o, 0.0))
+            res.append(o)
+        F.window_copies(items)
+        return (None,) + tuple(res)
+
+
+class ForkFn(torch.autograd.Function):
+    """n aliases of one tensor for n consumers: the backward sums their
+    gradients in one HIP launch (jabd_sum_multi_f32) instead of the autograd
+    engine's pairwise ATen adds."""
+
+    @staticmethod
+    def forward(ctx, x, n):
+        ctx.set_materialize_grads(False)
+        return tuple(x.view_as(x) for _ in range(n))
+
+    @staticmethod
+    def backward(ctx, *gs):
+        gs = [g if g.is_contiguous() else g.contiguous() for g in gs if g is not None]
+        if not gs:
+            return None, None
+        if len(gs) == 1:
+            return gs[0], None
+        out = torch.empty_like(gs[0], memory_format=torch.contiguous_format)
+        ptrs = (ctypes.c_void_p * len(gs))(*[g.data_ptr() for g in gs])
+        call("jabd_sum_multi_f32", len(gs), ptrs, out.numel(), out.data_ptr(), _st())
+        return out, None
+
+
+def fork(x, n):
+    """n autograd aliases of x (ForkFn); x itself when it needs no gradient."""
+    if not x.requires_grad or not torch.is_grad_enabled():
+        return (x,) * n
+    return ForkFn.apply(x, n)
+
+
+def _padded(spec_ts):
+    """[(tensor, padded shape, fill)] -> padded tensors (one PadFn launch)."""
+    return PadFn.apply(tuple((tuple(shape), fill) for _, shape, fill in spec_ts),
+                       *[t for t, _, _ in spec_ts])
+
+
 def _padw(weight, cout=None, cin=None):
-    """Zero-pad a conv weight's out/in channels (autograd-tracked)."""
-    w = weight
-    if cout is not None and cout > w.shape[0]:
-        w = torch.cat([w, w.new_zeros((cout - w.shape[0],) + tuple(w.shape[1:]))], 0)
-    if cin is not None and cin > w.shape[1]:
-        w = torch.cat([w, w.new_zeros((w.shape[0], cin - w.shape[1]) + tuple(w.shape[2:]))], 1)
-    return w
+    """Zero-pad a conv weight's out/in channels (autograd-tracked, one launch)."""
+    co = max(cout or 0, weight.shape[0])
+    ci = max(cin or 0, weight.shape[1])
+    if (co, ci) == tuple(weight.shape[:2]):
+        return weight
+    return _padded([(weight, (co, ci) + tuple(weight.shape[2:]), 0.0)])[0]
 
 
 def conv(x, m, stride=1, pad=0, nchw_in=False):
@@ -791,7 +883,7 @@ def _dgrad_1x1_res(dy, weight, res):
 
 def _dw_fwd(x, weight, stride):
     C, _, k, _ = weight.shape
-    wt = weight.detach().reshape(C, k * k).t().contiguous()
+    wt = F.transpose(weight.detach().reshape(C, k * k))  # tap-major [k*k][C]
     y, _ = F.dwconv(x, wt, None, k, stride)
     return y, wt
 
@@ -1014,29 +1106,35 @@ def _r50_block(blk, x):
     return bn_act(t, blk.bn3, "relu", res=idn)
 
 
-def nlm_train(nlm, src, lateral=None):
+def _nlm_params(nlm):
+    return (nlm.f_query.weight, nlm.f_query.bias, nlm.f_key.weight, nlm.f_key.bias,
+            nlm.f_value.weight, nlm.f_value.bias, nlm.W.weight, nlm.W.bias)
+
+
+def nlm_train(nlm, src, lateral=None, nw=None):
     """ch=4: lateral + NLM(nearest(src)) fused (lateral=None: NLM(src)).
     Other widths: lateral + NLM(src) composed from ConvFn / AdaptivePoolFn /
-    NlmAttnFn (src already at the output size)."""
+    NlmAttnFn (src already at the output size).  nw: the module's eight
+    parameters or autograd aliases of them (the FPN runs one NLM twice)."""
+    nw = _nlm_params(nlm) if nw is None else nw
     if nlm.ch == 4:
-        nw = (nlm.f_query.weight, nlm.f_query.bias, nlm.f_key.weight, nlm.f_key.bias,
-              nlm.f_value.weight, nlm.f_value.bias, nlm.W.weight, nlm.W.bias)
         return NlmFn.apply(src, lateral, *nw, tuple(nlm.psp.sizes))
     from .modules import AdaptivePoolFn
     x = src.contiguous()
     B, h, w, C = x.shape
     sizes = tuple(nlm.psp.sizes)
     S = sum(s_ * s_ for s_ in sizes)
-    q = conv(x, nlm.f_query)
+    q = ConvFn.apply(x, nw[0], nw[1], 1, 0, False)
     pooled = AdaptivePoolFn.apply(x, sizes).view(B, S, 1, C)
-    kp = conv(pooled, nlm.f_key).view(B, S, nlm.ch)
-    vp = conv(pooled, nlm.f_value).view(B, S, nlm.ch)
-    y = conv(NlmAttnFn.apply(q, kp, vp), nlm.W)
+    kp = ConvFn.apply(pooled, nw[2], nw[3], 1, 0, False).view(B, S, nlm.ch)
+    vp = ConvFn.apply(pooled, nw[4], nw[5], 1, 0, False).view(B, S, nlm.ch)
+    y = ConvFn.apply(NlmAttnFn.apply(q, kp, vp), nw[6], nw[7], 1, 0, False)
     return Add3Fn.apply(y, x, lateral)
 
 
-def fpn_up_train(fpn, nlm, src, lateral):
-    """lateral + [NLM](up(src -> lateral's size)) in training mode."""
+def fpn_up_train(fpn, nlm, src, lateral, nw=None):
+    """lateral + [NLM](up(src -> lateral's size)) in training mode; nw: the
+    NLM's parameters (or aliases, see nlm_train)."""
     mode = getattr(fpn, "upsample_mode", "nearest")
     if nlm is None:
         if mode == "nearest":
@@ -1044,11 +1142,11 @@ def fpn_up_train(fpn, nlm, src, lateral):
         return Add3Fn.apply(UpsampleFn.apply(src, lateral.shape[1], lateral.shape[2], mode),
                             lateral, None)
     if mode == "nearest" and nlm.ch == 4:
-        return nlm_train(nlm, src, lateral)
+        return nlm_train(nlm, src, lateral, nw)
     up = UpsampleFn.apply(src, lateral.shape[1], lateral.shape[2], mode)
     if nlm.ch == 4:
-        return Add3Fn.apply(nlm_train(nlm, up), lateral, None)
-    return nlm_train(nlm, up, lateral)
+        return Add3Fn.apply(nlm_train(nlm, up, None, nw), lateral, None)
+    return nlm_train(nlm, up, lateral, nw)
 
 
 def fpn_train(fpn, feats, nlm=None, eca_ws=None, gate="sigmoid"):
@@ -1071,71 +1169,95 @@ def fpn_train(fpn, feats, nlm=None, eca_ws=None, gate="sigmoid"):
         lat.append(bn_act(y, o[1], "leaky", lk))
     o1, o2, o3 = lat
 
+    # one NLM module serves both up-merges: its parameters get one alias per
+    # use, so their two gradients are summed by ForkFn, not by autograd
+    nws = [None, None]
+    if nlm is not None:
+        nws = list(zip(*[fork(p_, 2) for p_ in _nlm_params(nlm)]))
+
     def up(s_, l_):
-        return fpn_up_train(fpn, nlm, s_, l_)
-    o2 = bn_act(conv(up(o3, o2), fpn.merge2[0], 1, 1), fpn.merge2[1], "leaky", lk)
-    o1 = bn_act(conv(up(o2, o1), fpn.merge1[0], 1, 1), fpn.merge1[1], "leaky", lk)
+        return fpn_up_train(fpn, nlm, s_, l_, nws.pop(0))
+    o3, o3u = fork(o3, 2)  # to the SSH and up-sampled into o2
+    o2 = bn_act(conv(up(o3u, o2), fpn.merge2[0], 1, 1), fpn.merge2[1], "leaky", lk)
+    o2, o2u = fork(o2, 2)
+    o1 = bn_act(conv(up(o2u, o1), fpn.merge1[0], 1, 1), fpn.merge1[1], "leaky", lk)
     return [o1, o2, o3]
 
 
 def ssh_train(ssh, o, eca_w=None, padded_out=False):
     """SSH forward (nets/layers.py:56-68) in training mode; eca_w: the head's
-    eca_fpn Conv1d weight applied on the two input convs' operand load.
+    eca_fpn Conv1d weight (or two autograd aliases of it, one per use)
+    applied on the two input convs' operand load.
     padded_out: when the quarter branches are zero-padded to a multiple of 4
-    channels, return (padded tensor, index of each real channel) instead of
-    copying the real channels out (the heads read the padded layout)."""
+    channels, return (padded tensor, (half, q, qp) layout) instead of copying
+    the real channels out (the heads read the padded layout)."""
     q = ssh.conv5X5_1[0].out_channels
     qp = _pad_to4(q)
+    # o feeds two convs, and so does the eca weight (one alias each, ForkFn)
+    ins = list(zip(fork(o, 2), fork(eca_w, 2) if isinstance(eca_w, torch.Tensor) else
+                   (eca_w if eca_w is not None else (None, None))))
 
     def first(w):
-        if eca_w is not None:
-            return EcaConvFn.apply(o, eca_w, w, 1, 1, "sigmoid")
-        return ConvFn.apply(o, w, None, 1, 1, False)
+        oi, ei = ins.pop(0)
+        if ei is not None:
+            return EcaConvFn.apply(oi, ei, w, 1, 1, "sigmoid")
+        return ConvFn.apply(oi, w, None, 1, 1, False)
 
     a = first(ssh.conv3X3[0].weight)
-    b1 = bn_act(first(_padw(ssh.conv5X5_1[0].weight, cout=qp)), ssh.conv5X5_1[1], "leaky",
-                ssh.leaky)
-    b = ConvFn.apply(b1, _padw(ssh.conv5X5_2[0].weight, cout=qp, cin=qp), None, 1, 1, False)
-    c1 = bn_act(ConvFn.apply(b1, _padw(ssh.conv7X7_2[0].weight, cout=qp, cin=qp), None, 1, 1,
-                             False), ssh.conv7X7_2[1], "leaky", ssh.leaky)
-    c = ConvFn.apply(c1, _padw(ssh.conv7x7_3[0].weight, cout=qp, cin=qp), None, 1, 1, False)
-    stats = []
     bns = (ssh.conv3X3[1], ssh.conv5X5_2[1], ssh.conv7x7_3[1])
-    gb = []
-    for bn, t in zip(bns, (a, b, c)):
-        C = t.shape[3]
-        pad = C - bn.weight.shape[0]
-        if pad:
-            g = torch.cat([bn.weight, bn.weight.new_zeros(pad)])
-            bt = torch.cat([bn.bias, bn.bias.new_zeros(pad)])
-            stats.append((None, None, bn.momentum, bn.eps))  # updated below
-        else:
-            g, bt = bn.weight, bn.bias
-            stats.append((bn.running_mean, bn.running_var, bn.momentum, bn.eps))
-        gb += [g, bt]
-        _count_batch(bn)
     if qp == q:
+        b1 = bn_act(first(ssh.conv5X5_1[0].weight), ssh.conv5X5_1[1], "leaky", ssh.leaky)
+        b1a, b1b = fork(b1, 2)
+        b = ConvFn.apply(b1a, ssh.conv5X5_2[0].weight, None, 1, 1, False)
+        c1 = bn_act(ConvFn.apply(b1b, ssh.conv7X7_2[0].weight, None, 1, 1, False),
+                    ssh.conv7X7_2[1], "leaky", ssh.leaky)
+        c = ConvFn.apply(c1, ssh.conv7x7_3[0].weight, None, 1, 1, False)
+        gb, stats = [], []
+        for bn in bns:
+            gb += [bn.weight, bn.bias]
+            stats.append((bn.running_mean, bn.running_var, bn.momentum, bn.eps))
+            _count_batch(bn)
         f = SshTailFn.apply(a, b, c, *gb, stats)
         return (f, None) if padded_out else f
-    # padded branches: track running stats on padded copies, then copy back
-    padded = []
-    for i, (bn, t) in enumerate(zip(bns, (a, b, c))):
-        if stats[i][0] is None:
-            pad = t.shape[3] - bn.weight.shape[0]
-            rm = torch.cat([bn.running_mean, bn.running_mean.new_zeros(pad)])
-            rv = torch.cat([bn.running_var, bn.running_var.new_ones(pad)])
-            stats[i] = (rm, rv, bn.momentum, bn.eps)
-            padded.append((bn, rm, rv))
+    # 10-channel quarter branches stored as qp channels: every padded weight,
+    # BN parameter and running statistic in one PadFn launch, the running
+    # statistics cropped back in one launch after the forward
+    convs = (ssh.conv5X5_1[0], ssh.conv5X5_2[0], ssh.conv7X7_2[0], ssh.conv7x7_3[0])
+    pbns = (ssh.conv5X5_1[1], ssh.conv7X7_2[1], ssh.conv5X5_2[1], ssh.conv7x7_3[1])
+    spec = [(convs[0].weight, (qp,) + tuple(convs[0].weight.shape[1:]), 0.0)]
+    spec += [(cv.weight, (qp, qp) + tuple(cv.weight.shape[2:]), 0.0) for cv in convs[1:]]
+    for bn in pbns:
+        spec += [(bn.weight, (qp,), 0.0), (bn.bias, (qp,), 0.0),
+                 (bn.running_mean, (qp,), 0.0), (bn.running_var, (qp,), 1.0)]
+    pt = _padded(spec)
+    w51, w52, w72, w73 = pt[:4]
+    pb = [pt[4 + 4 * i:8 + 4 * i] for i in range(4)]  # (g, b, rm, rv) per padded BN
+
+    def bn_p(x, i):
+        g, bt, rm, rv = pb[i]
+        y = BnActFn.apply(x, g, bt, None, rm, rv, "leaky", ssh.leaky, pbns[i].momentum,
+                          pbns[i].eps)
+        _count_batch(pbns[i])
+        return y
+
+    b1a, b1b = fork(bn_p(first(w51), 0), 2)
+    b = ConvFn.apply(b1a, w52, None, 1, 1, False)
+    c1 = bn_p(ConvFn.apply(b1b, w72, None, 1, 1, False), 1)
+    c = ConvFn.apply(c1, w73, None, 1, 1, False)
+    bn0 = bns[0]
+    gb = [bn0.weight, bn0.bias, pb[2][0], pb[2][1], pb[3][0], pb[3][1]]
+    stats = [(bn0.running_mean, bn0.running_var, bn0.momentum, bn0.eps),
+             (pb[2][2], pb[2][3], pbns[2].momentum, pbns[2].eps),
+             (pb[3][2], pb[3][3], pbns[3].momentum, pbns[3].eps)]
+    for bn in bns:
+        _count_batch(bn)
     f = SshTailFn.apply(a, b, c, *gb, stats)
     with torch.no_grad():
-        for bn, rm, rv in padded:
-            bn.running_mean.copy_(rm[: bn.running_mean.shape[0]])
-            bn.running_var.copy_(rv[: bn.running_var.shape[0]])
+        F.window_copies([(pb[i][2 + j], (bn.running_mean, bn.running_var)[j], 0.0)
+                         for i, bn in enumerate(pbns) for j in (0, 1)])
     half = a.shape[3]
     if padded_out:
-        idx = (list(range(half)) + list(range(half, half + q))
-               + list(range(half + qp, half + qp + q)))
-        return f, torch.tensor(idx, dtype=torch.long, device=f.device)
+        return f, (half, q, qp)
     # drop the zero pad channels of the 10-channel branches
     f = torch.cat([f[..., :half], f[..., half:half + q], f[..., half + qp:half + qp + q]], -1)
     return f.contiguous()
@@ -1148,11 +1270,12 @@ def _head(m, feats, eca_names, nlm):
     ew = m.eca_fpn.conv.weight
     if gate == "beca":
         from .ops import BecaFn
-        outs = [ssh_train(ssh, BecaFn.apply(o, ew.reshape(-1)), padded_out=True)
-                for o, ssh in zip((o1, o2, o3), (m.ssh1, m.ssh2, m.ssh3))]
-    else:
-        outs = [ssh_train(ssh, o, ew, padded_out=True)
-                for o, ssh in zip((o1, o2, o3), (m.ssh1, m.ssh2, m.ssh3))]
+        outs = [ssh_train(ssh, BecaFn.apply(o, e.reshape(-1)), padded_out=True)
+                for o, ssh, e in zip((o1, o2, o3), (m.ssh1, m.ssh2, m.ssh3), fork(ew, 3))]
+    else:  # the shared eca weight: one alias per use (two per SSH)
+        ews = fork(ew, 6)
+        outs = [ssh_train(ssh, o, ews[2 * i:2 * i + 2], padded_out=True)
+                for i, (o, ssh) in enumerate(zip((o1, o2, o3), (m.ssh1, m.ssh2, m.ssh3)))]
     wb = []
     for i in range(3):
         for h in (m.BboxHead[i], m.ClassHead[i], m.LandmarkHead[i]):
@@ -1174,10 +1297,15 @@ def _train_forward(model, kind, x):
         s = bn_act(conv(x, body.conv1, 2, 1, nchw_in=True), body.bn1, "hswish")
         feats = []
         from .engine import mnv3_stages
-        for stage in mnv3_stages(body):
+        stages = list(mnv3_stages(body))
+        for i, stage in enumerate(stages):
             for blk in stage:
                 s = _mnv3_block(blk, s)
-            feats.append(s)
+            if i + 1 < len(stages):  # feeds the next stage and the FPN
+                s, f = fork(s, 2)
+            else:
+                f = s
+            feats.append(f)
         return _head(model, feats, getattr(model, "eca_names", ("eca_40", "eca_80", "eca_160")),
                      model.fpn.nlm)
     body = model.body
@@ -1187,6 +1315,9 @@ def _train_forward(model, kind, x):
     for i in (1, 2, 3, 4):
         for blk in getattr(body, f"layer{i}"):
             s = _r50_block(blk, s)
-        if i >= 2:
+        if i in (2, 3):  # feeds the next stage and the FPN
+            s, f = fork(s, 2)
+            feats.append(f)
+        elif i == 4:
             feats.append(s)
     return _head(model, feats, ("eca_64", "eca_128", "eca_256"), model.fpn.Nlm)

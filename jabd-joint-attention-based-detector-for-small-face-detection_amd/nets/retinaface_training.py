@@ -16,6 +16,7 @@ import torch
 import torch.nn as nn
 
 from jabd_amd import ops
+from jabd_amd.functional import window_copies
 
 
 class _MultiBoxLossFn(torch.autograd.Function):
@@ -35,10 +36,12 @@ class _MultiBoxLossFn(torch.autograd.Function):
     def backward(ctx, g_l, g_c, g_lm):
         loc, conf, landm, loc_t, conf_t, landm_t, sel, counts = ctx.saved_tensors
         dev = loc.device
-        z = torch.zeros((), device=dev)
-        gout = torch.stack([g if g is not None else z for g in (g_l, g_c, g_lm)]).float()
+        # the three scalar gradients as one [3] vector, one launch
+        gout = torch.empty(3, dtype=torch.float32, device=dev)
+        window_copies([(g.detach().float().contiguous() if g is not None else None,
+                        gout[i:i + 1], 0.0) for i, g in enumerate((g_l, g_c, g_lm))])
         gl, gc, glm = ops.multibox_backward(loc, conf, landm, loc_t, conf_t, landm_t, sel,
-                                            gout.contiguous(), counts, ctx.diou)
+                                            gout, counts, ctx.diou)
         return gl, gc, glm, None, None, None, None, None, None
 
 

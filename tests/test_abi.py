@@ -46,6 +46,6 @@ def test_struct_mirrors_match_the_library():
     """ctypes mirrors of the argument structs have the C sizes (a field added
     on one side only would shift every later field)."""
     import ctypes
-    from jabd_amd._lib import ConvArgs, DwArgs, ExpDwArgs, lib
-    for i, cls in enumerate((ConvArgs, DwArgs, ExpDwArgs)):
+    from jabd_amd._lib import ConvArgs, DwArgs, ExpDwArgs, WindowCopy, lib
+    for i, cls in enumerate((ConvArgs, DwArgs, ExpDwArgs, WindowCopy)):
         assert lib().jabd_abi_struct_size(i) == ctypes.sizeof(cls), cls.__name__
