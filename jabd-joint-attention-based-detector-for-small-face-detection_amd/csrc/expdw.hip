@@ -436,6 +436,231 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
 }
 
 
+// ---------------------------------------------------------------------------
+// Stride-1 strip form: a workgroup owns one column strip (NPX = 16 NB input
+// columns, NPX - 2 PAD output columns) of a band of rows of one image, for EC
+// expanded channels, and walks down the band R rows at a time.  The expanded
+// rows live in an LDS ring of R + 2 PAD rows, so each expanded row is
+// computed once (no vertical halo recompute) and the band's fixed costs (item
+// decode, weight and bias loads, ECA reduction) are paid once per band, not
+// per 16x16 tile.  The input stages form one flat software pipeline over
+// (row step, 16-channel stage): the next stage's global loads are in flight
+// while the current stage's MFMAs, and at a step's end the epilogue and the
+// depthwise phase, run.
+// ---------------------------------------------------------------------------
+template <int K, int EC, int NB, int R>
+struct XsCfg {
+  static constexpr int PAD = K / 2;
+  static constexpr int NPX = 16 * NB, OWS = NPX - 2 * PAD;
+  static constexpr int NR = R + 2 * PAD;
+  static constexpr int EP = EC + 4;
+  static constexpr int NT = EC / 16, NC4 = EC / 4;
+  static constexpr int SPX = R * NPX;             // staged pixels per step
+  static constexpr int NPF = SPX * 4 / 256;       // float4 stage slots per thread
+  static constexpr int NBLK = R * NB * NT, BPW = NBLK / 4;
+  static constexpr int PW = 2, NSTRIP = OWS / PW;
+  static constexpr int ITEMS = R * NSTRIP * NC4;
+  static constexpr int SPAN = PW + K - 1;
+  static constexpr int LDS_X = 16 * SPX, LDS_E = NR * NPX * EP;
+  static_assert(SPX * 4 % 256 == 0 && NBLK % 4 == 0 && 4 % NT == 0, "strip shape");
+  static_assert(OWS % PW == 0, "strip width");
+  static_assert((LDS_X + LDS_E) * 4 + (K * K + 1) * EC * 4 <= 80 * 1024, "LDS");
+  static_assert(LDS_X >= 4 * 256, "ECA reduction buffer aliases the stage buffer");
+};
+
+template <int K, int EC, int NB, int R, int ACT>
+__global__ __launch_bounds__(256, 2) void expdw_strip_kernel(const jabd_expdw_args p,
+                                                             const XdDivs dv, int nitems,
+                                                             int nstrip, int hb) {
+  using C = XsCfg<K, EC, NB, R>;
+  __shared__ __attribute__((aligned(16))) float xs[C::LDS_X];
+  __shared__ __attribute__((aligned(16))) float er[C::LDS_E];
+  __shared__ float4 wsh[K * K + 1][C::NC4];
+  float4* red = reinterpret_cast<float4*>(xs);  // ECA reduction after the last step
+  // item -> (image, band, strip, channel chunk); the chunks of one strip on
+  // one XCD (blockIdx % 8), as in xd_item
+  const int i = blockIdx.x;
+  if (i >= nitems) return;
+  const int xcd = i & 7, q = i >> 3;
+  const int qn = fdiv(q, dv.nch);
+  const int chunk = q - qn * (int)dv.nch.d;
+  const int tile = qn * 8 + xcd;
+  if (tile >= p.B * (int)dv.tiles_img.d) return;
+  const int b = fdiv(tile, dv.tiles_img);
+  const int t_in = tile - b * (int)dv.tiles_img.d;
+  const int band = t_in / nstrip, strip = t_in - band * nstrip;
+  const int hb0 = band * hb, hb1 = min(hb0 + hb, p.OH);
+  const int ow0 = strip * C::OWS, iw0 = ow0 - C::PAD;
+  const int c0 = chunk * EC;
+  const int t = threadIdx.x, lane = t & 63, j = lane & 15, g = lane >> 4;
+  const int wave = t >> 6;
+  const int ntw = wave % C::NT;
+  const int nt = c0 / 16 + ntw;
+  const bool ntv = nt < p.Ntiles;
+  const int ntc = ntv ? nt : 0;
+  const f32x4* wpk = reinterpret_cast<const f32x4*>(p.we);
+  const int chb = c0 + 16 * ntw + 4 * g;
+  const bool chok = chb < p.E;
+  const float4 pbi = *reinterpret_cast<const float4*>(p.be + (chok ? chb : 0));
+  const f32x4 bias4 = (f32x4){pbi.x, pbi.y, pbi.z, pbi.w};
+  for (int u = t; u < (K * K + 1) * C::NC4; u += 256) {
+    const int tp = u / C::NC4, cc = c0 + 4 * (u - tp * C::NC4);
+    const float4 w = *reinterpret_cast<const float4*>((tp < K * K ? p.wd + tp * p.E : p.bd) +
+                                                      (cc < p.E ? cc : 0));
+    wsh[tp][u - tp * C::NC4] = cc < p.E ? w : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.x), (short)0, (int)(uint32_t)((int64_t)p.B * p.x_bs * 4), 0x00020000);
+  const int cq = ((t >> 4) & 3) * 4;
+  const int spx0 = (t >> 6) * 16 + (t & 15);
+  // expanded rows are computed from input row e0 = hb0 - PAD on, R per step
+  const int e0 = hb0 - C::PAD;
+  const int nsteps = (hb1 - hb0 + 2 * C::PAD + R - 1) / R;
+  const int nitem = nsteps * p.Kc;
+  float4 pf[C::NPF];
+  auto load_stage = [&](int it) {
+    const int s = it / p.Kc, kc = it - s * p.Kc;
+    const int cofs = 16 * kc + cq;
+    const uint32_t base = (uint32_t)(b * p.x_bs + cofs);
+    const bool cok = cofs < p.Cin;
+#pragma unroll
+    for (int u = 0; u < C::NPF; ++u) {
+      const int px = u * 64 + spx0;
+      const int r = px / C::NPX, c = px - r * C::NPX;
+      const int ih = e0 + s * R + r, iw = iw0 + c;
+      const bool ok = cok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      const uint32_t off = ok ? (base + (uint32_t)((ih * p.W + iw) * p.x_ps)) * 4u : 0xFFFFFFF0u;
+      pf[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+    }
+  };
+  int c4, sl;
+  dw_lane<C::NC4>(lane, c4, sl);
+  const int chl = 4 * c4;
+  const bool chv = c0 + chl < p.E;
+  float* yb = p.y + (int64_t)b * p.y_bs + c0 + chl;
+  float4 psum = make_float4(0.f, 0.f, 0.f, 0.f);
+  f32x4 acc[C::BPW];
+  load_stage(0);
+  for (int it = 0; it < nitem; ++it) {
+    const int s = it / p.Kc, kc = it - s * p.Kc;
+    if (kc == 0) {
+#pragma unroll
+      for (int u = 0; u < C::BPW; ++u) acc[u] = bias4;
+    }
+    f32x4 a = wpk[(kc * p.Ntiles + ntc) * 64 + lane];
+#pragma unroll
+    for (int u = 0; u < C::NPF; ++u)
+      *reinterpret_cast<float4*>(xs + ((cq / 4) * C::SPX + u * 64 + spx0) * 4) = pf[u];
+    if (!ntv) a = (f32x4){0.f, 0.f, 0.f, 0.f};
+    asm volatile("" : "+v"(a));
+    lds_barrier();
+    if (it + 1 < nitem) load_stage(it + 1);
+    if (ntv) {
+#pragma unroll
+      for (int u = 0; u < C::BPW; ++u) {
+        const int pb = (wave + 4 * u) / C::NT;
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(xs + (g * C::SPX + pb * 16 + j) * 4);
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bv.x, acc[u], 0, 0, 0);
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bv.y, acc[u], 0, 0, 0);
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bv.z, acc[u], 0, 0, 0);
+        acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bv.w, acc[u], 0, 0, 0);
+      }
+    }
+    if (kc + 1 < p.Kc) {
+      lds_barrier();
+      continue;
+    }
+    // step s complete: activated rows e0 + s R .. + R - 1 into the ring (zero
+    // outside the image: the depthwise conv zero-pads the activated map)
+#pragma unroll
+    for (int u = 0; u < C::BPW; ++u) {
+      const int pb = (wave + 4 * u) / C::NT;
+      const int px = pb * 16 + j;
+      const int r = px / C::NPX, c = px - r * C::NPX;
+      const int ih = e0 + s * R + r, iw = iw0 + c;
+      const bool ok = chok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+      const int slot = (s * R + r) % C::NR;
+      float4 o;
+      o.x = ok ? xd_act<ACT>(acc[u][0]) : 0.f;
+      o.y = ok ? xd_act<ACT>(acc[u][1]) : 0.f;
+      o.z = ok ? xd_act<ACT>(acc[u][2]) : 0.f;
+      o.w = ok ? xd_act<ACT>(acc[u][3]) : 0.f;
+      *reinterpret_cast<float4*>(er + (slot * C::NPX + c) * C::EP + 16 * ntw + 4 * g) = o;
+    }
+    lds_barrier();  // LDS only: keeps the next stage's loads in flight
+    // depthwise: output rows oh = hb0 + s R - 2 PAD + orow, those inside the band
+    if (chv) {
+      const float4 bias2 = wsh[K * K][c4];
+#pragma unroll 1
+      for (int pass = 0; pass * 256 < C::ITEMS; ++pass) {
+        const int item = (pass * 4 + wave) * (64 / C::NC4) + sl;
+        if (item >= R * C::NSTRIP) break;
+        const int orow = item / C::NSTRIP, st = item - orow * C::NSTRIP;
+        const int oh = hb0 + s * R - 2 * C::PAD + orow;
+        const int owb = ow0 + st * C::PW;
+        if (oh < hb0 || oh >= hb1 || owb >= p.OW) continue;
+        float4 a2[C::PW];
+#pragma unroll
+        for (int o = 0; o < C::PW; ++o) a2[o] = bias2;
+#pragma unroll 1
+        for (int kh = 0; kh < K; ++kh) {
+          const int slot = (oh - e0 - C::PAD + kh) % C::NR;
+          const float* rowp = er + (slot * C::NPX + st * C::PW) * C::EP + chl;
+          float4 row[C::SPAN];
+#pragma unroll
+          for (int c = 0; c < C::SPAN; ++c)
+            row[c] = *reinterpret_cast<const float4*>(rowp + c * C::EP);
+          float4 wk[K];
+#pragma unroll
+          for (int kw = 0; kw < K; ++kw) wk[kw] = wsh[kh * K + kw][c4];
+#pragma unroll
+          for (int o = 0; o < C::PW; ++o)
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw) {
+              const float4 xv = row[o + kw], wv = wk[kw];
+              a2[o].x = fmaf(xv.x, wv.x, a2[o].x);
+              a2[o].y = fmaf(xv.y, wv.y, a2[o].y);
+              a2[o].z = fmaf(xv.z, wv.z, a2[o].z);
+              a2[o].w = fmaf(xv.w, wv.w, a2[o].w);
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < C::PW; ++o) {
+          if (owb + o >= p.OW) break;
+          float4 v;
+          v.x = xd_act<ACT>(a2[o].x);
+          v.y = xd_act<ACT>(a2[o].y);
+          v.z = xd_act<ACT>(a2[o].z);
+          v.w = xd_act<ACT>(a2[o].w);
+          *reinterpret_cast<float4*>(yb + ((int64_t)oh * p.OW + owb + o) * p.y_ps) = v;
+          psum.x += v.x; psum.y += v.y; psum.z += v.z; psum.w += v.w;
+        }
+      }
+    }
+    // the next step's first stage rewrites xs only after this barrier; the
+    // ring rows this step read are rewritten after the next step's barriers
+    lds_barrier();
+  }
+  if (p.part) {
+    __syncthreads();
+    red[t] = psum;
+    __syncthreads();
+    if (t < C::NC4 && c0 + 4 * t < p.E) {
+      // threads holding channel quad t (dw_lane), summed in thread order
+      float4 sm = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int u = 0; u < 256; ++u) {
+        int cu, su;
+        dw_lane<C::NC4>(u & 63, cu, su);
+        if (cu != t) continue;
+        const float4 v = red[u];
+        sm.x += v.x; sm.y += v.y; sm.z += v.z; sm.w += v.w;
+      }
+      *reinterpret_cast<float4*>(p.part + ((int64_t)b * (int)dv.tiles_img.d + t_in) * p.E + c0 +
+                                 4 * t) = sm;
+    }
+  }
+}
+
 struct XdTile {
   int th, tw;
 };
@@ -477,8 +702,50 @@ static int xd_nw(const jabd_expdw_args& a, int EC) {
   return 4;
 }
 
+// Strip form (stride 1), JABD_EXPDW_STRIP=1 for A/B; off by default: it
+// measured slower than the 16x16 tile kernel on every stride-1 layer (b1
+// 295 vs 271 us, b3 405 vs 347, b12 525 vs 347, b15 346 vs 204;
+// tools/convbench.py --set xd): a row step carries less MFMA work per input
+// stage and per barrier than a tile, and the NB = 3 / EC = 32 form holds
+// 55 KB of LDS (2 workgroups per CU).  See DESIGN.md section 4.
+static bool xs_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("JABD_EXPDW_STRIP");
+    on = e && e[0] == '1' ? 1 : 0;
+  }
+  return on == 1;
+}
+
+struct XsPlan {
+  int nb, nstrip, hb, nband;
+};
+
+// strip width 16 NB input columns: the NB in {2, 3} with the fewest computed
+// columns (the smaller on ties); bands of 64 rows on maps >= 256 rows, else 32
+static XsPlan xs_plan(int OH, int OW, int k) {
+  XsPlan pl;
+  int best = 0;
+  for (int nb = 2; nb <= 3; ++nb) {
+    const int ows = 16 * nb - 2 * (k / 2);
+    const int ns = (int)cdiv(OW, ows);
+    if (!best || ns * 16 * nb < best) {
+      best = ns * 16 * nb;
+      pl.nb = nb;
+      pl.nstrip = ns;
+    }
+  }
+  pl.hb = OH >= 256 ? 64 : 32;
+  pl.nband = (int)cdiv(OH, pl.hb);
+  return pl;
+}
+
 extern "C" int64_t jabd_expand_dw_nblk(int32_t OH, int32_t OW, int32_t k, int32_t stride) {
   if (OH <= 0 || OW <= 0 || (stride != 1 && stride != 2)) return -1;
+  if (stride == 1 && xs_enabled()) {
+    const XsPlan pl = xs_plan(OH, OW, k);
+    return (int64_t)pl.nband * pl.nstrip;
+  }
   const XdTile tl = xd_tile(k, stride);
   return cdiv(OH, tl.th) * cdiv(OW, tl.tw);
 }
@@ -501,6 +768,39 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
                          a.Cin <= 160),
                "expand_dw: the fused skip branch needs stride 2, Cin <= 160, weights, bias and "
                "sy_ps %% 4 == 0");
+  if (a.stride == 1 && xs_enabled()) {
+    const XsPlan pl = xs_plan(a.OH, a.OW, a.k);
+    const int tiles_img = pl.nband * pl.nstrip;
+    JABD_REQUIRE(!a.part || a.nblk == tiles_img, "expand_dw: nblk %d != %d", a.nblk, tiles_img);
+    const int EC = a.E <= 16 ? 16 : 32;
+    const int nch = (int)cdiv(a.E, EC);
+    const int64_t nitems = cdiv((int64_t)a.B * tiles_img, 8) * 8 * nch;
+    JABD_REQUIRE(nitems < ((int64_t)1 << 31) && (int64_t)a.H * a.W * a.x_ps < ((int64_t)1 << 31) &&
+                     (int64_t)a.B * a.x_bs * 4 < ((int64_t)1 << 32) - 16,
+                 "expand_dw: problem too large for 32-bit indexing / buffer offsets (split the batch)");
+    const XdDivs dv{make_fastdiv((uint32_t)nch), make_fastdiv((uint32_t)tiles_img),
+                    make_fastdiv((uint32_t)pl.nstrip)};
+    hipStream_t st = as_stream(stream);
+#define XS_LAUNCH(K_, EC_, NB_, ACT_)                                                       \
+  expdw_strip_kernel<K_, EC_, NB_, 4, ACT_><<<(unsigned)nitems, 256, 0, st>>>(a, dv, (int)nitems, \
+                                                                             pl.nstrip, pl.hb)
+#define XS_ACTS(K_, EC_, NB_)                              \
+  if (a.k == K_ && EC == EC_ && pl.nb == NB_) {            \
+    if (a.act == ACT_RELU)                                 \
+      XS_LAUNCH(K_, EC_, NB_, ACT_RELU);                   \
+    else if (a.act == ACT_HSWISH)                          \
+      XS_LAUNCH(K_, EC_, NB_, ACT_HSWISH);                 \
+    else                                                   \
+      XS_LAUNCH(K_, EC_, NB_, ACT_NONE);                   \
+    return check_launch("expand_dw_strip");                \
+  }
+    XS_ACTS(3, 16, 2) XS_ACTS(3, 16, 3) XS_ACTS(3, 32, 2) XS_ACTS(3, 32, 3)
+    XS_ACTS(5, 16, 2) XS_ACTS(5, 16, 3) XS_ACTS(5, 32, 2) XS_ACTS(5, 32, 3)
+#undef XS_ACTS
+#undef XS_LAUNCH
+    set_error("expand_dw: no strip kernel for k=%d", a.k);
+    return JABD_EINVAL;
+  }
   const XdTile tl = xd_tile(a.k, a.stride);
   const int tiles_w = (int)cdiv(a.OW, tl.tw);
   const int tiles_img = (int)cdiv(a.OH, tl.th) * tiles_w;
