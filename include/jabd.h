@@ -411,6 +411,11 @@ typedef struct jabd_expdw_args {
 } jabd_expdw_args;
 int64_t jabd_expand_dw_nblk(int32_t OH, int32_t OW, int32_t k, int32_t stride);
 int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_t stream);
+/* Kernel form of jabd_expand_dw_nhwc_f32 (same results bit for bit): 1 = one
+ * work item per workgroup, 2 = wave-specialised persistent workgroups, 0 =
+ * the default (1, or 2 with JABD_EXPDW_WS=1).  Returns the
+ * previous setting.  For A/B timing and the equivalence test. */
+int jabd_expand_dw_select(int32_t form);
 
 /* Per-(image, block, channel) sums of an NHWC tensor (ECA pooling of a tensor
  * not produced by the dw kernel: C3/C4/C5 and the FPN outputs). */

@@ -31,7 +31,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // Phase-skip mask for timing experiments only (tools/xd_variant.sh builds
 // libraries with -DXD_SKIP=n; results are wrong): 1 expand MFMAs, 2 expanded-
-// tile LDS writes, 4 depthwise phase, 8 ECA reduce, 16 input loads.
+// tile LDS writes, 4 depthwise phase, 8 ECA reduce, 16 input loads;
+// expdw_ws_kernel: 32 expand-wave MFMAs, 64 depthwise-wave depthwise phase,
+// 128 expand-wave input loads (out-of-range offsets: zeros, no traffic), 256
+// expand-wave epilogue (activation + expanded-tile writes).
 #ifndef XD_SKIP
 #define XD_SKIP 0
 #endif
@@ -661,9 +664,389 @@ __global__ __launch_bounds__(256, 2) void expdw_strip_kernel(const jabd_expdw_ar
   }
 }
 
+// ---------------------------------------------------------------------------
+// Wave-specialised persistent form (JABD_EXPDW_WS=1; off by default, see
+// xw_enabled).  Phase-skip builds of expdw1_kernel (XD_SKIP) showed its
+// expand-MFMA and depthwise phases are additive in wall time (skipping both
+// saves the sum of skipping each): the resident workgroups run their phases
+// in step and never overlap matrix work with vector work.  Here one
+// workgroup per CU (XW_NE expand waves + 4 depthwise waves) walks its items
+// (item = blockIdx.x + n * gridDim.x, same XCD-aware decode) as a two-role
+// pipeline:
+//  * expand waves: wave w owns pixel blocks w, w + XW_NE, ... of the staged
+//    tile for every 16-channel n-tile; its B operands (pixel j, channel quad
+//    g of a 16-channel stage) are loaded straight into registers through the
+//    buffer descriptor (no LDS staging, no barrier per stage) from a D-deep
+//    ring of stages that runs across item boundaries; the activated tile is
+//    written to expanded buffer (item & 1);
+//  * depthwise waves: the depthwise phase, ECA partials and the fused
+//    skip branch of the previous item from the other buffer.
+// Step n: expand item n while the depthwise waves finish item n - 1; one
+// LDS-only barrier per step.  Each output element is computed by exactly the
+// operation sequence of expdw1_kernel (accumulators start at the bias, the
+// same k order of MFMAs, the same depthwise lane map, tap order and ECA
+// reduction), so the two kernels agree bit for bit.
+// ---------------------------------------------------------------------------
+// expand waves per workgroup (the depthwise waves are always 4)
+#ifndef XW_NE
+#define XW_NE 4
+#endif
+template <int K, int S, int TH, int TW, int EC, bool SKIP>
+struct XwCfg {
+  using C = XdCfg<K, S, TH, TW, EC>;
+  static constexpr int NE = XW_NE, NT = 64 * (NE + 4);
+  static constexpr int NBW = (C::NPB + NE - 1) / NE;  // pixel blocks per expand wave
+  static constexpr int SKC = SKIP ? 160 : 4;
+  // dynamic LDS: expanded buffers, depthwise taps, ECA partials, skip taps
+  static constexpr int OFF_W = 2 * C::LDS_E * 4;
+  static constexpr int OFF_R = OFF_W + 2 * (K * K + 1) * C::NC4 * 16;
+  static constexpr int OFF_S = OFF_R + 2 * 4 * C::NC4 * 16;
+  static constexpr int BYTES = OFF_S + 10 * (SKC / 4) * 16;
+  static_assert(BYTES <= 160 * 1024, "LDS");
+};
+
+template <int NBW, int NNT>
+struct XwSlot {
+  float4 b[NBW];
+  f32x4 a[NNT];
+  float4 bias[NNT];
+  float4 taps;  // depthwise tap / bias float4 (thread t < NWD) of the item's chunk
+};
+
+template <int NBW, int NNT>
+__device__ __forceinline__ void xw_touch(XwSlot<NBW, NNT>& sl) {
+#pragma unroll
+  for (int u = 0; u < NBW; ++u)
+    asm volatile("" : "+v"(sl.b[u].x), "+v"(sl.b[u].y), "+v"(sl.b[u].z), "+v"(sl.b[u].w));
+#pragma unroll
+  for (int nt = 0; nt < NNT; ++nt) {
+    asm volatile("" : "+v"(sl.a[nt]));
+    asm volatile("" : "+v"(sl.bias[nt].x), "+v"(sl.bias[nt].y), "+v"(sl.bias[nt].z),
+                 "+v"(sl.bias[nt].w));
+  }
+  asm volatile("" : "+v"(sl.taps.x), "+v"(sl.taps.y), "+v"(sl.taps.z), "+v"(sl.taps.w));
+}
+
+// One stage's MFMAs of an expand wave: blocks u < NBU, n-tiles nt < NTU, k
+// order x, y, z, w per accumulator (as expdw1_kernel), independent
+// accumulators interleaved.
+template <int NBU, int NTU, int NBW, int NNT>
+__device__ __forceinline__ void xw_mfma(f32x4 (&acc)[NBW][NNT], const XwSlot<NBW, NNT>& sl) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int u = 0; u < NBU; ++u)
+#pragma unroll
+      for (int nt = 0; nt < NTU; ++nt) {
+        const float av = e == 0 ? sl.a[nt].x : e == 1 ? sl.a[nt].y : e == 2 ? sl.a[nt].z : sl.a[nt].w;
+        const float bv = e == 0 ? sl.b[u].x : e == 1 ? sl.b[u].y : e == 2 ? sl.b[u].z : sl.b[u].w;
+        acc[u][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[u][nt], 0, 0, 0);
+      }
+}
+
+template <int K, int S, int TH, int TW, int EC, int ACT, bool SKIP, int D>
+__global__ __launch_bounds__(64 * (XW_NE + 4)) void expdw_ws_kernel(const jabd_expdw_args p, const XdDivs dv,
+                                                      int nitems) {
+  using C = XdCfg<K, S, TH, TW, EC>;
+  using W = XwCfg<K, S, TH, TW, EC, SKIP>;
+  constexpr int NBW = W::NBW, NNT = C::NNT, NC4 = C::NC4, NE = W::NE;
+  constexpr int NWD = (K * K + 1) * NC4;
+  static_assert(NWD <= 64 * NE, "taps: one float4 per expand thread");
+  extern __shared__ __attribute__((aligned(16))) unsigned char xw_smem[];
+  float* ebuf = reinterpret_cast<float*>(xw_smem);                            // [2][LDS_E]
+  float4* wsh = reinterpret_cast<float4*>(xw_smem + W::OFF_W);                // [2][K*K+1][NC4]
+  float4* red = reinterpret_cast<float4*>(xw_smem + W::OFF_R);                // [2][4][NC4]
+  float4* sws = reinterpret_cast<float4*>(xw_smem + W::OFF_S);                // [10][SKC/4]
+  const int G = gridDim.x;
+  const int nmine = (nitems - (int)blockIdx.x + G - 1) / G;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  if (SKIP) {
+    for (int i = t; i < 10 * (p.Cin >> 2); i += W::NT) {
+      const int q = i / (p.Cin >> 2), c4 = i - q * (p.Cin >> 2);
+      sws[q * (W::SKC / 4) + c4] =
+          *reinterpret_cast<const float4*>((q < 9 ? p.sw + q * p.Cin : p.sb) + 4 * c4);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.x), (short)0, (int)(uint32_t)((int64_t)p.B * p.x_bs * 4), 0x00020000);
+  auto decode = [&](int n, XdItem& it) -> bool {
+    it = XdItem{0, 0, 0, 0, 0, 0, 0};
+    return n < nmine && xd_item<K, S, TH, TW, EC>(p, (int)blockIdx.x + n * G, dv, nitems, it);
+  };
+
+  if (wave < NE) {
+    // ------------------------------------------------------------- expand
+    const int j = lane & 15, g = lane >> 4;
+    const f32x4* wpk = reinterpret_cast<const f32x4*>(p.we);
+    const int U = (nmine * p.Kc + D - 1) / D * D;  // stages, padded to the ring depth
+    int ls = 0, lkc = 0;                            // load cursor (item seq, stage)
+    XdItem li;
+    bool lv = decode(0, li);
+    // per-item load state of the load cursor's item: byte offsets of each
+    // block's (pixel, channel 4g) at stage 0 (0xFFFFFFF0: out of the image /
+    // tile, reads zeros), weight / bias / tap indices; a stage then only adds
+    // its 64-byte channel offset (the address arithmetic stays out of the
+    // per-stage instruction stream)
+    uint32_t boff[NBW];
+    int aoff[NNT], boffb[NNT];
+    const float* tptr = p.bd;
+    auto prep = [&]() {
+#pragma unroll
+      for (int u = 0; u < NBW; ++u) {
+        const int pb = wave + NE * u;
+        const int px = pb * 16 + j;
+        const int r = px / C::IW, c = px - r * C::IW;
+        const int ih = li.ih0 + r, iw = li.iw0 + c;
+        const bool ok = lv && px < C::IPX && (unsigned)ih < (unsigned)p.H &&
+                        (unsigned)iw < (unsigned)p.W && !(XD_SKIP & 128);
+        boff[u] = ok ? (uint32_t)(li.b * p.x_bs + (ih * p.W + iw) * p.x_ps + 4 * g) * 4u
+                     : 0xFFFFF000u;  // stays out of range (host: x < 0xFFFFF000 bytes) + 64 Kc
+      }
+#pragma unroll
+      for (int nt = 0; nt < NNT; ++nt) {
+        const int ntg = li.c0 / 16 + nt;
+        aoff[nt] = (lv && ntg < p.Ntiles ? ntg : 0) * 64 + lane;
+        const int chb = li.c0 + 16 * nt + 4 * g;
+        boffb[nt] = chb < p.E ? chb : 0;
+      }
+      const int dd = t < NWD ? t : 0;
+      const int tp = dd / NC4, cc = li.c0 + 4 * (dd - tp * NC4);
+      tptr = (tp < K * K ? p.wd + tp * p.E : p.bd) + (cc < p.E ? cc : 0);
+    };
+    prep();
+    auto issue = [&](XwSlot<NBW, NNT>& sl) {
+      // channels past Cin read zeros: the offset is raised out of range by a
+      // max (no select / branch per load)
+      const uint32_t lim = 16 * lkc + 4 * g < p.Cin ? 0u : 0xFFFFF000u;
+#pragma unroll
+      for (int u = 0; u < NBW; ++u) {
+        const uint32_t off = max(boff[u] + 64u * (uint32_t)lkc, lim);
+        sl.b[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+      }
+#pragma unroll
+      for (int nt = 0; nt < NNT; ++nt) {
+        sl.a[nt] = wpk[aoff[nt] + lkc * p.Ntiles * 64];
+        sl.bias[nt] = *reinterpret_cast<const float4*>(p.be + boffb[nt]);
+      }
+      sl.taps = *reinterpret_cast<const float4*>(tptr);
+      if (++lkc == p.Kc) {
+        lkc = 0;
+        ++ls;
+        lv = decode(ls, li);
+        prep();
+      }
+    };
+    int cs = 0, ckc = 0;  // consume cursor
+    XdItem ci;
+    bool cv = decode(0, ci);
+    f32x4 acc[NBW][NNT];
+    float4 taps = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto stage = [&](XwSlot<NBW, NNT>& sl) {
+      // retire this slot's loads on every path here: a load left pending on
+      // a path that skips its consumer (an unused n-tile, an invalid item)
+      // makes the compiler wait before the slot's registers are reused,
+      // draining the other slots' loads too (one stage of latency cover)
+      xw_touch(sl);
+      if (ckc == 0) {
+        taps = sl.taps;
+#pragma unroll
+        for (int u = 0; u < NBW; ++u)
+#pragma unroll
+          for (int nt = 0; nt < NNT; ++nt)
+            acc[u][nt] = (f32x4){sl.bias[nt].x, sl.bias[nt].y, sl.bias[nt].z, sl.bias[nt].w};
+      }
+      // every wave runs the full NBW x NNT block of MFMAs: blocks past the
+      // tile read zeros, n-tiles past E and invalid items compute values
+      // the epilogue never stores (a uniform branch per variant made the
+      // compiler shuffle accumulators between variants)
+      if (!(XD_SKIP & 32)) xw_mfma<NBW, NNT>(acc, sl);
+      issue(sl);  // this slot's registers now take the stage D ahead
+      if (ckc == p.Kc - 1 && cs < nmine) {
+        if (cv && !(XD_SKIP & 256)) {
+          float* eb = ebuf + (cs & 1) * C::LDS_E;
+#pragma unroll
+          for (int u = 0; u < NBW; ++u) {
+            const int pb = wave + NE * u;
+            if (pb >= C::NPB) continue;
+            const int px = pb * 16 + j;
+            const int r = px / C::IW, c = px - r * C::IW;
+            const int ih = ci.ih0 + r, iw = ci.iw0 + c;
+            const bool pok = px < C::IPX && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+#pragma unroll
+            for (int nt = 0; nt < NNT; ++nt) {
+              const bool ok = pok && ci.c0 + 16 * nt + 4 * g < p.E;
+              float4 o;
+              o.x = ok ? xd_act<ACT>(acc[u][nt][0]) : 0.f;
+              o.y = ok ? xd_act<ACT>(acc[u][nt][1]) : 0.f;
+              o.z = ok ? xd_act<ACT>(acc[u][nt][2]) : 0.f;
+              o.w = ok ? xd_act<ACT>(acc[u][nt][3]) : 0.f;
+              *reinterpret_cast<float4*>(eb + px * C::EP + 16 * nt + 4 * g) = o;
+            }
+          }
+          if (t < NWD) {
+            const int tp = t / NC4, cc = ci.c0 + 4 * (t - tp * NC4);
+            const bool ok = cc < p.E;
+            wsh[(cs & 1) * NWD + t] =
+                make_float4(ok ? taps.x : 0.f, ok ? taps.y : 0.f, ok ? taps.z : 0.f, ok ? taps.w : 0.f);
+          }
+        }
+        if (!(XD_SKIP & 512)) lds_barrier();  // end of step cs: buffers (cs & 1) hold item cs
+      }
+      if (++ckc == p.Kc) {
+        ckc = 0;
+        ++cs;
+        cv = decode(cs, ci);
+      }
+    };
+    XwSlot<NBW, NNT> sl[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) issue(sl[d]);
+    for (int u = 0; u < U; u += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) stage(sl[d]);
+    }
+    if (!(XD_SKIP & 512)) lds_barrier();  // the depthwise waves' last step
+    return;
+  }
+  if (XD_SKIP & 512) return;
+
+  // ------------------------------------------------------------- depthwise
+  const int dt = t - 64 * NE, dwv = wave - NE;
+  auto finalize = [&](int n) {  // ECA partial of item n from red[n & 1]
+    XdItem it;
+    if (dwv != 0 || !decode(n, it) || !p.part) return;
+    if (lane < NC4 && it.c0 + 4 * lane < p.E) {
+      const float4* rb = red + (n & 1) * 4 * NC4;
+      float4 v[4];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) v[w] = rb[w * NC4 + lane];
+#pragma unroll
+      for (int h = 2; h >= 1; h >>= 1)
+#pragma unroll
+        for (int w = 0; w < h; ++w) {
+          v[w].x += v[w + h].x;
+          v[w].y += v[w + h].y;
+          v[w].z += v[w + h].z;
+          v[w].w += v[w + h].w;
+        }
+      *reinterpret_cast<float4*>(p.part + ((int64_t)it.b * (int)dv.tiles_img.d + it.t_in) * p.E +
+                                 it.c0 + 4 * lane) = v[0];
+    }
+  };
+  int c4, sl;
+  dw_lane<NC4>(lane, c4, sl);
+  const int chl = 4 * c4;
+  constexpr int SPW = 64 / NC4;
+  lds_barrier();  // the expand waves' step 0 (item 0)
+  for (int n = 0; n < nmine; ++n) {
+    XdItem it;
+    const bool valid = decode(n, it);
+    if (valid && SKIP && it.c0 == 0) {
+      // skip branch dw3x3/s2 + bias on x: output (orow, ocol), channel quad sq
+      const int nq = p.Cin >> 2;
+      for (int i = dt; i < 64 * nq; i += 256) {
+        const int sq = i >> 6, op = i & 63, orow = op / TW, ocol = op - orow * TW;
+        const int oh = it.oh0 + orow, ow = it.ow0 + ocol;
+        if (orow >= TH || oh >= p.OH || ow >= p.OW) continue;
+        float4 v = sws[9 * (W::SKC / 4) + sq];
+        const uint32_t base = (uint32_t)(it.b * p.x_bs + 4 * sq);
+#pragma unroll 1
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const int ih = 2 * oh + kh - 1, iw = 2 * ow + kw - 1;
+            const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+            const uint32_t off = ok ? (base + (uint32_t)((ih * p.W + iw) * p.x_ps)) * 4u : 0xFFFFFFF0u;
+            const float4 xv =
+                __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+            const float4 wv = sws[(kh * 3 + kw) * (W::SKC / 4) + sq];
+            v.x = fmaf(xv.x, wv.x, v.x);
+            v.y = fmaf(xv.y, wv.y, v.y);
+            v.z = fmaf(xv.z, wv.z, v.z);
+            v.w = fmaf(xv.w, wv.w, v.w);
+          }
+        *reinterpret_cast<float4*>(p.sy + (int64_t)it.b * p.sy_bs +
+                                   ((int64_t)oh * p.OW + ow) * p.sy_ps + 4 * sq) = v;
+      }
+    }
+    float4 psum = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (valid && it.c0 + chl < p.E && !(XD_SKIP & 64)) {
+      const float* eb = ebuf + (n & 1) * C::LDS_E;
+      const float4* wb = wsh + (n & 1) * (K * K + 1) * NC4;
+      const float4 bias2 = wb[K * K * NC4 + c4];
+      float* yb = p.y + (int64_t)it.b * p.y_bs + it.c0 + chl;
+#pragma unroll 1
+      for (int pass = 0; pass * 256 < C::ITEMS; ++pass) {
+        const int strip = (pass * 4 + dwv) * SPW + sl;
+        if (strip >= TH * C::NSTRIP) break;
+        const int orow = strip / C::NSTRIP, st = strip - orow * C::NSTRIP;
+        const int oh = it.oh0 + orow, owb = it.ow0 + st * C::PW;
+        if (oh >= p.OH || owb >= p.OW) continue;
+        float4 a2[C::PW];
+#pragma unroll
+        for (int o = 0; o < C::PW; ++o) a2[o] = bias2;
+#pragma unroll 1
+        for (int kh = 0; kh < K; ++kh) {
+          const float* rowp = eb + ((orow * S + kh) * C::IW + st * C::PW * S) * C::EP + chl;
+          float4 row[C::SPAN];
+#pragma unroll
+          for (int c = 0; c < C::SPAN; ++c)
+            row[c] = *reinterpret_cast<const float4*>(rowp + c * C::EP);
+          float4 wk[K];
+#pragma unroll
+          for (int kw = 0; kw < K; ++kw) wk[kw] = wb[(kh * K + kw) * NC4 + c4];
+#pragma unroll
+          for (int o = 0; o < C::PW; ++o)
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw) {
+              const float4 xv = row[o * S + kw], wv = wk[kw];
+              a2[o].x = fmaf(xv.x, wv.x, a2[o].x);
+              a2[o].y = fmaf(xv.y, wv.y, a2[o].y);
+              a2[o].z = fmaf(xv.z, wv.z, a2[o].z);
+              a2[o].w = fmaf(xv.w, wv.w, a2[o].w);
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < C::PW; ++o) {
+          if (owb + o >= p.OW) break;
+          float4 v;
+          v.x = xd_act<ACT>(a2[o].x);
+          v.y = xd_act<ACT>(a2[o].y);
+          v.z = xd_act<ACT>(a2[o].z);
+          v.w = xd_act<ACT>(a2[o].w);
+          *reinterpret_cast<float4*>(yb + ((int64_t)oh * p.OW + owb + o) * p.y_ps) = v;
+          psum.x += v.x; psum.y += v.y; psum.z += v.z; psum.w += v.w;
+        }
+      }
+    }
+    if (p.part) {
+      constexpr int NX = NC4 == 8 ? 3 : 4;
+      constexpr int X8[3] = {12, 20, 32}, X4[4] = {4, 8, 16, 32};
+#pragma unroll
+      for (int r = 0; r < NX; ++r) {
+        const int off = NC4 == 8 ? X8[r] : X4[r];
+        psum.x += __shfl_xor(psum.x, off);
+        psum.y += __shfl_xor(psum.y, off);
+        psum.z += __shfl_xor(psum.z, off);
+        psum.w += __shfl_xor(psum.w, off);
+      }
+      if (lane < NC4) red[(n & 1) * 4 * NC4 + dwv * NC4 + lane] = psum;
+      if (n >= 1) finalize(n - 1);
+    }
+    lds_barrier();
+  }
+  if (p.part && nmine >= 1) finalize(nmine - 1);
+}
+
 struct XdTile {
   int th, tw;
 };
+
+// expand-wave load ring depth (stages in flight) of expdw_ws_kernel
+#ifndef XW_D
+#define XW_D 2
+#endif
 
 static XdTile xd_tile(int k, int s) {
   (void)k;
@@ -717,6 +1100,46 @@ static bool xs_enabled() {
   return on == 1;
 }
 
+// Wave-specialised persistent kernel (expdw_ws_kernel): off by default —
+// bit-identical to expdw1_kernel but measured 13% slower over the twelve
+// C2 layer shapes (3.50 vs 3.10 ms in tools/convbench.py --set xd; parity on
+// the K >= 112 layers, 17-33% slower on the one- and two-stage layers, see
+// DESIGN.md section 4).  JABD_EXPDW_WS=1 or jabd_expand_dw_select(2) selects it.
+static int xw_form = 0;  // jabd_expand_dw_select
+static bool xw_enabled() {
+  static int env = -1;
+  if (env < 0) {
+    const char* e = getenv("JABD_EXPDW_WS");
+    env = e && e[0] == '1' ? 1 : 0;
+  }
+  return xw_form ? xw_form == 2 : env == 1;
+}
+
+template <int K, int S, int TH, int TW, int EC, int ACT, bool SKIP>
+static int xw_launch(const jabd_expdw_args& a, const XdDivs& dv, int64_t nitems, hipStream_t st) {
+  constexpr int D = XW_D;
+  auto kern = expdw_ws_kernel<K, S, TH, TW, EC, ACT, SKIP, D>;
+  constexpr int bytes = XwCfg<K, S, TH, TW, EC, SKIP>::BYTES;
+  static int occ = -1, ncu = 0;
+  if (occ < 0) {
+    int dev = 0;
+    JABD_HIP(hipGetDevice(&dev));
+    JABD_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    JABD_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    int o = 0;
+    JABD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, XwCfg<K, S, TH, TW, EC, SKIP>::NT,
+                                                          bytes));
+    occ = o < 1 ? 1 : o;
+  }
+  // expand-wave input offsets use 0xFFFFF000 + 64 Kc as "out of range"
+  JABD_REQUIRE((int64_t)a.B * a.x_bs * 4 <= 0xFFFFF000ll - 1024,
+               "expand_dw: input must be < 4 GiB - 5 KiB (split the batch)");
+  const int64_t cap = (int64_t)ncu * occ;
+  const int grid = (int)(nitems < cap ? nitems : cap);
+  kern<<<grid, XwCfg<K, S, TH, TW, EC, SKIP>::NT, bytes, st>>>(a, dv, (int)nitems);
+  return check_launch("expand_dw_ws");
+}
+
 struct XsPlan {
   int nb, nstrip, hb, nband;
 };
@@ -738,6 +1161,12 @@ static XsPlan xs_plan(int OH, int OW, int k) {
   pl.hb = OH >= 256 ? 64 : 32;
   pl.nband = (int)cdiv(OH, pl.hb);
   return pl;
+}
+
+extern "C" int jabd_expand_dw_select(int32_t form) {
+  const int prev = xw_form;
+  xw_form = form == 1 || form == 2 ? form : 0;
+  return prev;
 }
 
 extern "C" int64_t jabd_expand_dw_nblk(int32_t OH, int32_t OW, int32_t k, int32_t stride) {
@@ -829,6 +1258,25 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
                   make_fastdiv((uint32_t)tiles_w)};
   JABD_REQUIRE((int64_t)a.B * a.x_bs * 4 < ((int64_t)1 << 32) - 16,
                "expand_dw: input must be < 4 GiB (buffer-descriptor offsets)");
+  if (xw_enabled()) {
+#define XW_ACT(K_, S_, TH_, TW_, EC_, SK_)                                         \
+  {                                                                              \
+    if (a.act == ACT_RELU) return xw_launch<K_, S_, TH_, TW_, EC_, ACT_RELU, SK_>(a, dv, nitems, st);     \
+    if (a.act == ACT_HSWISH) return xw_launch<K_, S_, TH_, TW_, EC_, ACT_HSWISH, SK_>(a, dv, nitems, st); \
+    return xw_launch<K_, S_, TH_, TW_, EC_, ACT_NONE, SK_>(a, dv, nitems, st);                           \
+  }
+#define XW_CASE(K_, S_, TH_, TW_, EC_)                          \
+  if (a.k == K_ && a.stride == S_ && EC == EC_) {               \
+    if (S_ == 2 && a.sy) XW_ACT(K_, S_, TH_, TW_, EC_, true)    \
+    XW_ACT(K_, S_, TH_, TW_, EC_, false)                        \
+  }
+    XW_CASE(3, 1, 16, 16, 16) XW_CASE(3, 1, 16, 16, 32)
+    XW_CASE(5, 1, 16, 16, 16) XW_CASE(5, 1, 16, 16, 32)
+    XW_CASE(3, 2, 8, 8, 16) XW_CASE(3, 2, 8, 8, 32)
+    XW_CASE(5, 2, 8, 8, 16) XW_CASE(5, 2, 8, 8, 32)
+#undef XW_CASE
+#undef XW_ACT
+  }
 #define XD_LAUNCH(K_, S_, TH_, TW_, EC_, ACT_)                                                \
   do {                                                                                        \
     if (S_ == 2 && a.sy && nw == 8)                                                           \

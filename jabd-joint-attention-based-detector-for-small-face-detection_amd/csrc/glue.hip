@@ -45,14 +45,36 @@ __global__ void transpose_kernel(const float* __restrict__ src, int rows, int co
   }
 }
 
-// out[c] = sum over rows r (in order) of part[r][c]
-__global__ void colsum_kernel(const float* __restrict__ part, int64_t rows, int C,
-                              float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// out[c] = sum over rows r of part[r][c] in a fixed order: a workgroup owns
+// CB channels; its RG = 1024 / CB row groups each sum rows g, g + RG, ... in
+// order, then the RG partials are added pairwise in a fixed tree (the
+// decomposition depends only on (rows, C), so the result is deterministic).
+// One thread per channel walking all rows serially took ~290 us per call at
+// 2048 rows (15 calls per MNv3 training step).
+__global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ part, int64_t rows,
+                                                      int C, int CB, float* __restrict__ out) {
+  __shared__ float red[1024];
+  const int RG = 1024 / CB;
+  const int t = threadIdx.x, cl = t % CB, g = t / CB;
+  const int c = blockIdx.x * CB + cl;
   float s = 0.f;
-  for (int64_t r = 0; r < rows; ++r) s += part[r * C + c];
-  out[c] = s;
+  if (g < RG && c < C) {
+    const float* p = part + c;
+    int64_t r = g;
+    for (; r + 3 * RG < rows; r += 4 * RG) {
+      const float v0 = p[r * C], v1 = p[(r + RG) * C], v2 = p[(r + 2 * RG) * C],
+                  v3 = p[(r + 3 * RG) * C];
+      s += v0; s += v1; s += v2; s += v3;
+    }
+    for (; r < rows; r += RG) s += p[r * C];
+  }
+  red[t] = s;
+  __syncthreads();
+  for (int h = 1; h < RG; h <<= 1) {  // pairwise: group g += group g + h
+    if (g % (2 * h) == 0 && g + h < RG) red[t] += red[t + h * CB];
+    __syncthreads();
+  }
+  if (g == 0 && c < C) out[c] = red[t];
 }
 
 struct SumSet {
@@ -202,6 +224,7 @@ extern "C" int jabd_transpose_f32(const float* src, int32_t rows, int32_t cols, 
 extern "C" int jabd_colsum_f32(const float* part, int64_t rows, int32_t C, float* out,
                                jabd_stream_t stream) {
   JABD_REQUIRE(part && out && rows > 0 && C > 0, "colsum: bad arguments");
-  colsum_kernel<<<(unsigned)cdiv(C, 64), 64, 0, as_stream(stream)>>>(part, rows, C, out);
+  const int CB = C < 64 ? C : 64;
+  colsum_kernel<<<(unsigned)cdiv(C, CB), 1024, 0, as_stream(stream)>>>(part, rows, C, CB, out);
   return check_launch("colsum");
 }

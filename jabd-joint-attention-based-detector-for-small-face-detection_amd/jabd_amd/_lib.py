@@ -171,6 +171,7 @@ SIGNATURES = {
     "jabd_dwconv_nhwc_f32": [ctypes.POINTER(DwArgs), c_vp],
     "jabd_expand_dw_nblk": [c_i32, c_i32, c_i32, c_i32],
     "jabd_expand_dw_nhwc_f32": [ctypes.POINTER(ExpDwArgs), c_vp],
+    "jabd_expand_dw_select": [c_i32],
     "jabd_channel_sum_f32": [c_vp, c_i64, c_i32, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp],
     "jabd_partial_reduce_f32": [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp],
     "jabd_eca_gate_f32": [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_i32, c_vp, c_vp,

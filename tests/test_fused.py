@@ -206,3 +206,47 @@ def test_eca_gates_multi_equal_per_tensor(cuda):
         xc = x.contiguous()
         ref = F.eca_gate(F.channel_sums(xc), xc.shape[1] * xc.shape[2], w, "sigmoid")
         assert torch.equal(s, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", BLOCKS + [(3, 24, 72, 1, "none")],
+                         ids=lambda s: "k%d_c%d_e%d_s%d_%s" % s)
+@pytest.mark.parametrize("bhw", [(4, 96, 80), (3, 37, 29), (1, 1, 2)])
+def test_expand_dw_forms_bit_identical(cuda, spec, bhw):
+    """The wave-specialised persistent kernel (expand waves feeding
+    double-buffered tiles to depthwise waves) and the one-item-per-workgroup
+    kernel compute every output with the same operation sequence: y, the ECA
+    partials and the fused skip branch must be bit-identical.  (4, 96, 80)
+    gives several items per persistent workgroup (the expanded-buffer and
+    tap/partial rings wrap), (1, 1, 2) a grid smaller than the CU count."""
+    from jabd_amd import functional as F
+    from jabd_amd._lib import lib
+    k, cin, E, s, act = spec
+    B, H, W = bhw
+    g = torch.Generator().manual_seed(k * 7 + cin + E + H)
+    conv1 = torch.nn.Conv2d(cin, E, 1)
+    conv2 = torch.nn.Conv2d(E, E, k, s, k // 2, groups=E)
+    sdw = torch.nn.Conv2d(cin, cin, 3, 2, 1, groups=cin)
+    with torch.no_grad():
+        for c in (conv1, conv2, sdw):
+            c.weight.copy_(torch.randn(c.weight.shape, generator=g) / c.weight[0].numel() ** 0.5)
+            c.bias.copy_(0.3 * torch.randn(c.bias.shape, generator=g))
+    pk = F.pack_conv(conv1.to(cuda))
+    tapmajor = lambda c: (c.weight.detach().reshape(c.weight.shape[0], -1).t().contiguous().to(cuda),  # noqa: E731
+                          c.bias.detach().contiguous().to(cuda))
+    dw_w, dw_b = tapmajor(conv2)
+    skw, skb = tapmajor(sdw)
+    x = torch.randn(B, H, W, cin, generator=g).to(cuda)
+    outs = []
+    try:
+        for form in (1, 2):
+            lib().jabd_expand_dw_select(form)
+            if s == 2:
+                outs.append(F.expand_dw(x, pk, dw_w, dw_b, k, s, act=act, skip=(skw, skb)))
+            else:
+                outs.append(F.expand_dw(x, pk, dw_w, dw_b, k, s, act=act))
+    finally:
+        lib().jabd_expand_dw_select(0)
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

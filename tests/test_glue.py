@@ -60,13 +60,18 @@ def test_transpose(cuda, shape):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(2, 16, 16, 32), (3, 7, 9, 12), (1, 128, 128, 40)])
+@pytest.mark.parametrize("shape", [(2, 16, 16, 32), (3, 7, 9, 12), (1, 128, 128, 40),
+                                   (32, 64, 64, 40), (4, 16, 16, 200), (5, 8, 8, 3)])
 def test_channel_total(cuda, shape):
+    """Fixed-order parallel reduction: within 1e-6 of fp64, bitwise repeatable
+    (2048 partial rows at the C4 bias-gradient shape, C > 64 over several
+    workgroups, C not a multiple of 4)."""
     from jabd_amd import functional as F
     x = torch.randn(shape, device=cuda)
     ref = x.double().sum((0, 1, 2))
     got = F.channel_total(x)
     assert float((got.double() - ref).abs().max()) <= 1e-6 * float(x.abs().sum((0, 1, 2)).max())
+    assert torch.equal(got, F.channel_total(x))
 
 
 @pytest.mark.gpu

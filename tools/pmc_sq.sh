@@ -3,6 +3,7 @@
 # Usage on the GPU box: bash tools/pmc_sq.sh [shapes]   (default b2.xd,b12.xd)
 set -o pipefail
 SH=${1:-b2.xd,b12.xd}
+MATCH=${2:-expdw1}
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/xdpmc
@@ -15,4 +16,4 @@ for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $O/p$i -o run -- python3 tools/convbench.py --set xd --only $SH --reps 3 > $O/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $O/p$i.log; exit 1; }
 done
-python3 tools/pmc_kernel.py $O/p1 $O/p2 $O/p3 --match expdw1 > $O/summary.txt
+python3 tools/pmc_kernel.py $O/p1 $O/p2 $O/p3 --match $MATCH > $O/summary.txt
