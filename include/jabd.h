@@ -564,6 +564,20 @@ int jabd_bn_act_bwd_ex_f32(const float* dy, int32_t lddy, int32_t dyc0, const fl
                            const float* beta, int32_t act, float slope, const float* dys,
                            const float* dya, int64_t hw, float* part, float* dgamma,
                            float* dbeta, float* dx, float* dres, jabd_stream_t stream);
+/* Depthwise data gradient fused with the backward partials of the BatchNorm
+ * that produced the depthwise input (nets/mobilenetV3.py:141-142, bn1 + act
+ * -> conv2): de = dgrad(dy, w) is written to dz (bn1's output gradient), and
+ * bn1's backward — dgamma, dbeta, dx = the input gradient of bn1 (x = bn1's
+ * input e_pre, NHWC contiguous) — follows as jabd_bn_act_bwd_f32 would give
+ * it, without its separate pass over de and x.  part: >=
+ * jabd_dw_dgrad_bn_part_floats(B, H, W, C) floats. */
+int64_t jabd_dw_dgrad_bn_part_floats(int32_t B, int32_t H, int32_t W, int32_t C);
+int jabd_dw_dgrad_bn_bwd_f32(const float* dy, const float* w, int32_t B, int32_t H, int32_t W,
+                             int32_t C, int32_t OH, int32_t OW, int32_t k, int32_t stride,
+                             int32_t pad, const float* x, const float* mean, const float* invstd,
+                             const float* gamma, const float* beta, int32_t act, float slope,
+                             float* part, float* dgamma, float* dbeta, float* dz, float* dx,
+                             jabd_stream_t stream);
 /* n <= 4 ECA pools + gates in two launches (the head's per-level gates,
  * nets/retinaface_r.py:208-224): host arrays of n entries; tensor i is NHWC
  * with B images at x[i] (+ b * x_bs[i], pixel stride x_ps[i]), HW[i] pixels,

@@ -40,6 +40,9 @@ __device__ __forceinline__ float act_d(float z, int act, float slope) {
 
 constexpr int kRedThreads = 256;
 
+// Rows whose loads a BN reduction thread issues before accumulating them.
+constexpr int kBnBatch = 8;
+
 // Rows per block of the BN reductions (>= 1 pass of the block).
 static int64_t bn_rows_per_blk(int64_t M, int C) {
   const int C4 = C / 4;
@@ -68,15 +71,26 @@ __global__ __launch_bounds__(kRedThreads) void bn_stats_part_kernel(
     const int cg = cgb + t % lanes;
     const bool cv = cg < C4;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
-    if (r0 < rows_pass) {
-      const float4 sh = cv ? reinterpret_cast<const float4*>(x)[cg] : make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int64_t m = m0 + r0; cv && m < m1; m += rows_pass) {
-        float4 v = reinterpret_cast<const float4*>(x + m * ldx)[cg];
+    if (r0 < rows_pass && cv) {
+      const float4 sh = reinterpret_cast<const float4*>(x)[cg];
+      auto acc = [&](float4 v) {
         v.x -= sh.x; v.y -= sh.y; v.z -= sh.z; v.w -= sh.w;
         s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
         q.x = fmaf(v.x, v.x, q.x); q.y = fmaf(v.y, v.y, q.y);
         q.z = fmaf(v.z, v.z, q.z); q.w = fmaf(v.w, v.w, q.w);
+      };
+      // kBnBatch rows' loads in flight before their (in-order) accumulation:
+      // one load per iteration left each wave one HBM round trip per row
+      int64_t m = m0 + r0;
+      for (; m + (kBnBatch - 1) * rows_pass < m1; m += kBnBatch * rows_pass) {
+        float4 v[kBnBatch];
+#pragma unroll
+        for (int u = 0; u < kBnBatch; ++u)
+          v[u] = reinterpret_cast<const float4*>(x + (m + u * rows_pass) * ldx)[cg];
+#pragma unroll
+        for (int u = 0; u < kBnBatch; ++u) acc(v[u]);
       }
+      for (; m < m1; m += rows_pass) acc(reinterpret_cast<const float4*>(x + m * ldx)[cg]);
     }
     __syncthreads();
     rs[t] = s;
@@ -188,6 +202,9 @@ __device__ __forceinline__ EwMap ew_map(int lanes, int C4) {
 }
 
 // y = act((x - mean) * invstd * gamma + beta [+ res])
+// RES / TR: residual / dy-transform operand present (compile time: a runtime
+// select of a float4 operand was lowered through scratch)
+template <bool RES>
 __global__ __launch_bounds__(kRedThreads) void bn_act_fwd_kernel(
     const float* __restrict__ x, int ldx, int64_t M, int C, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ gamma,
@@ -200,18 +217,13 @@ __global__ __launch_bounds__(kRedThreads) void bn_act_fwd_kernel(
   const float4 is = *reinterpret_cast<const float4*>(invstd + c);
   const float4 gm = *reinterpret_cast<const float4*>(gamma + c);
   const float4 bt = *reinterpret_cast<const float4*>(beta + c);
-#pragma unroll 2
-  for (int k = 0; k < kEwIters; ++k) {
-    const int64_t m = e.m0 + (int64_t)k * e.rows_pass;
-    if (m >= M) break;
-    const float4 v = *reinterpret_cast<const float4*>(x + m * ldx + c);
+  auto one = [&](int64_t m, float4 v, float4 r) {
     float4 o;
     o.x = (v.x - mu.x) * is.x * gm.x + bt.x;
     o.y = (v.y - mu.y) * is.y * gm.y + bt.y;
     o.z = (v.z - mu.z) * is.z * gm.z + bt.z;
     o.w = (v.w - mu.w) * is.w * gm.w + bt.w;
-    if (res) {
-      const float4 r = *reinterpret_cast<const float4*>(res + m * ldr + c);
+    if (RES) {
       o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
     }
     o.x = act_f(o.x, act, slope);
@@ -219,6 +231,26 @@ __global__ __launch_bounds__(kRedThreads) void bn_act_fwd_kernel(
     o.z = act_f(o.z, act, slope);
     o.w = act_f(o.w, act, slope);
     *reinterpret_cast<float4*>(y + m * ldy + yc0 + c) = o;
+  };
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e.m0 + (int64_t)(kEwIters - 1) * e.rows_pass < M) {
+    // full block: every row's loads in flight first
+    float4 v[kEwIters], r[kEwIters];
+#pragma unroll
+    for (int k = 0; k < kEwIters; ++k) {
+      const int64_t m = e.m0 + (int64_t)k * e.rows_pass;
+      v[k] = *reinterpret_cast<const float4*>(x + m * ldx + c);
+      r[k] = RES ? *reinterpret_cast<const float4*>(res + m * ldr + c) : z4;
+    }
+#pragma unroll
+    for (int k = 0; k < kEwIters; ++k) one(e.m0 + (int64_t)k * e.rows_pass, v[k], r[k]);
+    return;
+  }
+  for (int k = 0; k < kEwIters; ++k) {
+    const int64_t m = e.m0 + (int64_t)k * e.rows_pass;
+    if (m >= M) break;
+    one(m, *reinterpret_cast<const float4*>(x + m * ldx + c),
+        RES ? *reinterpret_cast<const float4*>(res + m * ldr + c) : z4);
   }
 }
 
@@ -245,11 +277,7 @@ __global__ __launch_bounds__(kRedThreads) void bn_act_fwd_sum_kernel(
     const float4 gm = *reinterpret_cast<const float4*>(gamma + c);
     const float4 bt = *reinterpret_cast<const float4*>(beta + c);
     const int64_t m0 = (int64_t)blockIdx.x * rp * kEwIters + r0;
-#pragma unroll 2
-    for (int k = 0; k < kEwIters; ++k) {
-      const int64_t m = m0 + (int64_t)k * rp;
-      if (m >= M) break;
-      const float4 v = *reinterpret_cast<const float4*>(x + m * C + c);
+    auto one = [&](int64_t m, float4 v) {
       float4 o;
       o.x = act_f((v.x - mu.x) * is.x * gm.x + bt.x, act, slope);
       o.y = act_f((v.y - mu.y) * is.y * gm.y + bt.y, act, slope);
@@ -257,6 +285,20 @@ __global__ __launch_bounds__(kRedThreads) void bn_act_fwd_sum_kernel(
       o.w = act_f((v.w - mu.w) * is.w * gm.w + bt.w, act, slope);
       *reinterpret_cast<float4*>(y + m * C + c) = o;
       acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+    };
+    if (m0 + (int64_t)(kEwIters - 1) * rp < M) {  // full block: loads first
+      float4 v[kEwIters];
+#pragma unroll
+      for (int k = 0; k < kEwIters; ++k)
+        v[k] = *reinterpret_cast<const float4*>(x + (m0 + (int64_t)k * rp) * C + c);
+#pragma unroll
+      for (int k = 0; k < kEwIters; ++k) one(m0 + (int64_t)k * rp, v[k]);
+    } else {
+      for (int k = 0; k < kEwIters; ++k) {
+        const int64_t m = m0 + (int64_t)k * rp;
+        if (m >= M) break;
+        one(m, *reinterpret_cast<const float4*>(x + m * C + c));
+      }
     }
   }
   red[t] = acc;
@@ -285,6 +327,7 @@ __device__ __forceinline__ float4 dy_transform(float4 g, const float* __restrict
                      fmaf(g.w, sc.w, ad.w));
 }
 
+template <bool RES, bool TR>
 __global__ __launch_bounds__(kRedThreads) void bn_bwd_part_kernel(
     const float* __restrict__ dy, int lddy, int dyc0, const float* __restrict__ x, int ldx,
     const float* __restrict__ res, int ldr, int64_t M, int C, const float* __restrict__ mean,
@@ -310,12 +353,8 @@ __global__ __launch_bounds__(kRedThreads) void bn_bwd_part_kernel(
       const float4 is = *reinterpret_cast<const float4*>(invstd + c);
       const float4 gm = *reinterpret_cast<const float4*>(gamma + c);
       const float4 bt = *reinterpret_cast<const float4*>(beta + c);
-      for (int64_t m = m0 + r0; m < m1; m += rows_pass) {
-        const float4 v = *reinterpret_cast<const float4*>(x + m * ldx + c);
-        float4 g = *reinterpret_cast<const float4*>(dy + m * lddy + dyc0 + c);
-        if (dys) g = dy_transform(g, dys, dya, m / hw, C, c);
-        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (res) r = *reinterpret_cast<const float4*>(res + m * ldr + c);
+      auto acc = [&](int64_t m, float4 v, float4 g, float4 r) {
+        if (TR) g = dy_transform(g, dys, dya, m / hw, C, c);
         float xh[4] = {(v.x - mu.x) * is.x, (v.y - mu.y) * is.y, (v.z - mu.z) * is.z,
                        (v.w - mu.w) * is.w};
         float gg[4] = {g.x, g.y, g.z, g.w};
@@ -328,7 +367,27 @@ __global__ __launch_bounds__(kRedThreads) void bn_bwd_part_kernel(
         s.x += dz[0]; s.y += dz[1]; s.z += dz[2]; s.w += dz[3];
         q.x = fmaf(dz[0], xh[0], q.x); q.y = fmaf(dz[1], xh[1], q.y);
         q.z = fmaf(dz[2], xh[2], q.z); q.w = fmaf(dz[3], xh[3], q.w);
+      };
+      const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      int64_t m = m0 + r0;
+      // kBnBatch / 2 rows (x, dy and the residual) in flight, accumulated in order
+      constexpr int NB = kBnBatch / 2;
+      for (; m + (NB - 1) * rows_pass < m1; m += NB * rows_pass) {
+        float4 v[NB], g[NB], r[NB];
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+          const int64_t mu_ = m + u * rows_pass;
+          v[u] = *reinterpret_cast<const float4*>(x + mu_ * ldx + c);
+          g[u] = *reinterpret_cast<const float4*>(dy + mu_ * lddy + dyc0 + c);
+          r[u] = RES ? *reinterpret_cast<const float4*>(res + mu_ * ldr + c) : z4;
+        }
+#pragma unroll
+        for (int u = 0; u < NB; ++u) acc(m + u * rows_pass, v[u], g[u], r[u]);
       }
+      for (; m < m1; m += rows_pass)
+        acc(m, *reinterpret_cast<const float4*>(x + m * ldx + c),
+            *reinterpret_cast<const float4*>(dy + m * lddy + dyc0 + c),
+            RES ? *reinterpret_cast<const float4*>(res + m * ldr + c) : z4);
     }
     __syncthreads();
     rs[t] = s;
@@ -359,6 +418,7 @@ __global__ __launch_bounds__(kFinThreads) void bn_bwd_final_kernel(
 }
 
 // dx = gamma*invstd*(dz - sum(dz)/M - xhat*sum(dz*xhat)/M); dres = dz
+template <bool RES, bool TR>
 __global__ __launch_bounds__(kRedThreads) void bn_bwd_apply_kernel(
     const float* __restrict__ dy, int lddy, int dyc0, const float* __restrict__ x, int ldx,
     const float* __restrict__ res, int ldr, int64_t M, int C, const float* __restrict__ mean,
@@ -380,15 +440,9 @@ __global__ __launch_bounds__(kRedThreads) void bn_bwd_apply_kernel(
     a1[j] = sdz[c + j] * invM;
     a2[j] = sdzx[c + j] * invM;
   }
-#pragma unroll 2
-  for (int k = 0; k < kEwIters; ++k) {
-    const int64_t m = e.m0 + (int64_t)k * e.rows_pass;
-    if (m >= M) break;
-    const float4 v = *reinterpret_cast<const float4*>(x + m * ldx + c);
-    float4 g = *reinterpret_cast<const float4*>(dy + m * lddy + dyc0 + c);
-    if (dys) g = dy_transform(g, dys, dya, m / hw, C, c);
-    float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (res) r = *reinterpret_cast<const float4*>(res + m * ldr + c);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto one = [&](int64_t m, float4 v, float4 g, float4 r) {
+    if (TR) g = dy_transform(g, dys, dya, m / hw, C, c);
     const float vv[4] = {v.x, v.y, v.z, v.w}, gg[4] = {g.x, g.y, g.z, g.w},
                 rr[4] = {r.x, r.y, r.z, r.w};
     float o[4], dzo[4];
@@ -403,6 +457,31 @@ __global__ __launch_bounds__(kRedThreads) void bn_bwd_apply_kernel(
     if (dres)
       *reinterpret_cast<float4*>(dres + m * (int64_t)C + c) =
           make_float4(dzo[0], dzo[1], dzo[2], dzo[3]);
+  };
+  // half-blocks of rows with every load in flight before the math
+  constexpr int NH = kEwIters / 2;
+  for (int h = 0; h < 2; ++h) {
+    const int64_t mb = e.m0 + (int64_t)h * NH * e.rows_pass;
+    if (mb + (int64_t)(NH - 1) * e.rows_pass < M) {
+      float4 v[NH], g[NH], r[NH];
+#pragma unroll
+      for (int k = 0; k < NH; ++k) {
+        const int64_t m = mb + (int64_t)k * e.rows_pass;
+        v[k] = *reinterpret_cast<const float4*>(x + m * ldx + c);
+        g[k] = *reinterpret_cast<const float4*>(dy + m * lddy + dyc0 + c);
+        r[k] = RES ? *reinterpret_cast<const float4*>(res + m * ldr + c) : z4;
+      }
+#pragma unroll
+      for (int k = 0; k < NH; ++k) one(mb + (int64_t)k * e.rows_pass, v[k], g[k], r[k]);
+      continue;
+    }
+    for (int k = 0; k < NH; ++k) {
+      const int64_t m = mb + (int64_t)k * e.rows_pass;
+      if (m >= M) break;
+      one(m, *reinterpret_cast<const float4*>(x + m * ldx + c),
+          *reinterpret_cast<const float4*>(dy + m * lddy + dyc0 + c),
+          RES ? *reinterpret_cast<const float4*>(res + m * ldr + c) : z4);
+    }
   }
 }
 
@@ -1036,6 +1115,111 @@ __global__ __launch_bounds__(256) void dw_dgrad_strip_kernel(
     if (iw0 + q < W) xrow[(int64_t)(iw0 + q) * C4] = acc[q];
 }
 
+// Depthwise data gradient with the following BatchNorm's backward partials
+// fused in (MNv3 Block_eca: e = act(bn1(e_pre)) feeds the depthwise conv, so
+// its data gradient de is bn1's output gradient).  Each thread computes the
+// de strip as dw_dgrad_strip_kernel does (same tap order: bit-identical de),
+// stores it, loads e_pre at the same pixels and accumulates dz = de *
+// act'(xhat * gamma + beta), sum dz and sum dz * xhat (as bn_bwd_part_kernel);
+// a workgroup walks `spb` strip rows and writes part[blockIdx.x][0|1][c] for
+// its channels, rows added in a fixed order (deterministic).  Saves
+// bn_bwd_part's pass over de and e_pre (the block's largest tensors).
+template <int K, int S, int PW>
+__global__ __launch_bounds__(256) void dw_dgrad_bn_kernel(
+    const float* __restrict__ dy, const float* __restrict__ w, int H, int W, int C, int OH, int OW,
+    int nstrip, int64_t items, int lanes, int spb, float* __restrict__ dx,
+    const float* __restrict__ xb, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ gamma, const float* __restrict__ beta, int act, float slope,
+    float* __restrict__ part) {
+  constexpr int PAD = K / 2;
+  constexpr int OFF = floordiv_c(PAD - K + 1, S);
+  constexpr int L = (PW - 1 + PAD - S * OFF) / S + 1;
+  __shared__ float4 rs[256], rq[256];
+  const int C4 = C >> 2;
+  const int t = threadIdx.x;
+  const int rows_pass = 256 / lanes;
+  const int r0 = t / lanes;
+  const int cg = blockIdx.y * lanes + t % lanes;
+  const bool tv = r0 < rows_pass && cg < C4;
+  float4 sS = make_float4(0.f, 0.f, 0.f, 0.f), sQ = sS;
+  if (tv) {
+    const int c = cg * 4;
+    const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+    const float4 is = *reinterpret_cast<const float4*>(invstd + c);
+    const float4 gm = *reinterpret_cast<const float4*>(gamma + c);
+    const float4 bt = *reinterpret_cast<const float4*>(beta + c);
+    for (int sp = 0; sp < spb; ++sp) {
+      const int64_t it = ((int64_t)blockIdx.x * spb + sp) * rows_pass + r0;
+      if (it >= items) break;
+      const int row = (int)(it / nstrip), strip = (int)(it - (int64_t)row * nstrip);
+      const int b = row / H, ih = row - b * H;
+      const int iw0 = strip * PW;
+      const int ow0 = iw0 / S + OFF;
+      float4 acc[PW];
+#pragma unroll
+      for (int q = 0; q < PW; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int kh = 0; kh < K; ++kh) {
+        const int nh = ih + PAD - kh;
+        if (nh < 0 || (S == 2 && (nh & 1))) continue;
+        const int oh = nh / S;
+        if (oh >= OH) continue;
+        const float4* drow =
+            reinterpret_cast<const float4*>(dy + (((int64_t)b * OH + oh) * OW) * C) + cg;
+        float4 seg[L];
+#pragma unroll
+        for (int j = 0; j < L; ++j) {
+          const int ow = ow0 + j;
+          seg[j] = (ow >= 0 && ow < OW) ? drow[(int64_t)ow * C4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        float4 wk[K];
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw) wk[kw] = reinterpret_cast<const float4*>(w + (kh * K + kw) * C)[cg];
+#pragma unroll
+        for (int q = 0; q < PW; ++q)
+#pragma unroll
+          for (int kw = 0; kw < K; ++kw) {
+            if (((q + PAD - kw) % S + S) % S) continue;
+            const int j = (q + PAD - kw - S * OFF) / S;
+            fma4(acc[q], seg[j], wk[kw]);
+          }
+      }
+      const int64_t rb = (((int64_t)b * H + ih) * W) * C4 + cg;
+      float4* xrow = reinterpret_cast<float4*>(dx) + rb;
+      const float4* brow = reinterpret_cast<const float4*>(xb) + rb;
+#pragma unroll
+      for (int q = 0; q < PW; ++q) {
+        if (iw0 + q >= W) break;
+        xrow[(int64_t)(iw0 + q) * C4] = acc[q];
+        const float4 xv = brow[(int64_t)(iw0 + q) * C4];
+        const float xh[4] = {(xv.x - mu.x) * is.x, (xv.y - mu.y) * is.y, (xv.z - mu.z) * is.z,
+                             (xv.w - mu.w) * is.w};
+        const float gg[4] = {acc[q].x, acc[q].y, acc[q].z, acc[q].w};
+        const float gmm[4] = {gm.x, gm.y, gm.z, gm.w}, btt[4] = {bt.x, bt.y, bt.z, bt.w};
+        float dz[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dz[e] = gg[e] * act_d(xh[e] * gmm[e] + btt[e], act, slope);
+        sS.x += dz[0]; sS.y += dz[1]; sS.z += dz[2]; sS.w += dz[3];
+        sQ.x = fmaf(dz[0], xh[0], sQ.x); sQ.y = fmaf(dz[1], xh[1], sQ.y);
+        sQ.z = fmaf(dz[2], xh[2], sQ.z); sQ.w = fmaf(dz[3], xh[3], sQ.w);
+      }
+    }
+  }
+  rs[t] = sS;
+  rq[t] = sQ;
+  __syncthreads();
+  if (t < lanes && cg < C4) {
+    float4 S_ = make_float4(0.f, 0.f, 0.f, 0.f), Q_ = S_;
+    for (int r = 0; r < rows_pass; ++r) {
+      const float4 a = rs[r * lanes + t], q = rq[r * lanes + t];
+      S_.x += a.x; S_.y += a.y; S_.z += a.z; S_.w += a.w;
+      Q_.x += q.x; Q_.y += q.y; Q_.z += q.z; Q_.w += q.w;
+    }
+    reinterpret_cast<float4*>(part + (int64_t)blockIdx.x * 2 * C)[cg] = S_;
+    reinterpret_cast<float4*>(part + (int64_t)blockIdx.x * 2 * C + C)[cg] = Q_;
+  }
+}
+
 // part[blk][tap][c] = sum over this block's output strips of dy * x(tap)
 template <int K, int S, int PW>
 __global__ __launch_bounds__(256) void dw_wgrad_strip_kernel(
@@ -1376,7 +1560,8 @@ extern "C" int jabd_bn_act_fwd_f32(const float* x, int32_t ldx, int64_t M, int32
   if (M == 0 || C == 0) return JABD_OK;
   int lanes;
   const dim3 grid = ew_grid(M, C, lanes);
-  bn_act_fwd_kernel<<<grid, kRedThreads, 0, as_stream(stream)>>>(
+  (res ? bn_act_fwd_kernel<true> : bn_act_fwd_kernel<false>)<<<grid, kRedThreads, 0,
+                                                                as_stream(stream)>>>(
       x, ldx, M, C, mean, invstd, gamma, beta, res, ldr, act, slope, y, ldy, yc0, lanes);
   return check_launch("bn_act_fwd");
 }
@@ -1438,18 +1623,22 @@ extern "C" int jabd_bn_act_bwd_ex_f32(const float* dy, int32_t lddy, int32_t dyc
   JABD_REQUIRE(!dys || (dya && hw > 0 && M % hw == 0), "bn_act_bwd: dy transform needs dya, hw");
   hipStream_t st = as_stream(stream);
   const int64_t per = bn_rows_per_blk(M, C), nblk = cdiv(M, per);
-  bn_bwd_part_kernel<<<(unsigned)nblk, kRedThreads, 0, st>>>(dy, lddy, dyc0, x, ldx, res, ldr, M,
-                                                            C, mean, invstd, gamma, beta, act,
-                                                            slope, per, part, dys, dya, hw);
+  auto part_k = res ? (dys ? bn_bwd_part_kernel<true, true> : bn_bwd_part_kernel<true, false>)
+                    : (dys ? bn_bwd_part_kernel<false, true> : bn_bwd_part_kernel<false, false>);
+  part_k<<<(unsigned)nblk, kRedThreads, 0, st>>>(dy, lddy, dyc0, x, ldx, res, ldr, M, C, mean,
+                                                invstd, gamma, beta, act, slope, per, part, dys,
+                                                dya, hw);
   if (int e = check_launch("bn_bwd_part")) return e;
   bn_bwd_final_kernel<<<(unsigned)cdiv(C, kFinLanes), kFinThreads, 0, st>>>(part, nblk, C,
                                                                             dbeta, dgamma);
   if (int e = check_launch("bn_bwd_final")) return e;
   int lanes;
   const dim3 grid = ew_grid(M, C, lanes);
-  bn_bwd_apply_kernel<<<grid, kRedThreads, 0, st>>>(dy, lddy, dyc0, x, ldx, res, ldr, M, C, mean,
-                                                    invstd, gamma, beta, act, slope, dbeta,
-                                                    dgamma, dx, dres, lanes, dys, dya, hw);
+  auto apply_k = res ? (dys ? bn_bwd_apply_kernel<true, true> : bn_bwd_apply_kernel<true, false>)
+                     : (dys ? bn_bwd_apply_kernel<false, true> : bn_bwd_apply_kernel<false, false>);
+  apply_k<<<grid, kRedThreads, 0, st>>>(dy, lddy, dyc0, x, ldx, res, ldr, M, C, mean, invstd,
+                                        gamma, beta, act, slope, dbeta, dgamma, dx, dres, lanes,
+                                        dys, dya, hw);
   return check_launch("bn_bwd_apply");
 }
 
@@ -1671,6 +1860,64 @@ extern "C" int jabd_dw_dgrad_f32(const float* dy, const float* w, int32_t B, int
   DG_CASE(3, 1, 8) DG_CASE(3, 2, 8) DG_CASE(5, 1, 8) DG_CASE(5, 2, 8)
 #undef DG_CASE
   return check_launch("dw_dgrad");
+}
+
+// Workgroups of dw_dgrad_bn_kernel along the strip rows: ~8192 (each walks
+// spb rows of rows_pass strips), so bn_bwd_final reads few partial rows.
+static void dgbn_plan(int B, int H, int W, int C, int& nblk, int& spb) {
+  const int C4 = C / 4, lanes = C4 < 64 ? C4 : 64, rows_pass = 256 / lanes;
+  const int64_t items = (int64_t)B * H * cdiv(W, 8);
+  const int64_t groups = cdiv(items, rows_pass);
+  spb = (int)cdiv(groups, 8192);
+  nblk = (int)cdiv(groups, spb);
+}
+
+extern "C" int64_t jabd_dw_dgrad_bn_part_floats(int32_t B, int32_t H, int32_t W, int32_t C) {
+  if (B <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 4) return -1;
+  int nblk, spb;
+  dgbn_plan(B, H, W, C, nblk, spb);
+  return (int64_t)nblk * 2 * C;
+}
+
+extern "C" int jabd_dw_dgrad_bn_bwd_f32(const float* dy, const float* w, int32_t B, int32_t H,
+                                        int32_t W, int32_t C, int32_t OH, int32_t OW, int32_t k,
+                                        int32_t stride, int32_t pad, const float* x,
+                                        const float* mean, const float* invstd,
+                                        const float* gamma, const float* beta, int32_t act,
+                                        float slope, float* part, float* dgamma, float* dbeta,
+                                        float* dz, float* dx, jabd_stream_t stream) {
+  JABD_REQUIRE(dy && w && x && mean && invstd && gamma && beta && part && dgamma && dbeta && dz &&
+                   dx && C % 4 == 0 && B > 0 && H > 0 && W > 0,
+               "dw_dgrad_bn_bwd: bad args");
+  JABD_REQUIRE((k == 3 || k == 5) && pad == k / 2 && (stride == 1 || stride == 2) &&
+                   OH == (H + 2 * pad - k) / stride + 1 && OW == (W + 2 * pad - k) / stride + 1,
+               "dw_dgrad_bn_bwd: unsupported geometry");
+  const int C4 = C / 4, lanes = C4 < 64 ? C4 : 64;
+  int nblk, spb;
+  dgbn_plan(B, H, W, C, nblk, spb);
+  hipStream_t st = as_stream(stream);
+  const int nstrip = (int)cdiv(W, 8);
+  const int64_t items = (int64_t)B * H * nstrip;
+  const dim3 g((unsigned)nblk, (unsigned)cdiv(C4, lanes));
+#define DGB_CASE(K_, S_)                                                                       \
+  if (k == K_ && stride == S_)                                                                 \
+    dw_dgrad_bn_kernel<K_, S_, 8><<<g, 256, 0, st>>>(dy, w, H, W, C, OH, OW, nstrip, items,    \
+                                                     lanes, spb, dz, x, mean, invstd, gamma,    \
+                                                     beta, act, slope, part);
+  DGB_CASE(3, 1) DGB_CASE(3, 2) DGB_CASE(5, 1) DGB_CASE(5, 2)
+#undef DGB_CASE
+  if (int e = check_launch("dw_dgrad_bn")) return e;
+  bn_bwd_final_kernel<<<(unsigned)cdiv(C, kFinLanes), kFinThreads, 0, st>>>(part, nblk, C, dbeta,
+                                                                            dgamma);
+  if (int e = check_launch("bn_bwd_final")) return e;
+  const int64_t M = (int64_t)B * H * W;
+  int elanes;
+  const dim3 grid = ew_grid(M, C, elanes);
+  bn_bwd_apply_kernel<false, false><<<grid, kRedThreads, 0, st>>>(dz, C, 0, x, C, nullptr, 0, M, C,
+                                                                  mean, invstd,
+                                                    gamma, beta, act, slope, dbeta, dgamma, dx,
+                                                    nullptr, elanes, nullptr, nullptr, 1);
+  return check_launch("bn_bwd_apply");
 }
 
 extern "C" int64_t jabd_dw_wgrad_part_floats(int64_t M, int32_t C, int32_t k) {

@@ -207,6 +207,10 @@ SIGNATURES = {
     "jabd_dw_dgrad_f32": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
                           c_i32, c_vp, c_vp],
     "jabd_dw_wgrad_part_floats": [c_i64, c_i32, c_i32],
+    "jabd_dw_dgrad_bn_part_floats": [c_i32, c_i32, c_i32, c_i32],
+    "jabd_dw_dgrad_bn_bwd_f32": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
+                                 c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_f32, c_vp,
+                                 c_vp, c_vp, c_vp, c_vp, c_vp],
     "jabd_dw_wgrad_f32": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
                           c_i32, c_vp, c_vp, c_vp],
     "jabd_eca_bwd_f32": [c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp,
@@ -250,6 +254,7 @@ _RESTYPE = {"jabd_version": ctypes.c_char_p, "jabd_dw_nblk": ctypes.c_int64,
             "jabd_bn_nblk": ctypes.c_int64, "jabd_conv_wgrad_part_floats": ctypes.c_int64,
             "jabd_conv_wgrad_eca_part_floats": ctypes.c_int64, "jabd_bn_sum_nblk": ctypes.c_int64,
             "jabd_dw_wgrad_part_floats": ctypes.c_int64,
+            "jabd_dw_dgrad_bn_part_floats": ctypes.c_int64,
             "jabd_adam_num_chunks": ctypes.c_int64, "jabd_beca_ws_floats": ctypes.c_int64,
             "jabd_adaptive_pool_ws_floats": ctypes.c_int64,
             "jabd_abi_struct_size": ctypes.c_int64, "jabd_conv_workspace_size": ctypes.c_int64,

@@ -39,6 +39,9 @@ FUSED_BLOCKS = __import__("os").environ.get("JABD_FUSED_BLOCKS", "1") != "0"
 ECA_WGRAD = __import__("os").environ.get("JABD_ECA_WGRAD", "1") != "0"
 # JABD_ECA_SUMS=0: the ECA pool of a block reads d in its own pass (A/B)
 ECA_SUMS = __import__("os").environ.get("JABD_ECA_SUMS", "1") != "0"
+# JABD_DW_BN_FUSE=0: bn1's backward partials from their own pass over de and
+# e_pre instead of the depthwise data-gradient kernel (A/B)
+DW_BN_FUSE = __import__("os").environ.get("JABD_DW_BN_FUSE", "1") != "0"
 
 
 _ZEROS = {}
@@ -905,6 +908,27 @@ def _dw_bwd(dy, x, wt, k, stride, want_dx=True):
     return dx, dw
 
 
+def _dw_bn_bwd(dy, x, wt, k, stride, x_bn, st, act):
+    """Backward of d = dwconv(act(bn(x_bn))) with x = act(bn(x_bn)): the
+    depthwise data gradient carries bn's backward partials
+    (jabd_dw_dgrad_bn_bwd_f32).  Returns (dx_bn, dgamma, dbeta, dW)."""
+    g, b, mean, invstd = st
+    B, H, W, C = x.shape
+    OH, OW = dy.shape[1], dy.shape[2]
+    nparts = int(lib().jabd_dw_dgrad_bn_part_floats(B, H, W, C))
+    part = torch.empty(nparts, dtype=torch.float32, device=x.device)
+    dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
+    dbeta = torch.empty_like(dgamma)
+    dz = torch.empty_like(x)
+    dx = torch.empty_like(x)
+    call("jabd_dw_dgrad_bn_bwd_f32", dy.data_ptr(), wt.data_ptr(), B, H, W, C, OH, OW, k, stride,
+         k // 2, x_bn.data_ptr(), mean.data_ptr(), invstd.data_ptr(), g.data_ptr(), b.data_ptr(),
+         ACT[act], 0.0, part.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), dz.data_ptr(),
+         dx.data_ptr(), _st())
+    _, dw = _dw_bwd(dy, x, wt, k, stride, want_dx=False)
+    return dx, dgamma, dbeta, dw
+
+
 class MNv3BlockFn(torch.autograd.Function):
     """One Block_eca (nets/mobilenetV3.py:94-150) forward and backward as a
     single autograd node, so the backward can fuse what per-op nodes cannot:
@@ -999,8 +1023,11 @@ class MNv3BlockFn(torch.autograd.Function):
                  _st())
         # ECA gate terms; BN2's backward applies dd = da * scale + dmean
         dd_pre, dg2, db2, _ = _bn_bwd(da, d_pre, st2, act, dys=scale, dya=dmean)
-        de, dW2 = _dw_bwd(dd_pre, e, wt2, k, stride)
-        de_pre, dg1, db1, _ = _bn_bwd(de, e_pre, st1, act)
+        if DW_BN_FUSE:
+            de_pre, dg1, db1, dW2 = _dw_bn_bwd(dd_pre, e, wt2, k, stride, e_pre, st1, act)
+        else:
+            de, dW2 = _dw_bwd(dd_pre, e, wt2, k, stride)
+            de_pre, dg1, db1, _ = _bn_bwd(de, e_pre, st1, act)
         dW1 = _wgrad(s, de_pre, blk.conv1.weight, 1, 0)
         # skip branch -> its input gradient, then conv1's data gradient adds it
         sk = blk.skip

@@ -321,3 +321,50 @@ def test_bnactfn_grads_wide(cuda, c, act, h, w):
     (yg * _nhwc(dy.float()).to(cuda)).sum().backward()
     _check([_nchw(xg.grad), gg.grad, bg.grad], [xr.grad, gr.grad, br.grad],
            ["dx", "dgamma", "dbeta"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,k,s,bhw,act", [(64, 3, 2, (4, 64, 48), "relu"), (72, 5, 1, (3, 37, 29), "relu"),
+                                           (240, 3, 2, (2, 30, 34), "hswish"),
+                                           (480, 3, 1, (3, 32, 48), "hswish"), (16, 3, 1, (2, 9, 5), "relu")])
+def test_dw_dgrad_bn_fused(cuda, c, k, s, bhw, act):
+    """MNv3 block backward through bn1 + act -> depthwise conv: the fused
+    depthwise data gradient + bn1 backward partials (jabd_dw_dgrad_bn_bwd_f32)
+    against the two-pass form (jabd_dw_dgrad_f32 then jabd_bn_act_bwd_f32):
+    the depthwise gradient bit-identical, dgamma / dbeta / dx within fp32
+    reassociation of the partial sums; and both against float64 autograd."""
+    from jabd_amd import train as T
+    B, H, W = bhw
+    g = torch.Generator().manual_seed(c + k * 10 + s)
+    x_bn = torch.randn(B, H, W, c, generator=g) * 2 + 0.5
+    gamma = 1 + 0.3 * torch.randn(c, generator=g)
+    beta = 0.2 * torch.randn(c, generator=g)
+    w = torch.randn(c, 1, k, k, generator=g) / k
+    OH = (H + 2 * (k // 2) - k) // s + 1
+    OW = (W + 2 * (k // 2) - k) // s + 1
+    dy = torch.randn(B, OH, OW, c, generator=g)
+    # float64 reference: e = act(bn(x_bn)) (batch statistics), d = dwconv(e)
+    xr = _nchw(x_bn).double().requires_grad_()
+    gr, br = gamma.double().requires_grad_(), beta.double().requires_grad_()
+    e = tF.batch_norm(xr, None, None, gr, br, True, 0.0, 1e-5)
+    e = tF.relu(e) if act == "relu" else tF.hardswish(e)
+    d = tF.conv2d(e, w.double(), None, s, k // 2, 1, c)
+    d.backward(_nchw(dy).double())
+    dev = torch.device(cuda)
+    bn = torch.nn.BatchNorm2d(c).to(dev)
+    with torch.no_grad():
+        bn.weight.copy_(gamma)
+        bn.bias.copy_(beta)
+    xg = x_bn.to(dev)
+    e_g, st = T._bn_fwd(xg, bn, act)
+    wt = T.F.transpose(w.to(dev).reshape(c, k * k))
+    dyg = dy.to(dev)
+    dx1, dg1, db1, dw1 = T._dw_bn_bwd(dyg, e_g, wt, k, s, xg, st, act)
+    de, dw2 = T._dw_bwd(dyg, e_g, wt, k, s)
+    dx2, dg2, db2, _ = T._bn_bwd(de, xg, st, act)
+    torch.cuda.synchronize()
+    assert torch.equal(dw1, dw2)
+    for a, b in ((dx1, dx2), (dg1, dg2), (db1, db2)):
+        assert rel_err(a.cpu(), b.cpu()) < 1e-5
+    _check([_nchw(dx1.cpu()), dg1.cpu(), db1.cpu()], [xr.grad, gr.grad, br.grad],
+           ["dx", "dgamma", "dbeta"])
