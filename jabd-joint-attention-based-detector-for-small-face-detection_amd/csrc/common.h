@@ -34,6 +34,18 @@ __device__ __forceinline__ float hsigmoid_f(float v) {
 }
 __device__ __forceinline__ float hswish_f(float v) { return v * hsigmoid_f(v); }
 
+// c + a * b per component as two packed v_pk_fma_f32 (one IEEE fma per
+// element, the same result as four fmaf; the compiler emits scalar v_fma_f32
+// for the float4 form, half the VALU rate).
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float4 fma4pk(float4 a, float4 b, float4 c) {
+  const f32x2_t r0 =
+      __builtin_elementwise_fma((f32x2_t){a.x, a.y}, (f32x2_t){b.x, b.y}, (f32x2_t){c.x, c.y});
+  const f32x2_t r1 =
+      __builtin_elementwise_fma((f32x2_t){a.z, a.w}, (f32x2_t){b.z, b.w}, (f32x2_t){c.z, c.w});
+  return make_float4(r0.x, r0.y, r1.x, r1.y);
+}
+
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 

@@ -24,13 +24,7 @@ __device__ __forceinline__ float dw_act(float v, int act, float slope) {
 constexpr int kDwThreads = 256;
 constexpr int kPW = 4;
 
-__device__ __forceinline__ float4 f4fma(float4 a, float4 w, float4 c) {
-  c.x = fmaf(a.x, w.x, c.x);
-  c.y = fmaf(a.y, w.y, c.y);
-  c.z = fmaf(a.z, w.z, c.z);
-  c.w = fmaf(a.w, w.w, c.w);
-  return c;
-}
+__device__ __forceinline__ float4 f4fma(float4 a, float4 w, float4 c) { return fma4pk(a, w, c); }
 
 template <int K, int S>
 __global__ __launch_bounds__(kDwThreads) void dw_kernel(const DwArgs p, int strips_per_blk) {

@@ -275,10 +275,7 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
               const int px = (2 * orow + kh + C::PAD - 1) * C::IW + 2 * ocol + kw + C::PAD - 1;
               const float4 xv = *reinterpret_cast<const float4*>(xq + px * 4);
               const float4 wv = sws[kh * 3 + kw][sq];
-              v.x = fmaf(xv.x, wv.x, v.x);
-              v.y = fmaf(xv.y, wv.y, v.y);
-              v.z = fmaf(xv.z, wv.z, v.z);
-              v.w = fmaf(xv.w, wv.w, v.w);
+              v = fma4pk(xv, wv, v);
             }
           *reinterpret_cast<float4*>(p.sy + (int64_t)it.b * p.sy_bs +
                                      ((int64_t)oh * p.OW + ow) * p.sy_ps + sc) = v;
@@ -379,10 +376,7 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
 #pragma unroll
           for (int kw = 0; kw < K; ++kw) {
             const float4 xv = row[o * S + kw], wv = wk[kw];
-            a2[o].x = fmaf(xv.x, wv.x, a2[o].x);
-            a2[o].y = fmaf(xv.y, wv.y, a2[o].y);
-            a2[o].z = fmaf(xv.z, wv.z, a2[o].z);
-            a2[o].w = fmaf(xv.w, wv.w, a2[o].w);
+            a2[o] = fma4pk(xv, wv, a2[o]);
           }
       }
 #pragma unroll
@@ -621,10 +615,7 @@ __global__ __launch_bounds__(256, 2) void expdw_strip_kernel(const jabd_expdw_ar
 #pragma unroll
             for (int kw = 0; kw < K; ++kw) {
               const float4 xv = row[o + kw], wv = wk[kw];
-              a2[o].x = fmaf(xv.x, wv.x, a2[o].x);
-              a2[o].y = fmaf(xv.y, wv.y, a2[o].y);
-              a2[o].z = fmaf(xv.z, wv.z, a2[o].z);
-              a2[o].w = fmaf(xv.w, wv.w, a2[o].w);
+              a2[o] = fma4pk(xv, wv, a2[o]);
             }
         }
 #pragma unroll
@@ -961,10 +952,7 @@ __global__ __launch_bounds__(64 * (XW_NE + 4)) void expdw_ws_kernel(const jabd_e
             const float4 xv =
                 __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
             const float4 wv = sws[(kh * 3 + kw) * (W::SKC / 4) + sq];
-            v.x = fmaf(xv.x, wv.x, v.x);
-            v.y = fmaf(xv.y, wv.y, v.y);
-            v.z = fmaf(xv.z, wv.z, v.z);
-            v.w = fmaf(xv.w, wv.w, v.w);
+            v = fma4pk(xv, wv, v);
           }
         *reinterpret_cast<float4*>(p.sy + (int64_t)it.b * p.sy_bs +
                                    ((int64_t)oh * p.OW + ow) * p.sy_ps + 4 * sq) = v;
@@ -1001,10 +989,7 @@ __global__ __launch_bounds__(64 * (XW_NE + 4)) void expdw_ws_kernel(const jabd_e
 #pragma unroll
             for (int kw = 0; kw < K; ++kw) {
               const float4 xv = row[o * S + kw], wv = wk[kw];
-              a2[o].x = fmaf(xv.x, wv.x, a2[o].x);
-              a2[o].y = fmaf(xv.y, wv.y, a2[o].y);
-              a2[o].z = fmaf(xv.z, wv.z, a2[o].z);
-              a2[o].w = fmaf(xv.w, wv.w, a2[o].w);
+              a2[o] = fma4pk(xv, wv, a2[o]);
             }
         }
 #pragma unroll

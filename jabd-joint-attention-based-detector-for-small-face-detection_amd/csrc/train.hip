@@ -1055,8 +1055,7 @@ static int64_t wgrad_chunks(const ConvArgs& a) {
 // segments are loaded once per kernel row and reused across the k taps in
 // registers; no per-element index division.
 __device__ __forceinline__ void fma4(float4& a, const float4 x, const float4 y) {
-  a.x = fmaf(x.x, y.x, a.x); a.y = fmaf(x.y, y.y, a.y);
-  a.z = fmaf(x.z, y.z, a.z); a.w = fmaf(x.w, y.w, a.w);
+  a = fma4pk(x, y, a);
 }
 
 __host__ __device__ constexpr int floordiv_c(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }

@@ -4,7 +4,7 @@
 # forward, the training steps and C5 NMS.  Raw rocprofv3 output stays in
 # /tmp on the box; only logs and the per-kernel CSV summaries go to
 # gpurun_out/<round>/ (the merge-back is capped at 64 MiB).
-# Usage on the GPU box: bash tools/gpu_profile.sh r02
+# Usage on the GPU box: bash tools/gpu_profile.sh r03
 set -o pipefail
 R=${1:-r02}
 cd $GRAFT_REPO_ROOT
