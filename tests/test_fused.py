@@ -80,7 +80,7 @@ def test_expand_dw_parity(cuda, spec, hw):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("act", ["hswish", "relu", "none"])
-@pytest.mark.parametrize("hw", [(37, 29), (128, 96), (1, 2)])
+@pytest.mark.parametrize("hw", [(37, 29), (128, 96), (1, 2), (17, 130), (6, 1024)])
 def test_stem_parity(cuda, act, hw):
     """MNv3 stem (nets/mobilenetV3.py:455-457,511): conv3x3/s2/p1 3->16 on the
     NCHW input + folded bias + act, NHWC out, vs torch fp32 conv2d."""
