@@ -388,6 +388,15 @@ typedef struct jabd_dw_args {
 /* Number of per-image partial-sum blocks the dw kernel uses (size of part). */
 int64_t jabd_dw_nblk(int64_t B, int64_t OH, int64_t OW, int64_t C);
 int jabd_dwconv_nhwc_f32(const jabd_dw_args* args, jabd_stream_t stream);
+/* Training form (nets/mobilenetV3.py:142, conv2 -> bn2): the depthwise conv
+ * (args->part must be NULL) that also writes the BatchNorm statistics of its
+ * output as shifted partial sums stats_part [jabd_dwconv_stats_nblk][2][C]
+ * around shift[C] (the output at pixel (0, 0) of image 0, also written);
+ * jabd_bn_stats_final_f32 turns them into mean / invstd and the running
+ * statistics, replacing jabd_bn_stats_f32's pass over the output. */
+int64_t jabd_dwconv_stats_nblk(int64_t B, int64_t OH, int64_t OW, int64_t C);
+int jabd_dwconv_stats_f32(const jabd_dw_args* args, float* stats_part, float* shift,
+                          jabd_stream_t stream);
 
 /* A1 fused block front half (eval) — nets/mobilenetV3.py:141-142: expand 1x1
  * conv (+ folded bn1, packed like jabd_conv_args.w, Kc = ceil(Cin/16)) + act
@@ -530,6 +539,11 @@ int jabd_heads_wpack_f32(float* wb, float* wc, float* wl, const float* bb, const
 int64_t jabd_bn_nblk(int64_t M, int32_t C);
 /* mean/invstd of x over M rows (biased var); running stats updated in place
  * (running_var with the unbiased estimate) when non-null. */
+/* jabd_bn_stats_f32's final step for partials written by a producer
+ * (jabd_dwconv_stats_f32): shift[c] is the value they were taken around. */
+int jabd_bn_stats_final_f32(const float* shift, const float* part, int64_t nblk, int64_t M,
+                            int32_t C, float* mean, float* invstd, float* running_mean,
+                            float* running_var, float momentum, float eps, jabd_stream_t stream);
 int jabd_bn_stats_f32(const float* x, int32_t ldx, int64_t M, int32_t C, float* part,
                       float* mean, float* invstd, float* running_mean, float* running_var,
                       float momentum, float eps, jabd_stream_t stream);

@@ -26,8 +26,17 @@ constexpr int kPW = 4;
 
 __device__ __forceinline__ float4 f4fma(float4 a, float4 w, float4 c) { return fma4pk(a, w, c); }
 
-template <int K, int S>
-__global__ __launch_bounds__(kDwThreads) void dw_kernel(const DwArgs p, int strips_per_blk) {
+// ST: also the BatchNorm statistics of the output for the training forward
+// (MNv3 Block_eca bn2 follows the depthwise conv): per workgroup the shifted
+// sums sum(y - sh), sum((y - sh)^2) of its outputs, rows added in a fixed
+// order, to stp[blk][0|1][C] (blk = blockIdx.y * gridDim.x + blockIdx.x) in
+// bn_stats_part's format; sh = the output at pixel (0, 0) of image 0, which
+// every workgroup recomputes with the main loop's tap order (workgroup (0, 0)
+// writes it to shift[] for bn_stats_final).  Saves bn2's statistics pass.
+template <int K, int S, bool ST>
+__global__ __launch_bounds__(kDwThreads) void dw_kernel(const DwArgs p, int strips_per_blk,
+                                                       float* __restrict__ stp,
+                                                       float* __restrict__ shift) {
   constexpr int SPAN = (kPW - 1) * S + K;
   const int CG = p.C >> 2;
   const int SP = kDwThreads / CG;  // strips in flight per pass
@@ -49,6 +58,29 @@ __global__ __launch_bounds__(kDwThreads) void dw_kernel(const DwArgs p, int stri
     if (p.bias) bias = reinterpret_cast<const float4*>(p.bias)[cg];
   }
   float4 psum = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 sh = make_float4(0.f, 0.f, 0.f, 0.f), ss = sh, sq = sh;
+  if (ST && active) {
+    float4 a0 = bias;
+    const float* x0 = p.x + 4 * cg;  // image 0
+#pragma unroll
+    for (int kh = 0; kh < K; ++kh) {
+      const int ih = -p.pad + kh;
+      if (ih < 0 || ih >= p.H) continue;
+#pragma unroll
+      for (int kw = 0; kw < K; ++kw) {
+        const int iw = -p.pad + kw;
+        const float4 r = (iw >= 0 && iw < p.W)
+                             ? *reinterpret_cast<const float4*>(x0 + ((int64_t)ih * p.W + iw) * p.x_ps)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+        a0 = f4fma(r, wr[kh * K + kw], a0);
+      }
+    }
+    sh.x = dw_act(a0.x, p.act, p.slope);
+    sh.y = dw_act(a0.y, p.act, p.slope);
+    sh.z = dw_act(a0.z, p.act, p.slope);
+    sh.w = dw_act(a0.w, p.act, p.slope);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && sp == 0) reinterpret_cast<float4*>(shift)[cg] = sh;
+  }
 
   for (int it = 0; active && it * SP < strips_per_blk; ++it) {
     const int64_t s = s0 + it * SP + sp;
@@ -86,6 +118,30 @@ __global__ __launch_bounds__(kDwThreads) void dw_kernel(const DwArgs p, int stri
       v.w = dw_act(acc[o].w, p.act, p.slope);
       *reinterpret_cast<float4*>(yb + ((int64_t)oh * p.OW + ow0 + o) * p.y_ps) = v;
       psum.x += v.x; psum.y += v.y; psum.z += v.z; psum.w += v.w;
+      if (ST) {
+        const float4 d = make_float4(v.x - sh.x, v.y - sh.y, v.z - sh.z, v.w - sh.w);
+        ss.x += d.x; ss.y += d.y; ss.z += d.z; ss.w += d.w;
+        sq.x = fmaf(d.x, d.x, sq.x); sq.y = fmaf(d.y, d.y, sq.y);
+        sq.z = fmaf(d.z, d.z, sq.z); sq.w = fmaf(d.w, d.w, sq.w);
+      }
+    }
+  }
+
+  if (ST) {
+    __shared__ float4 rs[kDwThreads], rq[kDwThreads];
+    rs[tid] = ss;
+    rq[tid] = sq;
+    __syncthreads();
+    if (tid < CG) {
+      float4 S_ = make_float4(0.f, 0.f, 0.f, 0.f), Q_ = S_;
+      for (int q = 0; q < SP; ++q) {
+        const float4 a = rs[q * CG + tid], b = rq[q * CG + tid];
+        S_.x += a.x; S_.y += a.y; S_.z += a.z; S_.w += a.w;
+        Q_.x += b.x; Q_.y += b.y; Q_.z += b.z; Q_.w += b.w;
+      }
+      const int64_t blk = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+      reinterpret_cast<float4*>(stp + blk * 2 * p.C)[tid] = S_;
+      reinterpret_cast<float4*>(stp + blk * 2 * p.C + p.C)[tid] = Q_;
     }
   }
 
@@ -139,10 +195,10 @@ extern "C" int jabd_dwconv_nhwc_f32(const jabd_dw_args* args, jabd_stream_t stre
   JABD_REQUIRE(!a.part || a.nblk == nblk, "dw: nblk %d != %lld", a.nblk, (long long)nblk);
   dim3 grid((unsigned)nblk, (unsigned)a.B);
   hipStream_t st = as_stream(stream);
-#define DW_CASE(K, S)                                                        \
-  if (a.k == K && a.stride == S) {                                          \
-    dw_kernel<K, S><<<grid, kDwThreads, 0, st>>>(a, (int)per);             \
-    return check_launch("dwconv");                                          \
+#define DW_CASE(K, S)                                                                       \
+  if (a.k == K && a.stride == S) {                                                         \
+    dw_kernel<K, S, false><<<grid, kDwThreads, 0, st>>>(a, (int)per, nullptr, nullptr);    \
+    return check_launch("dwconv");                                                         \
   }
   DW_CASE(3, 1)
   DW_CASE(3, 2)
@@ -150,5 +206,38 @@ extern "C" int jabd_dwconv_nhwc_f32(const jabd_dw_args* args, jabd_stream_t stre
   DW_CASE(5, 2)
 #undef DW_CASE
   set_error("dw: unsupported k=%d stride=%d", a.k, a.stride);
+  return JABD_EINVAL;
+}
+
+extern "C" int64_t jabd_dwconv_stats_nblk(int64_t B, int64_t OH, int64_t OW, int64_t C) {
+  const int64_t n = jabd_dw_nblk(B, OH, OW, C);
+  return n < 0 ? n : n * B;
+}
+
+extern "C" int jabd_dwconv_stats_f32(const jabd_dw_args* args, float* stats_part, float* shift,
+                                     jabd_stream_t stream) {
+  JABD_REQUIRE(args && stats_part && shift, "dw_stats: null args");
+  const DwArgs& a = *args;
+  JABD_REQUIRE(a.x && a.w && a.y && !a.part, "dw_stats: null pointer / ECA partials not supported");
+  JABD_REQUIRE(a.C % 4 == 0 && a.C / 4 <= kDwThreads && a.x_ps % 4 == 0 && a.y_ps % 4 == 0,
+               "dw_stats: channel layout");
+  JABD_REQUIRE(a.OH == (a.H + 2 * a.pad - a.k) / a.stride + 1 &&
+                   a.OW == (a.W + 2 * a.pad - a.k) / a.stride + 1,
+               "dw_stats: output size mismatch");
+  const int64_t per = dw_strips_per_blk(a.B, a.OH, a.OW, a.C);
+  const int64_t nblk = jabd_dw_nblk(a.B, a.OH, a.OW, a.C);
+  dim3 grid((unsigned)nblk, (unsigned)a.B);
+  hipStream_t st = as_stream(stream);
+#define DWS_CASE(K, S)                                                                      \
+  if (a.k == K && a.stride == S) {                                                         \
+    dw_kernel<K, S, true><<<grid, kDwThreads, 0, st>>>(a, (int)per, stats_part, shift);    \
+    return check_launch("dwconv_stats");                                                   \
+  }
+  DWS_CASE(3, 1)
+  DWS_CASE(3, 2)
+  DWS_CASE(5, 1)
+  DWS_CASE(5, 2)
+#undef DWS_CASE
+  set_error("dw_stats: unsupported k=%d stride=%d", a.k, a.stride);
   return JABD_EINVAL;
 }

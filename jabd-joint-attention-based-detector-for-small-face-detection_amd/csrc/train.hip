@@ -1533,6 +1533,20 @@ extern "C" int64_t jabd_bn_nblk(int64_t M, int32_t C) {
   return cdiv(M, bn_rows_per_blk(M, C));
 }
 
+// The final half of jabd_bn_stats_f32 for partials a producer wrote in
+// bn_stats_part's format (shift[c] = the value the partials were taken
+// around): mean, invstd and the running-statistics update.
+extern "C" int jabd_bn_stats_final_f32(const float* shift, const float* part, int64_t nblk,
+                                       int64_t M, int32_t C, float* mean, float* invstd,
+                                       float* running_mean, float* running_var, float momentum,
+                                       float eps, jabd_stream_t stream) {
+  JABD_REQUIRE(shift && part && mean && invstd && nblk > 0 && M > 0 && C > 0,
+               "bn_stats_final: bad args");
+  bn_stats_final_kernel<<<(unsigned)cdiv(C, kFinLanes), kFinThreads, 0, as_stream(stream)>>>(
+      shift, part, nblk, M, C, momentum, eps, mean, invstd, running_mean, running_var);
+  return check_launch("bn_stats_final");
+}
+
 extern "C" int jabd_bn_stats_f32(const float* x, int32_t ldx, int64_t M, int32_t C, float* part,
                                  float* mean, float* invstd, float* running_mean,
                                  float* running_var, float momentum, float eps,

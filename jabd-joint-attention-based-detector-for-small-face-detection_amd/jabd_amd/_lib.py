@@ -169,6 +169,10 @@ SIGNATURES = {
     "jabd_stem_nchw_f32": [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp],
     "jabd_dw_nblk": [c_i64, c_i64, c_i64, c_i64],
     "jabd_dwconv_nhwc_f32": [ctypes.POINTER(DwArgs), c_vp],
+    "jabd_dwconv_stats_nblk": [c_i64, c_i64, c_i64, c_i64],
+    "jabd_dwconv_stats_f32": [ctypes.POINTER(DwArgs), c_vp, c_vp, c_vp],
+    "jabd_bn_stats_final_f32": [c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_f32,
+                                c_f32, c_vp],
     "jabd_expand_dw_nblk": [c_i32, c_i32, c_i32, c_i32],
     "jabd_expand_dw_nhwc_f32": [ctypes.POINTER(ExpDwArgs), c_vp],
     "jabd_expand_dw_select": [c_i32],
@@ -255,6 +259,7 @@ _RESTYPE = {"jabd_version": ctypes.c_char_p, "jabd_dw_nblk": ctypes.c_int64,
             "jabd_conv_wgrad_eca_part_floats": ctypes.c_int64, "jabd_bn_sum_nblk": ctypes.c_int64,
             "jabd_dw_wgrad_part_floats": ctypes.c_int64,
             "jabd_dw_dgrad_bn_part_floats": ctypes.c_int64,
+            "jabd_dwconv_stats_nblk": ctypes.c_int64,
             "jabd_adam_num_chunks": ctypes.c_int64, "jabd_beca_ws_floats": ctypes.c_int64,
             "jabd_adaptive_pool_ws_floats": ctypes.c_int64,
             "jabd_abi_struct_size": ctypes.c_int64, "jabd_conv_workspace_size": ctypes.c_int64,

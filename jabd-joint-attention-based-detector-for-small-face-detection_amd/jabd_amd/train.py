@@ -40,7 +40,8 @@ ECA_WGRAD = __import__("os").environ.get("JABD_ECA_WGRAD", "1") != "0"
 # JABD_ECA_SUMS=0: the ECA pool of a block reads d in its own pass (A/B)
 ECA_SUMS = __import__("os").environ.get("JABD_ECA_SUMS", "1") != "0"
 # JABD_DW_BN_FUSE=0: bn1's backward partials from their own pass over de and
-# e_pre instead of the depthwise data-gradient kernel (A/B)
+# e_pre instead of the depthwise data-gradient kernel, and bn2's statistics
+# from their own pass over d_pre instead of the depthwise forward (A/B)
 DW_BN_FUSE = __import__("os").environ.get("JABD_DW_BN_FUSE", "1") != "0"
 
 
@@ -802,20 +803,24 @@ def conv(x, m, stride=1, pad=0, nchw_in=False):
 
 
 # ----------------------------------------------------------------------------- fused block
-def _bn_fwd(x, bn, act, slope=0.0, res=None, sums=False):
+def _bn_fwd(x, bn, act, slope=0.0, res=None, sums=False, stats=None):
     """Batch-stat BN (+res) + act of NHWC x; running buffers updated in place.
     Returns (y, (gamma, beta, mean, invstd)); sums=True adds the per-image
     channel-sum partials of y ([B, nblk, C], written by the apply pass) or
-    None when the map size does not fit its row blocks."""
+    None when the map size does not fit its row blocks.  stats = (mean,
+    invstd) already computed by x's producer (running buffers updated there)."""
     B, H, W, C = x.shape
     M = B * H * W
-    nblk = int(lib().jabd_bn_nblk(M, C))
-    part = torch.empty((nblk, 2, C), dtype=torch.float32, device=x.device)
-    mean = torch.empty(C, dtype=torch.float32, device=x.device)
-    invstd = torch.empty_like(mean)
-    call("jabd_bn_stats_f32", x.data_ptr(), C, M, C, part.data_ptr(), mean.data_ptr(),
-         invstd.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
-         float(bn.momentum), float(bn.eps), _st())
+    if stats is not None:
+        mean, invstd = stats
+    else:
+        nblk = int(lib().jabd_bn_nblk(M, C))
+        part = torch.empty((nblk, 2, C), dtype=torch.float32, device=x.device)
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        invstd = torch.empty_like(mean)
+        call("jabd_bn_stats_f32", x.data_ptr(), C, M, C, part.data_ptr(), mean.data_ptr(),
+             invstd.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+             float(bn.momentum), float(bn.eps), _st())
     g = bn.weight.detach()
     b = bn.bias.detach()
     y = torch.empty_like(x)
@@ -891,6 +896,35 @@ def _dw_fwd(x, weight, stride):
     return y, wt
 
 
+def _dw_fwd_bn_stats(x, weight, stride, bn):
+    """_dw_fwd whose kernel also takes the batch statistics of its output for
+    the following BatchNorm (jabd_dwconv_stats_f32 + jabd_bn_stats_final_f32;
+    running buffers updated).  Returns (y, wt, (mean, invstd))."""
+    C, _, k, _ = weight.shape
+    wt = F.transpose(weight.detach().reshape(C, k * k))
+    B, H, W, _ = x.shape
+    pad = k // 2
+    OH = (H + 2 * pad - k) // stride + 1
+    OW = (W + 2 * pad - k) // stride + 1
+    y = torch.empty((B, OH, OW, C), dtype=torch.float32, device=x.device)
+    a = F.DwArgs()
+    a.x, a.x_bs, a.x_ps = x.data_ptr(), x.stride(0), C
+    a.B, a.H, a.W, a.C = B, H, W, C
+    a.w, a.bias = wt.data_ptr(), None
+    a.y, a.y_bs, a.y_ps = y.data_ptr(), y.stride(0), C
+    a.OH, a.OW, a.k, a.stride, a.pad, a.act = OH, OW, k, stride, pad, ACT["none"]
+    nblk = int(lib().jabd_dwconv_stats_nblk(B, OH, OW, C))
+    part = torch.empty((nblk, 2, C), dtype=torch.float32, device=x.device)
+    shift = torch.empty(C, dtype=torch.float32, device=x.device)
+    call("jabd_dwconv_stats_f32", ctypes.byref(a), part.data_ptr(), shift.data_ptr(), _st())
+    mean = torch.empty(C, dtype=torch.float32, device=x.device)
+    invstd = torch.empty_like(mean)
+    call("jabd_bn_stats_final_f32", shift.data_ptr(), part.data_ptr(), nblk, B * OH * OW, C,
+         mean.data_ptr(), invstd.data_ptr(), bn.running_mean.data_ptr(),
+         bn.running_var.data_ptr(), float(bn.momentum), float(bn.eps), _st())
+    return y, wt, (mean, invstd)
+
+
 def _dw_bwd(dy, x, wt, k, stride, want_dx=True):
     B, H, W, C = x.shape
     OH, OW = dy.shape[1], dy.shape[2]
@@ -949,8 +983,12 @@ class MNv3BlockFn(torch.autograd.Function):
         k, stride = blk.kernel_size, blk.stride
         e_pre = _conv_fwd(s, blk.conv1.weight)
         e, st1 = _bn_fwd(e_pre, blk.bn1, act)
-        d_pre, wt2 = _dw_fwd(e, blk.conv2.weight, stride)
-        d, st2, psum = _bn_fwd(d_pre, blk.bn2, act, sums=True)
+        if DW_BN_FUSE:
+            d_pre, wt2, bst2 = _dw_fwd_bn_stats(e, blk.conv2.weight, stride, blk.bn2)
+            d, st2, psum = _bn_fwd(d_pre, blk.bn2, act, sums=True, stats=bst2)
+        else:
+            d_pre, wt2 = _dw_fwd(e, blk.conv2.weight, stride)
+            d, st2, psum = _bn_fwd(d_pre, blk.bn2, act, sums=True)
         B, OH, OW, E = d.shape
         w1 = blk.eca.conv.weight.detach().reshape(-1).float().contiguous()
         if psum is None:

@@ -368,3 +368,40 @@ def test_dw_dgrad_bn_fused(cuda, c, k, s, bhw, act):
         assert rel_err(a.cpu(), b.cpu()) < 1e-5
     _check([_nchw(dx1.cpu()), dg1.cpu(), db1.cpu()], [xr.grad, gr.grad, br.grad],
            ["dx", "dgamma", "dbeta"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,k,s,bhw,scale", [(72, 3, 1, (4, 40, 36), 1.0), (120, 5, 1, (3, 17, 29), 50.0),
+                                             (240, 3, 2, (2, 30, 34), 1.0), (672, 5, 2, (3, 16, 16), 50.0)])
+def test_dw_fwd_bn_stats(cuda, c, k, s, bhw, scale):
+    """bn2's batch statistics taken by the depthwise forward kernel
+    (jabd_dwconv_stats_f32 + jabd_bn_stats_final_f32) against the separate
+    statistics pass (jabd_bn_stats_f32): the conv output bit-identical, mean,
+    invstd and the running buffers within fp32 reassociation, including x50
+    inputs whose mean dwarfs their spread (the shifted sums must not cancel)."""
+    from jabd_amd import train as T
+    B, H, W = bhw
+    g = torch.Generator().manual_seed(c + k + s)
+    x = (torch.randn(B, H, W, c, generator=g) + 3.0) * scale
+    w = torch.randn(c, 1, k, k, generator=g) / k
+    dev = torch.device(cuda)
+    bns = []
+    for _ in range(2):
+        bn = torch.nn.BatchNorm2d(c).to(dev)
+        with torch.no_grad():
+            bn.running_mean.copy_(torch.linspace(-1, 1, c))
+            bn.running_var.copy_(torch.linspace(0.5, 2, c))
+        bns.append(bn)
+    xg, wg = x.to(dev), w.to(dev)
+    y1, _, (m1, i1) = T._dw_fwd_bn_stats(xg, wg, s, bns[0])
+    y2, _ = T._dw_fwd(xg, wg, s)
+    _, (_, _, m2, i2) = T._bn_fwd(y2, bns[1], "none")
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    assert rel_err(m1.cpu(), m2.cpu()) < 1e-6
+    assert rel_err(i1.cpu(), i2.cpu()) < 1e-5
+    assert rel_err(bns[0].running_mean.cpu(), bns[1].running_mean.cpu()) < 1e-6
+    assert rel_err(bns[0].running_var.cpu(), bns[1].running_var.cpu()) < 1e-5
+    ref = y2.double()
+    var = ref.var((0, 1, 2), unbiased=False)
+    assert rel_err(i1.cpu(), (var + bns[0].eps).rsqrt().cpu()) < 1e-5
