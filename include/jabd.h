@@ -365,6 +365,17 @@ int jabd_conv_pack_f32(const float* w, int32_t cout, int32_t cin, int32_t kh, in
                        int32_t transposed, int32_t Kc, int32_t Ntiles, float* wp, int32_t K8,
                        int32_t NT32, float* wp32, jabd_stream_t stream);
 int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t stream);
+/* Training forward of a 1x1 conv followed by BatchNorm (MNv3 Block_eca
+ * conv1 -> bn1, nets/mobilenetV3.py:141-143 / :160-170): the streaming 1x1
+ * kernel also writes the shifted batch-statistics partials of its output,
+ * part [nblk][2][Cout] around shift [Cout] (the output at pixel 0), which
+ * jabd_bn_stats_final_f32 turns into mean / invstd.  No gate, second
+ * source or residual.  _nblk returns the partial rows the layer needs, 0 when
+ * the statistics form does not serve it (the caller then runs
+ * jabd_conv2d_nhwc_f32 + jabd_bn_stats_f32). */
+int64_t jabd_conv1x1_bn_stats_nblk(const jabd_conv_args* args);
+int jabd_conv1x1_bn_stats_f32(const jabd_conv_args* args, float* part, int64_t nblk,
+                              float* shift, jabd_stream_t stream);
 
 /* A1 MobileNetV3 stem — nets/mobilenetV3.py:455-457,511: conv3x3/s2/p1 3->16
  * on the NCHW input [B,3,H,W] with folded BN (w [27][16] tap-major, bias [16])

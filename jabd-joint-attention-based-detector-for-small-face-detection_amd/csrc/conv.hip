@@ -758,7 +758,7 @@ static bool conv_generic_only() {
 
 namespace jabd {
 int conv1x1_m32_dispatch(const ConvArgs& a, hipStream_t st, bool kxk);
-int conv1x1_stream_dispatch(const ConvArgs& a, hipStream_t st);
+int conv1x1_stream_dispatch(const ConvArgs& a, hipStream_t st, StreamStats* ss = nullptr);
 }
 
 // Which 1x1 kernel: the 32x32x2 LDS-weight kernel (conv32.hip) pays off when
@@ -776,9 +776,11 @@ static bool use_conv32(const ConvArgs& a) {
   return a.Cout >= 96 && K >= 96;
 }
 
-extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t stream) {
+// Argument checks shared by the conv entry points; fills a (M, flags) and
+// reports whether the fast 1x1 kernels take the layout.
+static int conv_setup(const jabd_conv_args* args, ConvArgs& a, bool& fast1x1, bool& vec4) {
   JABD_REQUIRE(args, "conv: null args");
-  ConvArgs a = *args;
+  a = *args;
   JABD_REQUIRE(a.x && a.w && a.y, "conv: null pointer");
   JABD_REQUIRE(a.B > 0 && a.Cin > 0 && a.Cout > 0 && a.KH > 0 && a.KW > 0 && a.stride > 0,
                "conv: bad shape");
@@ -815,16 +817,14 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
     a.flags = v4 ? 1 : 0;
     JABD_REQUIRE(!a.y2 || v4, "conv: split output needs the vector epilogue layout");
   }
-  const bool vec4 = !a.nchw_in && a.Cin % 4 == 0 && a.x_ps % 4 == 0 && a.x_c0 % 4 == 0 &&
-                    (reinterpret_cast<uintptr_t>(a.x) & 15) == 0;
-  hipStream_t st = as_stream(stream);
-  const int tn = a.tn;
-  JABD_REQUIRE(a.Ntiles % tn == 0, "conv: Ntiles %% tn != 0");
+  vec4 = !a.nchw_in && a.Cin % 4 == 0 && a.x_ps % 4 == 0 && a.x_c0 % 4 == 0 &&
+         (reinterpret_cast<uintptr_t>(a.x) & 15) == 0;
+  JABD_REQUIRE(a.tn > 0 && a.Ntiles % a.tn == 0, "conv: Ntiles %% tn != 0");
   const int64_t OHW = (int64_t)a.OH * a.OW;
   const int64_t maxps = std::max<int64_t>(std::max<int64_t>(a.x_ps, a.y_ps),
                                           std::max<int64_t>(a.res ? a.res_ps : 0,
                                                             a.x2 ? a.x2_ps : 0));
-  const bool fast1x1 =
+  fast1x1 =
       is1x1 && !a.tconv && vec4 && (a.flags & 1) && !a.y2 && a.x_bs == OHW * a.x_ps &&
       a.y_bs == OHW * a.y_ps && (!a.res || a.res_bs == OHW * a.res_ps) &&
       (!a.ascale || a.ascale_bs % 4 == 0) &&
@@ -832,6 +832,50 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
                                   : (a.x2_stride > 1 && a.x2_bs % a.x2_ps == 0 &&
                                      a.x2_bs * a.B < ((int64_t)1 << 31)))) &&
       (a.M + 64) * (maxps + 16) < ((int64_t)1 << 31) && !conv_generic_only();
+  return 0;
+}
+
+// The statistics form of the streaming 1x1 conv serves the layer iff the
+// plain entry point would route it to the streaming kernel and it carries no
+// gate, second source or residual.
+static bool conv_stats_form(const ConvArgs& a, bool fast1x1) {
+  return fast1x1 && !use_conv32(a) && !a.reserved1 && !a.ascale && !a.x2 && !a.res;
+}
+
+extern "C" int64_t jabd_conv1x1_bn_stats_nblk(const jabd_conv_args* args) {
+  ConvArgs a;
+  bool fast1x1 = false, vec4 = false;
+  if (conv_setup(args, a, fast1x1, vec4) != JABD_OK || !conv_stats_form(a, fast1x1)) return 0;
+  jabd::StreamStats ss{nullptr, nullptr, 0, true};
+  if (jabd::conv1x1_stream_dispatch(a, nullptr, &ss) != 0) return 0;
+  return ss.nblk;
+}
+
+extern "C" int jabd_conv1x1_bn_stats_f32(const jabd_conv_args* args, float* part, int64_t nblk,
+                                         float* shift, jabd_stream_t stream) {
+  ConvArgs a;
+  bool fast1x1 = false, vec4 = false;
+  const int e = conv_setup(args, a, fast1x1, vec4);
+  if (e != JABD_OK) return e;
+  JABD_REQUIRE(conv_stats_form(a, fast1x1),
+               "conv1x1_bn_stats: layer not served by the streaming statistics form");
+  jabd::StreamStats ss{part, shift, nblk, false};
+  const int r = jabd::conv1x1_stream_dispatch(a, as_stream(stream), &ss);
+  JABD_REQUIRE(r >= 0, "conv1x1_bn_stats: no streaming kernel for this shape");
+  return r;
+}
+
+extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t stream) {
+  ConvArgs a;
+  bool fast1x1 = false, vec4 = false;
+  {
+    const int e = conv_setup(args, a, fast1x1, vec4);
+    if (e != JABD_OK) return e;
+  }
+  const bool is1x1 = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
+  hipStream_t st = as_stream(stream);
+  const int tn = a.tn;
+  const int64_t OHW = (int64_t)a.OH * a.OW;
   if (fast1x1 && use_conv32(a)) {
     const int r = conv1x1_m32_dispatch(a, st, false);
     if (r >= 0) return r;

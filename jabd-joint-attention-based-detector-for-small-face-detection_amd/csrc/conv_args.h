@@ -13,4 +13,11 @@ enum {
   ACT_HSIGMOID = JABD_ACT_HSIGMOID,
   ACT_SIGMOID = JABD_ACT_SIGMOID,
 };
+// conv1x1_stream_dispatch's statistics form (jabd_conv1x1_bn_stats_*)
+struct StreamStats {
+  float* part;
+  float* shift;
+  int64_t nblk;
+  bool query;
+};
 }  // namespace jabd

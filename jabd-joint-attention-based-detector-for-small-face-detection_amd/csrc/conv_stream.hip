@@ -57,9 +57,17 @@ struct CsCfg {
   static constexpr int NW = KC * TN > 24 ? 8 : 4;
 };
 
-template <int TN, int KC, int X2, bool AS>
-__global__ __launch_bounds__((CsCfg<TN, KC>::NW * 64)) void conv1x1_stream_kernel(const ConvArgs p,
-                                                                                int nblk, int ohw) {
+// ST: also the BatchNorm statistics of the output for the training forward
+// (MNv3 Block_eca conv1 -> bn1; no gate, residual or second source): per
+// workgroup the shifted sums sum(y - sh), sum((y - sh)^2) over its blocks,
+// reduced in a fixed order to stp[blockIdx.x][0|1][Cout] (bn_stats_part's
+// format) around sh = the output at pixel 0, which every workgroup computes
+// with the same MFMA sequence as the real pixel 0 (workgroup 0 stores it to
+// shift[] for bn_stats_final).  Saves bn1's statistics pass over the
+// expanded tensor.
+template <int TN, int KC, int X2, bool AS, bool ST = false>
+__global__ __launch_bounds__((CsCfg<TN, KC>::NW * 64)) void conv1x1_stream_kernel(
+    const ConvArgs p, int nblk, int ohw, float* __restrict__ stp, float* __restrict__ shift) {
   constexpr int NW = CsCfg<TN, KC>::NW, NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   f32x4* wl = reinterpret_cast<f32x4*>(smem);
@@ -81,7 +89,44 @@ __global__ __launch_bounds__((CsCfg<TN, KC>::NW * 64)) void conv1x1_stream_kerne
   __syncthreads();
   const int nwv = gridDim.x * NW;
   int blk = blockIdx.x * NW + wave;
-  if (blk >= nblk) return;  // no barrier below
+  // ST: the shift (pixel 0's output, channels 16u + 4g .. +3 in every lane)
+  float4 sh[ST ? TN : 1], ss[ST ? TN : 1], sq[ST ? TN : 1];
+  if (ST) {
+    f32x4 a0[TN];
+#pragma unroll
+    for (int u = 0; u < TN; ++u) {
+      const int n0 = 16 * u + 4 * g;
+      const float4 bb = p.bias && n0 < p.Cout ? *reinterpret_cast<const float4*>(p.bias + n0)
+                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+      a0[u] = (f32x4){bb.x, bb.y, bb.z, bb.w};
+    }
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      if (kc >= p.Kc) break;
+      const int kq = kc * 16 + 4 * g;
+      const float4 a = kq < p.Cin ? *reinterpret_cast<const float4*>(p.x + p.x_c0 + kq)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < TN; ++u) {
+        const f32x4 w = wl[(kc * TN + u) * 64 + lane];
+        a0[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.x, a.x, a0[u], 0, 0, 0);
+        a0[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.y, a.y, a0[u], 0, 0, 0);
+        a0[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.z, a.z, a0[u], 0, 0, 0);
+        a0[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(w.w, a.w, a0[u], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < TN; ++u) {
+      sh[u] = make_float4(cs_act(a0[u][0], p.act, p.slope), cs_act(a0[u][1], p.act, p.slope),
+                          cs_act(a0[u][2], p.act, p.slope), cs_act(a0[u][3], p.act, p.slope));
+      ss[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      sq[u] = ss[u];
+      const int n0 = 16 * u + 4 * g;
+      if (blockIdx.x == 0 && wave == 0 && j == 0 && n0 < p.Cout)
+        *reinterpret_cast<float4*>(shift + n0) = sh[u];
+    }
+  }
+  if (!ST && blk >= nblk) return;  // no barrier below (ST: the reduction has one)
   const int M = (int)p.M, Cin = p.Cin, Ktot = p.Cin + (X2 ? p.Cin2 : 0);
   const int c4n = Cin >> 2;
   const float* xg = p.x + p.x_c0;
@@ -110,9 +155,9 @@ __global__ __launch_bounds__((CsCfg<TN, KC>::NW * 64)) void conv1x1_stream_kerne
   }
   float4 A[KC];
 #pragma unroll
-  for (int kc = 0; kc < KC; ++kc) A[kc] = issue(blk, kc);
+  for (int kc = 0; kc < KC; ++kc) A[kc] = issue(blk < nblk ? blk : 0, kc);
 
-  for (;;) {
+  for (; blk < nblk;) {
     const int nxt = blk + nwv;
     const int bnx = nxt < nblk ? nxt : blk;  // last block: harmless re-read
     const int m = blk * 16 + j;
@@ -174,11 +219,50 @@ __global__ __launch_bounds__((CsCfg<TN, KC>::NW * 64)) void conv1x1_stream_kerne
           v.z = cs_act(v.z, p.act, p.slope);
           v.w = cs_act(v.w, p.act, p.slope);
           *reinterpret_cast<float4*>(p.y + m * p.y_ps + p.y_c0 + n0) = v;
+          if (ST) {
+            const float4 d = make_float4(v.x - sh[u].x, v.y - sh[u].y, v.z - sh[u].z, v.w - sh[u].w);
+            ss[u].x += d.x; ss[u].y += d.y; ss[u].z += d.z; ss[u].w += d.w;
+            sq[u].x = fmaf(d.x, d.x, sq[u].x); sq[u].y = fmaf(d.y, d.y, sq[u].y);
+            sq[u].z = fmaf(d.z, d.z, sq[u].z); sq[u].w = fmaf(d.w, d.w, sq[u].w);
+          }
         }
       }
     }
     if (nxt >= nblk) break;
     blk = nxt;
+  }
+  if (ST) {
+    // lanes j of a channel quad g: xor-tree over j (fixed order), then the
+    // waves in order through LDS (the weights are dead by now)
+#pragma unroll
+    for (int u = 0; u < TN; ++u)
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) {
+        ss[u].x += __shfl_xor(ss[u].x, off); ss[u].y += __shfl_xor(ss[u].y, off);
+        ss[u].z += __shfl_xor(ss[u].z, off); ss[u].w += __shfl_xor(ss[u].w, off);
+        sq[u].x += __shfl_xor(sq[u].x, off); sq[u].y += __shfl_xor(sq[u].y, off);
+        sq[u].z += __shfl_xor(sq[u].z, off); sq[u].w += __shfl_xor(sq[u].w, off);
+      }
+    __syncthreads();
+    float4* red = reinterpret_cast<float4*>(smem);  // [NW][2][TN * 4]
+    if (j == 0) {
+#pragma unroll
+      for (int u = 0; u < TN; ++u) {
+        red[(wave * 2 + 0) * TN * 4 + 4 * u + g] = ss[u];
+        red[(wave * 2 + 1) * TN * 4 + 4 * u + g] = sq[u];
+      }
+    }
+    __syncthreads();
+    if (t < 2 * TN * 4) {
+      const int which = t / (TN * 4), q = t - which * (TN * 4);  // q = 4u + g: channels 4q..
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int w = 0; w < NW; ++w) {
+        const float4 a = red[(w * 2 + which) * TN * 4 + q];
+        v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+      }
+      if (4 * q < p.Cout)
+        *reinterpret_cast<float4*>(stp + ((int64_t)blockIdx.x * 2 + which) * p.Cout + 4 * q) = v;
+    }
   }
 }
 
@@ -214,8 +298,12 @@ static int stream_grid(Kern kern, int threads, size_t lds, int64_t nwg) {
 // Called from jabd_conv2d_nhwc_f32 for the fast-1x1 layouts (contiguous NHWC
 // rows, v4 epilogue, x2 at the same resolution).  Returns -1 when the shape is
 // not one this kernel serves.
-int conv1x1_stream_dispatch(const ConvArgs& a, hipStream_t st) {
+// ss != nullptr: the statistics form (ST; no gate, no second source, no
+// residual).  ss->query: only report the grid (= partial rows) in ss->nblk;
+// otherwise launch and require ss->nblk to match it.
+int conv1x1_stream_dispatch(const ConvArgs& a, hipStream_t st, StreamStats* ss) {
   if (!conv_stream_on()) return -1;
+  if (ss && (a.x2 || a.ascale || a.res || stream_kc(a.Kc) > 4)) return -1;
   const int TN = a.Ntiles, KC = stream_kc(a.Kc);
   if (TN < 1 || TN > 5 || KC < 0) return -1;
   if (a.x2 && a.x2_stride != 1) return -1;
@@ -241,9 +329,35 @@ int conv1x1_stream_dispatch(const ConvArgs& a, hipStream_t st) {
     if ((a.Kc * TN > 24) != (nw_ == 8)) return -1;                                          \
     const int grid = stream_grid(kern, nw_ * 64, lds, cdiv(nblk, nw_));                     \
     if (grid < 1) return -1;                                                                \
-    kern<<<grid, nw_ * 64, lds, st>>>(a, (int)nblk, (int)ohw);                              \
+    kern<<<grid, nw_ * 64, lds, st>>>(a, (int)nblk, (int)ohw, nullptr, nullptr);            \
     return check_launch("conv1x1_stream");                                                  \
   } while (0)
+#define CS_LAUNCH_ST(TN_, KC_)                                                              \
+  do {                                                                                      \
+    auto kern = conv1x1_stream_kernel<TN_, KC_, 0, false, true>;                            \
+    constexpr int nw_ = CsCfg<TN_, KC_>::NW;                                                \
+    if ((a.Kc * TN > 24) != (nw_ == 8)) return -1;                                          \
+    const int grid = stream_grid(kern, nw_ * 64, lds, cdiv(nblk, nw_));                     \
+    if (grid < 1) return -1;                                                                \
+    if (ss->query) {                                                                        \
+      ss->nblk = grid;                                                                      \
+      return 0;                                                                             \
+    }                                                                                       \
+    JABD_REQUIRE(ss->nblk == grid && ss->part && ss->shift,                                 \
+                 "conv1x1_bn_stats: %lld partial rows given, kernel grid %d",               \
+                 (long long)ss->nblk, grid);                                                \
+    kern<<<grid, nw_ * 64, lds, st>>>(a, (int)nblk, (int)ohw, ss->part, ss->shift);         \
+    return check_launch("conv1x1_stream_stats");                                            \
+  } while (0)
+#define CS_FLAGS_ST(TN_, KC_) \
+  if (ss && TN == TN_ && KC == KC_) CS_LAUNCH_ST(TN_, KC_);
+  CS_FLAGS_ST(1, 1) CS_FLAGS_ST(2, 1) CS_FLAGS_ST(3, 1) CS_FLAGS_ST(4, 1) CS_FLAGS_ST(5, 1)
+  CS_FLAGS_ST(1, 2) CS_FLAGS_ST(2, 2) CS_FLAGS_ST(3, 2) CS_FLAGS_ST(4, 2) CS_FLAGS_ST(5, 2)
+  CS_FLAGS_ST(1, 3) CS_FLAGS_ST(2, 3) CS_FLAGS_ST(3, 3) CS_FLAGS_ST(4, 3) CS_FLAGS_ST(5, 3)
+  CS_FLAGS_ST(1, 4) CS_FLAGS_ST(2, 4) CS_FLAGS_ST(3, 4) CS_FLAGS_ST(4, 4) CS_FLAGS_ST(5, 4)
+  if (ss) return -1;
+#undef CS_FLAGS_ST
+#undef CS_LAUNCH_ST
 #define CS_FLAGS(TN_, KC_)                      \
   if (TN == TN_ && KC == KC_) {                 \
     if (x2 == 0 && !as) CS_LAUNCH(TN_, KC_, 0, false); \

@@ -41,7 +41,9 @@ ECA_WGRAD = __import__("os").environ.get("JABD_ECA_WGRAD", "1") != "0"
 ECA_SUMS = __import__("os").environ.get("JABD_ECA_SUMS", "1") != "0"
 # JABD_DW_BN_FUSE=0: bn1's backward partials from their own pass over de and
 # e_pre instead of the depthwise data-gradient kernel, and bn2's statistics
-# from their own pass over d_pre instead of the depthwise forward (A/B)
+# from their own pass over d_pre instead of the depthwise forward, and bn1's
+# statistics from their own pass over e_pre instead of conv1's streaming kernel
+# (A/B)
 DW_BN_FUSE = __import__("os").environ.get("JABD_DW_BN_FUSE", "1") != "0"
 
 
@@ -877,6 +879,33 @@ def _conv_fwd(x, weight, bias=None, stride=1, pad=0, ascale=None):
     return y
 
 
+def _conv_fwd_bn_stats(x, weight, bn):
+    """Bias-free 1x1 _conv_fwd whose streaming kernel also takes the batch
+    statistics of its output for the following BatchNorm
+    (jabd_conv1x1_bn_stats_f32 + jabd_bn_stats_final_f32; running buffers
+    updated).  Returns (y, (mean, invstd)), or (y, None) when the statistics
+    form does not serve the layer (the caller's _bn_fwd then takes them)."""
+    pk = _packed(weight, transposed=False)
+    B, H, W, _ = x.shape
+    y = torch.empty((B, H, W, pk.Cout), dtype=torch.float32, device=x.device)
+    a = _conv_args(x, pk, y, 1, 0)
+    nblk = int(lib().jabd_conv1x1_bn_stats_nblk(ctypes.byref(a))) if pk.KH == 1 else 0
+    if nblk <= 0:
+        call("jabd_conv2d_nhwc_f32", ctypes.byref(a), _st())
+        return y, None
+    C = pk.Cout
+    part = torch.empty((nblk, 2, C), dtype=torch.float32, device=x.device)
+    shift = torch.empty(C, dtype=torch.float32, device=x.device)
+    call("jabd_conv1x1_bn_stats_f32", ctypes.byref(a), part.data_ptr(), nblk, shift.data_ptr(),
+         _st())
+    mean = torch.empty(C, dtype=torch.float32, device=x.device)
+    invstd = torch.empty_like(mean)
+    call("jabd_bn_stats_final_f32", shift.data_ptr(), part.data_ptr(), nblk, B * H * W, C,
+         mean.data_ptr(), invstd.data_ptr(), bn.running_mean.data_ptr(),
+         bn.running_var.data_ptr(), float(bn.momentum), float(bn.eps), _st())
+    return y, (mean, invstd)
+
+
 def _dgrad_1x1_res(dy, weight, res):
     """dx = dgrad of a 1x1 / stride-1 conv, + res added in the GEMM epilogue."""
     pk = _packed(weight, transposed=True)
@@ -981,8 +1010,11 @@ class MNv3BlockFn(torch.autograd.Function):
     def forward(ctx, blk, s, *params):
         act = blk.act_name
         k, stride = blk.kernel_size, blk.stride
-        e_pre = _conv_fwd(s, blk.conv1.weight)
-        e, st1 = _bn_fwd(e_pre, blk.bn1, act)
+        if DW_BN_FUSE:
+            e_pre, bst1 = _conv_fwd_bn_stats(s, blk.conv1.weight, blk.bn1)
+        else:
+            e_pre, bst1 = _conv_fwd(s, blk.conv1.weight), None
+        e, st1 = _bn_fwd(e_pre, blk.bn1, act, stats=bst1)
         if DW_BN_FUSE:
             d_pre, wt2, bst2 = _dw_fwd_bn_stats(e, blk.conv2.weight, stride, blk.bn2)
             d, st2, psum = _bn_fwd(d_pre, blk.bn2, act, sums=True, stats=bst2)

@@ -405,3 +405,51 @@ def test_dw_fwd_bn_stats(cuda, c, k, s, bhw, scale):
     ref = y2.double()
     var = ref.var((0, 1, 2), unbiased=False)
     assert rel_err(i1.cpu(), (var + bns[0].eps).rsqrt().cpu()) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,bhw,scale", [(16, 16, (4, 64, 64), 1.0), (16, 64, (2, 128, 96), 1.0),
+                                                (24, 72, (3, 33, 47), 50.0), (40, 80, (2, 20, 20), 1.0),
+                                                (20, 36, (1, 7, 9), 50.0), (64, 48, (2, 16, 16), 1.0),
+                                                (40, 120, (2, 20, 20), 1.0)])
+def test_conv1x1_bn_stats(cuda, cin, cout, bhw, scale):
+    """bn1's batch statistics taken by conv1's streaming 1x1 kernel
+    (jabd_conv1x1_bn_stats_f32 + jabd_bn_stats_final_f32) against the
+    separate statistics pass: the conv output bit-identical to the plain
+    entry point, mean / invstd / running buffers within fp32 reassociation,
+    incl. x50 inputs with a large mean (shifted sums must not cancel) and a
+    ragged last 16-pixel block.  Layers the statistics form does not serve
+    fall back to (y, None)."""
+    from jabd_amd import train as T
+    B, H, W = bhw
+    g = torch.Generator().manual_seed(cin * cout)
+    x = (torch.randn(B, H, W, cin, generator=g) + 2.0) * scale
+    w = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    dev = torch.device(cuda)
+    bns = []
+    for _ in range(2):
+        bn = torch.nn.BatchNorm2d(cout).to(dev)
+        with torch.no_grad():
+            bn.running_mean.copy_(torch.linspace(-1, 1, cout))
+            bn.running_var.copy_(torch.linspace(0.5, 2, cout))
+        bns.append(bn)
+    xg, wg = x.to(dev), w.to(dev)
+    y1, st = T._conv_fwd_bn_stats(xg, wg, bns[0])
+    y2 = T._conv_fwd(xg, wg)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    if cout > 80:
+        assert st is None
+        return
+    assert st is not None, "streaming statistics form expected to serve this layer"
+    m1, i1 = st
+    _, (_, _, m2, i2) = T._bn_fwd(y2, bns[1], "none")
+    torch.cuda.synchronize()
+    assert rel_err(m1.cpu(), m2.cpu()) < 1e-6
+    assert rel_err(i1.cpu(), i2.cpu()) < 1e-5
+    assert rel_err(bns[0].running_mean.cpu(), bns[1].running_mean.cpu()) < 1e-6
+    assert rel_err(bns[0].running_var.cpu(), bns[1].running_var.cpu()) < 1e-5
+    ref = y2.double()
+    assert rel_err(m1.cpu().double(), ref.mean((0, 1, 2)).cpu()) < 1e-6
+    var = ref.var((0, 1, 2), unbiased=False)
+    assert rel_err(i1.cpu(), (var + bns[0].eps).rsqrt().cpu()) < 1e-5
