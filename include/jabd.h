@@ -408,6 +408,14 @@ int jabd_dwconv_nhwc_f32(const jabd_dw_args* args, jabd_stream_t stream);
 int64_t jabd_dwconv_stats_nblk(int64_t B, int64_t OH, int64_t OW, int64_t C);
 int jabd_dwconv_stats_f32(const jabd_dw_args* args, float* stats_part, float* shift,
                           jabd_stream_t stream);
+/* jabd_dwconv_stats_f32 whose input is act(bn(x)) of the stored pre-BN tensor
+ * args->x, applied on load: (x - mean) * invstd * gamma + beta, then act
+ * (NONE/RELU/LEAKY/HSWISH) — MNv3 Block_eca bn1 + act feeding conv2
+ * (nets/mobilenetV3.py:141-145), so the activated expansion is never
+ * written; zero padding applies to the activated input. */
+int jabd_dwconv_bnin_stats_f32(const jabd_dw_args* args, const float* mean, const float* invstd,
+                               const float* gamma, const float* beta, int32_t act, float slope,
+                               float* stats_part, float* shift, jabd_stream_t stream);
 
 /* A1 fused block front half (eval) — nets/mobilenetV3.py:141-142: expand 1x1
  * conv (+ folded bn1, packed like jabd_conv_args.w, Kc = ceil(Cin/16)) + act
@@ -630,6 +638,14 @@ int64_t jabd_dw_wgrad_part_floats(int64_t M, int32_t C, int32_t k);
 int jabd_dw_wgrad_f32(const float* x, const float* dy, int32_t B, int32_t H, int32_t W, int32_t C,
                       int32_t OH, int32_t OW, int32_t k, int32_t stride, int32_t pad, float* part,
                       float* dw, jabd_stream_t stream);
+/* jabd_dw_wgrad_f32 of the BN-input depthwise conv (jabd_dwconv_bnin_stats_f32):
+ * the input taps recomputed from the pre-BN tensor x_bn with the same
+ * expression. */
+int jabd_dw_wgrad_bnin_f32(const float* x_bn, const float* dy, int32_t B, int32_t H, int32_t W,
+                           int32_t C, int32_t OH, int32_t OW, int32_t k, int32_t stride,
+                           int32_t pad, const float* mean, const float* invstd, const float* gamma,
+                           const float* beta, int32_t act, float slope, float* part, float* dw,
+                           jabd_stream_t stream);
 /* ECA backward.  The consumer saw a = x * scale[b][c]; given da:
  *   dx = da * scale + (d mean)/HW  through the gate, Conv1d and average pool,
  *   dw1d [k] the Conv1d weight gradient.  mean/scale are the forward's

@@ -46,6 +46,40 @@ __device__ __forceinline__ float4 fma4pk(float4 a, float4 b, float4 c) {
   return make_float4(r0.x, r0.y, r1.x, r1.y);
 }
 
+// BatchNorm + activation applied on load by the BN-input depthwise kernels
+// (dwconv.hip forward, train.hip weight gradient; both use this, so they see
+// the same values): act(x * a + c), a = invstd * gamma, c = beta - mean * a.
+struct DwBnCoef {
+  float4 a, c;
+};
+
+__device__ __forceinline__ DwBnCoef dw_bn_coef(const float* mean, const float* invstd,
+                                               const float* gamma, const float* beta, int cg) {
+  const float4 mu = reinterpret_cast<const float4*>(mean)[cg];
+  const float4 is = reinterpret_cast<const float4*>(invstd)[cg];
+  const float4 gm = reinterpret_cast<const float4*>(gamma)[cg];
+  const float4 bt = reinterpret_cast<const float4*>(beta)[cg];
+  DwBnCoef k;
+  k.a = make_float4(is.x * gm.x, is.y * gm.y, is.z * gm.z, is.w * gm.w);
+  k.c = make_float4(fmaf(-mu.x, k.a.x, bt.x), fmaf(-mu.y, k.a.y, bt.y), fmaf(-mu.z, k.a.z, bt.z),
+                    fmaf(-mu.w, k.a.w, bt.w));
+  return k;
+}
+
+// act: 1 relu, 2 leaky, 3 hswish (JABD_ACT_*), else identity
+__device__ __forceinline__ float4 dw_bn_in(float4 v, const DwBnCoef& k, int act, float slope) {
+  float4 z = fma4pk(v, k.a, k.c);
+  if (act == 1) {
+    z.x = fmaxf(z.x, 0.f); z.y = fmaxf(z.y, 0.f); z.z = fmaxf(z.z, 0.f); z.w = fmaxf(z.w, 0.f);
+  } else if (act == 2) {
+    z.x = z.x > 0.f ? z.x : z.x * slope; z.y = z.y > 0.f ? z.y : z.y * slope;
+    z.z = z.z > 0.f ? z.z : z.z * slope; z.w = z.w > 0.f ? z.w : z.w * slope;
+  } else if (act == 3) {
+    z.x = hswish_f(z.x); z.y = hswish_f(z.y); z.z = hswish_f(z.z); z.w = hswish_f(z.w);
+  }
+  return z;
+}
+
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 

@@ -33,10 +33,25 @@ __device__ __forceinline__ float4 f4fma(float4 a, float4 w, float4 c) { return f
 // bn_stats_part's format; sh = the output at pixel (0, 0) of image 0, which
 // every workgroup recomputes with the main loop's tap order (workgroup (0, 0)
 // writes it to shift[] for bn_stats_final).  Saves bn2's statistics pass.
-template <int K, int S, bool ST>
+// IT: the input is act(bn(x)) of the stored pre-BN tensor x, applied on load
+// (MNv3 Block_eca bn1 + act feeding conv2) as act(x * a + c) with
+// a = invstd * gamma, c = beta - mean * a (dw_bn_in, shared with the weight
+// gradient in train.hip), in-bounds taps only (padding stays zero), so the
+// activated expansion is never written.
+struct DwBnIn {
+  const float* mean;
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
+  int act;
+  float slope;
+};
+
+template <int K, int S, bool ST, bool IT = false>
 __global__ __launch_bounds__(kDwThreads) void dw_kernel(const DwArgs p, int strips_per_blk,
                                                        float* __restrict__ stp,
-                                                       float* __restrict__ shift) {
+                                                       float* __restrict__ shift,
+                                                       const DwBnIn bi) {
   constexpr int SPAN = (kPW - 1) * S + K;
   const int CG = p.C >> 2;
   const int SP = kDwThreads / CG;  // strips in flight per pass
@@ -57,6 +72,12 @@ __global__ __launch_bounds__(kDwThreads) void dw_kernel(const DwArgs p, int stri
     for (int t = 0; t < K * K; ++t) wr[t] = reinterpret_cast<const float4*>(p.w + t * p.C)[cg];
     if (p.bias) bias = reinterpret_cast<const float4*>(p.bias)[cg];
   }
+  DwBnCoef bc{};
+  if (IT && active) bc = dw_bn_coef(bi.mean, bi.invstd, bi.gamma, bi.beta, cg);
+  auto ldx = [&](const float* ptr) -> float4 {
+    const float4 v = *reinterpret_cast<const float4*>(ptr);
+    return IT ? dw_bn_in(v, bc, bi.act, bi.slope) : v;
+  };
   float4 psum = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 sh = make_float4(0.f, 0.f, 0.f, 0.f), ss = sh, sq = sh;
   if (ST && active) {
@@ -69,9 +90,8 @@ __global__ __launch_bounds__(kDwThreads) void dw_kernel(const DwArgs p, int stri
 #pragma unroll
       for (int kw = 0; kw < K; ++kw) {
         const int iw = -p.pad + kw;
-        const float4 r = (iw >= 0 && iw < p.W)
-                             ? *reinterpret_cast<const float4*>(x0 + ((int64_t)ih * p.W + iw) * p.x_ps)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 r = (iw >= 0 && iw < p.W) ? ldx(x0 + ((int64_t)ih * p.W + iw) * p.x_ps)
+                                               : make_float4(0.f, 0.f, 0.f, 0.f);
         a0 = f4fma(r, wr[kh * K + kw], a0);
       }
     }
@@ -100,7 +120,7 @@ __global__ __launch_bounds__(kDwThreads) void dw_kernel(const DwArgs p, int stri
 #pragma unroll
       for (int c = 0; c < SPAN; ++c) {
         const int iw = iw0 + c;
-        row[c] = (iw >= 0 && iw < p.W) ? *reinterpret_cast<const float4*>(xr + (int64_t)iw * p.x_ps)
+        row[c] = (iw >= 0 && iw < p.W) ? ldx(xr + (int64_t)iw * p.x_ps)
                                        : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
@@ -197,7 +217,7 @@ extern "C" int jabd_dwconv_nhwc_f32(const jabd_dw_args* args, jabd_stream_t stre
   hipStream_t st = as_stream(stream);
 #define DW_CASE(K, S)                                                                       \
   if (a.k == K && a.stride == S) {                                                         \
-    dw_kernel<K, S, false><<<grid, kDwThreads, 0, st>>>(a, (int)per, nullptr, nullptr);    \
+    dw_kernel<K, S, false><<<grid, kDwThreads, 0, st>>>(a, (int)per, nullptr, nullptr, {}); \
     return check_launch("dwconv");                                                         \
   }
   DW_CASE(3, 1)
@@ -214,9 +234,10 @@ extern "C" int64_t jabd_dwconv_stats_nblk(int64_t B, int64_t OH, int64_t OW, int
   return n < 0 ? n : n * B;
 }
 
-extern "C" int jabd_dwconv_stats_f32(const jabd_dw_args* args, float* stats_part, float* shift,
-                                     jabd_stream_t stream) {
+static int dwconv_stats(const jabd_dw_args* args, float* stats_part, float* shift,
+                        const DwBnIn* bi, jabd_stream_t stream) {
   JABD_REQUIRE(args && stats_part && shift, "dw_stats: null args");
+  JABD_REQUIRE(!bi || (bi->mean && bi->invstd && bi->gamma && bi->beta), "dw_stats: null BN input");
   const DwArgs& a = *args;
   JABD_REQUIRE(a.x && a.w && a.y && !a.part, "dw_stats: null pointer / ECA partials not supported");
   JABD_REQUIRE(a.C % 4 == 0 && a.C / 4 <= kDwThreads && a.x_ps % 4 == 0 && a.y_ps % 4 == 0,
@@ -230,7 +251,11 @@ extern "C" int jabd_dwconv_stats_f32(const jabd_dw_args* args, float* stats_part
   hipStream_t st = as_stream(stream);
 #define DWS_CASE(K, S)                                                                      \
   if (a.k == K && a.stride == S) {                                                         \
-    dw_kernel<K, S, true><<<grid, kDwThreads, 0, st>>>(a, (int)per, stats_part, shift);    \
+    if (bi)                                                                                \
+      dw_kernel<K, S, true, true><<<grid, kDwThreads, 0, st>>>(a, (int)per, stats_part, shift, \
+                                                               *bi);                       \
+    else                                                                                   \
+      dw_kernel<K, S, true><<<grid, kDwThreads, 0, st>>>(a, (int)per, stats_part, shift, {}); \
     return check_launch("dwconv_stats");                                                   \
   }
   DWS_CASE(3, 1)
@@ -240,4 +265,19 @@ extern "C" int jabd_dwconv_stats_f32(const jabd_dw_args* args, float* stats_part
 #undef DWS_CASE
   set_error("dw_stats: unsupported k=%d stride=%d", a.k, a.stride);
   return JABD_EINVAL;
+}
+
+extern "C" int jabd_dwconv_stats_f32(const jabd_dw_args* args, float* stats_part, float* shift,
+                                     jabd_stream_t stream) {
+  return dwconv_stats(args, stats_part, shift, nullptr, stream);
+}
+
+extern "C" int jabd_dwconv_bnin_stats_f32(const jabd_dw_args* args, const float* mean,
+                                          const float* invstd, const float* gamma,
+                                          const float* beta, int32_t act, float slope,
+                                          float* stats_part, float* shift, jabd_stream_t stream) {
+  JABD_REQUIRE(act == ACT_NONE || act == ACT_RELU || act == ACT_LEAKY || act == ACT_HSWISH,
+               "dw_bnin: act %d not supported", act);
+  const DwBnIn bi{mean, invstd, gamma, beta, act, slope};
+  return dwconv_stats(args, stats_part, shift, &bi, stream);
 }

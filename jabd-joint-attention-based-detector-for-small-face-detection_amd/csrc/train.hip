@@ -1220,11 +1220,16 @@ __global__ __launch_bounds__(256) void dw_dgrad_bn_kernel(
 }
 
 // part[blk][tap][c] = sum over this block's output strips of dy * x(tap)
-template <int K, int S, int PW>
+// IT: x(tap) = act(bn(xs)) of the stored pre-BN tensor xs, recomputed on load
+// with dwconv.hip's BN-input forward expression (common.h dw_bn_in; in-bounds
+// taps only, padding stays zero).
+template <int K, int S, int PW, bool IT = false>
 __global__ __launch_bounds__(256) void dw_wgrad_strip_kernel(
     const float* __restrict__ x, const float* __restrict__ dy, int H, int W, int C, int OH,
     int OW, int nstrip, int64_t items, int64_t items_per_blk, int lanes,
-    float* __restrict__ part) {
+    float* __restrict__ part, const float* __restrict__ bmean = nullptr,
+    const float* __restrict__ binvstd = nullptr, const float* __restrict__ bgamma = nullptr,
+    const float* __restrict__ bbeta = nullptr, int bact = 0, float bslope = 0.f) {
   constexpr int PAD = K / 2;
   constexpr int L = (PW - 1) * S + K;
   __shared__ float4 red[256];
@@ -1237,6 +1242,9 @@ __global__ __launch_bounds__(256) void dw_wgrad_strip_kernel(
   float4 acc[K * K];
 #pragma unroll
   for (int q = 0; q < K * K; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  DwBnCoef bc{};
+  if (IT && active) bc = dw_bn_coef(bmean, binvstd, bgamma, bbeta, cg);
+  auto tf = [&](float4 v) -> float4 { return IT ? dw_bn_in(v, bc, bact, bslope) : v; };
   const int64_t i0 = (int64_t)blockIdx.x * items_per_blk;
   const int64_t i1 = min(i0 + items_per_blk, items);
   for (int64_t it = i0 + r0; active && it < i1; it += rows_pass) {
@@ -1258,7 +1266,7 @@ __global__ __launch_bounds__(256) void dw_wgrad_strip_kernel(
 #pragma unroll
       for (int j = 0; j < L; ++j) {
         const int iw = iw0 + j;
-        seg[j] = (iw >= 0 && iw < W) ? xrow[(int64_t)iw * C4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        seg[j] = (iw >= 0 && iw < W) ? tf(xrow[(int64_t)iw * C4]) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int kw = 0; kw < K; ++kw)
@@ -1937,10 +1945,14 @@ extern "C" int64_t jabd_dw_wgrad_part_floats(int64_t M, int32_t C, int32_t k) {
   return 1024 * (int64_t)k * k * C;
 }
 
-extern "C" int jabd_dw_wgrad_f32(const float* x, const float* dy, int32_t B, int32_t H, int32_t W,
-                                 int32_t C, int32_t OH, int32_t OW, int32_t k, int32_t stride,
-                                 int32_t pad, float* part, float* dw, jabd_stream_t stream) {
+static int dw_wgrad(const float* x, const float* dy, int32_t B, int32_t H, int32_t W, int32_t C,
+                    int32_t OH, int32_t OW, int32_t k, int32_t stride, int32_t pad,
+                    const float* bmean, const float* binvstd, const float* bgamma,
+                    const float* bbeta, int32_t bact, float bslope, float* part, float* dw,
+                    jabd_stream_t stream) {
   JABD_REQUIRE(x && dy && part && dw && C % 4 == 0 && B > 0, "dw_wgrad: bad args");
+  const bool it = bmean != nullptr;
+  JABD_REQUIRE(!it || (binvstd && bgamma && bbeta), "dw_wgrad: null BN input");
   JABD_REQUIRE((k == 3 || k == 5) && pad == k / 2 && (stride == 1 || stride == 2) &&
                    OH == (H + 2 * pad - k) / stride + 1 && OW == (W + 2 * pad - k) / stride + 1,
                "dw_wgrad: unsupported geometry");
@@ -1955,8 +1967,13 @@ extern "C" int jabd_dw_wgrad_f32(const float* x, const float* dy, int32_t B, int
     per = cdiv(per, rows_pass) * rows_pass;                                                     \
     nblk = cdiv(items, per);                                                                    \
     dim3 g((unsigned)nblk, (unsigned)cdiv(C4, lanes));                                          \
-    dw_wgrad_strip_kernel<K_, S_, PW_><<<g, 256, 0, st>>>(x, dy, H, W, C, OH, OW, nstrip, items, \
-                                                          per, lanes, part);                    \
+    if (it)                                                                                     \
+      dw_wgrad_strip_kernel<K_, S_, PW_, true><<<g, 256, 0, st>>>(                               \
+          x, dy, H, W, C, OH, OW, nstrip, items, per, lanes, part, bmean, binvstd, bgamma, bbeta, \
+          bact, bslope);                                                                        \
+    else                                                                                        \
+      dw_wgrad_strip_kernel<K_, S_, PW_><<<g, 256, 0, st>>>(x, dy, H, W, C, OH, OW, nstrip,      \
+                                                            items, per, lanes, part);           \
   }
   WG_CASE(3, 1, 8) WG_CASE(3, 2, 4) WG_CASE(5, 1, 4) WG_CASE(5, 2, 4)
 #undef WG_CASE
@@ -1966,6 +1983,24 @@ extern "C" int jabd_dw_wgrad_f32(const float* x, const float* dy, int32_t B, int
   wgrad_reduce2_kernel<<<(unsigned)cdiv(tot, rl), 256, 0, st>>>(part, nblk, k * k, C, 1, k * k, rl,
                                                                 dw);
   return check_launch("dw_wgrad_reduce");
+}
+
+extern "C" int jabd_dw_wgrad_f32(const float* x, const float* dy, int32_t B, int32_t H, int32_t W,
+                                 int32_t C, int32_t OH, int32_t OW, int32_t k, int32_t stride,
+                                 int32_t pad, float* part, float* dw, jabd_stream_t stream) {
+  return dw_wgrad(x, dy, B, H, W, C, OH, OW, k, stride, pad, nullptr, nullptr, nullptr, nullptr,
+                  0, 0.f, part, dw, stream);
+}
+
+extern "C" int jabd_dw_wgrad_bnin_f32(const float* x_bn, const float* dy, int32_t B, int32_t H,
+                                      int32_t W, int32_t C, int32_t OH, int32_t OW, int32_t k,
+                                      int32_t stride, int32_t pad, const float* mean,
+                                      const float* invstd, const float* gamma, const float* beta,
+                                      int32_t act, float slope, float* part, float* dw,
+                                      jabd_stream_t stream) {
+  JABD_REQUIRE(mean, "dw_wgrad_bnin: null mean");
+  return dw_wgrad(x_bn, dy, B, H, W, C, OH, OW, k, stride, pad, mean, invstd, gamma, beta, act,
+                  slope, part, dw, stream);
 }
 
 extern "C" int jabd_eca_bwd_f32(const float* da, const float* x, int64_t B, int64_t HW,

@@ -173,6 +173,8 @@ SIGNATURES = {
     "jabd_dwconv_nhwc_f32": [ctypes.POINTER(DwArgs), c_vp],
     "jabd_dwconv_stats_nblk": [c_i64, c_i64, c_i64, c_i64],
     "jabd_dwconv_stats_f32": [ctypes.POINTER(DwArgs), c_vp, c_vp, c_vp],
+    "jabd_dwconv_bnin_stats_f32": [ctypes.POINTER(DwArgs), c_vp, c_vp, c_vp, c_vp, c_i32, c_f32,
+                                   c_vp, c_vp, c_vp],
     "jabd_bn_stats_final_f32": [c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_f32,
                                 c_f32, c_vp],
     "jabd_expand_dw_nblk": [c_i32, c_i32, c_i32, c_i32],
@@ -219,6 +221,9 @@ SIGNATURES = {
                                  c_vp, c_vp, c_vp, c_vp, c_vp],
     "jabd_dw_wgrad_f32": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
                           c_i32, c_vp, c_vp, c_vp],
+    "jabd_dw_wgrad_bnin_f32": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
+                               c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_f32, c_vp, c_vp,
+                               c_vp],
     "jabd_eca_bwd_f32": [c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp,
                          c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
     "jabd_scale_bwd_f32": [c_vp, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp],

@@ -45,6 +45,13 @@ ECA_SUMS = __import__("os").environ.get("JABD_ECA_SUMS", "1") != "0"
 # statistics from their own pass over e_pre instead of conv1's streaming kernel
 # (A/B)
 DW_BN_FUSE = __import__("os").environ.get("JABD_DW_BN_FUSE", "1") != "0"
+# JABD_DW_BNIN=0: bn1 + act written out as e and read by conv2 and its weight
+# gradient, instead of applied on their loads from e_pre (A/B; needs
+# DW_BN_FUSE).  Only the 3x3 stride-2 blocks take it: their kernels load each
+# input element ~1.7 times, so the on-load BN stays under the HBM time it
+# saves; 3x3/s1 (4.5 loads per element) and 5x5 (3.4-10) turn VALU-bound
+# and lose (r03 C4 profile).
+DW_BNIN = __import__("os").environ.get("JABD_DW_BNIN", "1") != "0"
 
 
 _ZEROS = {}
@@ -805,6 +812,21 @@ def conv(x, m, stride=1, pad=0, nchw_in=False):
 
 
 # ----------------------------------------------------------------------------- fused block
+def _bn_stats(x, bn):
+    """Batch statistics (mean, invstd) of NHWC x for bn (jabd_bn_stats_f32;
+    running buffers updated)."""
+    B, H, W, C = x.shape
+    M = B * H * W
+    nblk = int(lib().jabd_bn_nblk(M, C))
+    part = torch.empty((nblk, 2, C), dtype=torch.float32, device=x.device)
+    mean = torch.empty(C, dtype=torch.float32, device=x.device)
+    invstd = torch.empty_like(mean)
+    call("jabd_bn_stats_f32", x.data_ptr(), C, M, C, part.data_ptr(), mean.data_ptr(),
+         invstd.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+         float(bn.momentum), float(bn.eps), _st())
+    return mean, invstd
+
+
 def _bn_fwd(x, bn, act, slope=0.0, res=None, sums=False, stats=None):
     """Batch-stat BN (+res) + act of NHWC x; running buffers updated in place.
     Returns (y, (gamma, beta, mean, invstd)); sums=True adds the per-image
@@ -925,10 +947,12 @@ def _dw_fwd(x, weight, stride):
     return y, wt
 
 
-def _dw_fwd_bn_stats(x, weight, stride, bn):
+def _dw_fwd_bn_stats(x, weight, stride, bn, bnin=None):
     """_dw_fwd whose kernel also takes the batch statistics of its output for
     the following BatchNorm (jabd_dwconv_stats_f32 + jabd_bn_stats_final_f32;
-    running buffers updated).  Returns (y, wt, (mean, invstd))."""
+    running buffers updated).  bnin = ((gamma, beta, mean, invstd), act): x
+    is the pre-BN tensor and the kernel convolves act(bn(x)), applied on load
+    (jabd_dwconv_bnin_stats_f32).  Returns (y, wt, (mean, invstd))."""
     C, _, k, _ = weight.shape
     wt = F.transpose(weight.detach().reshape(C, k * k))
     B, H, W, _ = x.shape
@@ -945,7 +969,13 @@ def _dw_fwd_bn_stats(x, weight, stride, bn):
     nblk = int(lib().jabd_dwconv_stats_nblk(B, OH, OW, C))
     part = torch.empty((nblk, 2, C), dtype=torch.float32, device=x.device)
     shift = torch.empty(C, dtype=torch.float32, device=x.device)
-    call("jabd_dwconv_stats_f32", ctypes.byref(a), part.data_ptr(), shift.data_ptr(), _st())
+    if bnin is None:
+        call("jabd_dwconv_stats_f32", ctypes.byref(a), part.data_ptr(), shift.data_ptr(), _st())
+    else:
+        (g1, b1, m1, i1), act1 = bnin
+        call("jabd_dwconv_bnin_stats_f32", ctypes.byref(a), m1.data_ptr(), i1.data_ptr(),
+             g1.data_ptr(), b1.data_ptr(), ACT[act1], 0.0, part.data_ptr(), shift.data_ptr(),
+             _st())
     mean = torch.empty(C, dtype=torch.float32, device=x.device)
     invstd = torch.empty_like(mean)
     call("jabd_bn_stats_final_f32", shift.data_ptr(), part.data_ptr(), nblk, B * OH * OW, C,
@@ -954,41 +984,55 @@ def _dw_fwd_bn_stats(x, weight, stride, bn):
     return y, wt, (mean, invstd)
 
 
-def _dw_bwd(dy, x, wt, k, stride, want_dx=True):
+def _dw_bwd(dy, x, wt, k, stride, want_dx=True, bnin=None):
+    """bnin: as in _dw_fwd_bn_stats (x pre-BN; the weight gradient's taps
+    recomputed as act(bn(x)), jabd_dw_wgrad_bnin_f32; needs want_dx=False)."""
     B, H, W, C = x.shape
     OH, OW = dy.shape[1], dy.shape[2]
     pad = k // 2
     dx = None
     if want_dx:
+        assert bnin is None
         dx = torch.empty_like(x)
         call("jabd_dw_dgrad_f32", dy.data_ptr(), wt.data_ptr(), B, H, W, C, OH, OW, k, stride,
              pad, dx.data_ptr(), _st())
     nparts = int(lib().jabd_dw_wgrad_part_floats(B * OH * OW, C, k))
     part = torch.empty(nparts, dtype=torch.float32, device=x.device)
     dw = torch.empty((C, 1, k, k), dtype=torch.float32, device=x.device)
-    call("jabd_dw_wgrad_f32", x.data_ptr(), dy.data_ptr(), B, H, W, C, OH, OW, k, stride, pad,
-         part.data_ptr(), dw.data_ptr(), _st())
+    if bnin is None:
+        call("jabd_dw_wgrad_f32", x.data_ptr(), dy.data_ptr(), B, H, W, C, OH, OW, k, stride, pad,
+             part.data_ptr(), dw.data_ptr(), _st())
+    else:
+        (g1, b1, m1, i1), act1 = bnin
+        call("jabd_dw_wgrad_bnin_f32", x.data_ptr(), dy.data_ptr(), B, H, W, C, OH, OW, k, stride,
+             pad, m1.data_ptr(), i1.data_ptr(), g1.data_ptr(), b1.data_ptr(), ACT[act1], 0.0,
+             part.data_ptr(), dw.data_ptr(), _st())
     return dx, dw
 
 
 def _dw_bn_bwd(dy, x, wt, k, stride, x_bn, st, act):
     """Backward of d = dwconv(act(bn(x_bn))) with x = act(bn(x_bn)): the
     depthwise data gradient carries bn's backward partials
-    (jabd_dw_dgrad_bn_bwd_f32).  Returns (dx_bn, dgamma, dbeta, dW)."""
+    (jabd_dw_dgrad_bn_bwd_f32).  x None: it was never stored (BN-input
+    forward) and the weight gradient recomputes it from x_bn.  Returns
+    (dx_bn, dgamma, dbeta, dW)."""
     g, b, mean, invstd = st
-    B, H, W, C = x.shape
+    B, H, W, C = x_bn.shape
     OH, OW = dy.shape[1], dy.shape[2]
     nparts = int(lib().jabd_dw_dgrad_bn_part_floats(B, H, W, C))
-    part = torch.empty(nparts, dtype=torch.float32, device=x.device)
-    dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
+    part = torch.empty(nparts, dtype=torch.float32, device=x_bn.device)
+    dgamma = torch.empty(C, dtype=torch.float32, device=x_bn.device)
     dbeta = torch.empty_like(dgamma)
-    dz = torch.empty_like(x)
-    dx = torch.empty_like(x)
+    dz = torch.empty_like(x_bn)
+    dx = torch.empty_like(x_bn)
     call("jabd_dw_dgrad_bn_bwd_f32", dy.data_ptr(), wt.data_ptr(), B, H, W, C, OH, OW, k, stride,
          k // 2, x_bn.data_ptr(), mean.data_ptr(), invstd.data_ptr(), g.data_ptr(), b.data_ptr(),
          ACT[act], 0.0, part.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), dz.data_ptr(),
          dx.data_ptr(), _st())
-    _, dw = _dw_bwd(dy, x, wt, k, stride, want_dx=False)
+    if x is None:
+        _, dw = _dw_bwd(dy, x_bn, wt, k, stride, want_dx=False, bnin=(st, act))
+    else:
+        _, dw = _dw_bwd(dy, x, wt, k, stride, want_dx=False)
     return dx, dgamma, dbeta, dw
 
 
@@ -1014,11 +1058,23 @@ class MNv3BlockFn(torch.autograd.Function):
             e_pre, bst1 = _conv_fwd_bn_stats(s, blk.conv1.weight, blk.bn1)
         else:
             e_pre, bst1 = _conv_fwd(s, blk.conv1.weight), None
-        e, st1 = _bn_fwd(e_pre, blk.bn1, act, stats=bst1)
-        if DW_BN_FUSE:
+        if DW_BN_FUSE and DW_BNIN and k == 3 and stride == 2:
+            # bn1 + act applied on conv2's loads: e is never written
+            if bst1 is None:
+                bst1 = _bn_stats(e_pre, blk.bn1)
+            st1 = (blk.bn1.weight.detach(), blk.bn1.bias.detach()) + tuple(bst1)
+            _count_batch(blk.bn1)
+            F.tap("bn", act, 0.0, e_pre, st1[2], st1[3], st1[0], st1[1], None)
+            e = None
+            d_pre, wt2, bst2 = _dw_fwd_bn_stats(e_pre, blk.conv2.weight, stride, blk.bn2,
+                                                bnin=(st1, act))
+            d, st2, psum = _bn_fwd(d_pre, blk.bn2, act, sums=True, stats=bst2)
+        elif DW_BN_FUSE:
+            e, st1 = _bn_fwd(e_pre, blk.bn1, act, stats=bst1)
             d_pre, wt2, bst2 = _dw_fwd_bn_stats(e, blk.conv2.weight, stride, blk.bn2)
             d, st2, psum = _bn_fwd(d_pre, blk.bn2, act, sums=True, stats=bst2)
         else:
+            e, st1 = _bn_fwd(e_pre, blk.bn1, act, stats=bst1)
             d_pre, wt2 = _dw_fwd(e, blk.conv2.weight, stride)
             d, st2, psum = _bn_fwd(d_pre, blk.bn2, act, sums=True)
         B, OH, OW, E = d.shape

@@ -453,3 +453,50 @@ def test_conv1x1_bn_stats(cuda, cin, cout, bhw, scale):
     assert rel_err(m1.cpu().double(), ref.mean((0, 1, 2)).cpu()) < 1e-6
     var = ref.var((0, 1, 2), unbiased=False)
     assert rel_err(i1.cpu(), (var + bns[0].eps).rsqrt().cpu()) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,k,s,bhw,act", [(64, 3, 2, (2, 66, 50), "relu"), (72, 3, 1, (3, 31, 29), "relu"),
+                                           (120, 5, 1, (2, 17, 19), "hswish"),
+                                           (240, 5, 2, (2, 21, 16), "hswish")])
+def test_dw_bnin(cuda, c, k, s, bhw, act):
+    """Depthwise forward and weight gradient with bn1 + act applied on load
+    from the pre-BN tensor (jabd_dwconv_bnin_stats_f32 /
+    jabd_dw_wgrad_bnin_f32) against the same kernels on the materialised
+    act(bn(x)) (jabd_bn_act_fwd_f32): outputs and statistics within fp32
+    rounding of the BN expression, padding applied to the activated input."""
+    from jabd_amd import train as T
+    B, H, W = bhw
+    g = torch.Generator().manual_seed(c * k + s)
+    x = torch.randn(B, H, W, c, generator=g) * 2.0 + 0.5
+    w = torch.randn(c, 1, k, k, generator=g) / k
+    dev = torch.device(cuda)
+    bn1 = torch.nn.BatchNorm2d(c).to(dev)
+    with torch.no_grad():
+        bn1.weight.copy_(torch.rand(c, generator=g) + 0.5)
+        bn1.bias.copy_(torch.randn(c, generator=g) * 0.3)
+    bn2s = [torch.nn.BatchNorm2d(c).to(dev) for _ in range(2)]
+    xg, wg = x.to(dev), w.to(dev)
+    e, st1 = T._bn_fwd(xg, bn1, act)
+    y1, _, (m1, i1) = T._dw_fwd_bn_stats(xg, wg, s, bn2s[0], bnin=(st1, act))
+    y2, wt, (m2, i2) = T._dw_fwd_bn_stats(e, wg, s, bn2s[1])
+    torch.cuda.synchronize()
+    # on-load form act(x * a + c) vs bn_act_fwd's act((x - mean) * invstd *
+    # gamma + beta): a few ulp per activated element
+    assert rel_err(y1.cpu(), y2.cpu()) < 2e-6
+    assert rel_err(m1.cpu(), m2.cpu()) < 1e-5
+    assert rel_err(i1.cpu(), i2.cpu()) < 1e-5
+    dy = torch.randn(y2.shape, generator=g).to(dev)
+    _, dw1 = T._dw_bwd(dy, xg, wt, k, s, want_dx=False, bnin=(st1, act))
+    _, dw2 = T._dw_bwd(dy, e, wt, k, s, want_dx=False)
+    torch.cuda.synchronize()
+    assert rel_err(dw1.cpu(), dw2.cpu()) < 2e-6
+    # plain fp32 reference of the whole chain
+    ref_e = torch.nn.functional.relu(
+        torch.nn.functional.batch_norm(x.permute(0, 3, 1, 2), None, None, bn1.weight.detach().cpu(),
+                                       bn1.bias.detach().cpu(), True, 0.0, bn1.eps)) \
+        if act == "relu" else torch.nn.functional.hardswish(
+        torch.nn.functional.batch_norm(x.permute(0, 3, 1, 2), None, None, bn1.weight.detach().cpu(),
+                                       bn1.bias.detach().cpu(), True, 0.0, bn1.eps))
+    ref_y = torch.nn.functional.conv2d(ref_e, w, None, s, k // 2, 1, c)
+    assert rel_err(y1.cpu().permute(0, 3, 1, 2), ref_y) < 1e-4
