@@ -602,7 +602,9 @@ int jabd_bn_act_bwd_ex_f32(const float* dy, int32_t lddy, int32_t dyc0, const fl
  * -> conv2): de = dgrad(dy, w) is written to dz (bn1's output gradient), and
  * bn1's backward — dgamma, dbeta, dx = the input gradient of bn1 (x = bn1's
  * input e_pre, NHWC contiguous) — follows as jabd_bn_act_bwd_f32 would give
- * it, without its separate pass over de and x.  part: >=
+ * it, without its separate pass over de and x.  dz == NULL: de is never
+ * stored; a second depthwise pass recomputes it and writes dx directly
+ * (saves de's write and read-back for a second read of dy).  part: >=
  * jabd_dw_dgrad_bn_part_floats(B, H, W, C) floats. */
 int64_t jabd_dw_dgrad_bn_part_floats(int32_t B, int32_t H, int32_t W, int32_t C);
 int jabd_dw_dgrad_bn_bwd_f32(const float* dy, const float* w, int32_t B, int32_t H, int32_t W,

@@ -1123,13 +1123,19 @@ __global__ __launch_bounds__(256) void dw_dgrad_strip_kernel(
 // a workgroup walks `spb` strip rows and writes part[blockIdx.x][0|1][c] for
 // its channels, rows added in a fixed order (deterministic).  Saves
 // bn_bwd_part's pass over de and e_pre (the block's largest tensors).
-template <int K, int S, int PW>
+// MODE 0: store de to dx + partials; 1: partials only (de not stored);
+// 2: the apply pass with de recomputed: dx = gamma * invstd * (dz - sdz / M -
+// xhat * sdzx / M) (bn_bwd_apply_kernel's expression) stored, no partials.
+// 1 + 2 replace 0 + bn_bwd_apply: de is never written nor read back, at the
+// price of a second read of dy (a quarter of de's size at stride 2).
+template <int K, int S, int PW, int MODE = 0>
 __global__ __launch_bounds__(256) void dw_dgrad_bn_kernel(
     const float* __restrict__ dy, const float* __restrict__ w, int H, int W, int C, int OH, int OW,
     int nstrip, int64_t items, int lanes, int spb, float* __restrict__ dx,
     const float* __restrict__ xb, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ gamma, const float* __restrict__ beta, int act, float slope,
-    float* __restrict__ part) {
+    float* __restrict__ part, const float* __restrict__ sdz = nullptr,
+    const float* __restrict__ sdzx = nullptr, int64_t M = 1) {
   constexpr int PAD = K / 2;
   constexpr int OFF = floordiv_c(PAD - K + 1, S);
   constexpr int L = (PW - 1 + PAD - S * OFF) / S + 1;
@@ -1147,6 +1153,15 @@ __global__ __launch_bounds__(256) void dw_dgrad_bn_kernel(
     const float4 is = *reinterpret_cast<const float4*>(invstd + c);
     const float4 gm = *reinterpret_cast<const float4*>(gamma + c);
     const float4 bt = *reinterpret_cast<const float4*>(beta + c);
+    float a1[4] = {}, a2[4] = {};
+    if (MODE == 2) {
+      const float invM = 1.f / (float)M;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a1[e] = sdz[c + e] * invM;
+        a2[e] = sdzx[c + e] * invM;
+      }
+    }
     for (int sp = 0; sp < spb; ++sp) {
       const int64_t it = ((int64_t)blockIdx.x * spb + sp) * rows_pass + r0;
       if (it >= items) break;
@@ -1189,21 +1204,30 @@ __global__ __launch_bounds__(256) void dw_dgrad_bn_kernel(
 #pragma unroll
       for (int q = 0; q < PW; ++q) {
         if (iw0 + q >= W) break;
-        xrow[(int64_t)(iw0 + q) * C4] = acc[q];
+        if (MODE == 0) xrow[(int64_t)(iw0 + q) * C4] = acc[q];
         const float4 xv = brow[(int64_t)(iw0 + q) * C4];
         const float xh[4] = {(xv.x - mu.x) * is.x, (xv.y - mu.y) * is.y, (xv.z - mu.z) * is.z,
                              (xv.w - mu.w) * is.w};
         const float gg[4] = {acc[q].x, acc[q].y, acc[q].z, acc[q].w};
         const float gmm[4] = {gm.x, gm.y, gm.z, gm.w}, btt[4] = {bt.x, bt.y, bt.z, bt.w};
+        const float iss[4] = {is.x, is.y, is.z, is.w};
         float dz[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) dz[e] = gg[e] * act_d(xh[e] * gmm[e] + btt[e], act, slope);
+        if (MODE == 2) {
+          float o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = gmm[e] * iss[e] * (dz[e] - a1[e] - xh[e] * a2[e]);
+          xrow[(int64_t)(iw0 + q) * C4] = make_float4(o[0], o[1], o[2], o[3]);
+          continue;
+        }
         sS.x += dz[0]; sS.y += dz[1]; sS.z += dz[2]; sS.w += dz[3];
         sQ.x = fmaf(dz[0], xh[0], sQ.x); sQ.y = fmaf(dz[1], xh[1], sQ.y);
         sQ.z = fmaf(dz[2], xh[2], sQ.z); sQ.w = fmaf(dz[3], xh[3], sQ.w);
       }
     }
   }
+  if (MODE == 2) return;
   rs[t] = sS;
   rq[t] = sQ;
   __syncthreads();
@@ -1907,7 +1931,7 @@ extern "C" int jabd_dw_dgrad_bn_bwd_f32(const float* dy, const float* w, int32_t
                                         const float* gamma, const float* beta, int32_t act,
                                         float slope, float* part, float* dgamma, float* dbeta,
                                         float* dz, float* dx, jabd_stream_t stream) {
-  JABD_REQUIRE(dy && w && x && mean && invstd && gamma && beta && part && dgamma && dbeta && dz &&
+  JABD_REQUIRE(dy && w && x && mean && invstd && gamma && beta && part && dgamma && dbeta &&
                    dx && C % 4 == 0 && B > 0 && H > 0 && W > 0,
                "dw_dgrad_bn_bwd: bad args");
   JABD_REQUIRE((k == 3 || k == 5) && pad == k / 2 && (stride == 1 || stride == 2) &&
@@ -1920,18 +1944,34 @@ extern "C" int jabd_dw_dgrad_bn_bwd_f32(const float* dy, const float* w, int32_t
   const int nstrip = (int)cdiv(W, 8);
   const int64_t items = (int64_t)B * H * nstrip;
   const dim3 g((unsigned)nblk, (unsigned)cdiv(C4, lanes));
+  const int64_t M = (int64_t)B * H * W;
+  // dz == NULL: the two-pass form (partials, then the apply with de
+  // recomputed; MODE 1 + 2), else de is stored to dz and applied (MODE 0)
 #define DGB_CASE(K_, S_)                                                                       \
-  if (k == K_ && stride == S_)                                                                 \
-    dw_dgrad_bn_kernel<K_, S_, 8><<<g, 256, 0, st>>>(dy, w, H, W, C, OH, OW, nstrip, items,    \
-                                                     lanes, spb, dz, x, mean, invstd, gamma,    \
-                                                     beta, act, slope, part);
+  if (k == K_ && stride == S_) {                                                               \
+    if (dz)                                                                                    \
+      dw_dgrad_bn_kernel<K_, S_, 8><<<g, 256, 0, st>>>(dy, w, H, W, C, OH, OW, nstrip, items,  \
+                                                       lanes, spb, dz, x, mean, invstd, gamma,  \
+                                                       beta, act, slope, part);                 \
+    else                                                                                       \
+      dw_dgrad_bn_kernel<K_, S_, 8, 1><<<g, 256, 0, st>>>(dy, w, H, W, C, OH, OW, nstrip,      \
+                                                          items, lanes, spb, nullptr, x, mean,  \
+                                                          invstd, gamma, beta, act, slope,      \
+                                                          part);                                \
+    if (int e = check_launch("dw_dgrad_bn")) return e;                                         \
+    bn_bwd_final_kernel<<<(unsigned)cdiv(C, kFinLanes), kFinThreads, 0, st>>>(part, nblk, C,   \
+                                                                              dbeta, dgamma);  \
+    if (int e = check_launch("bn_bwd_final")) return e;                                        \
+    if (!dz) {                                                                                 \
+      dw_dgrad_bn_kernel<K_, S_, 8, 2><<<g, 256, 0, st>>>(dy, w, H, W, C, OH, OW, nstrip,      \
+                                                          items, lanes, spb, dx, x, mean,       \
+                                                          invstd, gamma, beta, act, slope,      \
+                                                          nullptr, dbeta, dgamma, M);           \
+      return check_launch("dw_dgrad_bn_apply");                                                \
+    }                                                                                          \
+  }
   DGB_CASE(3, 1) DGB_CASE(3, 2) DGB_CASE(5, 1) DGB_CASE(5, 2)
 #undef DGB_CASE
-  if (int e = check_launch("dw_dgrad_bn")) return e;
-  bn_bwd_final_kernel<<<(unsigned)cdiv(C, kFinLanes), kFinThreads, 0, st>>>(part, nblk, C, dbeta,
-                                                                            dgamma);
-  if (int e = check_launch("bn_bwd_final")) return e;
-  const int64_t M = (int64_t)B * H * W;
   int elanes;
   const dim3 grid = ew_grid(M, C, elanes);
   bn_bwd_apply_kernel<false, false><<<grid, kRedThreads, 0, st>>>(dz, C, 0, x, C, nullptr, 0, M, C,

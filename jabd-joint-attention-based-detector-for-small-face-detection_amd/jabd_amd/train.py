@@ -52,6 +52,9 @@ DW_BN_FUSE = __import__("os").environ.get("JABD_DW_BN_FUSE", "1") != "0"
 # saves; 3x3/s1 (4.5 loads per element) and 5x5 (3.4-10) turn VALU-bound
 # and lose (r03 C4 profile).
 DW_BNIN = __import__("os").environ.get("JABD_DW_BNIN", "1") != "0"
+# JABD_DGBN_RECOMPUTE=0: bn1's backward stores de and applies from it instead
+# of recomputing de in a second depthwise pass (A/B)
+DGBN_RECOMPUTE = __import__("os").environ.get("JABD_DGBN_RECOMPUTE", "1") != "0"
 
 
 _ZEROS = {}
@@ -1023,11 +1026,14 @@ def _dw_bn_bwd(dy, x, wt, k, stride, x_bn, st, act):
     part = torch.empty(nparts, dtype=torch.float32, device=x_bn.device)
     dgamma = torch.empty(C, dtype=torch.float32, device=x_bn.device)
     dbeta = torch.empty_like(dgamma)
-    dz = torch.empty_like(x_bn)
+    # stride 2 only: there dy is a quarter of de; at stride 1 the kernel is
+    # not HBM-bound and the second depthwise pass costs more than de's
+    # write + read (r03 C4 profile)
+    dz = None if DGBN_RECOMPUTE and stride == 2 else torch.empty_like(x_bn)
     dx = torch.empty_like(x_bn)
     call("jabd_dw_dgrad_bn_bwd_f32", dy.data_ptr(), wt.data_ptr(), B, H, W, C, OH, OW, k, stride,
          k // 2, x_bn.data_ptr(), mean.data_ptr(), invstd.data_ptr(), g.data_ptr(), b.data_ptr(),
-         ACT[act], 0.0, part.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), dz.data_ptr(),
+         ACT[act], 0.0, part.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), _p(dz),
          dx.data_ptr(), _st())
     if x is None:
         _, dw = _dw_bwd(dy, x_bn, wt, k, stride, want_dx=False, bnin=(st, act))

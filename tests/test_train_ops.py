@@ -327,13 +327,17 @@ def test_bnactfn_grads_wide(cuda, c, act, h, w):
 @pytest.mark.parametrize("c,k,s,bhw,act", [(64, 3, 2, (4, 64, 48), "relu"), (72, 5, 1, (3, 37, 29), "relu"),
                                            (240, 3, 2, (2, 30, 34), "hswish"),
                                            (480, 3, 1, (3, 32, 48), "hswish"), (16, 3, 1, (2, 9, 5), "relu")])
-def test_dw_dgrad_bn_fused(cuda, c, k, s, bhw, act):
+@pytest.mark.parametrize("recompute", [True, False])
+def test_dw_dgrad_bn_fused(cuda, c, k, s, bhw, act, recompute, monkeypatch):
     """MNv3 block backward through bn1 + act -> depthwise conv: the fused
     depthwise data gradient + bn1 backward partials (jabd_dw_dgrad_bn_bwd_f32)
     against the two-pass form (jabd_dw_dgrad_f32 then jabd_bn_act_bwd_f32):
     the depthwise gradient bit-identical, dgamma / dbeta / dx within fp32
-    reassociation of the partial sums; and both against float64 autograd."""
+    reassociation of the partial sums; and both against float64 autograd.
+    recompute: de not stored, recomputed by a second depthwise pass that
+    writes dx (dz == NULL)."""
     from jabd_amd import train as T
+    monkeypatch.setattr(T, "DGBN_RECOMPUTE", recompute)
     B, H, W = bhw
     g = torch.Generator().manual_seed(c + k * 10 + s)
     x_bn = torch.randn(B, H, W, c, generator=g) * 2 + 0.5
