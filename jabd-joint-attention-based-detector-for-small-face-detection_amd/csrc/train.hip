@@ -318,14 +318,26 @@ __global__ __launch_bounds__(kRedThreads) void bn_act_fwd_sum_kernel(
 // dy' = dy * dys[b][c] + dya[b][c] (b = row / hw): the backward of an ECA
 // gate applied after this BN (x * s[b][c], and the pooled-mean term of the
 // gate's own gradient), fused here instead of a separate pass over dy.
-__device__ __forceinline__ float4 dy_transform(float4 g, const float* __restrict__ dys,
-                                               const float* __restrict__ dya, int64_t b, int C,
-                                               int c) {
-  const float4 sc = *reinterpret_cast<const float4*>(dys + b * C + c);
-  const float4 ad = *reinterpret_cast<const float4*>(dya + b * C + c);
-  return make_float4(fmaf(g.x, sc.x, ad.x), fmaf(g.y, sc.y, ad.y), fmaf(g.z, sc.z, ad.z),
-                     fmaf(g.w, sc.w, ad.w));
-}
+// The image's (dys, dya) row is cached: a thread's rows only increase, so the
+// 64-bit m / hw and the two loads happen once per image crossing instead of
+// once per row.
+struct DyImgCache {
+  int64_t lo = 0, hi = -1;
+  float4 sc, ad;
+  __device__ __forceinline__ float4 apply(float4 g, const float* __restrict__ dys,
+                                          const float* __restrict__ dya, int64_t m, int64_t hw,
+                                          int C, int c) {
+    if (m >= hi || m < lo) {
+      const int64_t b = m / hw;
+      lo = b * hw;
+      hi = lo + hw;
+      sc = *reinterpret_cast<const float4*>(dys + b * C + c);
+      ad = *reinterpret_cast<const float4*>(dya + b * C + c);
+    }
+    return make_float4(fmaf(g.x, sc.x, ad.x), fmaf(g.y, sc.y, ad.y), fmaf(g.z, sc.z, ad.z),
+                       fmaf(g.w, sc.w, ad.w));
+  }
+};
 
 template <bool RES, bool TR>
 __global__ __launch_bounds__(kRedThreads) void bn_bwd_part_kernel(
@@ -353,8 +365,9 @@ __global__ __launch_bounds__(kRedThreads) void bn_bwd_part_kernel(
       const float4 is = *reinterpret_cast<const float4*>(invstd + c);
       const float4 gm = *reinterpret_cast<const float4*>(gamma + c);
       const float4 bt = *reinterpret_cast<const float4*>(beta + c);
+      DyImgCache ic;
       auto acc = [&](int64_t m, float4 v, float4 g, float4 r) {
-        if (TR) g = dy_transform(g, dys, dya, m / hw, C, c);
+        if (TR) g = ic.apply(g, dys, dya, m, hw, C, c);
         float xh[4] = {(v.x - mu.x) * is.x, (v.y - mu.y) * is.y, (v.z - mu.z) * is.z,
                        (v.w - mu.w) * is.w};
         float gg[4] = {g.x, g.y, g.z, g.w};
@@ -441,8 +454,9 @@ __global__ __launch_bounds__(kRedThreads) void bn_bwd_apply_kernel(
     a2[j] = sdzx[c + j] * invM;
   }
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  DyImgCache ic;
   auto one = [&](int64_t m, float4 v, float4 g, float4 r) {
-    if (TR) g = dy_transform(g, dys, dya, m / hw, C, c);
+    if (TR) g = ic.apply(g, dys, dya, m, hw, C, c);
     const float vv[4] = {v.x, v.y, v.z, v.w}, gg[4] = {g.x, g.y, g.z, g.w},
                 rr[4] = {r.x, r.y, r.z, r.w};
     float o[4], dzo[4];
