@@ -48,27 +48,39 @@ __device__ __forceinline__ float4 fma4pk(float4 a, float4 b, float4 c) {
 
 // BatchNorm + activation applied on load by the BN-input depthwise kernels
 // (dwconv.hip forward, train.hip weight gradient; both use this, so they see
-// the same values): act(x * a + c), a = invstd * gamma, c = beta - mean * a.
+// the same values): act(z), z = fma((x - mean) * invstd, gamma, beta) — the
+// exact fp32 operation order of train.hip's bn_act_fwd and of the mask the
+// BN backward kernels (bn_bwd_*, dw_dgrad_bn) derive, so the forward's
+// activation region and the backward's mask agree element for element (a
+// folded x * a + c rounds differently next to a kink).  Packed: one
+// v_pk_add, one v_pk_mul and one v_pk_fma per two elements.
 struct DwBnCoef {
-  float4 a, c;
+  float4 nmu, is, g, b;  // -mean, invstd, gamma, beta
 };
 
 __device__ __forceinline__ DwBnCoef dw_bn_coef(const float* mean, const float* invstd,
                                                const float* gamma, const float* beta, int cg) {
   const float4 mu = reinterpret_cast<const float4*>(mean)[cg];
-  const float4 is = reinterpret_cast<const float4*>(invstd)[cg];
-  const float4 gm = reinterpret_cast<const float4*>(gamma)[cg];
-  const float4 bt = reinterpret_cast<const float4*>(beta)[cg];
   DwBnCoef k;
-  k.a = make_float4(is.x * gm.x, is.y * gm.y, is.z * gm.z, is.w * gm.w);
-  k.c = make_float4(fmaf(-mu.x, k.a.x, bt.x), fmaf(-mu.y, k.a.y, bt.y), fmaf(-mu.z, k.a.z, bt.z),
-                    fmaf(-mu.w, k.a.w, bt.w));
+  k.nmu = make_float4(-mu.x, -mu.y, -mu.z, -mu.w);
+  k.is = reinterpret_cast<const float4*>(invstd)[cg];
+  k.g = reinterpret_cast<const float4*>(gamma)[cg];
+  k.b = reinterpret_cast<const float4*>(beta)[cg];
   return k;
+}
+
+__device__ __forceinline__ float4 dw_bn_z(float4 v, const DwBnCoef& k) {
+  // x + (-mean) is x - mean exactly (IEEE); products and fma per element
+  const f32x2_t h0 = ((f32x2_t){v.x, v.y} + (f32x2_t){k.nmu.x, k.nmu.y}) * (f32x2_t){k.is.x, k.is.y};
+  const f32x2_t h1 = ((f32x2_t){v.z, v.w} + (f32x2_t){k.nmu.z, k.nmu.w}) * (f32x2_t){k.is.z, k.is.w};
+  const f32x2_t z0 = __builtin_elementwise_fma(h0, (f32x2_t){k.g.x, k.g.y}, (f32x2_t){k.b.x, k.b.y});
+  const f32x2_t z1 = __builtin_elementwise_fma(h1, (f32x2_t){k.g.z, k.g.w}, (f32x2_t){k.b.z, k.b.w});
+  return make_float4(z0.x, z0.y, z1.x, z1.y);
 }
 
 // act: 1 relu, 2 leaky, 3 hswish (JABD_ACT_*), else identity
 __device__ __forceinline__ float4 dw_bn_in(float4 v, const DwBnCoef& k, int act, float slope) {
-  float4 z = fma4pk(v, k.a, k.c);
+  float4 z = dw_bn_z(v, k);
   if (act == 1) {
     z.x = fmaxf(z.x, 0.f); z.y = fmaxf(z.y, 0.f); z.z = fmaxf(z.z, 0.f); z.w = fmaxf(z.w, 0.f);
   } else if (act == 2) {

@@ -34,10 +34,10 @@ __device__ __forceinline__ float4 f4fma(float4 a, float4 w, float4 c) { return f
 // every workgroup recomputes with the main loop's tap order (workgroup (0, 0)
 // writes it to shift[] for bn_stats_final).  Saves bn2's statistics pass.
 // IT: the input is act(bn(x)) of the stored pre-BN tensor x, applied on load
-// (MNv3 Block_eca bn1 + act feeding conv2) as act(x * a + c) with
-// a = invstd * gamma, c = beta - mean * a (dw_bn_in, shared with the weight
-// gradient in train.hip), in-bounds taps only (padding stays zero), so the
-// activated expansion is never written.
+// (MNv3 Block_eca bn1 + act feeding conv2) as act(fma((x - mean) * invstd,
+// gamma, beta)) — bn_act_fwd's and the BN backward's operation order
+// (common.h dw_bn_in, shared with the weight gradient in train.hip) — in-bounds
+// taps only (padding stays zero), so the activated expansion is never written.
 struct DwBnIn {
   const float* mean;
   const float* invstd;

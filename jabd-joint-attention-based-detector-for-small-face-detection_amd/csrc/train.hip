@@ -1227,7 +1227,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_bn_kernel(
         const float iss[4] = {is.x, is.y, is.z, is.w};
         float dz[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) dz[e] = gg[e] * act_d(xh[e] * gmm[e] + btt[e], act, slope);
+        for (int e = 0; e < 4; ++e) dz[e] = gg[e] * act_d(fmaf(xh[e], gmm[e], btt[e]), act, slope);
         if (MODE == 2) {
           float o[4];
 #pragma unroll

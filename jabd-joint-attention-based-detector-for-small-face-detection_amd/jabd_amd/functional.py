@@ -18,7 +18,9 @@ ACT = {"none": 0, "relu": 1, "leaky": 2, "hswish": 3, "hsigmoid": 4, "sigmoid": 
 # of a piecewise activation (ReLU / LeakyReLU / Hardswish / Hardsigmoid) or a
 # max-pool argmax, so the float64 oracle can be run with this path's own
 # masks.  tap(kind, *operands); kinds: "bn", "eca", "beca", "act", "ssh",
-# "maxpool".
+# "maxpool", and "stats" (src, x, mean, invstd, eps: every BatchNorm's batch
+# statistics with the tensor they were taken of and the kernel that took
+# them, for the at-size statistics checks).
 KINK_TAP = None
 
 # Split-K for small-grid k x k convs (conv32.hip m32_ksplit).  It regroups

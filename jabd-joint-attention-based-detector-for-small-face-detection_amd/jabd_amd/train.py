@@ -303,6 +303,7 @@ class BnActFn(torch.autograd.Function):
         invstd = torch.empty_like(mean)
         call("jabd_bn_stats_f32", x.data_ptr(), C, M, C, part.data_ptr(), mean.data_ptr(),
              invstd.data_ptr(), _p(rmean), _p(rvar), float(momentum), float(eps), _st())
+        F.tap("stats", "bn_stats", x, mean, invstd, eps)
         y = torch.empty_like(x)
         g = gamma.detach().contiguous()
         b = beta.detach().contiguous()
@@ -547,6 +548,7 @@ class SshTailFn(torch.autograd.Function):
             invstd = torch.empty_like(mean)
             call("jabd_bn_stats_f32", x.data_ptr(), C, M, C, part.data_ptr(), mean.data_ptr(),
                  invstd.data_ptr(), _p(rm), _p(rv), float(mom), float(eps), _st())
+            F.tap("stats", "bn_stats", x, mean, invstd, eps)
             gg, bb_ = g.detach().contiguous(), bt.detach().contiguous()
             call("jabd_bn_act_fwd_f32", x.data_ptr(), C, M, C, mean.data_ptr(),
                  invstd.data_ptr(), gg.data_ptr(), bb_.data_ptr(), None, C, ACT["relu"], 0.0,
@@ -827,6 +829,7 @@ def _bn_stats(x, bn):
     call("jabd_bn_stats_f32", x.data_ptr(), C, M, C, part.data_ptr(), mean.data_ptr(),
          invstd.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
          float(bn.momentum), float(bn.eps), _st())
+    F.tap("stats", "bn_stats", x, mean, invstd, bn.eps)
     return mean, invstd
 
 
@@ -848,6 +851,7 @@ def _bn_fwd(x, bn, act, slope=0.0, res=None, sums=False, stats=None):
         call("jabd_bn_stats_f32", x.data_ptr(), C, M, C, part.data_ptr(), mean.data_ptr(),
              invstd.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
              float(bn.momentum), float(bn.eps), _st())
+        F.tap("stats", "bn_stats", x, mean, invstd, bn.eps)
     g = bn.weight.detach()
     b = bn.bias.detach()
     y = torch.empty_like(x)
@@ -928,6 +932,7 @@ def _conv_fwd_bn_stats(x, weight, bn):
     call("jabd_bn_stats_final_f32", shift.data_ptr(), part.data_ptr(), nblk, B * H * W, C,
          mean.data_ptr(), invstd.data_ptr(), bn.running_mean.data_ptr(),
          bn.running_var.data_ptr(), float(bn.momentum), float(bn.eps), _st())
+    F.tap("stats", "conv1x1_stream", y, mean, invstd, bn.eps)
     return y, (mean, invstd)
 
 
@@ -984,6 +989,7 @@ def _dw_fwd_bn_stats(x, weight, stride, bn, bnin=None):
     call("jabd_bn_stats_final_f32", shift.data_ptr(), part.data_ptr(), nblk, B * OH * OW, C,
          mean.data_ptr(), invstd.data_ptr(), bn.running_mean.data_ptr(),
          bn.running_var.data_ptr(), float(bn.momentum), float(bn.eps), _st())
+    F.tap("stats", "dw" if bnin is None else "dw_bnin", y, mean, invstd, bn.eps)
     return y, wt, (mean, invstd)
 
 

@@ -29,7 +29,27 @@ kernel being wrong — or a real kernel error could be excused as a flip.
 Both oracle runs (float64 and float32) are replayed, so the float32 run's
 error against the float64 run is again pure rounding, and the per-tensor bar
 max(tol, 4x that error) no longer hides mask flips.
+
+The replay is bounded, so that it cannot adopt a wrong mask (one a backward
+kernel derived from a stale mean/invstd or the wrong residual):
+  * pairing tolerance 1e-3 (relative max difference); the one named
+    exception is a BatchNorm over 1x1 maps (the SE gate's, B samples per
+    channel), which amplifies fp32 rounding to ~1e-3 and pairs at 1e-2;
+  * rounding-level: when the float64 replay is followed by the float32 one
+    (as every caller does), each HIP pre-activation's distance from the
+    float64 oracle's must be within ROUND_FACTOR x the plain float32 oracle's
+    own distance from it (floor ROUND_FLOOR) — the HIP tensor may carry fp32
+    rounding, not an error of its own;
+  * every paired call counts its flips — elements whose region (side of a
+    kink, or max-pool argmax) differs between the HIP tensor and the oracle's
+    own; a call may flip at most max(FLIP_MIN, FLIP_FRAC * numel) elements,
+    each within the rounding distance above of its kink (for a max-pool: the
+    two window values within that of each other).
+A violation is reported through `unmatched`, which every caller asserts
+empty.
+`stats()` / JABD_KINK_LOG=<file> expose the pairing distances and flips.
 """
+import os
 import torch
 
 from jabd_amd import functional as JF
@@ -38,9 +58,34 @@ from oracle import model_ref
 _FAMILY = {"relu": "pos", "leaky": "pos", "hswish": "hswish", "hsigmoid": "hsig",
            "maxpool": "maxpool"}
 
+PAIR_TOL = 1e-3
+PAIR_TOL_SE = 1e-2
+FLIP_MIN = 8
+FLIP_FRAC = 2e-4
+ROUND_FACTOR = 8.0
+ROUND_FLOOR = 2e-6
+_ULP = 2.0 ** -23
+_DEV = "cpu"
+
 
 def _f32(t):
-    return t.detach().float().cpu()
+    return t.detach().float().to(_DEV)
+
+
+def _region(fam, z):
+    """Which side of each kink (PyTorch's *_backward conventions, as
+    oracle.model_ref._KinkFn)."""
+    if fam == "pos":
+        return (z > 0).to(torch.int8)
+    if fam == "hswish":
+        return torch.where(z < -3, 0, torch.where(z <= 3, 1, 2)).to(torch.int8)
+    return ((z > -3) & (z < 3)).to(torch.int8)
+
+
+def _kink_dist(fam, z):
+    if fam == "pos":
+        return z.abs()
+    return torch.minimum((z + 3).abs(), (z - 3).abs())
 
 
 def _fma32(a, b, c):
@@ -64,12 +109,21 @@ def _nchw(z):
 
 
 class Kinks:
-    def __init__(self, tol=1e-2):
+    def __init__(self, tol=PAIR_TOL, device="cpu"):
+        """device: where the recorded pre-activations are kept and compared
+        (the oracle run's device; "cuda" for the at-size tests, whose fp64
+        oracle runs on the GPU through PyTorch's own kernels)."""
         self.rec = []            # (family, [candidate float64 tensors])
         self.tol = tol
+        self.device = device
         self.used = set()
         self.matched = 0
-        self.unmatched = []      # (kind, shape) of oracle calls left on their own masks
+        self.unmatched = []      # (kind, shape, why) of oracle calls not cleanly paired
+        self.log = []            # (kind, shape, pairing distance, flips, worst flip in ulps)
+        self.nreplay = 0
+        self.calls = []          # this replay: (oracle z, scale, HIP pairing distance, worst flip)
+        self.prev = []           # the previous replay's calls
+        self.dtypes = []         # oracle dtype of each replay
 
     # ------------------------------------------------------------------ recording
     def _add(self, kind, z, nhwc=True):
@@ -80,6 +134,10 @@ class Kinks:
         self.rec.append((_FAMILY[kind], cands))
 
     def __call__(self, kind, *a):
+        global _DEV
+        _DEV = self.device
+        if kind == "stats":
+            return
         if kind == "bn":
             act, slope, x, mean, invstd, g, b, res = a
             self._add(act, _bn_z(x, mean, invstd, g, b, res))
@@ -89,7 +147,7 @@ class Kinks:
             k = w.numel()
             h = (k - 1) // 2
             B, C = mean.shape
-            z = torch.zeros((B, C), dtype=torch.float32)
+            z = torch.zeros((B, C), dtype=torch.float32, device=mean.device)
             for t in range(k):   # z = fma(w[t], mean[c + t - h], z), taps in order
                 sh = torch.zeros_like(mean)   # out-of-range taps: fma(w, 0, z) == z
                 lo, hi = max(0, h - t), min(C, C + h - t)
@@ -140,7 +198,34 @@ class Kinks:
                 out.append(z.reshape(shape))
         return out
 
+    def _tol(self, shape):
+        if len(shape) == 4 and shape[2] * shape[3] == 1:
+            return max(self.tol, PAIR_TOL_SE)     # SE gate: BN over B 1x1 samples
+        return self.tol
+
+    def _flips(self, fam, v, zo, scale):
+        """(count, worst distance from the kink in ulps of scale) of the
+        elements whose region differs between HIP tensor v and oracle zo."""
+        if fam == "maxpool":
+            _, io = torch.nn.functional.max_pool2d(zo, 3, 2, 1, return_indices=True)
+            _, iv = torch.nn.functional.max_pool2d(v, 3, 2, 1, return_indices=True)
+            diff = io != iv
+            n = int(diff.sum())
+            if not n:
+                return 0, 0.0
+            flat = zo.flatten(2)
+            gap = (flat.gather(2, io.flatten(2)) - flat.gather(2, iv.flatten(2))).abs()
+            return n, float(gap.flatten()[diff.flatten()].max()) / (scale * _ULP)
+        fo = "pos" if fam == "ssh" else fam
+        diff = _region(fo, v) != _region(fo, zo)
+        n = int(diff.sum())
+        if not n:
+            return 0, 0.0
+        return n, float(_kink_dist(fo, zo)[diff].max()) / (scale * _ULP)
+
     def match(self, kind, z):
+        if len(self.dtypes) < self.nreplay:
+            self.dtypes.append(self._pending_dtype or z.dtype)
         fam = _FAMILY[kind]
         zo = z.detach().double()
         scale = float(zo.abs().max()) or 1.0
@@ -149,18 +234,66 @@ class Kinks:
             if i in self.used or not (f == fam or (f == "ssh" and fam == "pos")):
                 continue
             for v in self._views(f, cands, zo.shape):
+                v = v.to(zo.device)
                 d = float((v - zo).abs().max()) / scale
                 if d < best[2]:
                     best = (i, v, d)
-        if best[0] is None or best[2] >= self.tol:
-            self.unmatched.append((kind, tuple(zo.shape), best[2]))
+        shape = tuple(zo.shape)
+        if best[0] is None or best[2] >= self._tol(shape):
+            self.unmatched.append((kind, shape, f"pairing {best[2]:.2e}"))
+            self._note(kind, shape, best[2], None, None)
             return None
+        n, worst = self._flips(fam, best[1], zo, scale)
+        d32 = self._rounding(kind, shape, zo)
+        self._note(kind, shape, best[2], n, worst, d32)
+        if n > max(FLIP_MIN, FLIP_FRAC * zo.numel()):
+            self.unmatched.append((kind, shape, f"{n} flips, worst {worst:.0f} ulp"))
+        self.calls.append((zo if z.dtype == torch.float64 else None, scale, best[2], worst))
         self.used.add(best[0])
         self.matched += 1
         return best[1]
 
-    def replay(self):
+    def _rounding(self, kind, shape, zo):
+        """In a float32 replay that follows a float64 one: this call's fp32
+        oracle distance from the fp64 oracle, and the check of the fp64
+        replay's HIP pairing distance (and flips) against it."""
+        i = len(self.calls)
+        if self.dtypes[-2:] != [torch.float64, torch.float32] or i >= len(self.prev):
+            return None
+        z64, scale, dh, worst = self.prev[i]
+        if z64 is None or tuple(z64.shape) != shape:
+            return None
+        d32 = float((zo - z64.to(zo.device)).abs().max()) / scale
+        lim = max(ROUND_FACTOR * d32, ROUND_FLOOR)
+        if dh > lim or worst * _ULP > lim:
+            self.unmatched.append((kind, shape, f"HIP {dh:.2e} / flip {worst * _ULP:.2e} from "
+                                   f"fp64 vs fp32 oracle {d32:.2e}"))
+        return d32
+
+    def _note(self, kind, shape, d, n, worst, d32=None):
+        self.log.append((kind, shape, d, n, worst))
+        path = os.environ.get("JABD_KINK_LOG")
+        if path:
+            with open(path, "a") as f:
+                f.write(f"{kind} {list(shape)} pair={d:.3e} flips={n} worst_ulp={worst} "
+                        f"o32={d32}\n")
+
+    def stats(self):
+        """(max pairing distance, total flips, worst flip in ulps) over the
+        paired calls so far."""
+        ok = [r for r in self.log if r[3] is not None]
+        return (max((r[2] for r in ok), default=0.0), sum(r[3] for r in ok),
+                max((r[4] for r in ok), default=0.0))
+
+    def replay(self, dtype=None):
+        """dtype: the oracle run's dtype (taken from the first call when
+        None)."""
         self.used = set()
+        if self.calls or self.nreplay:
+            self.prev = self.calls
+        self.calls = []
+        self.nreplay += 1
+        self._pending_dtype = dtype
         return _Install(self, "replay")
 
 

@@ -123,3 +123,57 @@ def test_bn_z_is_the_kernels_fma_order():
     exact = xh.double() * gm.double() + bt.double()
     assert z.dtype == torch.float32
     assert torch.equal(z, exact.float())
+
+
+def test_pairing_rejects_a_stale_operand():
+    """A recorded pre-activation 0.5% off (e.g. a backward mask taken from a
+    stale mean/invstd) no longer pairs: the tolerance is 1e-3, not 1e-2."""
+    spec, sd, x = _setup()
+    kk, _ = _recorded(sd, x, spec, torch.float64)
+    for _, cands in kk.rec:
+        cands[0].add_(5e-3 * float(cands[0].abs().max()))
+    with kk.replay():
+        _block_run(sd, x, torch.float64, spec)
+    assert kk.matched == 0 and len(kk.unmatched) == 4
+
+
+def test_flips_beyond_rounding_are_reported():
+    """Elements moved across the ReLU kink by more than fp32 rounding (here:
+    every |z| < 2e-4 max|z| negated, a pairing distance well inside 1e-3)
+    are flips the replay refuses to adopt silently; the fp32 run's own
+    rounding-level flips are accepted and counted."""
+    spec, sd, x = _setup()
+    kk, _ = _recorded(sd, x, spec, torch.float64)
+    fam0, cands = kk.rec[0]
+    z = cands[0]
+    near = z.abs() < 2e-4 * float(z.abs().max())
+    assert int(near.sum()) >= 1
+    z[near] = -z[near] - 1e-5 * float(z.abs().max())
+    with kk.replay():
+        _block_run(sd, x, torch.float64, spec)
+    assert any("flips" in u[2] for u in kk.unmatched), kk.unmatched
+    kk32, _ = _recorded(sd, x, spec, torch.float32)
+    with kk32.replay():
+        _block_run(sd, x, torch.float64, spec)
+    assert not kk32.unmatched
+    pair, flips, worst = kk32.stats()
+    assert flips >= 1 and worst <= 16 and pair < 1e-5   # the 2.2e-8 flip of the test above
+
+
+def test_rounding_check_against_the_fp32_oracle():
+    """The fp64-then-fp32 replay pair bounds each HIP tensor's distance from
+    the fp64 oracle by ROUND_FACTOR x the fp32 oracle's own: recorded fp32
+    tensors pass; one shifted by 3e-5 of its max (inside the 1e-3 pairing
+    tolerance, far outside fp32 rounding at this size) is reported."""
+    spec, sd, x = _setup()
+    for shift, expect in ((0.0, False), (3e-5, True)):
+        kk, _ = _recorded(sd, x, spec, torch.float32)
+        if shift:
+            z = kk.rec[1][1][0]
+            z.add_(shift * float(z.abs().max()))
+        with kk.replay():
+            _block_run(sd, x, torch.float64, spec)
+        assert not kk.unmatched
+        with kk.replay():
+            _block_run(sd, x, torch.float32, spec)
+        assert any("fp32 oracle" in u[2] for u in kk.unmatched) == expect, kk.unmatched

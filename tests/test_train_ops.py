@@ -485,8 +485,10 @@ def test_dw_bnin(cuda, c, k, s, bhw, act):
     y1, _, (m1, i1) = T._dw_fwd_bn_stats(xg, wg, s, bn2s[0], bnin=(st1, act))
     y2, wt, (m2, i2) = T._dw_fwd_bn_stats(e, wg, s, bn2s[1])
     torch.cuda.synchronize()
-    # on-load form act(x * a + c) vs bn_act_fwd's act((x - mean) * invstd *
-    # gamma + beta): a few ulp per activated element
+    # the on-load z is bn_act_fwd's fma((x - mean) * invstd, gamma, beta);
+    # ReLU is then bit-identical, the two Hardswish formulas a few ulp apart
+    if act == "relu":
+        assert torch.equal(y1, y2)
     assert rel_err(y1.cpu(), y2.cpu()) < 2e-6
     assert rel_err(m1.cpu(), m2.cpu()) < 1e-5
     assert rel_err(i1.cpu(), i2.cpu()) < 1e-5
@@ -494,6 +496,8 @@ def test_dw_bnin(cuda, c, k, s, bhw, act):
     _, dw1 = T._dw_bwd(dy, xg, wt, k, s, want_dx=False, bnin=(st1, act))
     _, dw2 = T._dw_bwd(dy, e, wt, k, s, want_dx=False)
     torch.cuda.synchronize()
+    if act == "relu":
+        assert torch.equal(dw1, dw2)
     assert rel_err(dw1.cpu(), dw2.cpu()) < 2e-6
     # plain fp32 reference of the whole chain
     ref_e = torch.nn.functional.relu(
@@ -504,3 +508,94 @@ def test_dw_bnin(cuda, c, k, s, bhw, act):
                                        bn1.bias.detach().cpu(), True, 0.0, bn1.eps))
     ref_y = torch.nn.functional.conv2d(ref_e, w, None, s, k // 2, 1, c)
     assert rel_err(y1.cpu().permute(0, 3, 1, 2), ref_y) < 1e-4
+
+
+def _near_kink_bn(C=64, n=16, seed=21):
+    """Per channel a BN (mean, invstd, gamma, beta) and n consecutive fp32
+    inputs straddling the point where z = (x - mean) * invstd * gamma + beta
+    crosses 0 (the ReLU kink), as numpy float32."""
+    import numpy as np
+    r = np.random.default_rng(seed)
+    mu = r.uniform(-1, 1, C).astype(np.float32)
+    inv = r.uniform(0.3, 3.0, C).astype(np.float32)
+    gam = (r.uniform(0.4, 1.6, C) * r.choice([-1, 1], C)).astype(np.float32)
+    bet = r.uniform(-0.6, 0.6, C).astype(np.float32)
+    x0 = (mu.astype(np.float64) - bet.astype(np.float64) / (inv.astype(np.float64) * gam)).astype(np.float32)
+    xs = np.empty((n, C), np.float32)
+    for c in range(C):
+        v = x0[c]
+        for _ in range(n // 2):
+            v = np.nextafter(v, np.float32(-np.inf))
+        for i in range(n):
+            xs[i, c] = v
+            v = np.nextafter(v, np.float32(np.inf))
+    return mu, inv, gam, bet, xs
+
+
+def _fma32_np(a, b, c):
+    import numpy as np
+    return (a.astype(np.float64) * b.astype(np.float64) + c.astype(np.float64)).astype(np.float32)
+
+
+def test_near_kink_inputs_separate_the_bn_forms():
+    """The inputs of test_dw_bnin_kink_masks are sensitive: the folded
+    on-load form fma(x, invstd * gamma, beta - mean * invstd * gamma) and
+    the BN kernels' fma((x - mean) * invstd, gamma, beta) put some of them on
+    different sides of the ReLU kink (so a forward that used the folded form
+    while the backward masks with the other would fail that test)."""
+    import numpy as np
+    mu, inv, gam, bet, xs = _near_kink_bn()
+    a = inv * gam
+    c = _fma32_np(-mu, a, bet)
+    z_fold = _fma32_np(xs, a[None], c[None])
+    z_bn = _fma32_np((xs - mu[None]) * inv[None], gam[None], bet[None])
+    flips = int(((z_fold > 0) != (z_bn > 0)).sum())
+    assert flips >= 5, flips
+    # and every channel's window does cross the kink under the BN form
+    assert bool(((z_bn > 0).any(0) & (z_bn <= 0).any(0)).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recompute", [True, False])
+def test_dw_bnin_kink_masks(cuda, recompute, monkeypatch):
+    """the BN-input depthwise forward's activation region must be
+    the mask its backward applies, element for element, next to the kink.
+    A centre-tap-only 3x3/s2 depthwise weight makes the forward output at
+    (oh, ow) = relu(z(x[2oh, 2ow])) and the input gradient reach only those
+    pixels; dy = 2^j on 16 of them makes bn1's dbeta = sum_j 2^j [z_j > 0]
+    an exact bit mask of the backward's region (sums of distinct powers of
+    two below 2^24 are exact in fp32)."""
+    import numpy as np
+    from jabd_amd import train as T
+    monkeypatch.setattr(T, "DGBN_RECOMPUTE", recompute)
+    C, n = 64, 16
+    mu, inv, gam, bet, xs = _near_kink_bn(C, n)
+    H = W = 16
+    x = np.empty((1, H, W, C), np.float32)
+    far = (mu - np.sign(gam) * 50.0 / (inv * np.abs(gam))).astype(np.float32)   # z ~ -50
+    x[:] = far
+    pos = [(2 * (j // 4), 2 * (j % 4)) for j in range(n)]
+    for j, (ih, iw) in enumerate(pos):
+        x[0, ih, iw] = xs[j]
+    dev = torch.device(cuda)
+    xg = torch.from_numpy(x).to(dev)
+    w = torch.zeros(C, 1, 3, 3)
+    w[:, 0, 1, 1] = 1.0
+    wg = w.to(dev)
+    st = tuple(torch.from_numpy(t).to(dev) for t in (gam, bet, mu, inv))
+    bn2 = torch.nn.BatchNorm2d(C).to(dev)
+    y, wt, _ = T._dw_fwd_bn_stats(xg, wg, 2, bn2, bnin=(st, "relu"))
+    dy = torch.zeros(1, 8, 8, C)
+    for j, (ih, iw) in enumerate(pos):
+        dy[0, ih // 2, iw // 2] = float(2 ** j)
+    dx, dgamma, dbeta, dw = T._dw_bn_bwd(dy.to(dev), None, wt, 3, 2, xg, st, "relu")
+    torch.cuda.synchronize()
+    yc = y.cpu().numpy()
+    fwd = np.stack([yc[0, ih // 2, iw // 2] > 0 for ih, iw in pos])          # [n, C]
+    bits = dbeta.cpu().numpy().astype(np.int64)
+    bwd = np.stack([(bits >> j) & 1 for j in range(n)]).astype(bool)
+    assert (dbeta.cpu().numpy() == bits).all()
+    bad = np.argwhere(fwd != bwd)
+    assert bad.size == 0, f"{len(bad)} elements: forward region != backward mask, e.g. {bad[:4]}"
+    # each channel's window straddles the kink, so the check is not vacuous
+    assert fwd.any(0).all() and (~fwd).any(0).all()
