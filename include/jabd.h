@@ -82,6 +82,25 @@ int jabd_batched_nms_f32(const float* boxes, int64_t box_stride,
 int jabd_nms_pair_stats(const void* ws, size_t ws_bytes, int64_t batch, int64_t n,
                         int64_t* tested, int32_t* hits, int32_t* dense, jabd_stream_t stream);
 
+/* The NMS pipeline's sort and scan (hand-written wavefront radix sort and
+ * scan, radix.hip), exported so they are tested on their own.  torchvision's
+ * nms sorts the scores descending, stable (utils/utils_bbox.py:275); the
+ * batched pipeline sorts [image | ~score | row] keys and its grid producer's
+ * cell keys with this sort, and forms its CSR offsets with this scan.
+ *   jabd_sort_u64: stable sort of n uint64 keys (with int32 values when
+ *     vals_in != NULL) by key bits [bit_lo, bit_lo + 8 npass), 1 <= npass <= 8,
+ *     n < 2^31; keys_in is not modified.  skip_ones != 0: keys equal to ~0
+ *     do not keep a lower pass from being skipped as constant (they sort last
+ *     either way).  Keys/values out must not alias the inputs.
+ *   jabd_scan_excl_i32: out[i] = in[0] + ... + in[i-1] (int32, exact). */
+int jabd_sort_workspace_size(int64_t n, int32_t with_values, size_t* bytes);
+int jabd_sort_u64(const uint64_t* keys_in, uint64_t* keys_out, const int32_t* vals_in,
+                  int32_t* vals_out, int64_t n, int32_t bit_lo, int32_t npass, int32_t skip_ones,
+                  void* ws, size_t ws_bytes, jabd_stream_t stream);
+int jabd_scan_workspace_size(int64_t n, size_t* bytes);
+int jabd_scan_excl_i32(const int32_t* in, int32_t* out, int64_t n, void* ws, size_t ws_bytes,
+                       jabd_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * predict.py:162-181 fused: decode + decode_landm + conf[:,1] + score filter
  * + NMS, for B images at once.  conf is the eval-mode softmax [B,A,2].

@@ -4,7 +4,8 @@
 // Pipeline per call (B images, up to n boxes each), all on one stream:
 //   1. nms_keys      one 64-bit key per row: [image:8 | ~score:32 | row:24];
 //                    rows failing the score filter get image 255 (sorted last).
-//   2. radix sort    hipcub DeviceRadixSort::SortKeys (ascending) — gives
+//   2. radix sort    radix.hip's wavefront LSD sort of the keys by bits 24-63
+//                    (stable; the input is in row order per image) — gives
 //                    every image's rows contiguous, in stable descending-score
 //                    order (ties by lower row index, as torch's stable sort).
 //   3. nms_gather    sorted boxes (float4) + areas + original row ids.
@@ -23,7 +24,6 @@
 //                    the kept rows + count.
 // Compile with -ffp-contract=off: IoU must round exactly like the CPU kernel
 // (no FMA in (x2-x1)*(y2-y1) or inter/(a+b-inter)).
-#include <hipcub/hipcub.hpp>
 #include <math.h>
 #include <stdlib.h>
 
@@ -33,6 +33,7 @@
 
 #include "common.h"
 #include "nms_internal.h"
+#include "radix.h"
 
 namespace jabd {
 
@@ -51,7 +52,7 @@ static bool nms_dense_only() {
   return v == 1;
 }
 
-// Images per sort pass: <= 254 and the sort size must fit hipcub's int.
+// Images per sort pass: <= 254 and the sort size must fit the sort's int32.
 static int64_t images_per_pass(int64_t batch, int64_t n) {
   int64_t c = batch < kMaxImg ? batch : kMaxImg;
   if (n > 0 && c * n > (int64_t)0x7fffffff) c = (int64_t)0x7fffffff / n;
@@ -1021,18 +1022,9 @@ __global__ __launch_bounds__(256) void nms_scan(
 }
 
 // ---------------------------------------------------------------------------
+// radix sort (keys + values) and scan workspace
 static size_t sort_temp_bytes(int64_t items) {
-  size_t bytes = 0;
-  (void)hipcub::DeviceRadixSort::SortKeys(nullptr, bytes, (const uint64_t*)nullptr,
-                                    (uint64_t*)nullptr, (int)items, 0, 64, (hipStream_t)0);
-  size_t b2 = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b2, (const uint64_t*)nullptr,
-                                           (uint64_t*)nullptr, (const int*)nullptr, (int*)nullptr,
-                                           (int)items, 0, 64, (hipStream_t)0);
-  size_t b3 = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b3, (const int*)nullptr, (int*)nullptr,
-                                         (int)items, (hipStream_t)0);
-  return std::max(bytes, std::max(b2, b3));
+  return std::max(radix_ws_bytes(items, true), scan_ws_bytes(items));
 }
 
 struct NmsWs {
@@ -1161,8 +1153,10 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
     nms_keys<<<g1, 256, 0, st>>>(scores, score_stride, score_bstride, n_valid, n, bc,
                                   score_thr, filter, (int)img0, w.kin, w.counts);
     if (int e = check_launch("nms_keys")) return e;
-    JABD_HIP(hipcub::DeviceRadixSort::SortKeys(w.tmp, w.tmp_bytes, w.kin, w.kout, (int)(bc * n),
-                                               0, 64, st));
+    // [image | ~score] (bits 24-63); rows are already in input order
+    if (int e = radix_sort64(w.kin, w.kout, nullptr, nullptr, (int64_t)bc * n, 24, 5, false,
+                             w.tmp, w.tmp_bytes, st))
+      return e;
     nms_gather<<<(unsigned)cdiv((int64_t)bc * n, 256), 256, 0, st>>>(
         w.kout, (int64_t)bc * n, boxes, box_stride, box_bstride, w.counts, bc, n, (int)img0,
         w.sbox, w.sarea, w.sidx, w.nanflag);
@@ -1181,8 +1175,9 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
       grid_keys<<<g1, 256, 0, st>>>(w.sbox, w.sarea, w.counts, n, inv_w, fcell, w.ext, w.kin,
                                      w.gval_in, w.dense);
       if (int e = check_launch("grid_keys")) return e;
-      JABD_HIP(hipcub::DeviceRadixSort::SortPairs(w.tmp, w.tmp_bytes, w.kin, w.kout, w.gval_in,
-                                                  w.gval_out, (int)(bc * n), 0, 64, st));
+      if (int e = radix_sort64(w.kin, w.kout, w.gval_in, w.gval_out, (int64_t)bc * n, 0, 8, true,
+                               w.tmp, w.tmp_bytes, st))
+        return e;
       grid_gather<<<(unsigned)cdiv((int64_t)bc * n, 256), 256, 0, st>>>(
           w.kout, w.gval_out, (int64_t)bc * n, w.sbox, w.sarea, n, w.gbox, w.garea);
       if (int e = check_launch("grid_gather")) return e;
@@ -1196,8 +1191,8 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
           w.runs, w.run_mask, iou_thr, w.cap, w.dense, w.diag, w.npairs, w.rowcnt, w.prow, w.pcol,
           w.pslot, w.tested);
       if (int e = check_launch("grid_pairs")) return e;
-      JABD_HIP(hipcub::DeviceScan::ExclusiveSum(w.tmp, w.tmp_bytes, w.rowcnt, w.rowoff,
-                                                (int)(bc * n), st));
+      if (int e = scan_excl_i32(w.rowcnt, w.rowoff, (int64_t)bc * n, w.tmp, w.tmp_bytes, st))
+        return e;
       dim3 gs((unsigned)std::min<int64_t>(cdiv(w.cap, 256), 512), bc);
       grid_scatter<<<gs, 256, 0, st>>>(w.npairs, w.dense, w.cap, n, w.prow, w.pcol, w.pslot,
                                        w.rowoff, w.csr);

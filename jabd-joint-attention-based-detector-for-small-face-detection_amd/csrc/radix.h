@@ -1,0 +1,20 @@
+// Internal: wavefront radix sort and exclusive scan (radix.hip), used by the
+// NMS pipeline (nms.hip) and exported for tests (jabd_sort_u64_f32 / jabd_scan_*).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace jabd {
+struct RadixWs {
+  int *ghist, *plan, *cnt, *off;
+  uint64_t* kalt;
+  int* valt;
+};
+size_t radix_ws_bytes(int64_t n, bool vals);
+// stable sort of n keys (and values, if vin) by bits [lo, lo + 8 npass);
+// kin is not modified; skip_ones: see radix.hip
+int radix_sort64(const uint64_t* kin, uint64_t* kout, const int* vin, int* vout, int64_t n,
+                 int lo, int npass, bool skip_ones, void* ws, size_t ws_bytes, hipStream_t st);
+size_t scan_ws_bytes(int64_t n);
+int scan_excl_i32(const int* in, int* out, int64_t n, void* ws, size_t ws_bytes, hipStream_t st);
+}  // namespace jabd

@@ -110,6 +110,10 @@ SIGNATURES = {
     "jabd_batched_nms_f32": [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
                              c_f64, c_f32, c_vp, c_vp, c_vp, c_size, c_vp],
     "jabd_nms_pair_stats": [c_vp, c_size, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp],
+    "jabd_sort_workspace_size": [c_i64, c_i32, c_sizep],
+    "jabd_sort_u64": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_size, c_vp],
+    "jabd_scan_workspace_size": [c_i64, c_sizep],
+    "jabd_scan_excl_i32": [c_vp, c_vp, c_i64, c_vp, c_size, c_vp],
     "jabd_detect_workspace_size": [c_i64, c_i64, c_sizep],
     "jabd_detect_f32": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_f32, c_f32, c_f32, c_f64,
                         c_vp, c_vp, c_vp, c_size, c_vp],
