@@ -89,7 +89,7 @@ int jabd_nms_pair_stats(const void* ws, size_t ws_bytes, int64_t batch, int64_t 
  * cell keys with this sort, and forms its CSR offsets with this scan.
  *   jabd_sort_u64: stable sort of n uint64 keys (with int32 values when
  *     vals_in != NULL) by key bits [bit_lo, bit_lo + 8 npass), 1 <= npass <= 8,
- *     n < 2^31; keys_in is not modified.  skip_ones != 0: keys equal to ~0
+ *     n < 2^30; keys_in is not modified.  skip_ones != 0: keys equal to ~0
  *     do not keep a lower pass from being skipped as constant (they sort last
  *     either way).  Keys/values out must not alias the inputs.
  *   jabd_scan_excl_i32: out[i] = in[0] + ... + in[i-1] (int32, exact). */
@@ -459,8 +459,9 @@ typedef struct jabd_expdw_args {
 int64_t jabd_expand_dw_nblk(int32_t OH, int32_t OW, int32_t k, int32_t stride);
 int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_t stream);
 /* Kernel form of jabd_expand_dw_nhwc_f32 (same results bit for bit): 1 = one
- * work item per workgroup, 2 = wave-specialised persistent workgroups, 0 =
- * the default (1, or 2 with JABD_EXPDW_WS=1).  Returns the
+ * work item per workgroup, 2 = wave-specialised persistent workgroups, 3 =
+ * persistent workgroups walking a fixed channel chunk's tiles, 0 = the
+ * default (1; 2 with JABD_EXPDW_WS=1, 3 with JABD_EXPDW2=1).  Returns the
  * previous setting.  For A/B timing and the equivalence test. */
 int jabd_expand_dw_select(int32_t form);
 

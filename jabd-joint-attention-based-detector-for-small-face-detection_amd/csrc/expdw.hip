@@ -20,146 +20,12 @@
 // in registers across the switch).  Workgroup ids are decoded XCD-aware: the
 // EC-chunks of one tile land on the same XCD (id % 8), so their re-reads of
 // the input tile hit that XCD's L2.
-#include <stdlib.h>
-
-#include "common.h"
-#include "conv_args.h"
+#include "expdw_shared.h"
 
 namespace jabd {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// Phase-skip mask for timing experiments only (tools/xd_variant.sh builds
-// libraries with -DXD_SKIP=n; results are wrong): 1 expand MFMAs, 2 expanded-
-// tile LDS writes, 4 depthwise phase, 8 ECA reduce, 16 input loads;
-// expdw_ws_kernel: 32 expand-wave MFMAs, 64 depthwise-wave depthwise phase,
-// 128 expand-wave input loads (out-of-range offsets: zeros, no traffic), 256
-// expand-wave epilogue (activation + expanded-tile writes).
-#ifndef XD_SKIP
-#define XD_SKIP 0
-#endif
-
-// Activation fixed at compile time (no per-element branch).  Hardswish
-// multiplies by 1/6 instead of dividing (<= 1 ulp from x*relu6(x+3)/6; an
-// IEEE divide is ~10 VALU instructions per element here).
-template <int ACT>
-__device__ __forceinline__ float xd_act(float v) {
-  if (ACT == ACT_RELU) return fmaxf(v, 0.f);  // one v_max (a select is cmp + cndmask)
-  if (ACT == ACT_HSWISH) return hswish_f(v);
-  return v;
-}
-
-template <int K, int S, int TH, int TW, int EC>
-struct XdCfg {
-  static constexpr int PAD = K / 2;
-  static constexpr int IH = (TH - 1) * S + K, IW = (TW - 1) * S + K;
-  static constexpr int IPX = IH * IW;
-  static constexpr int IPAD = (IPX + 15) / 16 * 16;
-  static constexpr int XP = 16;      // staged input: 4 quad planes of IPAD float4
-  static constexpr int EP = EC + 4;  // expanded-tile pitch
-  static constexpr int NPB = IPAD / 16, NNT = EC / 16, NBLK = NPB * NNT;
-  static constexpr int LDS_X = IPAD * XP, LDS_E = IPAD * EP;
-  static constexpr int LDS = LDS_X > LDS_E ? LDS_X : LDS_E;
-  static constexpr int PW = S == 1 ? 4 : 2, NSTRIP = TW / PW, NC4 = EC / 4;
-  static constexpr int ITEMS = TH * NSTRIP * NC4;
-  static constexpr int SPAN = (PW - 1) * S + K;
-  static_assert(TW % PW == 0 && 256 % NC4 == 0, "tile shape");
-  static_assert(LDS * 4 <= 160 * 1024, "LDS");
-  static_assert((K * K + 1) * NC4 <= 256, "dw taps: one float4 per thread");
-  static_assert(NC4 == 4 || NC4 == 8, "dw_lane: 16- or 32-channel chunks");
-};
-
-// Workgroup barrier for LDS hand-offs only.  __syncthreads() is also a
-// workgroup-scope fence on global memory, so the compiler drains every
-// outstanding global load (s_waitcnt vmcnt(0)) before it — which would
-// retire an in-flight register prefetch at the first barrier after it is
-// issued.  The LDS ordering this kernel needs is just lgkmcnt(0) + s_barrier.
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-struct XdItem {
-  int b, t_in, oh0, ow0, ih0, iw0, c0;
-};
-
-// n / d for 0 <= n < 2^31 by multiply-high and shift (host-built divisor):
-// the per-item decode would otherwise run three ~40-instruction integer
-// divisions on the scalar unit.
-struct FastDiv {
-  uint32_t m, l, d;
-};
-static FastDiv make_fastdiv(uint32_t d) {
-  uint32_t l = 0;
-  while ((1ull << l) < d) ++l;
-  const uint64_t m = ((((uint64_t)1 << l) - d) << 32) / d + 1;
-  return FastDiv{(uint32_t)m, l, d};
-}
-__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
-  return (int)((__umulhi((uint32_t)n, f.m) + (uint32_t)n) >> f.l);
-}
-struct XdDivs {
-  FastDiv nch, tiles_img, tiles_w;
-};
-
-template <int K, int S, int TH, int TW, int EC>
-__device__ __forceinline__ bool xd_item(const jabd_expdw_args& p, int i, const XdDivs& dv,
-                                        int nitems, XdItem& it) {
-  using C = XdCfg<K, S, TH, TW, EC>;
-  if (i >= nitems) return false;
-  const int xcd = i & 7;
-  const int q = i >> 3;
-  const int qn = fdiv(q, dv.nch);
-  const int chunk = q - qn * (int)dv.nch.d;
-  const int tile = qn * 8 + xcd;
-  if (tile >= p.B * (int)dv.tiles_img.d) return false;
-  it.b = fdiv(tile, dv.tiles_img);
-  it.t_in = tile - it.b * (int)dv.tiles_img.d;
-  const int ty = fdiv(it.t_in, dv.tiles_w), tx = it.t_in - ty * (int)dv.tiles_w.d;
-  it.oh0 = ty * TH;
-  it.ow0 = tx * TW;
-  it.ih0 = it.oh0 * S - C::PAD;
-  it.iw0 = it.ow0 * S - C::PAD;
-  it.c0 = chunk * EC;
-  return true;
-}
-
-// ---------------------------------------------------------------------------
-// One workgroup per work item (tile x EC-chunk), no state carried across
-// items (a persistent cross-item-prefetch form measured 5-30% slower on every
-// layer: SGPR spills, loop-carried operand copies).  The item is decoded
-// once; loads go through a buffer descriptor whose range check zeroes
-// out-of-image pixels (no branch per load); the expanded tile is built with
-// selects.  Latency hiding comes from the resident workgroups.
-//
-// LDS layouts (bank rules: MI355X_MICROARCH.md §LDS), all conflict-free:
-//  * staged input, channel-quad-major Xs[q][px][4] (q = 4 channels of the
-//    16-channel stage): an MFMA B read (pixel j, quad g per lane) hits slot
-//    px mod 16 in every ds_read_b128 lane group, and the stage stores (8
-//    contiguous lanes = 8 consecutive pixels of one quad) hit 8 distinct slots;
-//  * expanded tile [px][EC + 4]: the epilogue's 8-lane store groups are
-//    consecutive pixels (odd pitch in slots); the depthwise reads assign
-//    lanes to (strip, channel quad) so that each ds_read_b128 lane group
-//    reads 4 strips of one output row x 4 channel quads (dw_lane()).
-// ---------------------------------------------------------------------------
-// Depthwise-phase lane assignment.  The four ds_read_b128 lane groups are the
-// lane quads q = (l >> 2) & 7 of even popcount {0,3,5,6} and odd popcount
-// {1,2,4,7}, in each 32-lane half.  EC = 32 (8 channel quads): the parity
-// picks channel quads 0-3 / 4-7 and q >> 1 the strip; EC = 16: the group
-// picks the strip row.  Returns (channel quad, strip within the wave's slice).
-template <int NC4>
-__device__ __forceinline__ void dw_lane(int l, int& c4, int& sl) {
-  const int h = l >> 5, q = (l >> 2) & 7, par = __builtin_popcount(q) & 1, k = q >> 1;
-  if (NC4 == 8) {
-    c4 = (l & 3) + 4 * par;
-    sl = 4 * h + k;
-  } else {
-    c4 = l & 3;
-    sl = 4 * (2 * h + par) + k;
-  }
-}
-template <int K, int S, int TH, int TW, int EC, int ACT, int KP, bool SKIP = false, int NW = 4>
+template <int K, int S, int TH, int TW, int EC, int ACT, int KP, bool SKIP = false, int NW = 4,
+          int SKC = 160>
 __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_args p, const XdDivs dv,
                                                        int nitems) {
   using C = XdCfg<K, S, TH, TW, EC>;
@@ -167,12 +33,14 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
   constexpr int NPF = (C::IPAD * 4 + T - 1) / T;
   constexpr int BPW = (C::NBLK + NW - 1) / NW;  // MFMA blocks per wave
   static_assert(NW % C::NNT == 0, "waves split evenly over the 16-channel tiles");
-  constexpr int NWD = (K * K + 1) * C::NC4;
-  constexpr int SKC = SKIP ? 160 : 4;  // skip-branch taps staged in LDS (Cin <= 160)
+  constexpr int NWD = K * K * C::NC4;  // depthwise taps staged in LDS (bias: registers)
+  // skip-branch taps staged in LDS (SKC >= Cin), none without the skip branch
   __shared__ __attribute__((aligned(16))) float lds[C::LDS];
-  __shared__ float4 wsh[K * K + 1][C::NC4];
-  __shared__ float4 sws[10][SKC / 4];  // 9 taps + bias of the skip dw, channel quads
+  __shared__ float4 wsh[K * K][C::NC4];
+  __shared__ float4 sws[SKIP ? 10 : 1][SKIP ? SKC / 4 : 1];  // 9 taps + bias of the skip dw
   XdItem it;
+  XD_RT(0);
+  XD_T(1);
   if (!xd_item<K, S, TH, TW, EC>(p, blockIdx.x, dv, nitems, it)) return;
   const bool skip = SKIP && it.c0 == 0;
   if (skip) {
@@ -198,10 +66,15 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
   float4 pwd = make_float4(0.f, 0.f, 0.f, 0.f);
   if (t < NWD) {
     const int tp = t / C::NC4, cc = it.c0 + 4 * (t - tp * C::NC4);
-    const float4 w = *reinterpret_cast<const float4*>((tp < K * K ? p.wd + tp * p.E : p.bd) +
-                                                      (cc < p.E ? cc : 0));
+    const float4 w = *reinterpret_cast<const float4*>(p.wd + tp * p.E + (cc < p.E ? cc : 0));
     pwd = cc < p.E ? w : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  // depthwise lane map and its bias (consumed after the expand phase)
+  int c4, sl;
+  dw_lane<C::NC4>(lane, c4, sl);
+  const int chl = 4 * c4;
+  const bool chv = it.c0 + chl < p.E;
+  const float4 bias2 = *reinterpret_cast<const float4*>(p.bd + (chv ? it.c0 + chl : 0));
   // input stage loads through a buffer descriptor: an out-of-range slot gets
   // voffset 0xFFFFFFF0 and reads zeros (host: x < 4 GiB)
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
@@ -255,6 +128,7 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
       if (!ntv) a = (f32x4){0.f, 0.f, 0.f, 0.f};
       asm volatile("" : "+v"(a));
       lds_barrier();
+      if (kc == 0) XD_T(2);
       if (kc + KP < p.Kc) load_stage(kc + KP, pf[s]);
       // fused skip branch (stride 2, first chunk's workgroups): this stage's
       // 16 channels for output pixel t & 63, channel quad t >> 6 (waves 0-3), taps from LDS
@@ -300,6 +174,7 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
       lds_barrier();
     }
   }
+  XD_T(3);
   // expanded tile: act, zero outside the image / on padded channels
   if (XD_SKIP & 2) {
   } else if (interior) {
@@ -308,14 +183,14 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
       const int blk = wave + NW * u;
       if (blk < C::NBLK) {
         const int pb = blk / C::NNT;
-        const int px = pb * 16 + j, ch = 16 * ntw + 4 * g;
-        const bool ok = chok && (pb * 16 + 16 <= C::IPX || px < C::IPX);
+        const int px = pb * 16 + j, q = 4 * ntw + g;
         float4 o;
-        o.x = ok ? xd_act<ACT>(acc[u][0]) : 0.f;
-        o.y = ok ? xd_act<ACT>(acc[u][1]) : 0.f;
-        o.z = ok ? xd_act<ACT>(acc[u][2]) : 0.f;
-        o.w = ok ? xd_act<ACT>(acc[u][3]) : 0.f;
-        *reinterpret_cast<float4*>(lds + px * C::EP + ch) = o;
+        o.x = chok ? xd_act<ACT>(acc[u][0]) : 0.f;
+        o.y = chok ? xd_act<ACT>(acc[u][1]) : 0.f;
+        o.z = chok ? xd_act<ACT>(acc[u][2]) : 0.f;
+        o.w = chok ? xd_act<ACT>(acc[u][3]) : 0.f;
+        if (pb * 16 + 16 <= C::IPX || px < C::IPX)
+          *reinterpret_cast<float4*>(lds + (q * C::QP + px) * 4) = o;
       }
     }
   } else {
@@ -324,32 +199,27 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
       const int blk = wave + NW * u;
       if (blk < C::NBLK) {
         const int pb = blk / C::NNT;
-        const int px = pb * 16 + j, ch = 16 * ntw + 4 * g;
+        const int px = pb * 16 + j, q = 4 * ntw + g;
         const int r = px / C::IW, c = px - r * C::IW;
         const int ih = it.ih0 + r, iw = it.iw0 + c;
-        const bool ok = chok && px < C::IPX && (unsigned)ih < (unsigned)p.H &&
-                        (unsigned)iw < (unsigned)p.W;
+        const bool ok = chok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
         float4 o;
         o.x = ok ? xd_act<ACT>(acc[u][0]) : 0.f;
         o.y = ok ? xd_act<ACT>(acc[u][1]) : 0.f;
         o.z = ok ? xd_act<ACT>(acc[u][2]) : 0.f;
         o.w = ok ? xd_act<ACT>(acc[u][3]) : 0.f;
-        *reinterpret_cast<float4*>(lds + px * C::EP + ch) = o;
+        if (px < C::IPX) *reinterpret_cast<float4*>(lds + (q * C::QP + px) * 4) = o;
       }
     }
   }
   if (t < NWD) wsh[t / C::NC4][t % C::NC4] = pwd;
   __syncthreads();
+  XD_T(4);
 
   // depthwise phase
-  int c4, sl;
-  dw_lane<C::NC4>(lane, c4, sl);
-  const int chl = 4 * c4;
-  const bool chv = it.c0 + chl < p.E;
   constexpr int SPW = 64 / C::NC4;  // strips per wave per pass
   float4 psum = make_float4(0.f, 0.f, 0.f, 0.f);
   if (chv && !(XD_SKIP & 4)) {
-    const float4 bias2 = wsh[K * K][c4];
     float* yb = p.y + (int64_t)it.b * p.y_bs + it.c0 + chl;
 #pragma unroll 1
     for (int pass = 0; pass * T < C::ITEMS; ++pass) {
@@ -363,11 +233,11 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
       for (int o = 0; o < C::PW; ++o) a2[o] = bias2;
 #pragma unroll 1
       for (int kh = 0; kh < K; ++kh) {
-        const float* rowp = lds + ((orow * S + kh) * C::IW + st * C::PW * S) * C::EP + chl;
+        const float* rowp = lds + (c4 * C::QP + (orow * S + kh) * C::IW + st * C::PW * S) * 4;
         float4 row[C::SPAN];
 #pragma unroll
         for (int c = 0; c < C::SPAN; ++c)
-          row[c] = *reinterpret_cast<const float4*>(rowp + c * C::EP);
+          row[c] = *reinterpret_cast<const float4*>(rowp + c * 4);
         float4 wk[K];
 #pragma unroll
         for (int kw = 0; kw < K; ++kw) wk[kw] = wsh[kh * K + kw][c4];
@@ -392,6 +262,7 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
       }
     }
   }
+  XD_T(5);
   if (p.part && !(XD_SKIP & 8)) {
     // sum the lanes holding the same channel quad (dw_lane): EC = 32 -> lane
     // xor 12, 20 (the even-popcount quad permutations) and 32; EC = 16 ->
@@ -430,6 +301,8 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
                                  it.c0 + 4 * t) = sm;
     }
   }
+  XD_T(6);
+  XD_RT(7);
 }
 
 
@@ -1024,19 +897,21 @@ __global__ __launch_bounds__(64 * (XW_NE + 4)) void expdw_ws_kernel(const jabd_e
   if (p.part && nmine >= 1) finalize(nmine - 1);
 }
 
-struct XdTile {
-  int th, tw;
-};
-
 // expand-wave load ring depth (stages in flight) of expdw_ws_kernel
 #ifndef XW_D
 #define XW_D 2
 #endif
 
-static XdTile xd_tile(int k, int s) {
-  (void)k;
-  return s == 1 ? XdTile{16, 16} : XdTile{8, 8};
+// 3x3 stride 1: 14 x 16 outputs (16 x 18 = 288 input pixels, 18 MFMA blocks
+// with no padding; the 32-channel expanded tile is 37 KB, 4 workgroups per
+// CU where 16 x 16 (41.6 KB) allows 3); 5x5 stride 1: 16 x 16; stride 2: 8 x 8
+XdTile xd_tile(int k, int s) {
+  if (s == 1) return k == 3 ? XdTile{14, 16} : XdTile{16, 16};
+  return XdTile{8, 8};
 }
+
+// skip-branch LDS taps: the smallest staged channel count >= Cin
+int xd_skc(int cin) { return cin <= 40 ? 40 : cin <= 112 ? 112 : 160; }
 
 }  // namespace jabd
 
@@ -1099,6 +974,19 @@ static bool xw_enabled() {
   }
   return xw_form ? xw_form == 2 : env == 1;
 }
+// persistent per-chunk form (expdw2.hip): off by default — it halves the
+// VALU instructions per item (SQ counters: 294 vs 586 per wave on the 8x8
+// stride-2 tile) yet runs 5-65% slower per layer: the one-item workgroups'
+// turnover hides latency that a persistent workgroup waits out (DESIGN.md
+// section 4).  JABD_EXPDW2=1 or jabd_expand_dw_select(3) selects it.
+static bool x2_enabled() {
+  static int env = -1;
+  if (env < 0) {
+    const char* e = getenv("JABD_EXPDW2");
+    env = e && e[0] == '1' ? 1 : 0;
+  }
+  return xw_form ? xw_form == 3 : env == 1;
+}
 
 template <int K, int S, int TH, int TW, int EC, int ACT, bool SKIP>
 static int xw_launch(const jabd_expdw_args& a, const XdDivs& dv, int64_t nitems, hipStream_t st) {
@@ -1148,9 +1036,17 @@ static XsPlan xs_plan(int OH, int OW, int k) {
   return pl;
 }
 
+#if XD_TRACE
+extern "C" int jabd_xd_trace_set(void* buf) {
+  unsigned long long* p = static_cast<unsigned long long*>(buf);
+  JABD_HIP(hipMemcpyToSymbol(HIP_SYMBOL(xd_trace_buf), &p, sizeof(p)));
+  return JABD_OK;
+}
+#endif
+
 extern "C" int jabd_expand_dw_select(int32_t form) {
   const int prev = xw_form;
-  xw_form = form == 1 || form == 2 ? form : 0;
+  xw_form = form >= 1 && form <= 3 ? form : 0;
   return prev;
 }
 
@@ -1238,11 +1134,16 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
   JABD_REQUIRE((int64_t)a.B * a.x_bs * 4 < ((int64_t)1 << 32),
                "expand_dw: input must be < 4 GiB (split the batch)");
   const int nw = xd_nw(a, EC);
+  const int skc = xd_skc(a.Cin);
   hipStream_t st = as_stream(stream);
   const XdDivs dv{make_fastdiv((uint32_t)nch), make_fastdiv((uint32_t)tiles_img),
                   make_fastdiv((uint32_t)tiles_w)};
   JABD_REQUIRE((int64_t)a.B * a.x_bs * 4 < ((int64_t)1 << 32) - 16,
                "expand_dw: input must be < 4 GiB (buffer-descriptor offsets)");
+  if (x2_enabled() && !xw_enabled()) {
+    const int e = expdw2_dispatch(a, dv, nitems, EC, nch, st);
+    if (e != JABD_EINVAL) return e;   // else: no persistent instantiation, expdw1 below
+  }
   if (xw_enabled()) {
 #define XW_ACT(K_, S_, TH_, TW_, EC_, SK_)                                         \
   {                                                                              \
@@ -1255,7 +1156,7 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
     if (S_ == 2 && a.sy) XW_ACT(K_, S_, TH_, TW_, EC_, true)    \
     XW_ACT(K_, S_, TH_, TW_, EC_, false)                        \
   }
-    XW_CASE(3, 1, 16, 16, 16) XW_CASE(3, 1, 16, 16, 32)
+    XW_CASE(3, 1, 14, 16, 16) XW_CASE(3, 1, 14, 16, 32)
     XW_CASE(5, 1, 16, 16, 16) XW_CASE(5, 1, 16, 16, 32)
     XW_CASE(3, 2, 8, 8, 16) XW_CASE(3, 2, 8, 8, 32)
     XW_CASE(5, 2, 8, 8, 16) XW_CASE(5, 2, 8, 8, 32)
@@ -1266,6 +1167,12 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
   do {                                                                                        \
     if (S_ == 2 && a.sy && nw == 8)                                                           \
       expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1, true, 8><<<(unsigned)nitems, 512, 0, st>>>( \
+          a, dv, (int)nitems);                                                                \
+    else if (S_ == 2 && a.sy && skc == 40)                                                    \
+      expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1, true, 4, 40><<<(unsigned)nitems, 256, 0, st>>>( \
+          a, dv, (int)nitems);                                                                \
+    else if (S_ == 2 && a.sy && skc == 112)                                                   \
+      expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1, true, 4, 112><<<(unsigned)nitems, 256, 0, st>>>( \
           a, dv, (int)nitems);                                                                \
     else if (S_ == 2 && a.sy)                                                                 \
       expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1, true><<<(unsigned)nitems, 256, 0, st>>>( \
@@ -1293,7 +1200,7 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
       XD_LAUNCH(K_, S_, TH_, TW_, EC_, ACT_NONE);                         \
     return check_launch("expand_dw");                                     \
   }
-  XD_CASE(3, 1, 16, 16, 16) XD_CASE(3, 1, 16, 16, 32)
+  XD_CASE(3, 1, 14, 16, 16) XD_CASE(3, 1, 14, 16, 32)
   XD_CASE(5, 1, 16, 16, 16) XD_CASE(5, 1, 16, 16, 32)
   XD_CASE(3, 2, 8, 8, 16) XD_CASE(3, 2, 8, 8, 32)
   XD_CASE(5, 2, 8, 8, 16) XD_CASE(5, 2, 8, 8, 32)

@@ -9,17 +9,23 @@
 //   radix_hist     one pass over the keys: the histogram of every digit
 //                  position at once (LDS counters, one global add per bin)
 //   radix_plan     per pass: global digit bases (exclusive prefix over the
-//                  256 bins) and the skip flag — a pass whose keys all share
-//                  one digit is a copy (grid keys: the high cell bits)
+//                  256 bins), whether it runs (a pass whose keys all share one
+//                  digit is skipped) and which buffers it reads and writes, so
+//                  that the last pass that runs writes the output (the input
+//                  is never written; if no pass runs, the last one copies)
 //   per pass       radix_count  per 4096-key tile: digit counts -> cnt[d][tile]
 //                  radix_scan   one workgroup per digit: tile offsets
 //                               off[d][tile] = base[d] + sum of cnt[d][< tile]
 //                  radix_scatter per tile: the stable rank of each key among
 //                               the tile's keys of its digit, from wave ballots
 //                               (8 ballots give a lane its peers of the same
-//                               digit; lanes below it in the wave, then the
-//                               wave's earlier rounds, then the earlier waves)
-//                               — dst[off[d][tile] + rank] = key (+ value)
+//                               digit; lanes below it, the wave's earlier
+//                               rounds, then the earlier waves) —
+//                               dst[off[d][tile] + rank] = key (+ value).
+//                  A skipped pass exits at once in all three kernels.
+//                  (A one-launch pass with a decoupled look-back over the
+//                  tiles' published counts measured 2x slower per pass here:
+//                  the look-back is a chain of dependent cross-XCD loads.)
 // Keys equal to ~0 (the grid producer's "not binned") may be excluded from
 // the skip test of every pass but the last (skip_ones): such a key has digit
 // 255 everywhere, and the last pass, never skipped while they exist, puts
@@ -60,61 +66,6 @@ __global__ __launch_bounds__(kRT) void radix_hist(const uint64_t* __restrict__ k
   }
 }
 
-// plan[p]: [0..255] exclusive digit bases, [256] skip flag (one workgroup)
-__global__ __launch_bounds__(256) void radix_plan(const int* __restrict__ ghist, int npass,
-                                                  int* __restrict__ plan) {
-  __shared__ int s[256], mx[256], sm[256];
-  const int t = threadIdx.x;
-  for (int p = 0; p < npass; ++p) {
-    const int v = ghist[p * 256 + t];
-    s[t] = v;
-    mx[t] = v;
-    sm[t] = v;
-    __syncthreads();
-    for (int h = 128; h >= 1; h >>= 1) {
-      if (t < h) {
-        mx[t] = max(mx[t], mx[t + h]);
-        sm[t] += sm[t + h];
-      }
-      __syncthreads();
-    }
-    // exclusive prefix of s (Hillis-Steele in LDS)
-    for (int off = 1; off < 256; off <<= 1) {
-      const int a = t >= off ? s[t - off] : 0;
-      __syncthreads();
-      s[t] += a;
-      __syncthreads();
-    }
-    plan[p * 257 + t] = s[t] - v;
-    if (t == 0) plan[p * 257 + 256] = mx[0] == sm[0] ? 1 : 0;
-    __syncthreads();
-  }
-}
-
-__global__ __launch_bounds__(kRT) void radix_count(const uint64_t* __restrict__ k, int64_t n,
-                                                   int shift, const int* __restrict__ plan,
-                                                   int ntiles, int* __restrict__ cnt) {
-  if (plan[256]) return;  // skipped pass
-  __shared__ int h[256];
-  const int t = threadIdx.x;
-  h[t] = 0;
-  __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kTile;
-  uint64_t v[kRPer];
-#pragma unroll
-  for (int i = 0; i < kRPer; ++i) {
-    const int64_t idx = base + (int64_t)i * kRT + t;
-    v[i] = idx < n ? k[idx] : 0ull;
-  }
-#pragma unroll
-  for (int i = 0; i < kRPer; ++i) {
-    const int64_t idx = base + (int64_t)i * kRT + t;
-    if (idx < n) atomicAdd(&h[(int)((v[i] >> shift) & 255u)], 1);
-  }
-  __syncthreads();
-  cnt[(int64_t)t * ntiles + blockIdx.x] = h[t];
-}
-
 // inclusive wave scan (Hillis-Steele over the 64 lanes)
 __device__ __forceinline__ int wave_incl_scan(int x) {
   const int l = threadIdx.x & 63;
@@ -146,12 +97,80 @@ __device__ __forceinline__ int block_excl_scan(int x, int* tot) {
   return pre + inc - x;
 }
 
-// one workgroup per digit: off[d][tile] = base[d] + exclusive prefix of
-// cnt[d][.] along the tiles
+// plan[p * kPlan]: [0..255] exclusive digit bases, [256] mode (0 skipped,
+// 1 sorts, 2 copies), [257] source (0 input, 1 output, 2 alternate), [258]
+// destination (1 output, 2 alternate).  One workgroup.
+constexpr int kPlan = 260;
+__global__ __launch_bounds__(kRT) void radix_plan(const int* __restrict__ ghist, int npass,
+                                                  int* __restrict__ plan) {
+  __shared__ int run[kMaxPass];
+  const int t = threadIdx.x;
+  for (int p = 0; p < npass; ++p) {
+    const int v = ghist[p * 256 + t];
+    int tot;
+    const int ex = block_excl_scan(v, &tot);
+    plan[p * kPlan + t] = ex;
+    // one bin holds every key counted for this pass: nothing to reorder
+    const int full = __syncthreads_or(v == tot && tot > 0);
+    if (t == 0) run[p] = full ? 0 : 1;
+    __syncthreads();
+  }
+  if (t == 0) {
+    int m = 0;
+    for (int p = 0; p < npass; ++p) m += run[p];
+    if (m == 0) run[npass - 1] = 2;   // nothing to sort: the last pass copies
+    // the passes that run alternate buffers backwards from the output
+    int src = 0, left = m > 0 ? m : 1;
+    for (int p = 0; p < npass; ++p) {
+      plan[p * kPlan + 256] = run[p];
+      if (!run[p]) continue;
+      const int dst = ((left - 1) & 1) ? 2 : 1;
+      plan[p * kPlan + 257] = src;
+      plan[p * kPlan + 258] = dst;
+      src = dst;
+      --left;
+    }
+  }
+}
+
+__device__ __forceinline__ const uint64_t* rsel(int id, const uint64_t* a, const uint64_t* b,
+                                                 const uint64_t* c) {
+  return id == 0 ? a : (id == 1 ? b : c);
+}
+
+// per 4096-key tile: digit counts -> cnt[d][tile]
+__global__ __launch_bounds__(kRT) void radix_count(const uint64_t* __restrict__ kin,
+                                                   const uint64_t* __restrict__ kout,
+                                                   const uint64_t* __restrict__ kalt, int64_t n,
+                                                   int shift, const int* __restrict__ plan,
+                                                   int ntiles, int* __restrict__ cnt) {
+  if (plan[256] != 1) return;  // skipped or copy pass
+  const uint64_t* k = rsel(plan[257], kin, kout, kalt);
+  __shared__ int h[256];
+  const int t = threadIdx.x;
+  h[t] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  uint64_t v[kRPer];
+#pragma unroll
+  for (int i = 0; i < kRPer; ++i) {
+    const int64_t idx = base + (int64_t)i * kRT + t;
+    v[i] = idx < n ? k[idx] : 0ull;
+  }
+#pragma unroll
+  for (int i = 0; i < kRPer; ++i) {
+    const int64_t idx = base + (int64_t)i * kRT + t;
+    if (idx < n) atomicAdd(&h[(int)((v[i] >> shift) & 255u)], 1);
+  }
+  __syncthreads();
+  cnt[(int64_t)t * ntiles + blockIdx.x] = h[t];
+}
+
+// one workgroup per digit: off[d][tile] = base[d] + sum of cnt[d][< tile]
 __global__ __launch_bounds__(kRT) void radix_scan(const int* __restrict__ cnt,
                                                   const int* __restrict__ plan, int ntiles,
                                                   int* __restrict__ off) {
-  if (plan[256]) return;
+  if (plan[256] != 1) return;
   const int d = blockIdx.x;
   int carry = plan[d];
   const int* c = cnt + (int64_t)d * ntiles;
@@ -166,14 +185,23 @@ __global__ __launch_bounds__(kRT) void radix_scan(const int* __restrict__ cnt,
   }
 }
 
+// per tile: stable rank of each key among the tile's keys of its digit (wave
+// ballots), dst[off[d][tile] + rank] = key (+ value); a copy pass copies
 template <bool VALS>
 __global__ __launch_bounds__(kRT) void radix_scatter(
-    const uint64_t* __restrict__ ks, const int* __restrict__ vs, int64_t n, int shift,
-    const int* __restrict__ plan, const int* __restrict__ off, int ntiles,
-    uint64_t* __restrict__ kd, int* __restrict__ vd) {
+    const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout, uint64_t* __restrict__ kalt,
+    const int* __restrict__ vin, int* __restrict__ vout, int* __restrict__ valt, int64_t n,
+    int shift, const int* __restrict__ plan, const int* __restrict__ off, int ntiles) {
+  const int mode = plan[256];
+  if (mode == 0) return;
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  const int sid = plan[257], did = plan[258];
+  const uint64_t* ks = rsel(sid, kin, kout, kalt);
+  const int* vs = sid == 0 ? vin : (sid == 1 ? vout : valt);
+  uint64_t* kd = did == 1 ? kout : kalt;
+  int* vd = did == 1 ? vout : valt;
   const int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)w * kWaveKeys;
-  if (plan[256]) {  // every key has the same digit: a copy
+  if (mode == 2) {
     for (int r = 0; r < kWaveKeys / 64; ++r) {
       const int64_t idx = base + r * 64 + l;
       if (idx < n) {
@@ -183,7 +211,7 @@ __global__ __launch_bounds__(kRT) void radix_scatter(
     }
     return;
   }
-  __shared__ int wc[kRWaves][256];   // running count per (wave, digit)
+  __shared__ int wc[kRWaves][256];   // running count per (wave, digit), then wave prefix
   __shared__ int tb[256];            // this tile's offset per digit
 #pragma unroll
   for (int i = 0; i < kRWaves; ++i) wc[i][t] = 0;
@@ -219,7 +247,6 @@ __global__ __launch_bounds__(kRT) void radix_scatter(
     __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
-  // earlier waves' counts of each digit
   {
     int s = 0;
 #pragma unroll
@@ -292,7 +319,7 @@ template <typename A>
 static void carve_radix(A& a, int64_t n, bool vals, RadixWs* w) {
   const int nt = radix_ntiles(n);
   auto* gh = a.template take<int>(kMaxPass * 256);
-  auto* pl = a.template take<int>(kMaxPass * 257);
+  auto* pl = a.template take<int>(kMaxPass * kPlan);
   auto* cn = a.template take<int>((size_t)256 * nt);
   auto* of = a.template take<int>((size_t)256 * nt);
   auto* ka = a.template take<uint64_t>((size_t)n);
@@ -317,7 +344,7 @@ int radix_sort64(const uint64_t* kin, uint64_t* kout, const int* vin, int* vout,
                  int lo, int npass, bool skip_ones, void* ws, size_t ws_bytes, hipStream_t st) {
   JABD_REQUIRE(npass >= 1 && npass <= kMaxPass && lo >= 0 && lo + 8 * npass <= 64,
                "radix_sort64: bits [%d, %d)", lo, lo + 8 * npass);
-  JABD_REQUIRE(n >= 0 && n < ((int64_t)1 << 31), "radix_sort64: n = %lld", (long long)n);
+  JABD_REQUIRE(n >= 0 && n < ((int64_t)1 << 30), "radix_sort64: n = %lld", (long long)n);
   JABD_REQUIRE((vin == nullptr) == (vout == nullptr), "radix_sort64: values in and out");
   if (n == 0) return JABD_OK;
   const bool vals = vin != nullptr;
@@ -328,26 +355,20 @@ int radix_sort64(const uint64_t* kin, uint64_t* kout, const int* vin, int* vout,
   const int nt = radix_ntiles(n);
   JABD_HIP(hipMemsetAsync(w.ghist, 0, sizeof(int) * kMaxPass * 256, st));
   radix_hist<<<nt, kRT, 0, st>>>(kin, n, lo, npass, skip_ones ? 1 : 0, w.ghist);
-  radix_plan<<<1, 256, 0, st>>>(w.ghist, npass, w.plan);
+  radix_plan<<<1, kRT, 0, st>>>(w.ghist, npass, w.plan);
   if (int e = check_launch("radix_hist/plan")) return e;
-  // ping-pong so that the last pass writes kout: pass p reads src_p, writes dst_p
-  const uint64_t* ks = kin;
-  const int* vs = vin;
   for (int p = 0; p < npass; ++p) {
-    const bool to_out = ((npass - 1 - p) & 1) == 0;
-    uint64_t* kd = to_out ? kout : w.kalt;
-    int* vd = to_out ? vout : w.valt;
-    const int* pl = w.plan + p * 257;
+    const int* pl = w.plan + p * kPlan;
     const int sh = lo + 8 * p;
-    radix_count<<<nt, kRT, 0, st>>>(ks, n, sh, pl, nt, w.cnt);
+    radix_count<<<nt, kRT, 0, st>>>(kin, kout, w.kalt, n, sh, pl, nt, w.cnt);
     radix_scan<<<256, kRT, 0, st>>>(w.cnt, pl, nt, w.off);
     if (vals)
-      radix_scatter<true><<<nt, kRT, 0, st>>>(ks, vs, n, sh, pl, w.off, nt, kd, vd);
+      radix_scatter<true><<<nt, kRT, 0, st>>>(kin, kout, w.kalt, vin, vout, w.valt, n, sh, pl,
+                                               w.off, nt);
     else
-      radix_scatter<false><<<nt, kRT, 0, st>>>(ks, nullptr, n, sh, pl, w.off, nt, kd, nullptr);
+      radix_scatter<false><<<nt, kRT, 0, st>>>(kin, kout, w.kalt, nullptr, nullptr, nullptr, n,
+                                                sh, pl, w.off, nt);
     if (int e = check_launch("radix pass")) return e;
-    ks = kd;
-    vs = vd;
   }
   return JABD_OK;
 }

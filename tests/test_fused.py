@@ -214,9 +214,10 @@ def test_eca_gates_multi_equal_per_tensor(cuda):
 @pytest.mark.parametrize("bhw", [(4, 96, 80), (3, 37, 29), (1, 1, 2)])
 def test_expand_dw_forms_bit_identical(cuda, spec, bhw):
     """The wave-specialised persistent kernel (expand waves feeding
-    double-buffered tiles to depthwise waves) and the one-item-per-workgroup
-    kernel compute every output with the same operation sequence: y, the ECA
-    partials and the fused skip branch must be bit-identical.  (4, 96, 80)
+    double-buffered tiles to depthwise waves), the persistent per-chunk kernel
+    (expdw2.hip, the default) and the one-item-per-workgroup kernel compute
+    every output with the same operation sequence: y, the ECA partials and
+    the fused skip branch must be bit-identical.  (4, 96, 80)
     gives several items per persistent workgroup (the expanded-buffer and
     tap/partial rings wrap), (1, 1, 2) a grid smaller than the CU count."""
     from jabd_amd import functional as F
@@ -239,7 +240,7 @@ def test_expand_dw_forms_bit_identical(cuda, spec, bhw):
     x = torch.randn(B, H, W, cin, generator=g).to(cuda)
     outs = []
     try:
-        for form in (1, 2):
+        for form in (1, 2, 3):
             lib().jabd_expand_dw_select(form)
             if s == 2:
                 outs.append(F.expand_dw(x, pk, dw_w, dw_b, k, s, act=act, skip=(skw, skb)))
@@ -248,5 +249,6 @@ def test_expand_dw_forms_bit_identical(cuda, spec, bhw):
     finally:
         lib().jabd_expand_dw_select(0)
     torch.cuda.synchronize()
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            assert torch.equal(a, b)
