@@ -583,6 +583,26 @@ def pmc_traffic():
         return json.load(f)
 
 
+def step_roofline(name, step_ms, workload):
+    """Training-step roofline: the sum over the step's libjabd launches of
+    max(algorithmic FLOPs / fp32 MFMA peak, algorithmic bytes / HBM peak),
+    measured per launch by tools/train_roofline.py (committed as
+    profiles/<round>/<name>.json), divided by this run's step time."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", name + ".json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        r = json.load(f)
+    if r.get("workload") != workload:
+        return None
+    return {"bound": "per launch max(FLOP / %.1f TFLOP/s, bytes / %.0f TB/s), summed" %
+                     (r["peak_tflops"], r["peak_tbs"]),
+            "roof_ms": r["roof_ms"], "step_ms": step_ms, "frac": r["roof_ms"] / step_ms,
+            "launches": r["calls"], "workload": r["workload"],
+            "source": os.path.relpath(files[-1], ROOT)}
+
+
 def host_cores():
     """CPU budget of the CPU baseline: BASELINE.md asks for
     torch.set_num_threads(<physical cores>); the threads used are
@@ -825,6 +845,11 @@ def main():
             tr["C3_r50"] = train_bench("r50", args.r50_batch, args.size, max(2, args.train_steps // 2),
                                        2, device, None, rank, conv_roofline_steps=1)
             extra["roofline_r50"] = tr["C3_r50"].get("conv_roofline")
+        for k, fn, kind, b in (("C4_mnv3", "c4_step_roofline", "mnv3", args.batch),
+                               ("C3_r50", "c3_step_roofline", "r50", args.r50_batch)):
+            if k in tr:
+                tr[k]["roofline"] = step_roofline(
+                    fn, tr[k]["ms_per_step"], f"{kind} training bs{b} {args.size}x{args.size}")
         extra["train"] = tr
     if rank == 0:
         extra["forward_gflop_per_image"] = forward_flops(model, args.size, 1) / 1e9
