@@ -724,6 +724,17 @@ int jabd_adam_step_f32(const void* rows, const int64_t* chunks, int64_t nchunks,
 int jabd_maxpool_bwd_f32(const float* x, const float* dy, int32_t B, int32_t H, int32_t W,
                          int32_t C, int32_t k, int32_t stride, int32_t pad, float* dx,
                          jabd_stream_t stream);
+/* Training form (nets/resnet_pytorch_r.py:174-178 maxpool under autograd):
+ * the forward also writes idx uint8 [B, OH, OW, C], each output's argmax as
+ * its window position kh * k + kw (first maximum, NaN taking the place);
+ * the backward gathers idx + dy (bit-identical to jabd_maxpool_bwd_f32).
+ * C % 4 == 0, 16-byte aligned tensors. */
+int jabd_maxpool_idx_nhwc_f32(const float* x, int32_t B, int32_t H, int32_t W, int32_t C,
+                              int32_t k, int32_t stride, int32_t pad, float* y, uint8_t* idx,
+                              jabd_stream_t stream);
+int jabd_maxpool_bwd_idx_f32(const uint8_t* idx, const float* dy, int32_t B, int32_t H, int32_t W,
+                             int32_t C, int32_t k, int32_t stride, int32_t pad, float* dx,
+                             jabd_stream_t stream);
 /* CSAF/NLM backward (nets/retinaface_r.py:124-152).  attn: from dOut (grad
  * of lateral + NLM(x)) -> dq [M][4], dx_up [M][C] (= dOut + Wq^T dq), and
  * dK/dV [B][S][4] (part: [B][ceil(h*w/64)][S][8] scratch).  proj: PSP

@@ -1529,6 +1529,86 @@ __global__ __launch_bounds__(256) void maxpool_bwd4_kernel(const float* __restri
   reinterpret_cast<float4*>(dx)[i] = make_float4(acc[0], acc[1], acc[2], acc[3]);
 }
 
+// Training form of the stem max-pool (F.max_pool2d(3, 2, 1) in the R50 body,
+// nets/resnet_pytorch_r.py:174-178): the forward also keeps each output's
+// argmax as its window position (kh * k + kw, uint8 per channel; the first
+// maximum in scan order, a NaN taking the place — the rule the
+// recomputing backward above uses), so the backward gathers idx + dy
+// instead of re-reading and re-reducing every window that contains a pixel
+// (which ran from L2 at ~1.2 TB/s).  One thread per (output pixel, 4 channels).
+__global__ __launch_bounds__(256) void maxpool_idx4_kernel(const float* __restrict__ x, int H, int W,
+                                                           int C4, int OH, int OW, int k, int s,
+                                                           int pad, int total,
+                                                           float* __restrict__ y,
+                                                           uchar4* __restrict__ idx) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c4 = i % C4;
+  int r = i / C4;
+  const int ow = r % OW;
+  r /= OW;
+  const int oh = r % OH;
+  const int b = r / OH;
+  const float4* xb = reinterpret_cast<const float4*>(x) + (int64_t)b * H * W * C4 + c4;
+  float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  float best[4] = {0.f, 0.f, 0.f, 0.f};
+  int arg[4] = {-1, -1, -1, -1};
+  for (int a = 0; a < k; ++a) {
+    const int ih = oh * s - pad + a;
+    if (ih < 0 || ih >= H) continue;
+    for (int q = 0; q < k; ++q) {
+      const int iw = ow * s - pad + q;
+      if (iw < 0 || iw >= W) continue;
+      const float4 v4 = xb[(int64_t)(ih * W + iw) * C4];
+      const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        m[e] = (v[e] > m[e] || v[e] != v[e]) ? v[e] : m[e];   // the eval maxpool_kernel's value
+        if (arg[e] < 0 || v[e] > best[e] || v[e] != v[e]) {
+          best[e] = v[e];
+          arg[e] = a * k + q;
+        }
+      }
+    }
+  }
+  reinterpret_cast<float4*>(y)[i] = make_float4(m[0], m[1], m[2], m[3]);
+  idx[i] = make_uchar4((unsigned char)arg[0], (unsigned char)arg[1], (unsigned char)arg[2],
+                       (unsigned char)arg[3]);
+}
+
+// dx[pixel] = sum over the windows holding it (oh, then ow ascending — the
+// recomputing kernel's order) of dy where the window's argmax is this pixel
+__global__ __launch_bounds__(256) void maxpool_bwd_idx4_kernel(const uchar4* __restrict__ idx,
+                                                               const float* __restrict__ dy, int H,
+                                                               int W, int C4, int OH, int OW, int k,
+                                                               int s, int pad, int total,
+                                                               float* __restrict__ dx) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c4 = i % C4;
+  int r = i / C4;
+  const int iw = r % W;
+  r /= W;
+  const int ih = r % H;
+  const int b = r / H;
+  const int64_t ob = (int64_t)b * OH * OW * C4 + c4;
+  const int oh0 = max(0, (ih + pad - k + s) / s), oh1 = min(OH - 1, (ih + pad) / s);
+  const int ow0 = max(0, (iw + pad - k + s) / s), ow1 = min(OW - 1, (iw + pad) / s);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int oh = oh0; oh <= oh1; ++oh)
+    for (int ow = ow0; ow <= ow1; ++ow) {
+      const int me = (ih - (oh * s - pad)) * k + (iw - (ow * s - pad));
+      const int64_t o = ob + (int64_t)(oh * OW + ow) * C4;
+      const uchar4 a = idx[o];
+      const float4 g = reinterpret_cast<const float4*>(dy)[o];
+      if (a.x == me) acc[0] += g.x;
+      if (a.y == me) acc[1] += g.y;
+      if (a.z == me) acc[2] += g.z;
+      if (a.w == me) acc[3] += g.w;
+    }
+  reinterpret_cast<float4*>(dx)[i] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+}
+
 __global__ void maxpool_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy, int H,
                                    int W, int C, int OH, int OW, int k, int s, int pad,
                                    int64_t total, float* __restrict__ dx) {
@@ -2138,6 +2218,33 @@ extern "C" int jabd_heads_gather_f32(const float* gloc, const float* gconf, cons
   dim3 g((unsigned)cdiv(HW, 256), (unsigned)B);
   heads_gather_kernel<<<g, 256, 0, as_stream(stream)>>>(gloc, gconf, glandm, A, a_off, HW, dout);
   return check_launch("heads_gather");
+}
+
+extern "C" int jabd_maxpool_idx_nhwc_f32(const float* x, int32_t B, int32_t H, int32_t W,
+                                         int32_t C, int32_t k, int32_t stride, int32_t pad,
+                                         float* y, uint8_t* idx, jabd_stream_t stream) {
+  JABD_REQUIRE(x && y && idx && B > 0 && H > 0 && W > 0 && C > 0 && C % 4 == 0 && k > 0 &&
+                   k * k <= 255 && stride > 0,
+               "maxpool_idx: bad args");
+  const int OH = (H + 2 * pad - k) / stride + 1, OW = (W + 2 * pad - k) / stride + 1;
+  const int64_t t4 = (int64_t)B * OH * OW * (C / 4);
+  JABD_REQUIRE(t4 < ((int64_t)1 << 31) && (int64_t)B * H * W * (C / 4) < ((int64_t)1 << 31),
+               "maxpool_idx: too large");
+  maxpool_idx4_kernel<<<(unsigned)cdiv(t4, 256), 256, 0, as_stream(stream)>>>(
+      x, H, W, C / 4, OH, OW, k, stride, pad, (int)t4, y, reinterpret_cast<uchar4*>(idx));
+  return check_launch("maxpool_idx");
+}
+
+extern "C" int jabd_maxpool_bwd_idx_f32(const uint8_t* idx, const float* dy, int32_t B, int32_t H,
+                                        int32_t W, int32_t C, int32_t k, int32_t stride,
+                                        int32_t pad, float* dx, jabd_stream_t stream) {
+  JABD_REQUIRE(idx && dy && dx && C % 4 == 0, "maxpool_bwd_idx: bad args");
+  const int OH = (H + 2 * pad - k) / stride + 1, OW = (W + 2 * pad - k) / stride + 1;
+  const int64_t t4 = (int64_t)B * H * W * (C / 4);
+  JABD_REQUIRE(t4 < ((int64_t)1 << 31), "maxpool_bwd_idx: too large");
+  maxpool_bwd_idx4_kernel<<<(unsigned)cdiv(t4, 256), 256, 0, as_stream(stream)>>>(
+      reinterpret_cast<const uchar4*>(idx), dy, H, W, C / 4, OH, OW, k, stride, pad, (int)t4, dx);
+  return check_launch("maxpool_bwd_idx");
 }
 
 extern "C" int jabd_maxpool_bwd_f32(const float* x, const float* dy, int32_t B, int32_t H,

@@ -246,6 +246,10 @@ SIGNATURES = {
     "jabd_upsample_nearest_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp],
     "jabd_maxpool_bwd_f32": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp,
                              c_vp],
+    "jabd_maxpool_idx_nhwc_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp,
+                                  c_vp, c_vp],
+    "jabd_maxpool_bwd_idx_f32": [c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
+                                 c_vp, c_vp],
     "jabd_adam_num_chunks": [c_vp, c_i64],
     "jabd_adam_fill_chunks": [c_vp, c_i64, c_vp],
     "jabd_adam_step_f32": [c_vp, c_vp, c_i64, c_f64, c_f64, c_f64, c_f64, c_f64, c_f64, c_f64,

@@ -655,20 +655,30 @@ class HeadsFn(torch.autograd.Function):
 
 
 class MaxPoolFn(torch.autograd.Function):
+    """3x3/2/1 max-pool of the R50 stem; the forward keeps the argmax window
+    positions (uint8) so the backward is a gather of idx + dy."""
+
     @staticmethod
     def forward(ctx, x):
-        y = F.maxpool(x, 3, 2, 1)
+        B, H, W, C = x.shape
+        OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        x = x.contiguous()
+        y = torch.empty((B, OH, OW, C), dtype=torch.float32, device=x.device)
+        idx = torch.empty((B, OH, OW, C), dtype=torch.uint8, device=x.device)
+        call("jabd_maxpool_idx_nhwc_f32", x.data_ptr(), B, H, W, C, 3, 2, 1, y.data_ptr(),
+             idx.data_ptr(), _st())
         F.tap("maxpool", x)
-        ctx.save_for_backward(x)
+        ctx.save_for_backward(idx)
+        ctx.shape = (B, H, W, C)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        (x,) = ctx.saved_tensors
+        (idx,) = ctx.saved_tensors
         dy = dy.contiguous()
-        B, H, W, C = x.shape
-        dx = torch.empty_like(x)
-        call("jabd_maxpool_bwd_f32", x.data_ptr(), dy.data_ptr(), B, H, W, C, 3, 2, 1,
+        B, H, W, C = ctx.shape
+        dx = torch.empty((B, H, W, C), dtype=torch.float32, device=dy.device)
+        call("jabd_maxpool_bwd_idx_f32", idx.data_ptr(), dy.data_ptr(), B, H, W, C, 3, 2, 1,
              dx.data_ptr(), _st())
         return dx
 
@@ -1260,7 +1270,94 @@ def _mnv3_block(blk, s):
     return bn_act(p, blk.bn3, act, res=res)
 
 
+class R50BlockFn(torch.autograd.Function):
+    """One torchvision Bottleneck (nets/resnet_pytorch_r.py:122-143) forward
+    and backward as a single autograd node, so the gradient reaching the
+    block input from its two consumers (conv1 and the identity / downsample
+    branch) is summed in the epilogue of conv1's data-gradient GEMM instead
+    of by an autograd add over the block input (an ATen elementwise kernel
+    per block, ~15 ms per C3 step).  Inputs: the block, x, then the
+    parameters in _r50_params order."""
+
+    @staticmethod
+    def forward(ctx, blk, x, *params):
+        stride = blk.stride
+        B, H, W, _ = x.shape
+        t1p = _conv_fwd(x, blk.conv1.weight)
+        t1, st1 = _bn_fwd(t1p, blk.bn1, "relu")
+        t2p = _conv_fwd(t1, blk.conv2.weight, None, stride, 1)
+        t2, st2 = _bn_fwd(t2p, blk.bn2, "relu")
+        t3p = _conv_fwd(t2, blk.conv3.weight)
+        ds = blk.downsample
+        saved = ()
+        if ds is not None:
+            ip = _conv_fwd(x, ds[0].weight, None, stride, 0)
+            idn, sts = _bn_fwd(ip, ds[1], "none")
+            saved = (ip,)
+            ctx.sts = sts
+        else:
+            idn = x
+        out, st3 = _bn_fwd(t3p, blk.bn3, "relu", res=idn)
+        ctx.blk, ctx.st = blk, (st1, st2, st3)
+        ctx.hw = (H, W)
+        ctx.save_for_backward(x, t1p, t1, t2p, t2, t3p, idn, *saved)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        blk = ctx.blk
+        stride = blk.stride
+        H, W = ctx.hw
+        x, t1p, t1, t2p, t2, t3p, idn, *sv = ctx.saved_tensors
+        st1, st2, st3 = ctx.st
+        dout = dout.contiguous()
+        dp3, dg3, db3, dres = _bn_bwd(dout, t3p, st3, "relu", res=idn, want_dres=True)
+        dW3 = _wgrad(t2, dp3, blk.conv3.weight, 1, 0)
+        dt2 = _dgrad(dp3, blk.conv3.weight, 1, 0, t2.shape[1], t2.shape[2])
+        dp2, dg2, db2, _ = _bn_bwd(dt2, t2p, st2, "relu")
+        dW2 = _wgrad(t1, dp2, blk.conv2.weight, stride, 1)
+        dt1 = _dgrad(dp2, blk.conv2.weight, stride, 1, H, W)
+        dp1, dg1, db1, _ = _bn_bwd(dt1, t1p, st1, "relu")
+        dW1 = _wgrad(x, dp1, blk.conv1.weight, 1, 0)
+        grads = (dW1, dg1, db1, dW2, dg2, db2, dW3, dg3, db3)
+        if blk.downsample is not None:
+            (ip,) = sv
+            ds = blk.downsample
+            dip, dgs, dbs, _ = _bn_bwd(dres, ip, ctx.sts, "none")
+            dWs = _wgrad(x, dip, ds[0].weight, stride, 0)
+            ds_skip = _dgrad(dip, ds[0].weight, stride, 0, H, W)
+            grads += (dWs, dgs, dbs)
+        else:
+            ds_skip = dres
+        dx = _dgrad_1x1_res(dp1, blk.conv1.weight, ds_skip)
+        return (None, dx) + grads
+
+
+def _r50_params(blk):
+    ps = [blk.conv1.weight, blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight,
+          blk.bn2.bias, blk.conv3.weight, blk.bn3.weight, blk.bn3.bias]
+    if blk.downsample is not None:
+        ps += [blk.downsample[0].weight, blk.downsample[1].weight, blk.downsample[1].bias]
+    return ps
+
+
+def _r50_fused_ok(blk, x):
+    convs = [blk.conv1, blk.conv2, blk.conv3] + ([blk.downsample[0]] if blk.downsample is not None
+                                                 else [])
+    bns = [blk.bn1, blk.bn2, blk.bn3] + ([blk.downsample[1]] if blk.downsample is not None
+                                         else [])
+    return (R50_FUSED and x.shape[3] % 4 == 0 and blk.conv1.kernel_size == (1, 1) and
+            blk.conv1.stride == (1, 1) and all(c.bias is None for c in convs) and
+            all(b.weight.shape[0] % 4 == 0 and b.momentum is not None for b in bns))
+
+
+# JABD_R50_FUSED=0: the bottleneck as per-op autograd nodes (A/B)
+R50_FUSED = __import__("os").environ.get("JABD_R50_FUSED", "1") != "0"
+
+
 def _r50_block(blk, x):
+    if _r50_fused_ok(blk, x):
+        return R50BlockFn.apply(blk, x.contiguous(), *_r50_params(blk))
     t = bn_act(conv(x, blk.conv1), blk.bn1, "relu")
     t = bn_act(conv(t, blk.conv2, blk.stride, 1), blk.bn2, "relu")
     t = conv(t, blk.conv3)

@@ -599,3 +599,42 @@ def test_dw_bnin_kink_masks(cuda, recompute, monkeypatch):
     assert bad.size == 0, f"{len(bad)} elements: forward region != backward mask, e.g. {bad[:4]}"
     # each channel's window straddles the kink, so the check is not vacuous
     assert fwd.any(0).all() and (~fwd).any(0).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bhwc", [(2, 17, 23, 64), (1, 64, 64, 8), (3, 9, 8, 12)])
+def test_maxpool_idx_forms_bit_identical(cuda, bhwc):
+    """The training max-pool (argmax kept as a uint8 window position) gives
+    the eval max-pool's values and the recomputing backward's gradient bit for
+    bit — with exact ties (quantised inputs), -inf and NaN in the windows."""
+    import ctypes
+    from jabd_amd import functional as F
+    from jabd_amd._lib import call
+    B, H, W, C = bhwc
+    g = torch.Generator().manual_seed(B * H + C)
+    x = torch.round(torch.randn(B, H, W, C, generator=g) * 2) / 2      # many ties
+    x.view(-1)[::97] = float("-inf")
+    x.view(-1)[::211] = float("nan")
+    x = x.to(cuda)
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    y = torch.empty(B, OH, OW, C, device=cuda)
+    idx = torch.empty(B, OH, OW, C, dtype=torch.uint8, device=cuda)
+    call("jabd_maxpool_idx_nhwc_f32", x.data_ptr(), B, H, W, C, 3, 2, 1, y.data_ptr(),
+         idx.data_ptr(), st)
+    y_eval = F.maxpool(x, 3, 2, 1)
+    dy = torch.randn(B, OH, OW, C, generator=g).to(cuda)
+    dx1 = torch.empty_like(x)
+    dx2 = torch.empty_like(x)
+    call("jabd_maxpool_bwd_idx_f32", idx.data_ptr(), dy.data_ptr(), B, H, W, C, 3, 2, 1,
+         dx1.data_ptr(), st)
+    call("jabd_maxpool_bwd_f32", x.data_ptr(), dy.data_ptr(), B, H, W, C, 3, 2, 1,
+         dx2.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert torch.equal(y.nan_to_num(7.0), y_eval.nan_to_num(7.0))
+    assert torch.equal(dx1, dx2)
+    # and torch's own max_pool2d backward (first maximum, NaN propagating)
+    xc = x.permute(0, 3, 1, 2).cpu().double().requires_grad_()
+    yc = torch.nn.functional.max_pool2d(xc, 3, 2, 1)
+    yc.backward(dy.permute(0, 3, 1, 2).cpu().double())
+    assert torch.allclose(dx1.permute(0, 3, 1, 2).cpu().double(), xc.grad, rtol=1e-6, atol=1e-6)
