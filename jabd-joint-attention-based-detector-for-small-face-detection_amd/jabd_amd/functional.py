@@ -25,8 +25,27 @@ KINK_TAP = None
 
 # Split-K for small-grid k x k convs (conv32.hip m32_ksplit).  It regroups
 # the fp32 K sum, so an image's outputs then depend (in rounding only) on the
-# batch it was run in; set False for batch-invariant results.
-CONV_KSPLIT = True
+# batch it was run in.  Off by default (batched eval is batch-invariant: an
+# image gives the same bits at any batch size); the bs1 predict path turns it
+# on for its forward (jabd_amd.predict, `with split_k():`), where the R50's
+# late 3x3 convs would otherwise fill a few dozen workgroups.
+CONV_KSPLIT = False
+
+
+class split_k:
+    """Context manager: split-K on (or off) for the convs launched inside."""
+
+    def __init__(self, enabled=True):
+        self.enabled = enabled
+
+    def __enter__(self):
+        global CONV_KSPLIT
+        self.prev, CONV_KSPLIT = CONV_KSPLIT, self.enabled
+        return self
+
+    def __exit__(self, *exc):
+        global CONV_KSPLIT
+        CONV_KSPLIT = self.prev
 
 
 def tap(kind, *operands):

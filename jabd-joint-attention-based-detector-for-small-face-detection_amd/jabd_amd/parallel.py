@@ -60,7 +60,11 @@ class GradAllReduce:
         self.buckets = None      # [[param, ...], ...] in launch order
         self.plan_key = None     # requires_grad flags the plan was made under
         self.hooks = []
+        self.hooked = set()      # parameters whose post-accumulate hook is installed
+        self.replans = 0         # consecutive steps that had to plan again
         self._reset()
+        if overlap:
+            self._observe()
 
     # ---------------------------------------------------------------- buckets
     def _plan(self, params):
@@ -84,6 +88,17 @@ class GradAllReduce:
         self.works = {}
         self.next_launch = 0
         self.unplanned = False
+        self.fired = set()       # parameters whose gradient was accumulated this step
+
+    def _observe(self):
+        """Hooks that only record which parameters receive a gradient (the
+        first step's plan is made from them)."""
+        self.remove()
+        self.where = {}
+        for p in self.model.parameters():
+            if p.requires_grad:
+                self.hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+                self.hooked.add(p)
 
     def _key(self):
         return tuple(p.requires_grad for p in self.model.parameters())
@@ -101,8 +116,12 @@ class GradAllReduce:
         for p in self.model.parameters():
             if p.requires_grad:
                 self.hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+                self.hooked.add(p)
 
     def _on_grad(self, p):
+        self.fired.add(p)
+        if self.buckets is None:
+            return
         bi = self.where.get(p)
         if bi is None:
             self.unplanned = True
@@ -119,7 +138,13 @@ class GradAllReduce:
                 self.next_launch += 1
 
     def _with_grad(self):
-        return [p for p in self.model.parameters() if p.requires_grad and p.grad is not None]
+        """The parameters that received a gradient this step: those whose hook
+        fired (a stale .grad kept by zero_grad(set_to_none=False) does not
+        count), plus any un-hooked one (requires_grad switched on since the
+        hooks were installed) holding a gradient; with no hook fired at all
+        (gradients written by hand, no backward) every .grad counts."""
+        return [p for p in self.model.parameters() if p.requires_grad and p.grad is not None and
+                (not self.fired or p in self.fired or p not in self.hooked)]
 
     def _sync_all(self, params):
         for b in self._plan(params):
@@ -150,7 +175,13 @@ class GradAllReduce:
                 self.works[i].wait()
                 self._scatter(b, self.flat[i])
             self._reset()
+            self.replans = 0
             return
+        self.replans += 1
+        if self.replans == 3:
+            import warnings
+            warnings.warn("GradAllReduce: the gradient set changed on 3 consecutive steps; "
+                          "the all-reduce runs synchronously (no overlap with backward)")
         # first step, or the set of parameters with gradients changed: drain
         # what was launched (those sums went to flat copies, .grad is intact),
         # all-reduce this step synchronously and plan again from it
@@ -165,6 +196,7 @@ class GradAllReduce:
         for h in self.hooks:
             h.remove()
         self.hooks = []
+        self.hooked = set()
 
 
 def broadcast_buffers(model, src=0, group=None):

@@ -3,10 +3,71 @@ letterbox + preprocess_input (jabd_letterbox_f32) -> RetinaFace eval forward ->
 decode + score filter + NMS (jabd_detect_f32) -> retinaface_correct_boxes +
 pixel rescale (jabd_correct_boxes_f32).  Only the kept rows leave the device.
 """
+import os
+
 import numpy as np
 import torch
 
-from jabd_amd import ops
+from jabd_amd import functional as F
+from jabd_amd import hipmodule, ops
+
+# JABD_PREDICT_GRAPH=0: launch the forward + detect kernels one by one (A/B)
+PREDICT_GRAPH = os.environ.get("JABD_PREDICT_GRAPH", "1") != "0"
+
+
+class GraphedDetect:
+    """The eval forward + decode / filter / NMS of one input shape, captured
+    once as a HIP graph (torch.cuda.CUDAGraph) and replayed per image: a bs1
+    predict step is ~170 launches (R50) whose host-side dispatch (ctypes +
+    Python per launch) exceeded their GPU time (predict.py get_FPS,
+    predict.py:253-333).  The input is copied into the graph's static input;
+    the outputs are the graph's static (rows, n_keep) buffers, valid until
+    the next replay.  The forward runs with split-K on (functional.split_k),
+    as the eager bs1 predict path.  Invalid once the model's packs may have
+    changed (hipmodule generation)."""
+
+    def __init__(self, net, shape, priors, variances, conf_thres, nms_thres, device):
+        self.net, self.gen = net, hipmodule.generation()
+        self.x = torch.zeros(shape, dtype=torch.float32, device=device)
+        self.pri = priors
+        self.args = (variances, conf_thres, nms_thres)
+        cur = torch.cuda.current_stream(device)
+        side = torch.cuda.Stream(device=device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):   # packs, workspaces and lazy state first
+            for _ in range(2):
+                self._body()
+        cur.wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = self._body()
+
+    def _body(self):
+        with torch.no_grad(), F.split_k():
+            loc, conf, landm = self.net(self.x)
+            v, ct, nt = self.args
+            return ops.detect(loc, conf, landm, self.pri, v, ct, nt)
+
+    def __call__(self, x):
+        self.x.copy_(x)
+        self.graph.replay()
+        return self.out
+
+
+def graphed_detect(net, x, priors, variances, conf_thres=0.5, nms_thres=0.3):
+    """ops.detect(*net(x), ...) for a batch of the shape of x, through a HIP
+    graph cached on the module per (shape, device, thresholds, priors);
+    rebuilt when the module's eval packs may have changed."""
+    key = (tuple(x.shape), str(x.device), float(variances[0]), float(variances[1]),
+           float(conf_thres), float(nms_thres), priors.data_ptr())
+    cache = net.__dict__.setdefault("_jabd_graphs", {})
+    g = cache.get(key)
+    if g is None or g.gen != hipmodule.generation() or g.pri is not priors:
+        if len(cache) > 8:
+            cache.clear()
+        g = cache[key] = GraphedDetect(net, tuple(x.shape), priors, variances, conf_thres,
+                                       nms_thres, x.device)
+    return g(x)
 
 
 def detect_image(net, image, input_shape, cfg, confidence=0.5, nms_iou=0.3,
@@ -23,11 +84,28 @@ def detect_image(net, image, input_shape, cfg, confidence=0.5, nms_iou=0.3,
     x = ops.letterbox(img, (W, H), mean=(104.0, 117.0, 123.0))   # [1, 3, H, W]
     priors = Anchors(cfg, image_size=(H, W)).get_anchors().to(device).float().contiguous()
     with torch.no_grad():
-        loc, conf, landm = net(x)
-        rows, n_keep = ops.detect(loc, conf, landm, priors, cfg["variance"], confidence, nms_iou)
+        if PREDICT_GRAPH and not net.training:
+            priors = _cached_priors(net, cfg, H, W, device, priors)
+            rows, n_keep = graphed_detect(net, x, priors, cfg["variance"], confidence, nms_iou)
+        else:
+            with F.split_k():
+                loc, conf, landm = net(x)
+            rows, n_keep = ops.detect(loc, conf, landm, priors, cfg["variance"], confidence,
+                                      nms_iou)
         k = int(n_keep[0].item())
         if k == 0:
             return []
         det = rows[0, :k].contiguous()
         ops.correct_boxes(det, (H, W), (ih, iw), letterbox=letterbox_image, to_pixels=True)
     return det.cpu().numpy()
+
+
+def _cached_priors(net, cfg, H, W, device, priors):
+    """One priors tensor per (input size, device) on the module (the graph
+    keys on its storage)."""
+    cache = net.__dict__.setdefault("_jabd_priors", {})
+    key = (H, W, str(device))
+    p = cache.get(key)
+    if p is None or p.shape != priors.shape:
+        p = cache[key] = priors
+    return p

@@ -147,8 +147,9 @@ def test_benchmarked_batch_last_image(cuda, kind, B):
     model: R50 RetinaFace bs64, whose layer1 activations are [64,256,256,256]
     = 1.07e9 elements): images 0 and B-1 of the full batch equal bs1 runs of
     the same images bit for bit (per-image batch strides, no cross-image
-    mixing) with split-K off (functional.CONV_KSPLIT); with it on (the R50's
-    bs1 3x3 convs split their K sum over workgroups, conv32.hip m32_ksplit)
+    mixing) with split-K off (functional.CONV_KSPLIT, the default); with it on
+    (the bs1 predict path: the R50's bs1 3x3 convs split their K sum over
+    workgroups, conv32.hip m32_ksplit)
     the bs1 outputs differ only in fp32 rounding: each within the oracle bar,
     and apart by no more than their two oracle errors.  Image B-1 matches the
     oracle (nets/retinaface_r.py:304-343,
@@ -160,17 +161,15 @@ def test_benchmarked_batch_last_image(cuda, kind, B):
     gen = torch.Generator(device=cuda).manual_seed(77)
     x = torch.rand((B, 3, 1024, 1024), generator=gen, device=cuda) * 255.0 - 117.0
     from jabd_amd import functional as JF
+    assert JF.CONV_KSPLIT is False   # batched eval is batch-invariant by default
     with torch.no_grad():
         full = [t.clone() for t in mg(x)]
-        split = [t.clone() for t in mg(x[B - 1:B].contiguous())]
-        try:
-            JF.CONV_KSPLIT = False
-            for i in (0, B - 1):
-                one = mg(x[i:i + 1].contiguous())
-                for f, o, name in zip(full, one, ("loc", "conf", "landm")):
-                    assert torch.equal(f[i:i + 1], o), (i, name, rel_err(f[i:i + 1], o))
-        finally:
-            JF.CONV_KSPLIT = True
+        with JF.split_k():
+            split = [t.clone() for t in mg(x[B - 1:B].contiguous())]
+        for i in (0, B - 1):
+            one = mg(x[i:i + 1].contiguous())
+            for f, o, name in zip(full, one, ("loc", "conf", "landm")):
+                assert torch.equal(f[i:i + 1], o), (i, name, rel_err(f[i:i + 1], o))
         ref = fn(sd, x[B - 1:B].cpu(), "eval")
     for f, s, r, name in zip(full, split, ref, ("loc", "conf", "landm")):
         e, es, d = rel_err(f[B - 1:B], r), rel_err(s, r), rel_err(s, f[B - 1:B])

@@ -78,7 +78,7 @@ def _overlap_worker(rank, world, port, q):
         unused = torch.nn.Linear(3, 3)  # parameters that never get a gradient
         m.add_module("unused", unused)
         red = GradAllReduce(m, bucket_bytes=4096)  # several buckets
-        ok = red.hooks == []                  # nothing installed before the first step
+        ok = red.buckets is None              # no plan before the first step
         for step in range(3):
             x = torch.randn(5, 8, generator=torch.Generator().manual_seed(10 * step + rank))
             m.zero_grad()
@@ -170,6 +170,50 @@ def test_grad_allreduce_freeze_unfreeze_gloo():
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_freeze_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}
+
+
+def _stale_worker(rank, world, port, q):
+    """zero_grad(set_to_none=False) leaves a zero .grad on a
+    parameter that no longer receives a gradient.  The plan is made from the
+    parameters whose gradient hook fired, so that stale tensor is not
+    planned, the buckets complete from the hooks and no step re-plans."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from jabd_amd.parallel import GradAllReduce
+        torch.manual_seed(0)
+        m = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 2))
+        extra = torch.nn.Linear(2, 2)
+        m.add_module("extra", extra)
+        extra.weight.grad = torch.zeros_like(extra.weight)     # stale, from an earlier use
+        red = GradAllReduce(m, bucket_bytes=256)
+        ok = True
+        for step in range(4):
+            x = torch.randn(4, 8, generator=torch.Generator().manual_seed(step + 7 * rank))
+            m.zero_grad(set_to_none=False)
+            m[2](m[1](m[0](x))).sum().backward()
+            red()
+            planned = {id(p) for b in red.buckets for p in b}
+            ok &= id(extra.weight) not in planned
+            if step >= 1:
+                ok &= red.replans == 0
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_ignores_stale_zero_grads_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stale_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)

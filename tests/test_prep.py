@@ -197,3 +197,36 @@ def test_detect_c5_2048(cuda):
     got = rows[0, :k].cpu().numpy()
     np.testing.assert_array_equal(got[:, 4], ref[:, 4])        # scores: the same rows, in order
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,size", [("mnv3", 640), ("r50", 320)])
+def test_graphed_detect_equals_eager(cuda, kind, size):
+    """predict.py's per-image forward + decode + NMS replayed as one HIP graph
+    (jabd_amd.predict.graphed_detect) gives the eager launches' kept rows bit
+    for bit, on two different inputs through the same graph, and is rebuilt
+    after the packs change (load_state_dict bumps the generation)."""
+    import bench
+    from jabd_amd import functional as F
+    from jabd_amd import ops
+    from jabd_amd.predict import graphed_detect
+    from utils.anchors import Anchors
+    net, cfg = bench._weights_init_model(kind)
+    net = net.eval().to(cuda)
+    pri = Anchors(cfg, image_size=(size, size)).get_anchors().to(cuda).float()
+    var = cfg["variance"]
+    g = torch.Generator().manual_seed(size)
+    for _ in range(2):
+        x = (torch.rand(1, 3, size, size, generator=g) * 255 - 117).to(cuda)
+        with torch.no_grad():
+            with F.split_k():   # the predict path's setting (graphed_detect's too)
+                out = net(x)
+            r0, n0 = ops.detect(*out, pri, var, 0.5, 0.3)
+            r1, n1 = graphed_detect(net, x, pri, var, 0.5, 0.3)
+        k = int(n0[0])
+        assert int(n1[0]) == k and k > 0
+        assert torch.equal(r0[0, :k], r1[0, :k])
+    net.load_state_dict(net.state_dict())
+    with torch.no_grad():
+        r2, n2 = graphed_detect(net, x, pri, var, 0.5, 0.3)
+    assert int(n2[0]) == k and torch.equal(r2[0, :k], r0[0, :k])
