@@ -757,6 +757,8 @@ static bool conv_generic_only() {
 }
 
 namespace jabd {
+bool stem7_ok(const ConvArgs& a);
+int stem7_fwd_launch(const ConvArgs& a, hipStream_t st);
 int conv1x1_m32_dispatch(const ConvArgs& a, hipStream_t st, bool kxk);
 int conv1x1_stream_dispatch(const ConvArgs& a, hipStream_t st, StreamStats* ss = nullptr);
 }
@@ -876,6 +878,14 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
   hipStream_t st = as_stream(stream);
   const int tn = a.tn;
   const int64_t OHW = (int64_t)a.OH * a.OW;
+  // ResNet-50 7x7/s2 stem over the NCHW input (stem7.hip); JABD_STEM7=0 -> generic
+  static const bool stem7_on = [] {
+    const char* e = getenv("JABD_STEM7");
+    return !(e && e[0] == '0');
+  }();
+  if (stem7_on && stem7_ok(a) && (a.flags & 1) && (a.act == ACT_NONE || a.act == ACT_RELU) &&
+      a.Ntiles >= 4 && !conv_generic_only())
+    return stem7_fwd_launch(a, st);
   if (fast1x1 && use_conv32(a)) {
     const int r = conv1x1_m32_dispatch(a, st, false);
     if (r >= 0) return r;

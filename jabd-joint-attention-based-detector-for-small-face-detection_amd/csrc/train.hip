@@ -1814,12 +1814,29 @@ static void wgrad_launch_parts(const ConvArgs& a, int64_t per, int64_t nch, floa
   }
 }
 
+namespace jabd {
+bool stem7_ok(const ConvArgs& a);
+int64_t stem7_wgrad_groups(const ConvArgs& a);
+int stem7_wgrad_launch(const ConvArgs& a, float* part, hipStream_t st);
+}  // namespace jabd
+
+// ResNet-50 7x7/s2 stem (stem7.hip); JABD_STEM7=0 -> the tiled kernels
+static bool stem7_wgrad_on(const ConvArgs& a) {
+  static const bool on = [] {
+    const char* e = getenv("JABD_STEM7");
+    return !(e && e[0] == '0');
+  }();
+  return on && stem7_ok(a) && a.y_ps % 4 == 0 && a.y_c0 % 4 == 0 && a.y_bs % 4 == 0 &&
+         (reinterpret_cast<uintptr_t>(a.y) & 15) == 0;
+}
+
 extern "C" int64_t jabd_conv_wgrad_part_floats(const jabd_conv_args* args) {
   if (!args) return -1;
   ConvArgs a = *args;
   a.M = (int64_t)a.B * a.OH * a.OW;
   const int64_t KN = (int64_t)a.KH * a.KW * a.Cin * a.Cout;
   if (stem_wgrad_ok(a)) return stem_wgrad_waves(a) * KN;
+  if (stem7_wgrad_on(a)) return stem7_wgrad_groups(a) * KN;
   return wgrad_chunks(a) * KN;
 }
 
@@ -1844,6 +1861,14 @@ extern "C" int jabd_conv_wgrad_f32(const jabd_conv_args* args, float* part, floa
     const int64_t tot = (int64_t)K * a.Cout;
     wgrad_reduce2_kernel<<<(unsigned)cdiv(tot, 16), 256, 0, st>>>(part, nwv, K, a.Cout, a.Cin,
                                                                   a.KH * a.KW, 16, dw);
+    return check_launch("wgrad_reduce");
+  }
+  if (stem7_wgrad_on(a)) {
+    const int64_t ng = stem7_wgrad_groups(a);
+    if (int e = stem7_wgrad_launch(a, part, st)) return e;
+    const int64_t tot = (int64_t)K * a.Cout;
+    wgrad_reduce2_kernel<<<(unsigned)cdiv(tot, 64), 256, 0, st>>>(part, ng, K, a.Cout, a.Cin,
+                                                                  a.KH * a.KW, 64, dw);
     return check_launch("wgrad_reduce");
   }
   wgrad_launch_parts(a, per, nch, part, st);

@@ -215,7 +215,7 @@ def test_eca_gates_multi_equal_per_tensor(cuda):
 def test_expand_dw_forms_bit_identical(cuda, spec, bhw):
     """The wave-specialised persistent kernel (expand waves feeding
     double-buffered tiles to depthwise waves), the persistent per-chunk kernel
-    (expdw2.hip, the default) and the one-item-per-workgroup kernel compute
+    (expdw2.hip, opt-in) and the one-item-per-workgroup kernel (the default) compute
     every output with the same operation sequence: y, the ECA partials and
     the fused skip branch must be bit-identical.  (4, 96, 80)
     gives several items per persistent workgroup (the expanded-buffer and

@@ -52,12 +52,14 @@ def test_convfn_grads(cuda, cin, cout, k, s, h):
 @pytest.mark.gpu
 @pytest.mark.parametrize("cin,cout,k,s,h,w", [(3, 16, 3, 2, 64, 200), (3, 16, 3, 2, 37, 51),
                                               (3, 8, 3, 1, 20, 70), (1, 16, 5, 2, 33, 129),
-                                              (3, 64, 7, 2, 40, 44)])
+                                              (3, 64, 7, 2, 40, 44), (3, 64, 7, 2, 1, 3),
+                                              (3, 64, 7, 2, 131, 261), (3, 64, 7, 2, 256, 256)])
 def test_convfn_nchw_input_wgrad(cuda, cin, cout, k, s, h, w):
-    """Weight gradient of a conv on the NCHW network input: the MobileNetV3
-    stem shape (3x3/s2, 3 -> 16; stem_wgrad_kernel), widths/heights that are
-    not multiples of the 64-pixel segment, and the R50 7x7 stem (Cout 64:
-    the generic tiled kernel)."""
+    """Forward and weight gradient of a conv on the NCHW network input: the
+    MobileNetV3 stem shape (3x3/s2, 3 -> 16; stem_wgrad_kernel), widths and
+    heights that are not multiples of the 64-pixel segment, and the R50 7x7
+    stem (stem7.hip: 4x64 output tiles, a 1x2 output, ragged tiles in both
+    directions, several persistent tiles per workgroup)."""
     from jabd_amd.train import ConvFn
     g = torch.Generator().manual_seed(cin * 100 + h)
     x = torch.randn(2, cin, h, w, generator=g) * 50
@@ -71,6 +73,24 @@ def test_convfn_nchw_input_wgrad(cuda, cin, cout, k, s, h, w):
     assert rel_err(_nchw(yg.detach()), y.detach()) < TOL
     (yg * _nhwc(dy.float()).to(cuda)).sum().backward()
     _check([wg.grad], [wr.grad], ["dw"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("b,h,w", [(1, 64, 64), (2, 45, 300), (3, 129, 67)])
+def test_stem7_eval_bias_relu(cuda, b, h, w):
+    """The R50 stem's eval form (folded BN bias + ReLU in the stem7 epilogue,
+    jabd_amd.functional.conv) against float64 conv2d + bias + relu."""
+    from jabd_amd import functional as F
+    g = torch.Generator().manual_seed(h * w)
+    conv = torch.nn.Conv2d(3, 64, 7, 2, 3)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) / 147 ** 0.5)
+        conv.bias.copy_(torch.randn(64, generator=g))
+    x = torch.randn(b, 3, h, w, generator=g) * 30
+    ref = tF.relu(tF.conv2d(x.double(), conv.weight.double(), conv.bias.double(), 2, 3))
+    pk = F.pack_conv(conv.to(cuda))
+    y = F.conv(x.to(cuda), pk, stride=2, pad=3, act="relu", nchw_in=True)
+    assert rel_err(_nchw(y), ref) < TOL
 
 
 @pytest.mark.gpu
