@@ -327,6 +327,7 @@ def predict_fps(device, iters=100, warmup=10):
     import numpy as np
     from jabd_amd import functional as F
     from jabd_amd import ops
+    from jabd_amd.predict import PREDICT_GRAPH as graphs
     from jabd_amd.predict import detect_image, graphed_detect
     from utils.anchors import Anchors
     out = {}
@@ -349,7 +350,7 @@ def predict_fps(device, iters=100, warmup=10):
                     k = int(nk[0].item())
                     return rows[0, :k].cpu().numpy()
 
-            def step():   # the same work, replayed as one HIP graph (jabd_amd.predict)
+            def step():   # the same work, replayed as one HIP graph (opt-in, jabd_amd.predict)
                 with torch.no_grad():
                     rows, nk = graphed_detect(net, x, pri, var, 0.5, 0.3)
                     k = int(nk[0].item())
@@ -361,14 +362,16 @@ def predict_fps(device, iters=100, warmup=10):
             for _ in range(iters):
                 kept_e = step_eager()
             el_e = time.perf_counter() - t0
-            for _ in range(warmup):
-                step()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(iters):
-                kept = step()
-            el = time.perf_counter() - t0
-            assert np.array_equal(kept, kept_e), "graph replay differs from the eager launches"
+            kept, el = kept_e, el_e
+            if graphs:
+                for _ in range(warmup):
+                    step()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    kept = step()
+                el = time.perf_counter() - t0
+                assert np.array_equal(kept, kept_e), "graph replay differs from the eager launches"
             for _ in range(3):
                 detect_image(net, img, (size, size), cfg, 0.5, 0.3)
             torch.cuda.synchronize()
@@ -380,7 +383,7 @@ def predict_fps(device, iters=100, warmup=10):
                 cand = int((net(x)[1][0, :, 1] >= 0.5).sum())
             out[f"{kind}_{size}"] = {
                 "fps": iters / el, "ms_per_image": el / iters * 1e3,
-                "fps_eager_launches": iters / el_e,
+                "fps_eager_launches": iters / el_e, "graph": bool(graphs),
                 "detect_image_fps": (iters // 2) / el2, "iters": iters,
                 "anchors": int(pri.shape[0]), "candidates_ge_0.5": cand,
                 "kept": int(kept.shape[0])}
@@ -389,7 +392,8 @@ def predict_fps(device, iters=100, warmup=10):
     out["note"] = ("bs1 wall clock per iteration (host-side launch/ctypes/n_keep sync costs "
                    "included), as get_FPS; fps: forward + detect replayed as one HIP graph "
                    "(jabd_amd.predict.graphed_detect; kept rows checked equal to the eager "
-                   "launches), fps_eager_launches: the same kernels launched one by one; split-K "
+                   "launches, which fps_eager_launches times; JABD_PREDICT_GRAPH=0: eager only); "
+                   "split-K "
                    "on for the bs1 forward (functional.split_k; off in batched eval); "
                    "weights_init weights put ~half the anchors at a conf of ~0.5, so NMS runs "
                    "over thousands of candidates")

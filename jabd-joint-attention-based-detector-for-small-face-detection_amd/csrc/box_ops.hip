@@ -837,7 +837,8 @@ extern "C" int jabd_detect_f32(const float* loc, const float* conf, const float*
   if (batch == 0) return JABD_OK;
   hipStream_t st = as_stream(stream);
   if (num_priors == 0) {
-    JABD_HIP(hipMemsetAsync(n_keep, 0, sizeof(int64_t) * batch, st));
+    const FillRange fr{n_keep, (int64_t)sizeof(int64_t) * batch, 0u};
+    if (int e = fill_ranges(&fr, 1, st)) return e;
     return JABD_OK;
   }
   JABD_REQUIRE(loc && conf && landm && priors && out && n_keep, "detect: null pointer");
@@ -886,7 +887,10 @@ static int match_impl(bool raw, const float* targets, const int64_t* offsets, in
   hipStream_t st = as_stream(stream);
   Carve cv(ws, ws_bytes);
   int* forced = cv.take<int>(batch * num_priors);
-  JABD_HIP(hipMemsetAsync(forced, 0xff, sizeof(int) * batch * num_priors, st));  // -1
+  {
+    const FillRange fr{forced, (int64_t)sizeof(int) * batch * num_priors, 0xFFFFFFFFu};  // -1
+    if (int e = fill_ranges(&fr, 1, st)) return e;
+  }
   const float4* pri = reinterpret_cast<const float4*>(priors);
   dim3 g1((unsigned)max_gt, (unsigned)batch);
   match_best_prior_kernel<<<g1, 256, 0, st>>>(targets, offsets, pri, num_priors, forced);
@@ -952,8 +956,11 @@ static int loss_fwd_impl(const float* loc, const float* conf, const float* landm
   int* npos = cv.take<int>(B);
   int* npos1 = cv.take<int>(B);
   float* ce = cv.take<float>(B);
-  JABD_HIP(hipMemsetAsync(npos, 0, sizeof(int) * B, st));
-  JABD_HIP(hipMemsetAsync(npos1, 0, sizeof(int) * B, st));
+  {
+    const FillRange fr[2] = {{npos, (int64_t)sizeof(int) * B, 0u},
+                             {npos1, (int64_t)sizeof(int) * B, 0u}};
+    if (int e = fill_ranges(fr, 2, st)) return e;
+  }
   conf_max_partial<<<(unsigned)ng, kLossBlock, 0, st>>>(conf, B * A * 2, gpart);
   if (int e = check_launch("conf_max")) return e;
   dim3 g((unsigned)nblk, (unsigned)B);

@@ -110,6 +110,19 @@ struct Carve {
   bool ok() const { return used <= cap; }
 };
 
+// Several (pointer, bytes, 32-bit word) fills in one launch (fill.hip); bytes
+// and pointers 4-byte granular; ranges with bytes <= 0 are skipped.
+struct FillRange {
+  void* ptr;
+  int64_t bytes;
+  uint32_t value;
+};
+constexpr int kFillMax = 12;
+struct FillArgs {
+  FillRange r[kFillMax];
+};
+int fill_ranges(const FillRange* r, int n, hipStream_t st);
+
 // Size-only twin of Carve, used by the *_workspace_size queries so the
 // query and the carve can never disagree.
 struct Sizer {

@@ -447,12 +447,14 @@ __global__ __launch_bounds__(256) void m32_ksplit_reduce(const ConvArgs p, int k
   *reinterpret_cast<float4*>(p.y + m * p.y_ps + p.y_c0 + n) = v;
 }
 
-// K split of a forward k x k launch whose grid (`grid` workgroups) cannot fill
-// the device: enough splits for ~512 workgroups, each keeping >= 8 stages of
-// 32 channels; 1 = no split.  Needs a caller workspace (args.ws).
+// K split of a forward launch (k x k, or 1x1 with its K-concatenated second
+// source) whose grid (`grid` workgroups) cannot fill the device — R50 layer3/4
+// at bs1: enough splits for ~512 workgroups, each keeping >= 8 stages of 32
+// channels; 1 = no split.  Needs a caller workspace (args.ws).
 static int m32_ksplit(const ConvArgs& a, bool kxk, int64_t grid) {
-  if (!kxk || a.tconv || a.Cout % 4 || grid >= 256) return 1;
-  const int S = (a.KH * a.KW * a.Cin + kBK - 1) / kBK;
+  if (a.tconv || a.Cout % 4 || grid >= 256) return 1;
+  const int Kt = kxk ? a.KH * a.KW * a.Cin : a.Cin + (a.x2 ? a.Cin2 : 0);
+  const int S = (Kt + kBK - 1) / kBK;
   int ks = (int)std::min<int64_t>(8, (512 + grid - 1) / grid);
   ks = std::min(ks, S / 8);
   return ks >= 2 ? ks : 1;
@@ -517,13 +519,15 @@ using namespace jabd;
 extern "C" int64_t jabd_conv_workspace_size(const jabd_conv_args* args) {
   if (!args) return 0;
   const ConvArgs& a = *args;
-  if (!a.w32 || a.KH * a.KW == 1 || a.Cin % 32 || a.tconv || a.nchw_in || a.tn32 <= 0) return 0;
+  if (!a.w32 || a.Cin % 32 || a.tconv || a.nchw_in || a.tn32 <= 0) return 0;
+  // 1x1 / stride 1 / pad 0 takes the 32x32 kernel's 1x1 form, anything else its k x k form
+  const bool kxk = !(a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0);
   const int TM = a.tn32 <= 4 ? 2 : 1;
   const int64_t BM = 4 * 32 * TM;
   const int64_t OHW = (int64_t)a.OH * a.OW;
   const int64_t mtiles = a.ascale ? cdiv(OHW, BM) * a.B : cdiv((int64_t)a.B * OHW, BM);
   const int64_t grid = mtiles * (a.ntiles32 / a.tn32);
-  return m32_ksplit_bytes(a, m32_ksplit(a, true, grid));
+  return m32_ksplit_bytes(a, m32_ksplit(a, kxk, grid));
 }
 
 extern "C" int jabd_conv_pack_tn32(int cout) {

@@ -1118,7 +1118,8 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
                (long long)n);
   if (batch == 0) return JABD_OK;
   if (n == 0) {
-    JABD_HIP(hipMemsetAsync(n_keep, 0, sizeof(int64_t) * batch, st));
+    const FillRange fr{n_keep, (int64_t)sizeof(int64_t) * batch, 0u};
+    if (int e = fill_ranges(&fr, 1, st)) return e;
     return JABD_OK;
   }
   JABD_REQUIRE(ws_bytes >= nms_ws_bytes(batch, n), "nms: workspace %zu < %zu", ws_bytes,
@@ -1145,10 +1146,22 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
       set_error("nms: workspace carve overflow");
       return JABD_EWS;
     }
-    JABD_HIP(hipMemsetAsync(w.counts, 0, sizeof(int) * bc, st));
-    JABD_HIP(hipMemsetAsync(w.nanflag, 0, sizeof(int) * bc, st));
-    JABD_HIP(hipMemsetAsync(w.err, 0, sizeof(int), st));
-    JABD_HIP(hipMemsetAsync(w.nzcnt, 0, sizeof(int) * bc * n, st));
+    {  // every counter / table this pass starts from, one launch
+      const int64_t gb = grid ? 1 : 0;  // the grid path's tables
+      const FillRange fr[11] = {
+          {w.counts, (int64_t)sizeof(int) * bc, 0u},
+          {w.nanflag, (int64_t)sizeof(int) * bc, 0u},
+          {w.err, (int64_t)sizeof(int), 0u},
+          {w.nzcnt, (int64_t)sizeof(int) * bc * n, 0u},
+          {w.dense, (int64_t)sizeof(int) * bc, grid ? 0u : 1u},  // 1: every image dense
+          {w.npairs, gb * (int64_t)sizeof(int) * bc, 0u},
+          {w.tested, gb * (int64_t)sizeof(unsigned long long) * bc * 64, 0u},
+          {w.ext, gb * (int64_t)sizeof(unsigned) * bc * 4 * kNC, 0u},
+          {w.runs, gb * (int64_t)sizeof(CellRun) * ((int64_t)w.run_mask + 1), 0xFFFFFFFFu},
+          {w.diag, gb * (int64_t)sizeof(uint64_t) * bc * n, 0u},
+          {w.rowcnt, gb * (int64_t)sizeof(int) * bc * n, 0u}};
+      if (int e = fill_ranges(fr, 11, st)) return e;
+    }
     dim3 g1((unsigned)cdiv(n, 256), bc);
     nms_keys<<<g1, 256, 0, st>>>(scores, score_stride, score_bstride, n_valid, n, bc,
                                   score_thr, filter, (int)img0, w.kin, w.counts);
@@ -1162,13 +1175,6 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
         w.sbox, w.sarea, w.sidx, w.nanflag);
     if (int e = check_launch("nms_gather")) return e;
     if (grid) {
-      JABD_HIP(hipMemsetAsync(w.dense, 0, sizeof(int) * bc, st));
-      JABD_HIP(hipMemsetAsync(w.npairs, 0, sizeof(int) * bc, st));
-      JABD_HIP(hipMemsetAsync(w.tested, 0, sizeof(unsigned long long) * bc * 64, st));
-      JABD_HIP(hipMemsetAsync(w.ext, 0, sizeof(unsigned) * bc * 4 * kNC, st));
-      JABD_HIP(hipMemsetAsync(w.runs, 0xFF, sizeof(CellRun) * ((size_t)w.run_mask + 1), st));
-      JABD_HIP(hipMemsetAsync(w.diag, 0, sizeof(uint64_t) * bc * n, st));
-      JABD_HIP(hipMemsetAsync(w.rowcnt, 0, sizeof(int) * bc * n, st));
       dim3 ge((unsigned)cdiv(n, 256 * kExtPer), bc);
       grid_ext<<<ge, 256, 0, st>>>(w.sbox, w.sarea, w.counts, w.nanflag, n, inv_w, w.ext, w.dense);
       if (int e = check_launch("grid_ext")) return e;
@@ -1197,8 +1203,6 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
       grid_scatter<<<gs, 256, 0, st>>>(w.npairs, w.dense, w.cap, n, w.prow, w.pcol, w.pslot,
                                        w.rowoff, w.csr);
       if (int e = check_launch("grid_scatter")) return e;
-    } else {
-      JABD_HIP(hipMemsetD32Async((hipDeviceptr_t)w.dense, 1, bc, st));
     }
     nms_mask<<<2048, 256, 0, st>>>(w.sbox, w.sarea, w.counts, n, nb, bc, iou_thr, w.nanflag, w.dense,
                                  w.diag, w.nzcnt, w.ent_cb, w.ent_bits);

@@ -353,7 +353,10 @@ int radix_sort64(const uint64_t* kin, uint64_t* kout, const int* vin, int* vout,
   RadixWs w;
   carve_radix(cv, n, vals, &w);
   const int nt = radix_ntiles(n);
-  JABD_HIP(hipMemsetAsync(w.ghist, 0, sizeof(int) * kMaxPass * 256, st));
+  {
+    const FillRange fr{w.ghist, (int64_t)sizeof(int) * kMaxPass * 256, 0u};
+    if (int e = fill_ranges(&fr, 1, st)) return e;
+  }
   radix_hist<<<nt, kRT, 0, st>>>(kin, n, lo, npass, skip_ones ? 1 : 0, w.ghist);
   radix_plan<<<1, kRT, 0, st>>>(w.ghist, npass, w.plan);
   if (int e = check_launch("radix_hist/plan")) return e;

@@ -258,9 +258,10 @@ def conv(x, pk, stride=1, pad=0, act="none", slope=0.0, ascale=None, x2=None, x2
     a.nchw_in = 1 if nchw_in else 0
     a.reserved1 = _CONV_DBG
     ws = None
-    if CONV_KSPLIT and pk.KH * pk.KW > 1 and pk.w32 is not None and not nchw_in and y2 is None:
-        # a k x k conv whose output grid cannot fill the device (bs1) may split
-        # its K reduction over workgroups: give it the workspace it asks for
+    if CONV_KSPLIT and pk.w32 is not None and not nchw_in and y2 is None:
+        # a conv on the 32x32 kernel whose output grid cannot fill the device
+        # (bs1) may split its K reduction over workgroups: give it the
+        # workspace it asks for
         nbytes = int(lib().jabd_conv_workspace_size(ctypes.byref(a)))
         if nbytes > 0:
             ws = torch.empty(nbytes // 4, dtype=torch.float32, device=x.device)

@@ -152,7 +152,7 @@ def detect(loc, conf, landm, priors, variances, conf_threshold=0.5, nms_threshol
         raise ValueError("detect: shape mismatch")
     dev = loc.device
     out = torch.empty((B, A, 15), dtype=torch.float32, device=dev)
-    n_keep = torch.zeros((B,), dtype=torch.int64, device=dev)
+    n_keep = torch.empty((B,), dtype=torch.int64, device=dev)   # written by every call
     ws = _ws(_size_query("jabd_detect_workspace_size", B, A), dev)
     call("jabd_detect_f32", _p(loc), _p(conf), _p(landm), _p(priors), B, A,
          float(variances[0]), float(variances[1]), float(conf_threshold), float(nms_threshold),

@@ -11,7 +11,12 @@ import torch
 from jabd_amd import functional as F
 from jabd_amd import hipmodule, ops
 
-# JABD_PREDICT_GRAPH=0: launch the forward + detect kernels one by one (A/B)
+# JABD_PREDICT_GRAPH=0: launch the forward + detect kernels one by one (A/B).
+# The library initialises its workspaces with its own fill kernel (fill.hip),
+# not hipMemsetAsync: with captured memset nodes, a replay that followed an
+# eager detect launched after the capture read a wrong fill pattern and
+# faulted the device (ROCm 7, tools/graph_check.py --between det); with kernel
+# nodes only, interleaved eager calls and replays agree bit for bit.
 PREDICT_GRAPH = os.environ.get("JABD_PREDICT_GRAPH", "1") != "0"
 
 

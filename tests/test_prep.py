@@ -108,8 +108,11 @@ def test_detect_image_pipeline(cuda, lb):
     H, W = (128, 128) if lb else (96, 160)
     x = torch.from_numpy(prep_ref.preprocess(img, (W, H))).unsqueeze(0).to(cuda)
     pri = Anchors(cfg_mnet, image_size=(H, W)).get_anchors().to(cuda).float()
+    from jabd_amd import functional as F
     with torch.no_grad():
-        rows, nk = ops.detect(*net(x), pri, cfg_mnet["variance"], 0.3, 0.3)
+        with F.split_k():   # the bs1 predict path's conv setting (detect_image)
+            out = net(x)
+        rows, nk = ops.detect(*out, pri, cfg_mnet["variance"], 0.3, 0.3)
     k = int(nk[0])
     if k == 0:
         assert len(got) == 0
@@ -141,8 +144,9 @@ def test_detect_image_c1_640(cuda):
     x_ref = prep_ref.preprocess(img, (640, 640))
     x_dev = ops.letterbox(torch.from_numpy(img).to(cuda), (640, 640), mean=(104, 117, 123))
     assert np.array_equal(x_dev[0].cpu().numpy(), x_ref)
-    # stage 2: forward
-    with torch.no_grad():
+    # stage 2: forward (split-K on, as detect_image runs it)
+    from jabd_amd import functional as F
+    with torch.no_grad(), F.split_k():
         out = net(x_dev)
         ref = model_ref.retinaface_mnv3(sd, torch.from_numpy(x_ref)[None], "eval")
     for g, r in zip(out, ref):

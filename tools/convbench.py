@@ -62,6 +62,8 @@ R50 = [
     ("l1.c1", 16, 256, 256, 64, 64, 1, 1, 0, 0, 0, "relu"),
     ("l1.c2", 16, 256, 256, 64, 64, 3, 1, 0, 0, 0, "relu"),
     ("l1.c3", 16, 256, 256, 64, 256, 1, 1, 64, 0, 0, "relu"),
+    ("l1.c1b", 16, 256, 256, 256, 64, 1, 1, 0, 0, 0, "relu"),
+    ("l2.c1a", 16, 256, 256, 256, 128, 1, 1, 0, 0, 0, "relu"),
     ("l2.c1", 16, 128, 128, 512, 128, 1, 1, 0, 0, 0, "relu"),
     ("l2.c2", 16, 128, 128, 128, 128, 3, 1, 0, 0, 0, "relu"),
     ("l2.c3", 16, 128, 128, 128, 512, 1, 1, 0, 0, 1, "relu"),
