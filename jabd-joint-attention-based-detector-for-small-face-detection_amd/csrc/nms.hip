@@ -52,6 +52,21 @@ static bool nms_dense_only() {
   return v == 1;
 }
 
+// Images with at most this many candidates take the dense all-pairs mask even
+// on the grid path: a few hundred clustered boxes (bs1 predict) gave the grid
+// producer's per-box candidate walks 340 us of serial latency against ~10 us
+// for the parallel 64x64-block mask (MNv3 640^2 predict 606 -> 767 fps);
+// R50's 6.8k / 17k candidates measured equal either way.
+// JABD_NMS_DENSE_MAX=<n> for A/B (0 = grid whenever possible).
+static int nms_dense_max() {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("JABD_NMS_DENSE_MAX");
+    v = e ? atoi(e) : 8192;
+  }
+  return v;
+}
+
 // Images per sort pass: <= 254 and the sort size must fit the sort's int32.
 static int64_t images_per_pass(int64_t batch, int64_t n) {
   int64_t c = batch < kMaxImg ? batch : kMaxImg;
@@ -340,12 +355,15 @@ __global__ __launch_bounds__(256) void grid_ext(const float4* __restrict__ sbox,
                                                 const int* __restrict__ counts,
                                                 const int* __restrict__ nanflag, int64_t n,
                                                 float inv_w, unsigned* __restrict__ ext,
-                                                int* __restrict__ dense) {
+                                                int* __restrict__ dense, int dense_max) {
   __shared__ unsigned le[4 * kNC];
   const int t = threadIdx.x;
   const int b = blockIdx.y;
   for (int i = t; i < 4 * kNC; i += 256) le[i] = 0u;
-  if (blockIdx.x == 0 && t == 0 && nanflag[b]) atomicOr(&dense[b], 1);
+  // NaN boxes (1), or few enough candidates that the all-pairs mask is cheaper
+  // than the grid's per-box serial candidate walks (8)
+  if (blockIdx.x == 0 && t == 0 && (nanflag[b] || (dense_max > 0 && counts[b] <= dense_max)))
+    atomicOr(&dense[b], nanflag[b] ? 1 : 8);
   __syncthreads();
   const int cnt = counts[b];
   const int64_t base = (int64_t)blockIdx.x * 256 * kExtPer;
@@ -491,7 +509,7 @@ __global__ __launch_bounds__(256) void grid_pairs(
   const uint64_t k = skey[p];
   if (k == ~0ull) return;
   const int b = (int)(k >> 56);
-  if (dense[b] & 3) return;
+  if (dense[b] & 11) return;
   const int i = sval[p];
   const float4 bi = gbox[p];
   const float ai = garea[p];
@@ -1176,7 +1194,8 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
     if (int e = check_launch("nms_gather")) return e;
     if (grid) {
       dim3 ge((unsigned)cdiv(n, 256 * kExtPer), bc);
-      grid_ext<<<ge, 256, 0, st>>>(w.sbox, w.sarea, w.counts, w.nanflag, n, inv_w, w.ext, w.dense);
+      grid_ext<<<ge, 256, 0, st>>>(w.sbox, w.sarea, w.counts, w.nanflag, n, inv_w, w.ext, w.dense,
+                                   nms_dense_max());
       if (int e = check_launch("grid_ext")) return e;
       grid_keys<<<g1, 256, 0, st>>>(w.sbox, w.sarea, w.counts, n, inv_w, fcell, w.ext, w.kin,
                                      w.gval_in, w.dense);
