@@ -515,6 +515,13 @@ int jabd_heads_f32(const float* x, int64_t x_bs, int32_t x_ps, int32_t B, int32_
                    int32_t C, const float* wt, const float* bias, int64_t A, int64_t a_off,
                    int32_t softmax, float* loc, float* conf, float* landm,
                    jabd_stream_t stream);
+/* The same heads for wide levels (R50: C = 256), whose three 1x1 convs run
+ * as one GEMM (jabd_conv2d_nhwc_f32, C -> 32) into y [B][HW][32] (channels as
+ * wt above); this scatters y into loc / conf / landm at a_off, softmax over
+ * the conf pairs if asked (the same fp32 operations as jabd_heads_f32). */
+int jabd_heads_scatter_f32(const float* y, int32_t B, int64_t HW, int64_t A, int64_t a_off,
+                           int32_t softmax, float* loc, float* conf, float* landm,
+                           jabd_stream_t stream);
 
 /* ======================================================================== *
  * Training-graph glue (no PyTorch kernels in a training step)

@@ -514,6 +514,23 @@ static int launch_m32_as(const ConvArgs& a, hipStream_t st) {
 
 using namespace jabd;
 
+// Pixel tiles per wave of the 32x32 kernel (1: 32-pixel wave tiles, more and
+// shorter workgroups; 2: 64).  1 measured faster on GEMMs without a folded
+// ECA gate (R50 at bs16-64: 5-10%; at bs1, where the grid cannot fill the
+// device, R50 640^2 predict 230 -> 313 fps) and on small gated ones (bs1
+// MNv3 +3%); the gate's per-workgroup weight scaling makes them slower on
+// the large gated GEMMs (C2's project convs).  JABD_M32_TM=1|2 forces one.
+static int m32_tm(const ConvArgs& a) {
+  static int ftm = -1;
+  if (ftm < 0) {
+    const char* e = getenv("JABD_M32_TM");
+    ftm = e ? atoi(e) : 0;
+  }
+  if (a.tn32 > 4) return 1;
+  if (ftm == 1 || ftm == 2) return ftm;
+  return (!a.ascale || a.M < 65536) ? 1 : 2;
+}
+
 // N-tiles (32 output channels each) per workgroup for the 32x32 kernel.
 // Prefers a 64x128 wave tile (TM=2, TN<=4), else the exact-fit wide tile.
 extern "C" int64_t jabd_conv_workspace_size(const jabd_conv_args* args) {
@@ -522,7 +539,9 @@ extern "C" int64_t jabd_conv_workspace_size(const jabd_conv_args* args) {
   if (!a.w32 || a.Cin % 32 || a.tconv || a.nchw_in || a.tn32 <= 0) return 0;
   // 1x1 / stride 1 / pad 0 takes the 32x32 kernel's 1x1 form, anything else its k x k form
   const bool kxk = !(a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0);
-  const int TM = a.tn32 <= 4 ? 2 : 1;
+  ConvArgs am = a;
+  am.M = (int64_t)a.B * a.OH * a.OW;
+  const int TM = m32_tm(am);
   const int64_t BM = 4 * 32 * TM;
   const int64_t OHW = (int64_t)a.OH * a.OW;
   const int64_t mtiles = a.ascale ? cdiv(OHW, BM) * a.B : cdiv((int64_t)a.B * OHW, BM);
@@ -552,15 +571,7 @@ int conv1x1_m32_dispatch(const ConvArgs& a0, hipStream_t st, bool kxk) {
   a.Ntiles = a0.ntiles32;
 #define M32(TM_, TN_) \
   return kxk ? launch_m32<TM_, TN_, true>(a, st) : launch_m32<TM_, TN_, false>(a, st);
-  static int ftm = -1;  // JABD_M32_TM=1: 32-pixel wave tiles for TN <= 4 (A/B)
-  if (ftm < 0) {
-    const char* e = getenv("JABD_M32_TM");
-    ftm = e ? atoi(e) : 0;
-  }
-  // 32-pixel wave tiles (more, shorter workgroups) measured faster on large
-  // GEMMs without a folded ECA gate (R50: 5-10%); the gate's per-workgroup
-  // weight scaling makes them slower there
-  if (ftm == 1 || (ftm == 0 && !a0.ascale && a0.M >= 262144)) {
+  if (m32_tm(a0) == 1) {
     switch (a0.tn32) {
       case 1: M32(1, 1)
       case 2: M32(1, 2)

@@ -760,6 +760,27 @@ extern "C" int jabd_nlm_apply_f32(const float* src, int64_t src_bs, int32_t src_
   return check_launch("nlm_apply");
 }
 
+namespace jabd {
+__global__ void heads_scatter_kernel(const float4* __restrict__ y, int64_t HW, int64_t A,
+                                     int64_t a_off, int softmax, float4* __restrict__ loc,
+                                     float4* __restrict__ conf, float4* __restrict__ landm);
+}
+
+extern "C" int jabd_heads_scatter_f32(const float* y, int32_t B, int64_t HW, int64_t A,
+                                      int64_t a_off, int32_t softmax, float* loc, float* conf,
+                                      float* landm, jabd_stream_t stream) {
+  JABD_REQUIRE(y && loc && conf && landm && B > 0 && HW > 0, "heads_scatter: bad args");
+  JABD_REQUIRE(A % 2 == 0 && a_off % 2 == 0 && a_off + 2 * HW <= A, "heads_scatter: anchor range");
+  JABD_REQUIRE(((reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(loc) |
+                 reinterpret_cast<uintptr_t>(conf) | reinterpret_cast<uintptr_t>(landm)) & 15) == 0,
+               "heads_scatter: buffers must be 16-byte aligned");
+  dim3 g((unsigned)cdiv(HW * 8, 256), (unsigned)B);
+  heads_scatter_kernel<<<g, 256, 0, as_stream(stream)>>>(
+      reinterpret_cast<const float4*>(y), HW, A, a_off, softmax, reinterpret_cast<float4*>(loc),
+      reinterpret_cast<float4*>(conf), reinterpret_cast<float4*>(landm));
+  return check_launch("heads_scatter");
+}
+
 extern "C" int jabd_heads_f32(const float* x, int64_t x_bs, int32_t x_ps, int32_t B, int32_t HW,
                               int32_t C, const float* wt, const float* bias, int64_t A,
                               int64_t a_off, int32_t softmax, float* loc, float* conf,
@@ -774,6 +795,37 @@ extern "C" int jabd_heads_f32(const float* x, int64_t x_bs, int32_t x_ps, int32_
 }
 
 namespace jabd {
+// One thread per (position, float4 of the 32 head channels): q 0-1 loc (the
+// position's 2 anchor rows), q 2 conf (softmax per anchor pair), q 3-7 landm.
+// A and a_off are even, so every destination float4 is 16-byte aligned.
+__global__ __launch_bounds__(256) void heads_scatter_kernel(const float4* __restrict__ y,
+                                                            int64_t HW, int64_t A,
+                                                            int64_t a_off, int softmax,
+                                                            float4* __restrict__ loc,
+                                                            float4* __restrict__ conf,
+                                                            float4* __restrict__ landm) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (i >= HW * 8) return;
+  const int64_t p = i >> 3;
+  const int q = (int)(i & 7);
+  float4 v = y[((int64_t)b * HW) * 8 + i];
+  const int64_t row0 = (int64_t)b * A + a_off + 2 * p;  // the position's first anchor row
+  if (q < 2) {
+    loc[row0 + q] = v;
+  } else if (q == 2) {
+    if (softmax) {  // F.softmax over each anchor's 2 logits, as heads_kernel
+      float m = fmaxf(v.x, v.y), e0 = expf(v.x - m), e1 = expf(v.y - m), s = e0 + e1;
+      v.x = e0 / s; v.y = e1 / s;
+      m = fmaxf(v.z, v.w); e0 = expf(v.z - m); e1 = expf(v.w - m); s = e0 + e1;
+      v.z = e0 / s; v.w = e1 / s;
+    }
+    conf[row0 >> 1] = v;
+  } else {
+    landm[(row0 >> 1) * 5 + (q - 3)] = v;
+  }
+}
+
 // torchvision resnet50 stem maxpool (F.max_pool2d(3, 2, 1)) on NHWC, float4 lanes.
 __global__ void maxpool_kernel(const float* __restrict__ x, int H, int W, int C, int OH, int OW,
                                int k, int s, int pad, int64_t total4, float* __restrict__ y) {

@@ -195,6 +195,7 @@ SIGNATURES = {
                            c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                            c_vp],
     "jabd_maxpool_nhwc_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp],
+    "jabd_heads_scatter_f32": [c_vp, c_i32, c_i64, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp],
     "jabd_heads_f32": [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i64, c_i64, c_i32,
                        c_vp, c_vp, c_vp, c_vp],
     # training (A11)

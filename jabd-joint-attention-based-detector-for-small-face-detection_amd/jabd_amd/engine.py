@@ -46,6 +46,9 @@ CHUNK_ELEMS = (1 << 31) - 1
 # The head's three per-level ECA gates as one pool + gate launch pair
 # (F.eca_gates_multi); JABD_GATES_MULTI=0 launches them level by level (A/B).
 GATES_MULTI = os.environ.get("JABD_GATES_MULTI", "1") != "0"
+# Heads of >= 128-channel levels (R50) as one GEMM + scatter instead of
+# heads_kernel; JABD_HEADS_GEMM=0 for A/B.
+HEADS_GEMM = os.environ.get("JABD_HEADS_GEMM", "1") != "0"
 
 
 def _w1d(eca):
@@ -206,6 +209,13 @@ class _Head:
         self.eca_fpn = _w1d(m.eca_fpn)
         self.ssh = [s._jabd_cached(dev, lambda s=s: SSHPack(s)) for s in (m.ssh1, m.ssh2, m.ssh3)]
         self.heads = [heads_pack(m, i) for i in range(3)]
+        # wide levels (R50: 256 channels): the three heads as one MFMA GEMM
+        # plus a scatter; heads_kernel's per-position channel loop is serial
+        self.heads_gemm = [
+            F.pack_conv_cat([(m.BboxHead[i].conv1x1, None, None), (m.ClassHead[i].conv1x1, None, None),
+                             (m.LandmarkHead[i].conv1x1, None, None)])
+            if HEADS_GEMM and m.BboxHead[i].conv1x1.in_channels >= 128 else None
+            for i in range(3)]
 
     def _gate(self, f, w1d):
         if self.gate == "beca":
@@ -241,8 +251,11 @@ class _Head:
         for i, o in enumerate(levels):
             _, h, w, C = o.shape
             feat = self.ssh[i].forward(o, scs[i])
-            wt, bs = self.heads[i]
-            F.heads(feat, wt, bs, loc, conf, landm, a_off, softmax)
+            if self.heads_gemm[i] is not None:
+                F.heads_scatter(F.conv(feat, self.heads_gemm[i]), loc, conf, landm, a_off, softmax)
+            else:
+                wt, bs = self.heads[i]
+                F.heads(feat, wt, bs, loc, conf, landm, a_off, softmax)
             a_off += 2 * h * w
         return loc, conf, landm
 

@@ -530,6 +530,13 @@ def heads(x, wt, bias, loc, conf, landm, a_off, softmax):
          landm.data_ptr(), _stream())
 
 
+def heads_scatter(y, loc, conf, landm, a_off, softmax):
+    """y [B, h, w, 32] (the three heads as one 1x1 GEMM) -> loc / conf / landm rows."""
+    B, h, w, _ = y.shape
+    call("jabd_heads_scatter_f32", y.data_ptr(), B, h * w, loc.shape[1], a_off,
+         1 if softmax else 0, loc.data_ptr(), conf.data_ptr(), landm.data_ptr(), _stream())
+
+
 def adaptive_pool(x, sizes):
     """cat over sizes of AdaptiveAvgPool2d((s, s)) of NHWC x -> [B, S, C]."""
     B, H, W, C = x.shape
