@@ -43,11 +43,11 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
   XD_T(1);
   if (!xd_item<K, S, TH, TW, EC>(p, blockIdx.x, dv, nitems, it)) return;
   const bool skip = SKIP && it.c0 == 0;
-  if (skip) {
-    for (int i = threadIdx.x; i < 10 * (p.Cin >> 2); i += T) {
-      const int q = i / (p.Cin >> 2), c4 = i - q * (p.Cin >> 2);
-      sws[q][c4] = *reinterpret_cast<const float4*>((q < 9 ? p.sw + q * p.Cin : p.sb) + 4 * c4);
-    }
+  if (skip) {  // tap q (9 = bias) by wave, channel quad by lane: no division (Cin <= 256)
+    const int c4 = threadIdx.x & 63;
+    if (c4 < (p.Cin >> 2))
+      for (int q = threadIdx.x >> 6; q < 10; q += NW)
+        sws[q][c4] = *reinterpret_cast<const float4*>((q < 9 ? p.sw + q * p.Cin : p.sb) + 4 * c4);
   }
   // the whole input tile (halo included) inside the image: no per-pixel
   // bounds in the loads or the expanded-tile epilogue (most tiles)
@@ -60,9 +60,13 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
   const int ntc = ntv ? nt : 0;
   const f32x4* wpk = reinterpret_cast<const f32x4*>(p.we);
   // small operands first (consumed after the expand phase)
+  // padded expanded channels (chb >= E) start from a zero bias and see zero
+  // packed weights (or no MFMAs at all past Ntiles), so act(acc) is already
+  // the 0 the depthwise tile needs there: no per-element select
   const int chb = it.c0 + 16 * ntw + 4 * g;
   const bool chok = chb < p.E;
-  const float4 pbi = *reinterpret_cast<const float4*>(p.be + (chok ? chb : 0));
+  float4 pbi = *reinterpret_cast<const float4*>(p.be + (chok ? chb : 0));
+  if (!chok) pbi = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 pwd = make_float4(0.f, 0.f, 0.f, 0.f);
   if (t < NWD) {
     const int tp = t / C::NC4, cc = it.c0 + 4 * (t - tp * C::NC4);
@@ -184,11 +188,7 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
       if (blk < C::NBLK) {
         const int pb = blk / C::NNT;
         const int px = pb * 16 + j, q = 4 * ntw + g;
-        float4 o;
-        o.x = chok ? xd_act<ACT>(acc[u][0]) : 0.f;
-        o.y = chok ? xd_act<ACT>(acc[u][1]) : 0.f;
-        o.z = chok ? xd_act<ACT>(acc[u][2]) : 0.f;
-        o.w = chok ? xd_act<ACT>(acc[u][3]) : 0.f;
+        const float4 o = xd_act4<ACT>(make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]));
         if (pb * 16 + 16 <= C::IPX || px < C::IPX)
           *reinterpret_cast<float4*>(lds + (q * C::QP + px) * 4) = o;
       }
@@ -202,12 +202,9 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
         const int px = pb * 16 + j, q = 4 * ntw + g;
         const int r = px / C::IW, c = px - r * C::IW;
         const int ih = it.ih0 + r, iw = it.iw0 + c;
-        const bool ok = chok && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
-        float4 o;
-        o.x = ok ? xd_act<ACT>(acc[u][0]) : 0.f;
-        o.y = ok ? xd_act<ACT>(acc[u][1]) : 0.f;
-        o.z = ok ? xd_act<ACT>(acc[u][2]) : 0.f;
-        o.w = ok ? xd_act<ACT>(acc[u][3]) : 0.f;
+        const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        float4 o = xd_act4<ACT>(make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]));
+        if (!ok) o = make_float4(0.f, 0.f, 0.f, 0.f);
         if (px < C::IPX) *reinterpret_cast<float4*>(lds + (q * C::QP + px) * 4) = o;
       }
     }
@@ -252,11 +249,7 @@ __global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_arg
 #pragma unroll
       for (int o = 0; o < C::PW; ++o) {
         if (owb + o >= p.OW) break;
-        float4 v;
-        v.x = xd_act<ACT>(a2[o].x);
-        v.y = xd_act<ACT>(a2[o].y);
-        v.z = xd_act<ACT>(a2[o].z);
-        v.w = xd_act<ACT>(a2[o].w);
+        const float4 v = xd_act4<ACT>(a2[o]);
         *reinterpret_cast<float4*>(yb + ((int64_t)oh * p.OW + owb + o) * p.y_ps) = v;
         psum.x += v.x; psum.y += v.y; psum.z += v.z; psum.w += v.w;
       }

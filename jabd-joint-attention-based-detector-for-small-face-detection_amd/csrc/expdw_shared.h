@@ -50,9 +50,31 @@ __device__ unsigned long long* xd_trace_buf;
 // IEEE divide is ~10 VALU instructions per element here).
 template <int ACT>
 __device__ __forceinline__ float xd_act(float v) {
-  if (ACT == ACT_RELU) return fmaxf(v, 0.f);  // one v_max (a select is cmp + cndmask)
+  // one v_maximum_f32 (NaN-propagating, as torch.relu); fmaxf compiled to a
+  // canonicalising v_max plus the v_max (2 VALU per element)
+  if (ACT == ACT_RELU) return __builtin_elementwise_maximum(v, 0.f);
   if (ACT == ACT_HSWISH) return hswish_f(v);
   return v;
+}
+
+// xd_act on a float4 with the packed fp32 ALU where it applies: Hardswish as
+// two v_pk_fma + four v_med3 + two v_pk_mul instead of 12 scalar VALU
+// (the same IEEE operations per element as hswish_f: bit-identical).
+template <int ACT>
+__device__ __forceinline__ float4 xd_act4(float4 v) {
+  if (ACT == ACT_HSWISH) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 k = {1.f / 6.f, 1.f / 6.f}, h = {0.5f, 0.5f};
+    const f2 a = {v.x, v.y}, b = {v.z, v.w};
+    f2 ta = __builtin_elementwise_fma(a, k, h), tb = __builtin_elementwise_fma(b, k, h);
+    ta.x = __builtin_amdgcn_fmed3f(ta.x, 0.f, 1.f);
+    ta.y = __builtin_amdgcn_fmed3f(ta.y, 0.f, 1.f);
+    tb.x = __builtin_amdgcn_fmed3f(tb.x, 0.f, 1.f);
+    tb.y = __builtin_amdgcn_fmed3f(tb.y, 0.f, 1.f);
+    const f2 ra = a * ta, rb = b * tb;
+    return make_float4(ra.x, ra.y, rb.x, rb.y);
+  }
+  return make_float4(xd_act<ACT>(v.x), xd_act<ACT>(v.y), xd_act<ACT>(v.z), xd_act<ACT>(v.w));
 }
 
 template <int K, int S, int TH, int TW, int EC>
