@@ -24,9 +24,19 @@
 
 namespace jabd {
 
+// Resident workgroups the register allocation must allow: 2, or 4 for the
+// skip form when its LDS leaves room for 4 (its extra live registers
+// otherwise cost a resident workgroup: 142 vs 114 VGPRs on the 3x3/s2 tile).
+template <int K, int S, int TH, int TW, int EC, bool SKIP, int NW, int SKC>
+constexpr int xd1_min_wg() {
+  using C = XdCfg<K, S, TH, TW, EC>;
+  constexpr int bytes = C::LDS * 4 + K * K * (EC / 4) * 16 + (SKIP ? 10 * (SKC / 4) * 16 : 16);
+  return (SKIP && NW == 4 && 4 * bytes <= 160 * 1024) ? 4 : 2;
+}
+
 template <int K, int S, int TH, int TW, int EC, int ACT, int KP, bool SKIP = false, int NW = 4,
           int SKC = 160>
-__global__ __launch_bounds__(64 * NW, 2) void expdw1_kernel(const jabd_expdw_args p, const XdDivs dv,
+__global__ __launch_bounds__(64 * NW, (xd1_min_wg<K, S, TH, TW, EC, SKIP, NW, SKC>())) void expdw1_kernel(const jabd_expdw_args p, const XdDivs dv,
                                                        int nitems) {
   using C = XdCfg<K, S, TH, TW, EC>;
   constexpr int T = 64 * NW;                  // threads
