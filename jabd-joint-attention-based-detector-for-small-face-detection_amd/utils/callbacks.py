@@ -2,10 +2,13 @@
 `.append_loss(value)` calls (reference interface: utils/callbacks.py:7-49,
 called at e.g. train_50_3_r.py:276,350).
 
-Host bookkeeping only, out of the hot path.  Each run
-gets its own directory under `log_dir`; every appended value goes to a text
-file (one value per line) as soon as it arrives, and a small dependency-free
-SVG chart of the curve and its running mean is rewritten beside it.
+Host bookkeeping only, out of the hot path.  As the
+reference: each run gets its own directory `log_dir/loss_<stamp>` (creating
+it fails if it exists, :17), and every appended value goes to
+`epoch_loss_<stamp>.txt` as `str(loss)` one per line (:21-23).  The chart is a
+small dependency-free SVG, `epoch_loss_<stamp>.svg`, with a running mean,
+where the reference draws `epoch_loss_<stamp>.png` with matplotlib and a
+Savitzky-Golay smoothing (:26-46): matplotlib is not a dependency here.
 """
 import os
 import time
@@ -14,32 +17,33 @@ import time
 class LossHistory:
     def __init__(self, log_dir):
         self.log_dir = log_dir
-        stamp = time.strftime("%Y_%m_%d_%H_%M_%S")
-        self.save_path = os.path.join(log_dir, "loss_" + stamp)
-        os.makedirs(self.save_path, exist_ok=True)
+        self.time_str = time.strftime("%Y_%m_%d_%H_%M_%S")
+        self.save_path = os.path.join(log_dir, "loss_" + self.time_str)
         self.losses = []
-        self._txt = os.path.join(self.save_path, "epoch_loss.txt")
-        self._svg = os.path.join(self.save_path, "epoch_loss.svg")
+        os.makedirs(self.save_path)
+        self._txt = os.path.join(self.save_path, "epoch_loss_" + self.time_str + ".txt")
+        self._svg = os.path.join(self.save_path, "epoch_loss_" + self.time_str + ".svg")
 
     def append_loss(self, loss):
-        value = float(loss)
-        self.losses.append(value)
+        self.losses.append(loss)
         with open(self._txt, "a") as f:
-            f.write(f"{value!r}\n")
+            f.write(str(loss))
+            f.write("\n")
         self._write_chart()
 
     # ---------------------------------------------------------------- chart
     def _running_mean(self, window=5):
         out, acc = [], 0.0
-        for i, v in enumerate(self.losses):
+        vals = [float(v) for v in self.losses]
+        for i, v in enumerate(vals):
             acc += v
             if i >= window:
-                acc -= self.losses[i - window]
+                acc -= vals[i - window]
             out.append(acc / min(i + 1, window))
         return out
 
     def _write_chart(self, w=640, h=400, pad=40):
-        ys = self.losses
+        ys = [float(v) for v in self.losses]
         lo, hi = min(ys), max(ys)
         span = (hi - lo) or 1.0
         n = max(len(ys) - 1, 1)

@@ -106,14 +106,20 @@ def test_label_parsing_and_collate(tmp_path):
     assert isinstance(timgs, torch.Tensor) and timgs.shape == (2, 3, 4, 4)
 
 
-def test_loss_history(tmp_path):
+def test_loss_history(tmp_path, monkeypatch):
+    import time
     from utils.callbacks import LossHistory
+    monkeypatch.setattr(time, "strftime", lambda fmt, *a: "2026_01_02_03_04_05")
     h = LossHistory(str(tmp_path))
     for v in (3.0, 2.5, 2.0):
         h.append_loss(v)
     txt = [f for f in os.listdir(h.save_path) if f.endswith(".txt")]
-    assert len(txt) == 1
+    # the reference's names: loss_<stamp>/epoch_loss_<stamp>.txt (utils/callbacks.py:14,21)
+    assert txt == ["epoch_loss_" + h.time_str + ".txt"]
+    assert os.path.basename(h.save_path) == "loss_" + h.time_str
     assert open(os.path.join(h.save_path, txt[0])).read().split() == ["3.0", "2.5", "2.0"]
+    with pytest.raises(FileExistsError):   # a second run in the same second fails, as the reference's
+        LossHistory(str(tmp_path))
 
 
 def test_pack_cache_invalidation_events():
