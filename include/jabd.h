@@ -393,6 +393,20 @@ int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t stream);
  * the statistics form does not serve it (the caller then runs
  * jabd_conv2d_nhwc_f32 + jabd_bn_stats_f32). */
 int64_t jabd_conv1x1_bn_stats_nblk(const jabd_conv_args* args);
+/* Training forward of a bias-free conv followed by BatchNorm on the 32x32
+ * GEMM (the ResNet-50 bottleneck convs, nets/resnet_pytorch_r.py:122-143 —
+ * the reference's Conv2d then BatchNorm2d in train mode): the GEMM epilogue
+ * writes per-32-pixel-tile (mean, M2) rows into part, which a fixed-order
+ * fp64 combination turns into mean / invstd and the running-statistics
+ * update (momentum, unbiased variance), as jabd_bn_stats_f32 over y would.
+ * _part_floats returns the floats part needs (16-byte aligned), 0 when the
+ * form does not serve the layer (no bias / activation / gate / residual /
+ * second source / split output / transposed form; the caller then runs
+ * jabd_conv2d_nhwc_f32 + jabd_bn_stats_f32). */
+int64_t jabd_conv_bn_stats_part_floats(const jabd_conv_args* args);
+int jabd_conv_bn_stats_f32(const jabd_conv_args* args, float* part, int64_t part_floats,
+                           float* mean, float* invstd, float* running_mean, float* running_var,
+                           float momentum, float eps, jabd_stream_t stream);
 int jabd_conv1x1_bn_stats_f32(const jabd_conv_args* args, float* part, int64_t nblk,
                               float* shift, jabd_stream_t stream);
 

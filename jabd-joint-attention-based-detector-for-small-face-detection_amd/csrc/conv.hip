@@ -760,6 +760,11 @@ namespace jabd {
 bool stem7_ok(const ConvArgs& a);
 int stem7_fwd_launch(const ConvArgs& a, hipStream_t st);
 int conv1x1_m32_dispatch(const ConvArgs& a, hipStream_t st, bool kxk);
+int conv_m32_stats_dispatch(const ConvArgs& a, bool kxk, float* part, hipStream_t st);
+int64_t bn_rows_chunk_doubles(int64_t M, int C);
+int bn_rows_final_launch(const float* rows, int ldc, int64_t M, int C, double* chunks,
+                         float* mean, float* invstd, float* rmean, float* rvar, float momentum,
+                         float eps, hipStream_t st);
 int conv1x1_stream_dispatch(const ConvArgs& a, hipStream_t st, StreamStats* ss = nullptr);
 }
 
@@ -865,6 +870,69 @@ extern "C" int jabd_conv1x1_bn_stats_f32(const jabd_conv_args* args, float* part
   const int r = jabd::conv1x1_stream_dispatch(a, as_stream(stream), &ss);
   JABD_REQUIRE(r >= 0, "conv1x1_bn_stats: no streaming kernel for this shape");
   return r;
+}
+
+// The 32x32 GEMM's statistics form (conv32.hip, ST): a bias-free,
+// activation-free forward conv with no gate, residual, second source or
+// split output whose BatchNorm follows — the ResNet-50 bottleneck convs
+// (nets/resnet_pytorch_r.py:122-143).  The GEMM takes the shape even where
+// use_conv32's throughput heuristic would pick another kernel (the saved
+// statistics pass outweighs it); JABD_CONV_STATS32=0 turns the form off.
+static bool conv_m32_stats_form(const ConvArgs& a, bool fast1x1, bool vec4, bool& kxk) {
+  static const bool on = [] {
+    const char* e = getenv("JABD_CONV_STATS32");
+    return !(e && e[0] == '0');
+  }();
+  const bool is1x1 = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0;
+  kxk = !is1x1;
+  const int64_t OHW = (int64_t)a.OH * a.OW;
+  if (!on || conv_generic_only() || a.bias || a.res || a.ascale || a.x2 || a.y2 ||
+      a.act != ACT_NONE || a.tconv || a.nchw_in || !(a.flags & 1) || a.Cout % 4)
+    return false;
+  if (!a.w32 || a.tn32 < 1 || a.tn32 > 4 || a.ntiles32 % a.tn32 || a.ntiles32 * 32 < a.Cout)
+    return false;
+  if (is1x1) return fast1x1;
+  return vec4 && a.Cin % 32 == 0 && a.x_bs % 4 == 0 && a.y_bs == OHW * a.y_ps;
+}
+
+// floats of the statistics rows (ceil(M / 32) x 2 x ntiles32 * 32) followed
+// by the fp64 chunk sums (8-byte aligned)
+static int64_t conv_stats_rows_floats(const ConvArgs& a) {
+  return cdiv(a.M, (int64_t)32) * 2 * a.ntiles32 * 32;
+}
+
+extern "C" int64_t jabd_conv_bn_stats_part_floats(const jabd_conv_args* args) {
+  ConvArgs a;
+  bool fast1x1 = false, vec4 = false, kxk = false;
+  if (conv_setup(args, a, fast1x1, vec4) != JABD_OK || !conv_m32_stats_form(a, fast1x1, vec4, kxk))
+    return 0;
+  const int64_t rows = (conv_stats_rows_floats(a) + 1) & ~(int64_t)1;
+  return rows + 2 * bn_rows_chunk_doubles(a.M, a.Cout);
+}
+
+extern "C" int jabd_conv_bn_stats_f32(const jabd_conv_args* args, float* part, int64_t part_floats,
+                                      float* mean, float* invstd, float* running_mean,
+                                      float* running_var, float momentum, float eps,
+                                      jabd_stream_t stream) {
+  ConvArgs a;
+  bool fast1x1 = false, vec4 = false, kxk = false;
+  {
+    const int e = conv_setup(args, a, fast1x1, vec4);
+    if (e != JABD_OK) return e;
+  }
+  JABD_REQUIRE(conv_m32_stats_form(a, fast1x1, vec4, kxk),
+               "conv_bn_stats: layer not served by the 32x32 statistics form");
+  const int64_t rows = (conv_stats_rows_floats(a) + 1) & ~(int64_t)1;
+  JABD_REQUIRE(part && mean && invstd && part_floats >= rows + 2 * bn_rows_chunk_doubles(a.M, a.Cout),
+               "conv_bn_stats: part holds %lld floats, %lld needed", (long long)part_floats,
+               (long long)(rows + 2 * bn_rows_chunk_doubles(a.M, a.Cout)));
+  JABD_REQUIRE(((uintptr_t)part & 15) == 0, "conv_bn_stats: part must be 16-byte aligned");
+  hipStream_t st = as_stream(stream);
+  const int r = conv_m32_stats_dispatch(a, kxk, part, st);
+  if (r != JABD_OK) return r < 0 ? JABD_EINVAL : r;
+  return bn_rows_final_launch(part, a.ntiles32 * 32, a.M, a.Cout,
+                              reinterpret_cast<double*>(part + rows), mean, invstd, running_mean,
+                              running_var, momentum, eps, st);
 }
 
 extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t stream) {

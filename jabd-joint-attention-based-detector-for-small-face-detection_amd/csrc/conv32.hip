@@ -64,8 +64,14 @@ constexpr int kGateLds = 1024;   // ECA gate channels staged in LDS
 // KXK: k x k implicit GEMM (tap-major K; every 32-channel stage lies inside
 // one tap, host guarantees Cin % 32 == 0, no K-concat source); stride-1
 // transposed form (tconv) for the data gradient.
-template <int TM, int TN, bool KXK, bool AS>
+template <int TM, int TN, bool KXK, bool AS, bool ST = false>
 // AS: the ECA gate (ascale) is set — staged in LDS, applied at the weight store.
+// ST (TM = 1, training forward, no bias / residual / act): the epilogue also
+// writes the following BatchNorm's statistics per 32-pixel wave tile, row
+// r = 4 mb + wave of part[r][0|1][Ntiles*32]: the tile's mean and sum of
+// squared deviations (Sum (y - sh) and Sum (y - sh)^2 around the tile's first
+// pixel, then mean = sh + S/n, M2 = Q - S^2/n); jabd_bn_stats_final_rows_f32
+// combines the rows exactly (Chan) in a fixed order.
 // phase >= 0 (KXK, stride-2 tconv): this launch covers only the output
 // pixels (2i + ph, 2j + pw), phase = 2 ph + pw, and only the taps that reach
 // them — the sub-pixel decomposition of a strided data gradient (the other
@@ -340,6 +346,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
   if constexpr (TM == 1) {
     float* ep = reinterpret_cast<float*>(sB_) + wave * 32 * kEpiPitch;
     const int ep_px = lane >> 3, ep_q = lane & 7;
+    const int srow = mb * 4 + wave;  // ST: this wave tile's statistics row (flat M tiling)
 #pragma unroll
     for (int t = 0; t < TM; ++t) {
       // the tile's pixel rows (pm < 0: past M) for the 8-pixel store groups
@@ -360,11 +367,19 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
                           acc[t][u][4 * c + 3]);
         wave_lds_sync32();
         const int n = nb0 + 4 * ep_q;
+        float4 ss = make_float4(0.f, 0.f, 0.f, 0.f), sq = ss, sh = ss;
+        if constexpr (ST) sh = *reinterpret_cast<const float4*>(ep + 4 * ep_q);  // pixel 0
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int px = ep_px + 8 * r;
           if (prow[r] < 0 || n >= p.Cout) continue;
           float4 v = *reinterpret_cast<const float4*>(ep + px * kEpiPitch + 4 * ep_q);
+          if constexpr (ST) {
+            const float dx = v.x - sh.x, dy = v.y - sh.y, dz = v.z - sh.z, dw = v.w - sh.w;
+            ss.x += dx; ss.y += dy; ss.z += dz; ss.w += dw;
+            sq.x = fmaf(dx, dx, sq.x); sq.y = fmaf(dy, dy, sq.y);
+            sq.z = fmaf(dz, dz, sq.z); sq.w = fmaf(dw, dw, sq.w);
+          }
           if (p.bias) {
             const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
             v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
@@ -379,6 +394,28 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
           v.z = act32(v.z, p.act, p.slope);
           v.w = act32(v.w, p.act, p.slope);
           *reinterpret_cast<float4*>(p.y + (int64_t)mrow[r] * p.y_ps + p.y_c0 + n) = v;
+        }
+        if constexpr (ST) {
+          // the 8 lanes of one channel quad (lane xor 8, 16, 32), fixed order
+#pragma unroll
+          for (int off = 8; off <= 32; off <<= 1) {
+            ss.x += __shfl_xor(ss.x, off); ss.y += __shfl_xor(ss.y, off);
+            ss.z += __shfl_xor(ss.z, off); ss.w += __shfl_xor(ss.w, off);
+            sq.x += __shfl_xor(sq.x, off); sq.y += __shfl_xor(sq.y, off);
+            sq.z += __shfl_xor(sq.z, off); sq.w += __shfl_xor(sq.w, off);
+          }
+          const int64_t cnt = min<int64_t>(32, p.M - (int64_t)srow * 32);
+          if (ep_px == 0 && cnt > 0 && n < p.Cout) {
+            const float inv = 1.f / (float)cnt;
+            const int ldc = p.Ntiles * 32;
+            float* pr = part + (int64_t)srow * 2 * ldc + n;
+            *reinterpret_cast<float4*>(pr) =
+                make_float4(fmaf(ss.x, inv, sh.x), fmaf(ss.y, inv, sh.y), fmaf(ss.z, inv, sh.z),
+                            fmaf(ss.w, inv, sh.w));
+            *reinterpret_cast<float4*>(pr + ldc) =
+                make_float4(fmaxf(sq.x - ss.x * ss.x * inv, 0.f), fmaxf(sq.y - ss.y * ss.y * inv, 0.f),
+                            fmaxf(sq.z - ss.z * ss.z * inv, 0.f), fmaxf(sq.w - ss.w * ss.w * inv, 0.f));
+          }
         }
         wave_lds_sync32();
       }
@@ -508,6 +545,32 @@ static int launch_m32_as(const ConvArgs& a, hipStream_t st) {
   conv1x1_m32_kernel<TM, TN, KXK, AS><<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, per_img, -1,
                                                                      1, nullptr);
   return check_launch("conv1x1_m32");
+}
+
+// Forward conv on the 32x32 kernel with the BatchNorm statistics rows (ST):
+// 32-pixel wave tiles, no gate / split / bias / residual / activation.
+template <int TN, bool KXK>
+static int launch_m32_stats(const ConvArgs& a, float* part, hipStream_t st) {
+  const int64_t grid = cdiv(a.M, (int64_t)128) * (a.Ntiles / TN);
+  JABD_REQUIRE(grid < (int64_t)0x7fffffff, "conv32 stats: grid too large");
+  conv1x1_m32_kernel<1, TN, KXK, false, true><<<(unsigned)grid, 256, 0, st>>>(
+      a, (int)cdiv((int64_t)a.OH * a.OW, 128), 0, -1, 1, part);
+  return check_launch("conv1x1_m32 (BN statistics)");
+}
+
+int conv_m32_stats_dispatch(const ConvArgs& a0, bool kxk, float* part, hipStream_t st) {
+  ConvArgs a = a0;
+  a.w = a0.w32;
+  a.Ntiles = a0.ntiles32;
+#define MS(TN_) return kxk ? launch_m32_stats<TN_, true>(a, part, st) : launch_m32_stats<TN_, false>(a, part, st);
+  switch (a0.tn32) {
+    case 1: MS(1)
+    case 2: MS(2)
+    case 3: MS(3)
+    case 4: MS(4)
+    default: return -1;
+  }
+#undef MS
 }
 
 }  // namespace jabd

@@ -116,7 +116,8 @@ __global__ __launch_bounds__(kRedThreads) void bn_stats_part_kernel(
 // fixed-shape LDS tree over the rows.  Valid in threads t < kFinLanes.
 constexpr int kFinThreads = 1024, kFinLanes = 16, kFinRows = kFinThreads / kFinLanes;
 
-__device__ __forceinline__ void bn_final_sums(const float* __restrict__ part, int64_t nblk, int C,
+template <typename T>
+__device__ __forceinline__ void bn_final_sums(const T* __restrict__ part, int64_t nblk, int C,
                                               double& S, double& Q) {
   __shared__ double ls[kFinThreads], lq[kFinThreads];
   const int t = threadIdx.x;
@@ -126,7 +127,7 @@ __device__ __forceinline__ void bn_final_sums(const float* __restrict__ part, in
   if (c < C) {
     int64_t b = r;
     for (; b + 7 * kFinRows < nblk; b += 8 * kFinRows) {
-      float vs[8], vq[8];
+      T vs[8], vq[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         vs[u] = part[(b + u * kFinRows) * 2 * C + c];
@@ -158,8 +159,9 @@ __device__ __forceinline__ void bn_final_sums(const float* __restrict__ part, in
   Q = lq[t % kFinLanes];
 }
 
+template <typename T>
 __global__ __launch_bounds__(kFinThreads) void bn_stats_final_kernel(
-    const float* __restrict__ x, const float* __restrict__ part, int64_t nblk, int64_t M, int C,
+    const float* __restrict__ x, const T* __restrict__ part, int64_t nblk, int64_t M, int C,
     float momentum, float eps, float* __restrict__ mean, float* __restrict__ invstd,
     float* __restrict__ rmean, float* __restrict__ rvar) {
   double S, Q;
@@ -177,6 +179,66 @@ __global__ __launch_bounds__(kFinThreads) void bn_stats_final_kernel(
     const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
     rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
   }
+}
+
+// Statistics rows of a producer that takes them per 32-pixel tile (the 32x32
+// GEMM's ST epilogue, conv32.hip): rows[r][0][c] = the tile's mean,
+// rows[r][1][c] = its sum of squared deviations, r < nrow = ceil(M / 32),
+// row pitch 2 * ldc.  First stage of the exact combination: per chunk of
+// kRowChunk rows, in fp64 and row order, the sums around the shift
+// sh = rows[0][0][c] (tile 0's mean):
+//   S = sum n_r (mean_r - sh),  Q = sum M2_r + n_r (mean_r - sh)^2,
+// to out[chunk][0|1][c] (bn_stats_part's layout in double); the second stage
+// is bn_stats_final_kernel<double> with x = rows (shift = row 0's means).
+constexpr int kRowChunk = 64;
+
+__global__ __launch_bounds__(256) void bn_rows_chunk_kernel(const float* __restrict__ rows,
+                                                            int ldc, int64_t nrow, int64_t M,
+                                                            int C, double* __restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t chunk = i / C;
+  const int c = (int)(i - chunk * C);
+  const int64_t r0 = chunk * kRowChunk;
+  if (r0 >= nrow) return;
+  const int64_t r1 = min(r0 + kRowChunk, nrow);
+  const double sh = (double)rows[c];
+  double S = 0.0, Q = 0.0;
+  int64_t r = r0;
+  auto acc = [&](int64_t rr, float mu, float m2) {
+    const double n = (double)min<int64_t>(32, M - rr * 32);
+    const double d = (double)mu - sh;
+    S += n * d;
+    Q += (double)m2 + n * d * d;
+  };
+  for (; r + 8 <= r1; r += 8) {
+    float mu[8], m2[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      mu[u] = rows[(r + u) * 2 * ldc + c];
+      m2[u] = rows[(r + u) * 2 * ldc + ldc + c];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc(r + u, mu[u], m2[u]);
+  }
+  for (; r < r1; ++r) acc(r, rows[r * 2 * ldc + c], rows[r * 2 * ldc + ldc + c]);
+  out[chunk * 2 * C + c] = S;
+  out[chunk * 2 * C + C + c] = Q;
+}
+
+int64_t bn_rows_chunk_doubles(int64_t M, int C) {
+  return cdiv(cdiv(M, (int64_t)32), (int64_t)kRowChunk) * 2 * C;
+}
+
+int bn_rows_final_launch(const float* rows, int ldc, int64_t M, int C, double* chunks,
+                         float* mean, float* invstd, float* rmean, float* rvar, float momentum,
+                         float eps, hipStream_t st) {
+  const int64_t nrow = cdiv(M, (int64_t)32), nch = cdiv(nrow, (int64_t)kRowChunk);
+  bn_rows_chunk_kernel<<<(unsigned)cdiv(nch * C, (int64_t)256), 256, 0, st>>>(rows, ldc, nrow, M,
+                                                                             C, chunks);
+  if (int e = check_launch("bn_rows_chunk")) return e;
+  bn_stats_final_kernel<double><<<(unsigned)cdiv(C, kFinLanes), kFinThreads, 0, st>>>(
+      rows, chunks, nch, M, C, momentum, eps, mean, invstd, rmean, rvar);
+  return check_launch("bn_stats_final (rows)");
 }
 
 // Elementwise BN kernels: workgroup = `lanes` float4 channel groups x
@@ -1668,7 +1730,7 @@ extern "C" int jabd_bn_stats_final_f32(const float* shift, const float* part, in
                                        float eps, jabd_stream_t stream) {
   JABD_REQUIRE(shift && part && mean && invstd && nblk > 0 && M > 0 && C > 0,
                "bn_stats_final: bad args");
-  bn_stats_final_kernel<<<(unsigned)cdiv(C, kFinLanes), kFinThreads, 0, as_stream(stream)>>>(
+  bn_stats_final_kernel<float><<<(unsigned)cdiv(C, kFinLanes), kFinThreads, 0, as_stream(stream)>>>(
       shift, part, nblk, M, C, momentum, eps, mean, invstd, running_mean, running_var);
   return check_launch("bn_stats_final");
 }
@@ -1683,7 +1745,7 @@ extern "C" int jabd_bn_stats_f32(const float* x, int32_t ldx, int64_t M, int32_t
   const int64_t per = bn_rows_per_blk(M, C), nblk = cdiv(M, per);
   bn_stats_part_kernel<<<(unsigned)nblk, kRedThreads, 0, st>>>(x, ldx, M, C, per, part);
   if (int e = check_launch("bn_stats_part")) return e;
-  bn_stats_final_kernel<<<(unsigned)cdiv(C, kFinLanes), kFinThreads, 0, st>>>(
+  bn_stats_final_kernel<float><<<(unsigned)cdiv(C, kFinLanes), kFinThreads, 0, st>>>(
       x, part, nblk, M, C, momentum, eps, mean, invstd, running_mean, running_var);
   return check_launch("bn_stats_final");
 }

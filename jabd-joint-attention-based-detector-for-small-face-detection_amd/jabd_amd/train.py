@@ -923,15 +923,16 @@ def _conv_fwd_bn_stats(x, weight, bn):
     statistics of its output for the following BatchNorm
     (jabd_conv1x1_bn_stats_f32 + jabd_bn_stats_final_f32; running buffers
     updated).  Returns (y, (mean, invstd)), or (y, None) when the statistics
-    form does not serve the layer (the caller's _bn_fwd then takes them)."""
+    form does not serve the layer (the caller's _bn_fwd then takes them).
+    Layers the streaming form does not take (Cout > 80) go to the 32x32
+    GEMM's statistics form (_conv_fwd_stats)."""
     pk = _packed(weight, transposed=False)
     B, H, W, _ = x.shape
     y = torch.empty((B, H, W, pk.Cout), dtype=torch.float32, device=x.device)
     a = _conv_args(x, pk, y, 1, 0)
     nblk = int(lib().jabd_conv1x1_bn_stats_nblk(ctypes.byref(a))) if pk.KH == 1 else 0
     if nblk <= 0:
-        call("jabd_conv2d_nhwc_f32", ctypes.byref(a), _st())
-        return y, None
+        return _conv_fwd_stats(x, weight, bn)
     C = pk.Cout
     part = torch.empty((nblk, 2, C), dtype=torch.float32, device=x.device)
     shift = torch.empty(C, dtype=torch.float32, device=x.device)
@@ -943,6 +944,33 @@ def _conv_fwd_bn_stats(x, weight, bn):
          mean.data_ptr(), invstd.data_ptr(), bn.running_mean.data_ptr(),
          bn.running_var.data_ptr(), float(bn.momentum), float(bn.eps), _st())
     F.tap("stats", "conv1x1_stream", y, mean, invstd, bn.eps)
+    return y, (mean, invstd)
+
+
+def _conv_fwd_stats(x, weight, bn, stride=1, pad=0):
+    """Bias-free _conv_fwd on the 32x32 GEMM whose epilogue also takes the
+    batch statistics of its output for the following BatchNorm
+    (jabd_conv_bn_stats_f32: per-32-pixel-tile rows, combined in fp64 in a
+    fixed order; running buffers updated).  Returns (y, (mean, invstd)), or
+    (y, None) when the form does not serve the layer (the caller's _bn_fwd
+    then takes the statistics)."""
+    pk = _packed(weight, transposed=False)
+    B, H, W, _ = x.shape
+    OH = (H + 2 * pad - pk.KH) // stride + 1
+    OW = (W + 2 * pad - pk.KW) // stride + 1
+    y = torch.empty((B, OH, OW, pk.Cout), dtype=torch.float32, device=x.device)
+    a = _conv_args(x, pk, y, stride, pad)
+    nf = int(lib().jabd_conv_bn_stats_part_floats(ctypes.byref(a)))
+    if nf <= 0:
+        call("jabd_conv2d_nhwc_f32", ctypes.byref(a), _st())
+        return y, None
+    part = torch.empty(nf, dtype=torch.float32, device=x.device)
+    mean = torch.empty(pk.Cout, dtype=torch.float32, device=x.device)
+    invstd = torch.empty_like(mean)
+    call("jabd_conv_bn_stats_f32", ctypes.byref(a), part.data_ptr(), nf, mean.data_ptr(),
+         invstd.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+         float(bn.momentum), float(bn.eps), _st())
+    F.tap("stats", "conv32", y, mean, invstd, bn.eps)
     return y, (mean, invstd)
 
 
@@ -1283,21 +1311,22 @@ class R50BlockFn(torch.autograd.Function):
     def forward(ctx, blk, x, *params):
         stride = blk.stride
         B, H, W, _ = x.shape
-        t1p = _conv_fwd(x, blk.conv1.weight)
-        t1, st1 = _bn_fwd(t1p, blk.bn1, "relu")
-        t2p = _conv_fwd(t1, blk.conv2.weight, None, stride, 1)
-        t2, st2 = _bn_fwd(t2p, blk.bn2, "relu")
-        t3p = _conv_fwd(t2, blk.conv3.weight)
+        # each conv's GEMM epilogue also takes its BatchNorm's batch statistics
+        t1p, bs1 = _conv_fwd_stats(x, blk.conv1.weight, blk.bn1)
+        t1, st1 = _bn_fwd(t1p, blk.bn1, "relu", stats=bs1)
+        t2p, bs2 = _conv_fwd_stats(t1, blk.conv2.weight, blk.bn2, stride, 1)
+        t2, st2 = _bn_fwd(t2p, blk.bn2, "relu", stats=bs2)
+        t3p, bs3 = _conv_fwd_stats(t2, blk.conv3.weight, blk.bn3)
         ds = blk.downsample
         saved = ()
         if ds is not None:
-            ip = _conv_fwd(x, ds[0].weight, None, stride, 0)
-            idn, sts = _bn_fwd(ip, ds[1], "none")
+            ip, bss = _conv_fwd_stats(x, ds[0].weight, ds[1], stride, 0)
+            idn, sts = _bn_fwd(ip, ds[1], "none", stats=bss)
             saved = (ip,)
             ctx.sts = sts
         else:
             idn = x
-        out, st3 = _bn_fwd(t3p, blk.bn3, "relu", res=idn)
+        out, st3 = _bn_fwd(t3p, blk.bn3, "relu", res=idn, stats=bs3)
         ctx.blk, ctx.st = blk, (st1, st2, st3)
         ctx.hw = (H, W)
         ctx.save_for_backward(x, t1p, t1, t2p, t2, t3p, idn, *saved)

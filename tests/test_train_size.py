@@ -181,11 +181,12 @@ def test_bn_stats_mnv3_bs32_1024(cuda):
 
 @pytest.mark.gpu
 def test_bn_stats_r50_bs64_1024(cuda):
-    """C3's shape (R50, bs64, 1024²: layer1's BNs over 4.2 M pixels)."""
+    """C3's shape (R50, bs64, 1024²: layer1's BNs over 4.2 M pixels, taken
+    in the bottleneck convs' GEMM epilogue)."""
     from jabd_amd import synth
     from nets.retinaface_eca_nonlocal import RetinaFace
     from utils.config import cfg_re50
     m = init_for_parity(RetinaFace(cfg=cfg_re50, mode="train"), seed=18)
     x = synth.images(64, 1024, seed=45, device=cuda)
     worst = _stats_at_size(m, x, cuda)
-    assert worst["bn_stats"][3] >= 64 * 256 * 256
+    assert worst["conv32"][3] >= 64 * 256 * 256   # the bottleneck convs' epilogue statistics

@@ -74,6 +74,8 @@ def _ptr_args(name, args, sigs):
                     if v:
                         out.append(v)
             continue
+        if name == "jabd_conv_bn_stats_f32" and i == 1:   # the statistics rows: workspace
+            continue
         if t is ctypes.c_void_p:
             nxt = types[i + 1] if i + 1 < len(types) else None
             if nxt is ctypes.c_size_t:      # (ws, ws_bytes)
@@ -89,7 +91,7 @@ _INT_TYPES = (ctypes.c_int32, ctypes.c_int, ctypes.c_int64)
 
 def _flops(name, args, sigs=None):
     if name in ("jabd_conv2d_nhwc_f32", "jabd_conv_wgrad_f32", "jabd_conv1x1_bn_stats_f32",
-                "jabd_conv_wgrad_eca_f32"):
+                "jabd_conv_wgrad_eca_f32", "jabd_conv_bn_stats_f32"):
         a = args[0]._obj if hasattr(args[0], "_obj") else None
         if a is None:
             return 0.0
