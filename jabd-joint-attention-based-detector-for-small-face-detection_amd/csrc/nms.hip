@@ -58,6 +58,19 @@ static bool nms_dense_only() {
 // for the parallel 64x64-block mask (MNv3 640^2 predict 606 -> 767 fps);
 // R50's 6.8k / 17k candidates measured equal either way.
 // JABD_NMS_DENSE_MAX=<n> for A/B (0 = grid whenever possible).
+// Images of at most this many rows take the dense producer without the grid
+// producer's launches (its key sort, tables and pair pass are ~35 kernels of
+// fixed cost: at bs1 640^2, 16.8k rows, they cost more than the all-pairs
+// mask they could save).  JABD_NMS_DENSE_ROWS=<n> for A/B (0 = grid whenever
+// possible).
+static int64_t nms_dense_rows() {
+  static const int64_t v = [] {
+    const char* e = getenv("JABD_NMS_DENSE_ROWS");
+    return e ? (int64_t)atoll(e) : (int64_t)20480;
+  }();
+  return v;
+}
+
 static int nms_dense_max() {
   static int v = -2;
   if (v == -2) {
@@ -1146,7 +1159,7 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
   const int64_t per_pass = images_per_pass(batch, n);
   // log-area class width W' >= 1.01 * -ln(thr) (wider is always safe)
   // the pull scan keeps one kept word per row block in LDS next to its rings
-  const bool grid = iou_thr >= 0.0 && !nms_dense_only() &&
+  const bool grid = iou_thr >= 0.0 && !nms_dense_only() && n > nms_dense_rows() &&
                     nb * 8 + kPullStaticLds <= 160 * 1024;
   double wcls = iou_thr > 0.0 ? 1.01 * -std::log(iou_thr) : INFINITY;
   if (wcls < 0.2) wcls = 0.2;  // wider classes are always safe; keeps ln-range / W' < kNC

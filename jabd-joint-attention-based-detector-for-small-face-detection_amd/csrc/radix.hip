@@ -267,6 +267,143 @@ __global__ __launch_bounds__(kRT) void radix_scatter(
   }
 }
 
+// ---------------------------------------------------------------- small sorts
+// n <= kSmallMax (the bs1 predict's NMS keys: 16.8k at 640^2): the whole
+// sort in one 1024-thread workgroup — every pass's histogram in one sweep,
+// then per pass the tiles of 16 waves x 512 keys in order, each key's
+// stable rank among its tile's keys of its digit from wave ballots (as
+// radix_scatter), the tile's digit offsets from a running count in LDS.  One
+// launch instead of 2 + 3 per pass: at this size every kernel of the
+// multi-workgroup sort is a few microseconds of launch and drain.  The
+// passes' reads see the previous pass's stores after the barrier: one
+// workgroup is one CU, whose vector L1 its own stores write through.
+constexpr int kST = 1024, kSWaves = kST / 64, kSR = 8;
+constexpr int kSTile = kST * kSR;  // keys per tile
+constexpr int kSmallMax = 4 * kSTile;
+
+template <bool VALS>
+__global__ __launch_bounds__(kST) void radix_small(const uint64_t* __restrict__ kin,
+                                                   uint64_t* __restrict__ kout,
+                                                   uint64_t* __restrict__ kalt,
+                                                   const int* __restrict__ vin,
+                                                   int* __restrict__ vout, int* __restrict__ valt,
+                                                   int n, int lo, int npass, int skip_ones) {
+  __shared__ int hist[kMaxPass][256];
+  __shared__ int wc[kSWaves][256];
+  __shared__ int run[256];
+  __shared__ int wsum[4];
+  __shared__ int nones;
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  for (int i = t; i < kMaxPass * 256; i += kST) (&hist[0][0])[i] = 0;
+  if (t == 0) nones = 0;
+  __syncthreads();
+  for (int i = t; i < n; i += kST) {
+    const uint64_t key = kin[i];
+    const bool ones = skip_ones && key == ~0ull;
+    if (ones) atomicAdd(&nones, 1);
+    for (int p = ones ? npass - 1 : 0; p < npass; ++p)
+      atomicAdd(&hist[p][(int)((key >> (lo + 8 * p)) & 255u)], 1);
+  }
+  __syncthreads();
+  // passes that reorder anything (one bin holding every counted key: skipped)
+  unsigned runmask = 0;
+  for (int p = 0; p < npass; ++p) {
+    const int tot = p == npass - 1 ? n : n - nones;
+    const int full = __syncthreads_or(t < 256 && tot > 0 && hist[p][t] == tot);
+    if (!full) runmask |= 1u << p;
+  }
+  const int m = __popc(runmask);
+  if (m == 0) {
+    for (int i = t; i < n; i += kST) {
+      kout[i] = kin[i];
+      if (VALS) vout[i] = vin[i];
+    }
+    return;
+  }
+  const uint64_t lt = (1ull << l) - 1ull;
+  const uint64_t* ks = kin;
+  const int* vs = vin;
+  int left = m;
+  for (int p = 0; p < npass; ++p) {
+    if (!((runmask >> p) & 1u)) continue;
+    uint64_t* kd = ((left - 1) & 1) ? kalt : kout;
+    int* vd = ((left - 1) & 1) ? valt : vout;
+    --left;
+    const int shift = lo + 8 * p;
+    // digit bases: exclusive prefix of this pass's histogram (waves 0-3)
+    if (t < 256) {
+      const int v = hist[p][t];
+      int x = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (l >= o) x += y;
+      }
+      if (l == 63) wsum[w] = x;
+      run[t] = x - v;
+    }
+    __syncthreads();
+    if (t < 256) {
+      int add = 0;
+      for (int i = 0; i < w; ++i) add += wsum[i];
+      run[t] += add;
+    }
+    for (int tile0 = 0; tile0 < n; tile0 += kSTile) {
+      for (int i = t; i < kSWaves * 256; i += kST) (&wc[0][0])[i] = 0;
+      __syncthreads();
+      uint64_t key[kSR];
+      int val[kSR], rk[kSR], dg[kSR];
+      const int base = tile0 + w * (kSTile / kSWaves);
+#pragma unroll
+      for (int r = 0; r < kSR; ++r) {
+        const int idx = base + r * 64 + l;
+        const bool ok = idx < n;
+        key[r] = ok ? ks[idx] : 0ull;
+        val[r] = (VALS && ok) ? vs[idx] : 0;
+      }
+#pragma unroll
+      for (int r = 0; r < kSR; ++r) {
+        const bool ok = base + r * 64 + l < n;
+        const int d = (int)((key[r] >> shift) & 255u);
+        uint64_t peers = __ballot(ok);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          const uint64_t mb = __ballot((d >> b) & 1);
+          peers &= ((d >> b) & 1) ? mb : ~mb;
+        }
+        const int below = __popcll(peers & lt);
+        const int prev = wc[w][d];
+        dg[r] = d;
+        rk[r] = prev + below;
+        if (ok && below == 0) wc[w][d] = prev + __popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+      }
+      __syncthreads();
+      if (t < 256) {  // tile offsets per (wave, digit); run[] moves past the tile
+        int s = run[t];
+#pragma unroll
+        for (int i = 0; i < kSWaves; ++i) {
+          const int c = wc[i][t];
+          wc[i][t] = s;
+          s += c;
+        }
+        run[t] = s;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < kSR; ++r) {
+        if (base + r * 64 + l >= n) continue;
+        const int dst = wc[w][dg[r]] + rk[r];
+        kd[dst] = key[r];
+        if (VALS) vd[dst] = val[r];
+      }
+      __syncthreads();
+    }
+    ks = kd;
+    vs = vd;
+  }
+}
+
 // ---------------------------------------------------------------- exclusive int32 scan
 __global__ __launch_bounds__(kRT) void scan_reduce(const int* __restrict__ in, int64_t n,
                                                    int* __restrict__ bsum) {
@@ -334,6 +471,15 @@ static void carve_radix(A& a, int64_t n, bool vals, RadixWs* w) {
   }
 }
 
+// JABD_RADIX_SMALL=0: every size takes the multi-workgroup passes (A/B)
+static bool radix_small_off() {
+  static const bool off = [] {
+    const char* e = getenv("JABD_RADIX_SMALL");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
+
 size_t radix_ws_bytes(int64_t n, bool vals) {
   Sizer s;
   carve_radix(s, n, vals, (RadixWs*)nullptr);
@@ -352,6 +498,15 @@ int radix_sort64(const uint64_t* kin, uint64_t* kout, const int* vin, int* vout,
   Carve cv(ws, ws_bytes);
   RadixWs w;
   carve_radix(cv, n, vals, &w);
+  if (n <= kSmallMax && !radix_small_off()) {
+    if (vals)
+      radix_small<true><<<1, kST, 0, st>>>(kin, kout, w.kalt, vin, vout, w.valt, (int)n, lo, npass,
+                                           skip_ones ? 1 : 0);
+    else
+      radix_small<false><<<1, kST, 0, st>>>(kin, kout, w.kalt, nullptr, nullptr, nullptr, (int)n,
+                                            lo, npass, skip_ones ? 1 : 0);
+    return check_launch("radix_small");
+  }
   const int nt = radix_ntiles(n);
   {
     const FillRange fr{w.ghist, (int64_t)sizeof(int) * kMaxPass * 256, 0u};

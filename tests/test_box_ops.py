@@ -256,13 +256,15 @@ def test_nms_c5_full_config(cuda):
 @pytest.mark.gpu
 @pytest.mark.parametrize("thr", [0.3, 0.9])
 def test_nms_pair_capacity_dense_fallback(cuda, thr):
-    """Image 0 is one tight cluster of 12k near-identical boxes: every pair is a
-    grid candidate (n^2/2 = 7.2e7 pairs vs the workspace's 128 per box =
-    1.5e6, csrc/nms.hip kPairsPerBox), so its mask must come from the dense
+    """Image 0 is one tight cluster of 24k near-identical boxes: every pair is a
+    grid candidate (n^2/2 = 2.9e8 pairs vs the workspace's 128 per box =
+    3.1e6, csrc/nms.hip kPairsPerBox), so its mask must come from the dense
     fallback producer; image 1 (ordinary clustered boxes) stays on the grid
-    producer in the same call.  Both bit-exact vs the oracle."""
+    producer in the same call.  Both bit-exact vs the oracle.  (24k rows: the
+    grid producer runs for images above csrc/nms.hip's 20480-row dense
+    limit.)"""
     from jabd_amd import ops, synth
-    n = 12_000
+    n = 24_000
     rng = np.random.default_rng(17)
     ctr = 0.5 + rng.normal(0, 0.002, (n, 2))
     wh = 0.1 * (1 + rng.uniform(0, 0.05, (n, 2)))

@@ -40,7 +40,8 @@ def _ref(keys, vals, lo, npass):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1, 63, 4095, 4096, 4097, 70001, 800000])
+@pytest.mark.parametrize("n", [1, 63, 4095, 4096, 4097, 8193, 16800, 32768, 32769, 70001,
+                               800000])
 @pytest.mark.parametrize("lo,npass,vals", [(24, 5, False), (0, 8, True), (8, 3, True)])
 def test_sort_u64_vs_numpy_stable(cuda, n, lo, npass, vals):
     r = np.random.default_rng(n + lo)
@@ -91,6 +92,31 @@ def test_sort_nms_keys_and_skipped_passes(cuda):
     nv = int(valid.sum())
     assert np.array_equal(vo[:nv], vr[:nv])      # binned keys: stable, values follow
     assert np.array_equal(np.sort(vo[nv:]), np.sort(vr[nv:]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [700, 16800, 32768])
+def test_sort_small_skip_ones_and_copy(cuda, n):
+    """The one-workgroup form (n <= 32768, csrc/radix.hip radix_small):
+    grid-shaped keys with constant high bits (skipped passes) and ~0 keys
+    (skip_ones), and keys identical in every sorted bit (no pass runs: the
+    output is a copy)."""
+    r = np.random.default_rng(n)
+    gk = (np.uint64(3) << np.uint64(56)) | \
+        (r.integers(500, 503, n, dtype=np.uint64) << np.uint64(46)) | \
+        ((r.integers(0, 9, n, dtype=np.uint64) + np.uint64(1 << 17)) << np.uint64(18)) | \
+        (r.integers(0, 300, n, dtype=np.uint64) + np.uint64(1 << 17))
+    gk[r.random(n) < 0.05] = np.uint64(2 ** 64 - 1)
+    gv = np.arange(n, dtype=np.int32)
+    ko, vo = _sort(gk, gv, 0, 8, skip_ones=True)
+    assert np.array_equal(ko, np.sort(gk, kind="stable"))
+    kr, vr = _ref(gk, gv, 0, 8)
+    nv = int((ko != np.uint64(2 ** 64 - 1)).sum())
+    assert np.array_equal(vo[:nv], vr[:nv])
+    same = np.full(n, 0x1234_5678_9ABC_DEF0, dtype=np.uint64)
+    same[::7] ^= np.uint64(0xFF)         # differ only below the sorted bits
+    ko, vo = _sort(same, gv, 8, 7)
+    assert np.array_equal(ko, same) and np.array_equal(vo, gv)
 
 
 @pytest.mark.gpu

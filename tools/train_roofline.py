@@ -115,6 +115,15 @@ def _flops(name, args, sigs=None):
     return 0.0
 
 
+def _shape(args):
+    """Conv calls: 'B HxW Cin->Cout kKH sS [t]' of the argument struct, else ''."""
+    a = args[0]._obj if args and hasattr(args[0], "_obj") else None
+    if a is None or not hasattr(a, "KH"):
+        return ""
+    return (f"{a.B} {a.H}x{a.W} {a.Cin}->{a.Cout} k{a.KH} s{a.stride}" +
+            (" t" if a.tconv else ""))
+
+
 class Tracer:
     def __init__(self, nparams):
         from jabd_amd import _lib
@@ -149,7 +158,7 @@ class Tracer:
             e0.record()
             r = self.orig(name, *args)
             e1.record()
-            self.recs.append((name, e0, e1, _flops(name, args, self.sigs), nbytes))
+            self.recs.append((name, e0, e1, _flops(name, args, self.sigs), nbytes, _shape(args)))
             return r
         for m in mods:
             m.call = traced
@@ -199,10 +208,12 @@ def main():
         parallel.train_step(model, crit, opt, x, tg, pri)
     torch.cuda.synchronize()
     rows = []
-    for name, e0, e1, fl, nb in tr.recs:
+    for name, e0, e1, fl, nb, shp in tr.recs:
         us = e0.elapsed_time(e1) * 1e3
         roof = max(fl / (PEAK_TF * 1e12), nb / (PEAK_TBS * 1e12)) * 1e6
         rows.append({"call": name, "us": us, "gflop": fl / 1e9, "mbytes": nb / 1e6, "roof_us": roof})
+        if shp:
+            rows[-1]["shape"] = shp
     tot_us = sum(r["us"] for r in rows)
     tot_roof = sum(r["roof_us"] for r in rows)
     g = collections.OrderedDict()
