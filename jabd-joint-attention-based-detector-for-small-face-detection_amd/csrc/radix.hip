@@ -287,22 +287,42 @@ __global__ __launch_bounds__(kST) void radix_small(const uint64_t* __restrict__ 
                                                    uint64_t* __restrict__ kalt,
                                                    const int* __restrict__ vin,
                                                    int* __restrict__ vout, int* __restrict__ valt,
-                                                   int n, int lo, int npass, int skip_ones) {
+                                                   int n, int lo, int npass, int skip_ones,
+                                                   const int* __restrict__ n_dev) {
   __shared__ int hist[kMaxPass][256];
   __shared__ int wc[kSWaves][256];
   __shared__ int run[256];
   __shared__ int wsum[4];
   __shared__ int nones;
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  if (n_dev) {  // device-side count: the keys past it are ~0 in the output
+    const int nd = *n_dev;
+    const int nc = nd < n ? (nd > 0 ? nd : 0) : n;
+    for (int i = nc + t; i < n; i += kST) kout[i] = ~0ull;
+    n = nc;
+  }
   for (int i = t; i < kMaxPass * 256; i += kST) (&hist[0][0])[i] = 0;
   if (t == 0) nones = 0;
   __syncthreads();
-  for (int i = t; i < n; i += kST) {
-    const uint64_t key = kin[i];
-    const bool ones = skip_ones && key == ~0ull;
+  for (int i0 = 0; i0 < n; i0 += kST) {   // wave-uniform trip count (ballots inside)
+    const int i = i0 + t;
+    const bool ok = i < n;
+    const uint64_t key = ok ? kin[i] : 0ull;
+    const bool ones = ok && skip_ones && key == ~0ull;
     if (ones) atomicAdd(&nones, 1);
-    for (int p = ones ? npass - 1 : 0; p < npass; ++p)
-      atomicAdd(&hist[p][(int)((key >> (lo + 8 * p)) & 255u)], 1);
+    for (int p = 0; p < npass; ++p) {
+      const bool cnt = ok && (!ones || p == npass - 1);
+      const int d = (int)((key >> (lo + 8 * p)) & 255u);
+      // a digit shared by every counted lane (the high bytes of the scores)
+      // is one add instead of 64 serialised LDS atomics on one address
+      const uint64_t act = __ballot(cnt);
+      const int d0 = __shfl(d, act ? __ffsll((unsigned long long)act) - 1 : 0);
+      if (act && __ballot(cnt && d != d0) == 0) {
+        if (l == __ffsll((unsigned long long)act) - 1) atomicAdd(&hist[p][d0], __popcll(act));
+      } else if (cnt) {
+        atomicAdd(&hist[p][d], 1);
+      }
+    }
   }
   __syncthreads();
   // passes that reorder anything (one bin holding every counted key: skipped)
@@ -501,10 +521,10 @@ int radix_sort64(const uint64_t* kin, uint64_t* kout, const int* vin, int* vout,
   if (n <= kSmallMax && !radix_small_off()) {
     if (vals)
       radix_small<true><<<1, kST, 0, st>>>(kin, kout, w.kalt, vin, vout, w.valt, (int)n, lo, npass,
-                                           skip_ones ? 1 : 0);
+                                           skip_ones ? 1 : 0, nullptr);
     else
       radix_small<false><<<1, kST, 0, st>>>(kin, kout, w.kalt, nullptr, nullptr, nullptr, (int)n,
-                                            lo, npass, skip_ones ? 1 : 0);
+                                            lo, npass, skip_ones ? 1 : 0, nullptr);
     return check_launch("radix_small");
   }
   const int nt = radix_ntiles(n);
@@ -529,6 +549,24 @@ int radix_sort64(const uint64_t* kin, uint64_t* kout, const int* vin, int* vout,
     if (int e = check_launch("radix pass")) return e;
   }
   return JABD_OK;
+}
+
+int64_t radix_small_max() { return radix_small_off() ? 0 : kSmallMax; }
+
+int radix_sort64_devn(const uint64_t* kin, uint64_t* kout, const int* n_dev, int64_t n_cap,
+                      int lo, int npass, void* ws, size_t ws_bytes, hipStream_t st) {
+  JABD_REQUIRE(npass >= 1 && npass <= kMaxPass && lo >= 0 && lo + 8 * npass <= 64,
+               "radix_sort64_devn: bits [%d, %d)", lo, lo + 8 * npass);
+  JABD_REQUIRE(n_cap > 0 && n_cap <= kSmallMax && n_dev, "radix_sort64_devn: n_cap %lld",
+               (long long)n_cap);
+  if (radix_small_off()) return -1;
+  JABD_REQUIRE(ws_bytes >= radix_ws_bytes(n_cap, false), "radix_sort64_devn: workspace");
+  Carve cv(ws, ws_bytes);
+  RadixWs w;
+  carve_radix(cv, n_cap, false, &w);
+  radix_small<false><<<1, kST, 0, st>>>(kin, kout, w.kalt, nullptr, nullptr, nullptr, (int)n_cap,
+                                        lo, npass, 0, n_dev);
+  return check_launch("radix_small (device count)");
 }
 
 size_t scan_ws_bytes(int64_t n) { return align_up(sizeof(int) * (size_t)cdiv(n > 0 ? n : 1, kTile)); }

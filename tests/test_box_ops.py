@@ -128,6 +128,25 @@ def test_batched_nms_with_filter(cuda):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,nv", [(16800, 16800), (16800, 9001), (32768, 30000), (3000, 0)])
+def test_single_image_compacted_keys(cuda, n, nv):
+    """One image (the bs1 predict path: csrc/nms.hip nms_keys_compact + the
+    one-workgroup sort over the candidates alone) with the 0.5 score filter,
+    ~5% exact score ties and a valid-row limit n_valid, against the oracle on
+    the filtered rows; nv = 0: no candidate at all."""
+    from jabd_amd import ops, synth
+    bx, sc = synth.nms_boxes(1, n, seed=n + nv, tie_frac=0.05)
+    sc = sc - 0.25
+    keep, nk = ops.batched_nms(torch.from_numpy(bx).to(cuda), torch.from_numpy(sc).to(cuda),
+                               0.3, score_threshold=0.5,
+                               n_valid=torch.tensor([nv], dtype=torch.int64, device=cuda))
+    keep, nk = keep.cpu().numpy(), nk.cpu().numpy()
+    m = np.nonzero(sc[0][:nv] >= 0.5)[0]
+    ref = m[box_ref.nms(bx[0][m], sc[0][m], 0.3)] if len(m) else np.zeros(0, np.int64)
+    assert keep[0, : nk[0]].tolist() == ref.tolist()
+
+
+@pytest.mark.gpu
 def test_decode_parity(cuda):
     from jabd_amd import ops
     pri = box_ref.anchors(CFG_MNET, (256, 256))
