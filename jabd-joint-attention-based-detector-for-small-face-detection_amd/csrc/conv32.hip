@@ -486,14 +486,14 @@ __global__ __launch_bounds__(256) void m32_ksplit_reduce(const ConvArgs p, int k
 
 // K split of a forward launch (k x k, or 1x1 with its K-concatenated second
 // source) whose grid (`grid` workgroups) cannot fill the device — R50 layer3/4
-// at bs1: enough splits for ~512 workgroups, each keeping >= 8 stages of 32
+// at bs1: enough splits for ~512 workgroups, each keeping >= 4 stages of 32
 // channels; 1 = no split.  Needs a caller workspace (args.ws).
 static int m32_ksplit(const ConvArgs& a, bool kxk, int64_t grid) {
   if (a.tconv || a.Cout % 4 || grid >= 256) return 1;
   const int Kt = kxk ? a.KH * a.KW * a.Cin : a.Cin + (a.x2 ? a.Cin2 : 0);
   const int S = (Kt + kBK - 1) / kBK;
   int ks = (int)std::min<int64_t>(8, (512 + grid - 1) / grid);
-  ks = std::min(ks, S / 8);
+  ks = std::min(ks, S / 4);
   return ks >= 2 ? ks : 1;
 }
 static int64_t m32_ksplit_bytes(const ConvArgs& a, int ks) {
@@ -594,6 +594,25 @@ static int m32_tm(const ConvArgs& a) {
   return (!a.ascale || a.M < 65536) ? 1 : 2;
 }
 
+// N-tiles per workgroup to launch: the packing's tn32, or 1 for a gated GEMM
+// whose grid with tn32 could not fill the device (bs1 MNv3 projects at
+// 20^2-40^2: the 960 -> 160 ones ran 4 workgroups of 5 N-tiles; one N-tile
+// each gives 5x the workgroups: MNv3 640^2 predict 1005 -> 1070 fps).  Not
+// for the ungated R50 GEMMs: layer4 at 32^2 lost 220 -> 189 fps (1024^2
+// predict; its K-split already fills the device and 4x the workgroups each
+// re-read the pixel tile).  JABD_M32_TN1=0 keeps tn32 (A/B).
+static int m32_tn_launch(const ConvArgs& a) {
+  static const bool off = [] {
+    const char* e = getenv("JABD_M32_TN1");
+    return e && e[0] == '0';
+  }();
+  if (off || a.tn32 <= 1 || a.tconv || !a.ascale) return a.tn32;
+  const int64_t BM = 4 * 32 * m32_tm(a);
+  const int64_t OHW = (int64_t)a.OH * a.OW;
+  const int64_t mtiles = a.ascale ? cdiv(OHW, BM) * a.B : cdiv((int64_t)a.B * OHW, BM);
+  return mtiles * (a.ntiles32 / a.tn32) >= 256 ? a.tn32 : 1;
+}
+
 // N-tiles (32 output channels each) per workgroup for the 32x32 kernel.
 // Prefers a 64x128 wave tile (TM=2, TN<=4), else the exact-fit wide tile.
 extern "C" int64_t jabd_conv_workspace_size(const jabd_conv_args* args) {
@@ -604,11 +623,12 @@ extern "C" int64_t jabd_conv_workspace_size(const jabd_conv_args* args) {
   const bool kxk = !(a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0);
   ConvArgs am = a;
   am.M = (int64_t)a.B * a.OH * a.OW;
-  const int TM = m32_tm(am);
+  const int tn = m32_tn_launch(am);
+  const int TM = tn == a.tn32 ? m32_tm(am) : 1;
   const int64_t BM = 4 * 32 * TM;
   const int64_t OHW = (int64_t)a.OH * a.OW;
   const int64_t mtiles = a.ascale ? cdiv(OHW, BM) * a.B : cdiv((int64_t)a.B * OHW, BM);
-  const int64_t grid = mtiles * (a.ntiles32 / a.tn32);
+  const int64_t grid = mtiles * (a.ntiles32 / tn);
   return m32_ksplit_bytes(a, m32_ksplit(a, kxk, grid));
 }
 
@@ -634,6 +654,7 @@ int conv1x1_m32_dispatch(const ConvArgs& a0, hipStream_t st, bool kxk) {
   a.Ntiles = a0.ntiles32;
 #define M32(TM_, TN_) \
   return kxk ? launch_m32<TM_, TN_, true>(a, st) : launch_m32<TM_, TN_, false>(a, st);
+  if (m32_tn_launch(a0) == 1 && a0.tn32 > 1) M32(1, 1)
   if (m32_tm(a0) == 1) {
     switch (a0.tn32) {
       case 1: M32(1, 1)
