@@ -77,6 +77,15 @@ R50 = [
     ("l4.c2s2", 16, 64, 64, 512, 512, 3, 2, 0, 0, 0, "relu"),
     ("l3.c2as", 16, 64, 64, 256, 256, 3, 1, 0, 1, 0, "relu"),
 ]
+# C3 (R50 training, bs64 1024^2) short-K / narrow 1x1 forwards (no bias / act)
+R50T = [
+    ("t.l1.c3", 64, 256, 256, 64, 256, 1, 1, 0, 0, 0, "none"),
+    ("t.l1.c1", 64, 256, 256, 256, 64, 1, 1, 0, 0, 0, "none"),
+    ("t.l2.c3", 64, 128, 128, 128, 512, 1, 1, 0, 0, 0, "none"),
+    ("t.l2.c1", 64, 128, 128, 512, 128, 1, 1, 0, 0, 0, "none"),
+    ("t.l3.c3", 64, 64, 64, 256, 1024, 1, 1, 0, 0, 0, "none"),
+    ("t.l1.c2", 64, 256, 256, 64, 64, 3, 1, 0, 0, 0, "none"),
+]
 
 
 def ref(x, w2d, bias, k, stride, x2, sc, res, act):
@@ -216,7 +225,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="")
     args = ap.parse_args()
-    shapes = {"tr": TR, "mnv3": MNV3, "r50": R50, "all": MNV3 + R50, "xd": XD}[args.set]
+    shapes = {"tr": TR, "mnv3": MNV3, "r50": R50, "r50t": R50T, "all": MNV3 + R50, "xd": XD}[args.set]
     if args.only:
         shapes = [s for s in shapes if s[0] in args.only.split(",")]
     print("# JABD_CONV32=%s JABD_CONV_GENERIC=%s" % (os.environ.get("JABD_CONV32"),
