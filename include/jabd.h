@@ -403,6 +403,24 @@ int64_t jabd_conv1x1_bn_stats_nblk(const jabd_conv_args* args);
  * form does not serve the layer (no bias / activation / gate / residual /
  * second source / split output / transposed form; the caller then runs
  * jabd_conv2d_nhwc_f32 + jabd_bn_stats_f32). */
+/* Data gradient of a conv whose output is the dy of a training BatchNorm +
+ * act (ReLU / LeakyReLU / none; the R50 bottleneck's bn1 / bn2 backward,
+ * nets/resnet_pytorch_r.py:122-143): jabd_conv2d_nhwc_f32 on the 32x32 GEMM
+ * whose epilogue also reads the BatchNorm's input x (pixel stride x_ps) and
+ * writes per-32-pixel-tile sums of dz = dy act'(bn(x)) and dz xhat into
+ * part; jabd_bn_act_bwd_rows_f32 then finishes the BatchNorm backward
+ * without a reduction pass over dy and x.  _part_floats: 0 when the form does
+ * not serve the conv (bias / act / gate / residual / second source / split
+ * output, Cout % 32, a stride-2 transposed form). */
+int64_t jabd_conv_bn_bwd_part_floats(const jabd_conv_args* args);
+int jabd_conv_bn_bwd_sums_f32(const jabd_conv_args* args, const float* x, int32_t x_ps,
+                              const float* mean, const float* invstd, const float* gamma,
+                              const float* beta, int32_t act, float slope, float* part,
+                              int64_t part_floats, jabd_stream_t stream);
+int jabd_bn_act_bwd_rows_f32(float* part, const float* dy, const float* x, int64_t M,
+                             int32_t C, const float* mean, const float* invstd,
+                             const float* gamma, const float* beta, int32_t act, float slope,
+                             float* dgamma, float* dbeta, float* dx, jabd_stream_t stream);
 int64_t jabd_conv_bn_stats_part_floats(const jabd_conv_args* args);
 int jabd_conv_bn_stats_f32(const jabd_conv_args* args, float* part, int64_t part_floats,
                            float* mean, float* invstd, float* running_mean, float* running_var,

@@ -760,7 +760,9 @@ namespace jabd {
 bool stem7_ok(const ConvArgs& a);
 int stem7_fwd_launch(const ConvArgs& a, hipStream_t st);
 int conv1x1_m32_dispatch(const ConvArgs& a, hipStream_t st, bool kxk);
-int conv_m32_stats_dispatch(const ConvArgs& a, bool kxk, float* part, hipStream_t st);
+int conv_m32_stats_dispatch(const ConvArgs& a, bool kxk, float* part, const BnEpi& bb,
+                            hipStream_t st);
+int64_t bn_rows_sum_doubles(int64_t M, int C);
 int64_t bn_rows_chunk_doubles(int64_t M, int C);
 int bn_rows_final_launch(const float* rows, int ldc, int64_t M, int C, double* chunks,
                          float* mean, float* invstd, float* rmean, float* rvar, float momentum,
@@ -928,11 +930,66 @@ extern "C" int jabd_conv_bn_stats_f32(const jabd_conv_args* args, float* part, i
                (long long)(rows + 2 * bn_rows_chunk_doubles(a.M, a.Cout)));
   JABD_REQUIRE(((uintptr_t)part & 15) == 0, "conv_bn_stats: part must be 16-byte aligned");
   hipStream_t st = as_stream(stream);
-  const int r = conv_m32_stats_dispatch(a, kxk, part, st);
+  const int r = conv_m32_stats_dispatch(a, kxk, part, BnEpi{}, st);
   if (r != JABD_OK) return r < 0 ? JABD_EINVAL : r;
   return bn_rows_final_launch(part, a.ntiles32 * 32, a.M, a.Cout,
                               reinterpret_cast<double*>(part + rows), mean, invstd, running_mean,
                               running_var, momentum, eps, st);
+}
+
+// The BatchNorm-backward form (BB): a bias-free data gradient (1x1 plain,
+// or k x k transposed at stride 1) whose output is the dy of a BatchNorm +
+// ReLU / LeakyReLU / identity with Cout % 32 == 0 (the R50 bottleneck's bn1 /
+// bn2 backward, nets/resnet_pytorch_r.py:122-143).
+static bool conv_m32_bb_form(const ConvArgs& a, bool fast1x1, bool vec4, bool& kxk) {
+  static const bool on = [] {
+    const char* e = getenv("JABD_CONV_BNBWD32");
+    return !(e && e[0] == '0');
+  }();
+  const bool is1x1 = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && !a.tconv;
+  kxk = !is1x1;
+  const int64_t OHW = (int64_t)a.OH * a.OW;
+  if (!on || conv_generic_only() || a.bias || a.res || a.ascale || a.x2 || a.y2 ||
+      a.act != ACT_NONE || a.nchw_in || !(a.flags & 1) || a.Cout % 32)
+    return false;
+  if (!a.w32 || a.tn32 < 1 || a.tn32 > 4 || a.ntiles32 % a.tn32 || a.ntiles32 * 32 != a.Cout)
+    return false;
+  if (is1x1) return fast1x1;
+  return vec4 && a.Cin % 32 == 0 && a.x_bs % 4 == 0 && a.y_bs == OHW * a.y_ps &&
+         (!a.tconv || a.stride == 1);
+}
+
+extern "C" int64_t jabd_conv_bn_bwd_part_floats(const jabd_conv_args* args) {
+  ConvArgs a;
+  bool fast1x1 = false, vec4 = false, kxk = false;
+  if (conv_setup(args, a, fast1x1, vec4) != JABD_OK || !conv_m32_bb_form(a, fast1x1, vec4, kxk))
+    return 0;
+  return cdiv(a.M, (int64_t)32) * 2 * a.Cout + 2 * bn_rows_sum_doubles(a.M, a.Cout);
+}
+
+extern "C" int jabd_conv_bn_bwd_sums_f32(const jabd_conv_args* args, const float* x, int32_t x_ps,
+                                         const float* mean, const float* invstd,
+                                         const float* gamma, const float* beta, int32_t act,
+                                         float slope, float* part, int64_t part_floats,
+                                         jabd_stream_t stream) {
+  ConvArgs a;
+  bool fast1x1 = false, vec4 = false, kxk = false;
+  {
+    const int e = conv_setup(args, a, fast1x1, vec4);
+    if (e != JABD_OK) return e;
+  }
+  JABD_REQUIRE(conv_m32_bb_form(a, fast1x1, vec4, kxk),
+               "conv_bn_bwd_sums: layer not served by the 32x32 BatchNorm-backward form");
+  JABD_REQUIRE(x && mean && invstd && gamma && beta && part && x_ps % 4 == 0 && x_ps >= a.Cout &&
+                   (act == ACT_NONE || act == ACT_RELU || act == ACT_LEAKY),
+               "conv_bn_bwd_sums: bad BatchNorm arguments");
+  const int64_t need = cdiv(a.M, (int64_t)32) * 2 * a.Cout + 2 * bn_rows_sum_doubles(a.M, a.Cout);
+  JABD_REQUIRE(part_floats >= need && ((uintptr_t)part & 15) == 0,
+               "conv_bn_bwd_sums: part holds %lld floats, %lld needed (16-byte aligned)",
+               (long long)part_floats, (long long)need);
+  BnEpi bb{x, mean, invstd, gamma, beta, part, x_ps, act, slope};
+  const int r = conv_m32_stats_dispatch(a, kxk, nullptr, bb, as_stream(stream));
+  return r < 0 ? JABD_EINVAL : r;
 }
 
 extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t stream) {

@@ -64,7 +64,7 @@ constexpr int kGateLds = 1024;   // ECA gate channels staged in LDS
 // KXK: k x k implicit GEMM (tap-major K; every 32-channel stage lies inside
 // one tap, host guarantees Cin % 32 == 0, no K-concat source); stride-1
 // transposed form (tconv) for the data gradient.
-template <int TM, int TN, bool KXK, bool AS, bool ST = false>
+template <int TM, int TN, bool KXK, bool AS, bool ST = false, bool BB = false>
 // AS: the ECA gate (ascale) is set — staged in LDS, applied at the weight store.
 // ST (TM = 1, training forward, no bias / residual / act): the epilogue also
 // writes the following BatchNorm's statistics per 32-pixel wave tile, row
@@ -72,6 +72,11 @@ template <int TM, int TN, bool KXK, bool AS, bool ST = false>
 // squared deviations (Sum (y - sh) and Sum (y - sh)^2 around the tile's first
 // pixel, then mean = sh + S/n, M2 = Q - S^2/n); jabd_bn_stats_final_rows_f32
 // combines the rows exactly (Chan) in a fixed order.
+// BB (TM = 1, a data gradient whose output is the dy of a BatchNorm + act):
+// the epilogue also reads that BatchNorm's input x at the tile's pixels and
+// writes per 32-pixel wave tile the sums of dz = dy * act'(bn(x)) and of
+// dz * xhat (bn_bwd_part's terms) to bb.rows[r][0|1][Ntiles*32] — the
+// reduction pass over dy and x the BatchNorm backward would otherwise make.
 // phase >= 0 (KXK, stride-2 tconv): this launch covers only the output
 // pixels (2i + ph, 2j + pw), phase = 2 ph + pw, and only the taps that reach
 // them — the sub-pixel decomposition of a strided data gradient (the other
@@ -81,7 +86,8 @@ template <int TM, int TN, bool KXK, bool AS, bool ST = false>
 // the ks partials in order and applies the epilogue.
 __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, int mtiles_img,
                                                              int per_img, int phase, int ks,
-                                                             float* __restrict__ part) {
+                                                             float* __restrict__ part,
+                                                             const BnEpi bb) {
   constexpr int BM = 4 * 32 * TM;
   constexpr int NB4 = kG * TN * 64;            // float4 of one weight stage
   constexpr int NBT = (NB4 + 255) / 256;       // ... per thread
@@ -360,20 +366,54 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
       for (int u = 0; u < TN; ++u) {
         const int nb0 = (nb * TN + u) * 32;
         if (nb0 >= p.Cout) break;  // wave-uniform
+        const int n = nb0 + 4 * ep_q;
+        float4 ss = make_float4(0.f, 0.f, 0.f, 0.f), sq = ss, sh = ss;
+        float4 bmu = sh, bis = sh, bgm = sh, bbt = sh;
+        float4 bx[4];
+        if constexpr (BB) {  // issued before the LDS round trip: in flight across it
+          if (n < p.Cout) {
+            bmu = *reinterpret_cast<const float4*>(bb.mean + n);
+            bis = *reinterpret_cast<const float4*>(bb.invstd + n);
+            bgm = *reinterpret_cast<const float4*>(bb.gamma + n);
+            bbt = *reinterpret_cast<const float4*>(bb.beta + n);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r)   // the BatchNorm input at the tile's pixels, in flight
+            bx[r] = (prow[r] >= 0 && n < p.Cout)
+                        ? *reinterpret_cast<const float4*>(bb.x + (int64_t)mrow[r] * bb.x_ps + n)
+                        : sh;
+        }
 #pragma unroll
         for (int c = 0; c < 4; ++c)
           *reinterpret_cast<float4*>(ep + j * kEpiPitch + 8 * c + 4 * h) =
               make_float4(acc[t][u][4 * c], acc[t][u][4 * c + 1], acc[t][u][4 * c + 2],
                           acc[t][u][4 * c + 3]);
         wave_lds_sync32();
-        const int n = nb0 + 4 * ep_q;
-        float4 ss = make_float4(0.f, 0.f, 0.f, 0.f), sq = ss, sh = ss;
         if constexpr (ST) sh = *reinterpret_cast<const float4*>(ep + 4 * ep_q);  // pixel 0
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int px = ep_px + 8 * r;
           if (prow[r] < 0 || n >= p.Cout) continue;
           float4 v = *reinterpret_cast<const float4*>(ep + px * kEpiPitch + 4 * ep_q);
+          if constexpr (BB) {
+            // as bn_bwd_part / bn_bwd_apply (train.hip): xhat, act'(xhat gamma + beta)
+            const float xv[4] = {bx[r].x, bx[r].y, bx[r].z, bx[r].w};
+            const float mu[4] = {bmu.x, bmu.y, bmu.z, bmu.w}, is[4] = {bis.x, bis.y, bis.z, bis.w};
+            const float gm[4] = {bgm.x, bgm.y, bgm.z, bgm.w}, bt[4] = {bbt.x, bbt.y, bbt.z, bbt.w};
+            const float gv[4] = {v.x, v.y, v.z, v.w};
+            float dzs[4], dzx[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float xh = (xv[e] - mu[e]) * is[e];
+              const float z = fmaf(xh, gm[e], bt[e]);
+              const float d = bb.act == ACT_RELU ? (z > 0.f ? 1.f : 0.f)
+                              : bb.act == ACT_LEAKY ? (z > 0.f ? 1.f : bb.slope) : 1.f;
+              dzs[e] = gv[e] * d;
+              dzx[e] = dzs[e] * xh;
+            }
+            ss.x += dzs[0]; ss.y += dzs[1]; ss.z += dzs[2]; ss.w += dzs[3];
+            sq.x += dzx[0]; sq.y += dzx[1]; sq.z += dzx[2]; sq.w += dzx[3];
+          }
           if constexpr (ST) {
             const float dx = v.x - sh.x, dy = v.y - sh.y, dz = v.z - sh.z, dw = v.w - sh.w;
             ss.x += dx; ss.y += dy; ss.z += dz; ss.w += dw;
@@ -394,6 +434,21 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
           v.z = act32(v.z, p.act, p.slope);
           v.w = act32(v.w, p.act, p.slope);
           *reinterpret_cast<float4*>(p.y + (int64_t)mrow[r] * p.y_ps + p.y_c0 + n) = v;
+        }
+        if constexpr (BB) {
+#pragma unroll
+          for (int off = 8; off <= 32; off <<= 1) {
+            ss.x += __shfl_xor(ss.x, off); ss.y += __shfl_xor(ss.y, off);
+            ss.z += __shfl_xor(ss.z, off); ss.w += __shfl_xor(ss.w, off);
+            sq.x += __shfl_xor(sq.x, off); sq.y += __shfl_xor(sq.y, off);
+            sq.z += __shfl_xor(sq.z, off); sq.w += __shfl_xor(sq.w, off);
+          }
+          if (ep_px == 0 && (int64_t)srow * 32 < p.M && n < p.Cout) {
+            const int ldc = p.Ntiles * 32;
+            float* pr = bb.rows + (int64_t)srow * 2 * ldc + n;
+            *reinterpret_cast<float4*>(pr) = ss;
+            *reinterpret_cast<float4*>(pr + ldc) = sq;
+          }
         }
         if constexpr (ST) {
           // the 8 lanes of one channel quad (lane xor 8, 16, 32), fixed order
@@ -524,7 +579,8 @@ static int launch_m32_as(const ConvArgs& a, hipStream_t st) {
         const int64_t grid = cdiv(Mp, BM) * (a.Ntiles / TN);
         JABD_REQUIRE(grid < (int64_t)0x7fffffff, "conv32: grid too large");
         conv1x1_m32_kernel<TM, TN, KXK, AS><<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, 0,
-                                                                        2 * ph + pw, 1, nullptr);
+                                                                        2 * ph + pw, 1, nullptr,
+                                                                        BnEpi{});
         if (int e = check_launch("conv1x1_m32")) return e;
       }
     return JABD_OK;
@@ -536,33 +592,40 @@ static int launch_m32_as(const ConvArgs& a, hipStream_t st) {
   if (ks > 1 && a.ws_bytes >= m32_ksplit_bytes(a, ks)) {
     float* part = static_cast<float*>(a.ws);
     conv1x1_m32_kernel<TM, TN, KXK, AS><<<dim3((unsigned)grid, (unsigned)ks), 256, 0, st>>>(
-        a, (int)mt_img, per_img, -1, ks, part);
+        a, (int)mt_img, per_img, -1, ks, part, BnEpi{});
     if (int e = check_launch("conv1x1_m32 (split K)")) return e;
     const int64_t n4 = a.M * ((a.Cout + 3) / 4);
     m32_ksplit_reduce<<<(unsigned)cdiv(n4, 256), 256, 0, st>>>(a, ks, part);
     return check_launch("m32_ksplit_reduce");
   }
   conv1x1_m32_kernel<TM, TN, KXK, AS><<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, per_img, -1,
-                                                                     1, nullptr);
+                                                                     1, nullptr, BnEpi{});
   return check_launch("conv1x1_m32");
 }
 
 // Forward conv on the 32x32 kernel with the BatchNorm statistics rows (ST):
 // 32-pixel wave tiles, no gate / split / bias / residual / activation.
+// (bb.rows set: the BatchNorm-backward sums form instead)
 template <int TN, bool KXK>
-static int launch_m32_stats(const ConvArgs& a, float* part, hipStream_t st) {
+static int launch_m32_stats(const ConvArgs& a, float* part, const BnEpi& bb, hipStream_t st) {
   const int64_t grid = cdiv(a.M, (int64_t)128) * (a.Ntiles / TN);
   JABD_REQUIRE(grid < (int64_t)0x7fffffff, "conv32 stats: grid too large");
+  if (bb.rows) {
+    conv1x1_m32_kernel<1, TN, KXK, false, false, true><<<(unsigned)grid, 256, 0, st>>>(
+        a, (int)cdiv((int64_t)a.OH * a.OW, 128), 0, -1, 1, nullptr, bb);
+    return check_launch("conv1x1_m32 (BN backward sums)");
+  }
   conv1x1_m32_kernel<1, TN, KXK, false, true><<<(unsigned)grid, 256, 0, st>>>(
-      a, (int)cdiv((int64_t)a.OH * a.OW, 128), 0, -1, 1, part);
+      a, (int)cdiv((int64_t)a.OH * a.OW, 128), 0, -1, 1, part, BnEpi{});
   return check_launch("conv1x1_m32 (BN statistics)");
 }
 
-int conv_m32_stats_dispatch(const ConvArgs& a0, bool kxk, float* part, hipStream_t st) {
+int conv_m32_stats_dispatch(const ConvArgs& a0, bool kxk, float* part, const BnEpi& bb,
+                            hipStream_t st) {
   ConvArgs a = a0;
   a.w = a0.w32;
   a.Ntiles = a0.ntiles32;
-#define MS(TN_) return kxk ? launch_m32_stats<TN_, true>(a, part, st) : launch_m32_stats<TN_, false>(a, part, st);
+#define MS(TN_) return kxk ? launch_m32_stats<TN_, true>(a, part, bb, st) : launch_m32_stats<TN_, false>(a, part, bb, st);
   switch (a0.tn32) {
     case 1: MS(1)
     case 2: MS(2)

@@ -13,6 +13,16 @@ enum {
   ACT_HSIGMOID = JABD_ACT_HSIGMOID,
   ACT_SIGMOID = JABD_ACT_SIGMOID,
 };
+// The 32x32 GEMM's BatchNorm-backward epilogue (jabd_conv_bn_bwd_sums_f32):
+// the GEMM output is the dy of a BatchNorm (+ act) whose pre-BN input x and
+// parameters these are; rows: per-32-pixel-tile sums of dz and dz * xhat.
+struct BnEpi {
+  const float* x;
+  const float *mean, *invstd, *gamma, *beta;
+  float* rows;
+  int x_ps, act;
+  float slope;
+};
 // conv1x1_stream_dispatch's statistics form (jabd_conv1x1_bn_stats_*)
 struct StreamStats {
   float* part;

@@ -225,6 +225,44 @@ __global__ __launch_bounds__(256) void bn_rows_chunk_kernel(const float* __restr
   out[chunk * 2 * C + C + c] = Q;
 }
 
+// Plain fp64 sums of kRowChunk-row chunks of rows[r][0|1][C] (the 32x32
+// GEMM's BatchNorm-backward epilogue rows), in row order, to out[chunk][0|1][C].
+__global__ __launch_bounds__(256) void bn_rows_sum_kernel(const float* __restrict__ rows,
+                                                          int64_t nrow, int C,
+                                                          double* __restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t chunk = i / C;
+  const int c = (int)(i - chunk * C);
+  const int64_t r0 = chunk * kRowChunk;
+  if (r0 >= nrow) return;
+  const int64_t r1 = min(r0 + kRowChunk, nrow);
+  double S = 0.0, Q = 0.0;
+  int64_t r = r0;
+  for (; r + 8 <= r1; r += 8) {
+    float a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a[u] = rows[(r + u) * 2 * C + c];
+      b[u] = rows[(r + u) * 2 * C + C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      S += (double)a[u];
+      Q += (double)b[u];
+    }
+  }
+  for (; r < r1; ++r) {
+    S += (double)rows[r * 2 * C + c];
+    Q += (double)rows[r * 2 * C + C + c];
+  }
+  out[chunk * 2 * C + c] = S;
+  out[chunk * 2 * C + C + c] = Q;
+}
+
+int64_t bn_rows_sum_doubles(int64_t M, int C) {
+  return cdiv(cdiv(M, (int64_t)32), (int64_t)kRowChunk) * 2 * C;
+}
+
 int64_t bn_rows_chunk_doubles(int64_t M, int C) {
   return cdiv(cdiv(M, (int64_t)32), (int64_t)kRowChunk) * 2 * C;
 }
@@ -481,8 +519,9 @@ __global__ __launch_bounds__(kRedThreads) void bn_bwd_part_kernel(
   }
 }
 
+template <typename T>
 __global__ __launch_bounds__(kFinThreads) void bn_bwd_final_kernel(
-    const float* __restrict__ part, int64_t nblk, int C, float* __restrict__ dbeta,
+    const T* __restrict__ part, int64_t nblk, int C, float* __restrict__ dbeta,
     float* __restrict__ dgamma) {
   double S, Q;
   bn_final_sums(part, nblk, C, S, Q);
@@ -1830,8 +1869,8 @@ extern "C" int jabd_bn_act_bwd_ex_f32(const float* dy, int32_t lddy, int32_t dyc
                                                 invstd, gamma, beta, act, slope, per, part, dys,
                                                 dya, hw);
   if (int e = check_launch("bn_bwd_part")) return e;
-  bn_bwd_final_kernel<<<(unsigned)cdiv(C, kFinLanes), kFinThreads, 0, st>>>(part, nblk, C,
-                                                                            dbeta, dgamma);
+  bn_bwd_final_kernel<float><<<(unsigned)cdiv(C, kFinLanes), kFinThreads, 0, st>>>(
+      part, nblk, C, dbeta, dgamma);
   if (int e = check_launch("bn_bwd_final")) return e;
   int lanes;
   const dim3 grid = ew_grid(M, C, lanes);
@@ -1900,6 +1939,36 @@ extern "C" int64_t jabd_conv_wgrad_part_floats(const jabd_conv_args* args) {
   if (stem_wgrad_ok(a)) return stem_wgrad_waves(a) * KN;
   if (stem7_wgrad_on(a)) return stem7_wgrad_groups(a) * KN;
   return wgrad_chunks(a) * KN;
+}
+
+// BatchNorm + act backward from the sums a data-gradient GEMM took in its
+// epilogue (jabd_conv_bn_bwd_sums_f32's part: rows then the fp64 chunks):
+// fixed-order fp64 sums -> dbeta = sum dz, dgamma = sum dz * xhat, then the
+// apply pass dx = gamma invstd (dz - dbeta/M - xhat dgamma/M), as
+// jabd_bn_act_bwd_f32 without its reduction pass.
+extern "C" int jabd_bn_act_bwd_rows_f32(float* part, const float* dy, const float* x,
+                                        int64_t M, int32_t C, const float* mean,
+                                        const float* invstd, const float* gamma,
+                                        const float* beta, int32_t act, float slope,
+                                        float* dgamma, float* dbeta, float* dx,
+                                        jabd_stream_t stream) {
+  JABD_REQUIRE(part && dy && x && mean && invstd && gamma && beta && dgamma && dbeta && dx &&
+                   M > 0 && C > 0 && C % 32 == 0 && ((uintptr_t)part & 15) == 0,
+               "bn_act_bwd_rows: bad args");
+  hipStream_t st = as_stream(stream);
+  const int64_t nrow = cdiv(M, (int64_t)32), nch = cdiv(nrow, (int64_t)kRowChunk);
+  double* chunks = reinterpret_cast<double*>(part + nrow * 2 * C);
+  bn_rows_sum_kernel<<<(unsigned)cdiv(nch * C, (int64_t)256), 256, 0, st>>>(part, nrow, C, chunks);
+  if (int e = check_launch("bn_rows_sum")) return e;
+  bn_bwd_final_kernel<double><<<(unsigned)cdiv(C, kFinLanes), kFinThreads, 0, st>>>(
+      chunks, nch, C, dbeta, dgamma);
+  if (int e = check_launch("bn_bwd_final (rows)")) return e;
+  int lanes;
+  const dim3 grid = ew_grid(M, C, lanes);
+  bn_bwd_apply_kernel<false, false><<<grid, kRedThreads, 0, st>>>(
+      dy, C, 0, x, C, nullptr, C, M, C, mean, invstd, gamma, beta, act, slope, dbeta, dgamma, dx,
+      nullptr, lanes, nullptr, nullptr, 0);
+  return check_launch("bn_bwd_apply (rows)");
 }
 
 extern "C" int jabd_conv_wgrad_f32(const jabd_conv_args* args, float* part, float* dw,

@@ -173,6 +173,11 @@ SIGNATURES = {
     "jabd_conv1x1_bn_stats_f32": [ctypes.POINTER(ConvArgs), c_vp, c_i64, c_vp, c_vp],
     "jabd_conv_workspace_size": [ctypes.POINTER(ConvArgs)],
     "jabd_conv_bn_stats_part_floats": [ctypes.POINTER(ConvArgs)],
+    "jabd_conv_bn_bwd_part_floats": [ctypes.POINTER(ConvArgs)],
+    "jabd_conv_bn_bwd_sums_f32": [ctypes.POINTER(ConvArgs), c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
+                                  c_i32, c_f32, c_vp, c_i64, c_vp],
+    "jabd_bn_act_bwd_rows_f32": [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32,
+                                 c_f32, c_vp, c_vp, c_vp, c_vp],
     "jabd_conv_bn_stats_f32": [ctypes.POINTER(ConvArgs), c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,
                                c_f32, c_f32, c_vp],
     "jabd_stem_nchw_f32": [c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp],
@@ -281,6 +286,7 @@ _RESTYPE = {"jabd_version": ctypes.c_char_p, "jabd_dw_nblk": ctypes.c_int64,
             "jabd_dwconv_stats_nblk": ctypes.c_int64,
             "jabd_conv1x1_bn_stats_nblk": ctypes.c_int64,
             "jabd_conv_bn_stats_part_floats": ctypes.c_int64,
+            "jabd_conv_bn_bwd_part_floats": ctypes.c_int64,
             "jabd_adam_num_chunks": ctypes.c_int64, "jabd_beca_ws_floats": ctypes.c_int64,
             "jabd_adaptive_pool_ws_floats": ctypes.c_int64,
             "jabd_abi_struct_size": ctypes.c_int64, "jabd_conv_workspace_size": ctypes.c_int64,

@@ -45,6 +45,9 @@ ECA_SUMS = __import__("os").environ.get("JABD_ECA_SUMS", "1") != "0"
 # statistics from their own pass over e_pre instead of conv1's streaming kernel
 # (A/B)
 DW_BN_FUSE = __import__("os").environ.get("JABD_DW_BN_FUSE", "1") != "0"
+# R50 bn1 / bn2 backward sums in the data-gradient GEMM's epilogue
+# (_dgrad_bn_sums); JABD_BN_BWD_EPI=0 keeps the separate reduction pass (A/B)
+BN_BWD_EPI = __import__("os").environ.get("JABD_BN_BWD_EPI", "1") != "0"
 # JABD_DW_BNIN=0: bn1 + act written out as e and read by conv2 and its weight
 # gradient, instead of applied on their loads from e_pre (A/B; needs
 # DW_BN_FUSE).  Only the 3x3 stride-2 blocks take it: their kernels load each
@@ -974,6 +977,41 @@ def _conv_fwd_stats(x, weight, bn, stride=1, pad=0):
     return y, (mean, invstd)
 
 
+def _dgrad_bn_sums(dy, weight, stride, pad, H, W, x, st, act):
+    """_dgrad whose output is the dy of the BatchNorm (+ act) st of x: the
+    32x32 GEMM's epilogue also takes that BatchNorm backward's sums
+    (jabd_conv_bn_bwd_sums_f32).  Returns (dx, part) — part None when the
+    form does not serve the conv (then _bn_bwd takes the sums itself)."""
+    pk = _packed(weight, transposed=True)
+    B = dy.shape[0]
+    dx = torch.empty((B, H, W, pk.Cout), dtype=torch.float32, device=dy.device)
+    plain = pk.KH == 1 and pk.KW == 1 and stride == 1 and pad == 0
+    a = _conv_args(dy, pk, dx, stride, pad, tconv=not plain, OH=H, OW=W)
+    nf = int(lib().jabd_conv_bn_bwd_part_floats(ctypes.byref(a))) if BN_BWD_EPI else 0
+    if nf <= 0 or not x.is_contiguous():
+        call("jabd_conv2d_nhwc_f32", ctypes.byref(a), _st())
+        return dx, None
+    g, b, mean, invstd = st
+    part = torch.empty(nf, dtype=torch.float32, device=dy.device)
+    call("jabd_conv_bn_bwd_sums_f32", ctypes.byref(a), x.data_ptr(), x.shape[3], mean.data_ptr(),
+         invstd.data_ptr(), g.data_ptr(), b.data_ptr(), ACT[act], 0.0, part.data_ptr(), nf,
+         _st())
+    return dx, part
+
+
+def _bn_bwd_rows(dy, x, st, act, part):
+    """_bn_bwd (no residual) from the sums _dgrad_bn_sums took."""
+    g, b, mean, invstd = st
+    B, H, W, C = x.shape
+    dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
+    dbeta = torch.empty_like(dgamma)
+    dx = torch.empty_like(x)
+    call("jabd_bn_act_bwd_rows_f32", part.data_ptr(), dy.data_ptr(), x.data_ptr(), B * H * W, C,
+         mean.data_ptr(), invstd.data_ptr(), g.data_ptr(), b.data_ptr(), ACT[act], 0.0,
+         dgamma.data_ptr(), dbeta.data_ptr(), dx.data_ptr(), _st())
+    return dx, dgamma, dbeta, None
+
+
 def _dgrad_1x1_res(dy, weight, res):
     """dx = dgrad of a 1x1 / stride-1 conv, + res added in the GEMM epilogue."""
     pk = _packed(weight, transposed=True)
@@ -1342,11 +1380,15 @@ class R50BlockFn(torch.autograd.Function):
         dout = dout.contiguous()
         dp3, dg3, db3, dres = _bn_bwd(dout, t3p, st3, "relu", res=idn, want_dres=True)
         dW3 = _wgrad(t2, dp3, blk.conv3.weight, 1, 0)
-        dt2 = _dgrad(dp3, blk.conv3.weight, 1, 0, t2.shape[1], t2.shape[2])
-        dp2, dg2, db2, _ = _bn_bwd(dt2, t2p, st2, "relu")
+        # the data-gradient GEMMs also take the next BatchNorm backward's sums
+        dt2, pt2 = _dgrad_bn_sums(dp3, blk.conv3.weight, 1, 0, t2.shape[1], t2.shape[2], t2p,
+                                  st2, "relu")
+        dp2, dg2, db2, _ = (_bn_bwd_rows(dt2, t2p, st2, "relu", pt2) if pt2 is not None
+                            else _bn_bwd(dt2, t2p, st2, "relu"))
         dW2 = _wgrad(t1, dp2, blk.conv2.weight, stride, 1)
-        dt1 = _dgrad(dp2, blk.conv2.weight, stride, 1, H, W)
-        dp1, dg1, db1, _ = _bn_bwd(dt1, t1p, st1, "relu")
+        dt1, pt1 = _dgrad_bn_sums(dp2, blk.conv2.weight, stride, 1, H, W, t1p, st1, "relu")
+        dp1, dg1, db1, _ = (_bn_bwd_rows(dt1, t1p, st1, "relu", pt1) if pt1 is not None
+                            else _bn_bwd(dt1, t1p, st1, "relu"))
         dW1 = _wgrad(x, dp1, blk.conv1.weight, 1, 0)
         grads = (dW1, dg1, db1, dW2, dg2, db2, dW3, dg3, db3)
         if blk.downsample is not None:

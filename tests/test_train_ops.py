@@ -533,6 +533,48 @@ def test_conv_bn_stats32(cuda, cin, cout, k, stride, bhw, scale):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,k,stride,bhw,scale", [
+    (64, 256, 1, 1, (2, 40, 36), 1.0), (128, 512, 1, 1, (3, 17, 19), 50.0),
+    (64, 64, 3, 1, (2, 33, 31), 1.0), (128, 128, 3, 1, (1, 9, 7), 50.0),
+    (128, 128, 3, 2, (2, 34, 30), 1.0)])
+def test_dgrad_bn_bwd_sums(cuda, cin, cout, k, stride, bhw, scale):
+    """The R50 bn1 / bn2 backward sums taken in the data-gradient GEMM's
+    epilogue (jabd_conv_bn_bwd_sums_f32 + jabd_bn_act_bwd_rows_f32) against
+    the plain data gradient + jabd_bn_act_bwd_ex_f32 (its own reduction pass):
+    the data gradient, dx, dgamma and dbeta within fp32 reassociation, incl.
+    x50 inputs with a large mean and ragged tiles; a stride-2 transposed conv
+    is not served (part None)."""
+    from jabd_amd import train as T
+    B, H, W = bhw
+    pad = k // 2
+    OH, OW = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    g = torch.Generator().manual_seed(cin + 7 * cout + k)
+    dev = torch.device(cuda)
+    w = (torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5).to(dev)
+    dy = torch.randn(B, OH, OW, cout, generator=g).to(dev)
+    x = ((torch.randn(B, H, W, cin, generator=g) + 2.0) * scale).to(dev)   # the BN's input
+    xm = x.reshape(-1, cin).double()
+    mean = xm.mean(0).float()
+    invstd = (xm.var(0, unbiased=False) + 1e-5).rsqrt().float()
+    gam = (1 + 0.3 * torch.randn(cin, generator=g)).to(dev)
+    bet = (0.2 * torch.randn(cin, generator=g)).to(dev)
+    st = (gam, bet, mean, invstd)
+    d1, part = T._dgrad_bn_sums(dy, w, stride, pad, H, W, x, st, "relu")
+    d2 = T._dgrad(dy, w, stride, pad, H, W)
+    torch.cuda.synchronize()
+    assert rel_err(d1.cpu(), d2.cpu()) < 1e-5
+    if stride == 2:
+        assert part is None
+        return
+    assert part is not None, "the BatchNorm-backward form expected to serve this conv"
+    r1 = T._bn_bwd_rows(d1, x, st, "relu", part)
+    r2 = T._bn_bwd(d1, x, st, "relu")
+    torch.cuda.synchronize()
+    for a, b, name in zip(r1[:3], r2[:3], ("dx", "dgamma", "dbeta")):
+        assert rel_err(a.cpu(), b.cpu()) < 1e-5, name
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("c,k,s,bhw,act", [(64, 3, 2, (2, 66, 50), "relu"), (72, 3, 1, (3, 31, 29), "relu"),
                                            (120, 5, 1, (2, 17, 19), "hswish"),
                                            (240, 5, 2, (2, 21, 16), "hswish")])

@@ -74,7 +74,8 @@ def _ptr_args(name, args, sigs):
                     if v:
                         out.append(v)
             continue
-        if name == "jabd_conv_bn_stats_f32" and i == 1:   # the statistics rows: workspace
+        if (name, i) in (("jabd_conv_bn_stats_f32", 1), ("jabd_conv_bn_bwd_sums_f32", 9),
+                         ("jabd_bn_act_bwd_rows_f32", 0)):   # the epilogue rows: workspace
             continue
         if t is ctypes.c_void_p:
             nxt = types[i + 1] if i + 1 < len(types) else None
@@ -91,11 +92,11 @@ _INT_TYPES = (ctypes.c_int32, ctypes.c_int, ctypes.c_int64)
 
 def _flops(name, args, sigs=None):
     if name in ("jabd_conv2d_nhwc_f32", "jabd_conv_wgrad_f32", "jabd_conv1x1_bn_stats_f32",
-                "jabd_conv_wgrad_eca_f32", "jabd_conv_bn_stats_f32"):
+                "jabd_conv_wgrad_eca_f32", "jabd_conv_bn_stats_f32", "jabd_conv_bn_bwd_sums_f32"):
         a = args[0]._obj if hasattr(args[0], "_obj") else None
         if a is None:
             return 0.0
-        if name != "jabd_conv2d_nhwc_f32" or not a.tconv:
+        if name not in ("jabd_conv2d_nhwc_f32", "jabd_conv_bn_bwd_sums_f32") or not a.tconv:
             return 2.0 * a.B * a.OH * a.OW * (a.KH * a.KW * a.Cin + a.Cin2) * a.Cout
         return 2.0 * a.B * a.H * a.W * a.KH * a.KW * a.Cin * a.Cout
     if name == "jabd_expand_dw_nhwc_f32":
