@@ -1710,6 +1710,39 @@ __global__ __launch_bounds__(256) void maxpool_bwd_idx4_kernel(const uchar4* __r
   reinterpret_cast<float4*>(dx)[i] = make_float4(acc[0], acc[1], acc[2], acc[3]);
 }
 
+// Same gather with the index math per workgroup: block (x, ih, b) covers
+// 256 / C4 input columns of one input row, thread t -> channel quad
+// t % C4 (C4 a power of two), column t / C4 — no per-thread division of the
+// flat index (three 32-bit divisions per float4 of dx were the kernel's
+// bound at the R50 stem's 64 channels).  Same sums in the same order.
+__global__ __launch_bounds__(256) void maxpool_bwd_idx4_row_kernel(
+    const uchar4* __restrict__ idx, const float* __restrict__ dy, int H, int W, int c4s, int OH,
+    int OW, int k, int s, int pad, float* __restrict__ dx) {
+  const int C4 = 1 << c4s;
+  const int t = threadIdx.x;
+  const int c4 = t & (C4 - 1);
+  const int iw = blockIdx.x * (256 >> c4s) + (t >> c4s);
+  const int ih = blockIdx.y, b = blockIdx.z;
+  if (iw >= W) return;
+  const int64_t ob = (int64_t)b * OH * OW * C4 + c4;
+  const int oh0 = max(0, (ih + pad - k + s) / s), oh1 = min(OH - 1, (ih + pad) / s);
+  const int ow0 = max(0, (iw + pad - k + s) / s), ow1 = min(OW - 1, (iw + pad) / s);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int oh = oh0; oh <= oh1; ++oh)
+    for (int ow = ow0; ow <= ow1; ++ow) {
+      const int me = (ih - (oh * s - pad)) * k + (iw - (ow * s - pad));
+      const int64_t o = ob + (int64_t)(oh * OW + ow) * C4;
+      const uchar4 a = idx[o];
+      const float4 g = reinterpret_cast<const float4*>(dy)[o];
+      if (a.x == me) acc[0] += g.x;
+      if (a.y == me) acc[1] += g.y;
+      if (a.z == me) acc[2] += g.z;
+      if (a.w == me) acc[3] += g.w;
+    }
+  const int64_t i = (((int64_t)b * H + ih) * W + iw) * C4 + c4;
+  reinterpret_cast<float4*>(dx)[i] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+}
+
 __global__ void maxpool_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy, int H,
                                    int W, int C, int OH, int OW, int k, int s, int pad,
                                    int64_t total, float* __restrict__ dx) {
@@ -2398,6 +2431,15 @@ extern "C" int jabd_maxpool_bwd_idx_f32(const uint8_t* idx, const float* dy, int
   const int OH = (H + 2 * pad - k) / stride + 1, OW = (W + 2 * pad - k) / stride + 1;
   const int64_t t4 = (int64_t)B * H * W * (C / 4);
   JABD_REQUIRE(t4 < ((int64_t)1 << 31), "maxpool_bwd_idx: too large");
+  const int C4 = C / 4;
+  if ((C4 & (C4 - 1)) == 0 && C4 <= 64 && H <= 65535 && B <= 65535) {
+    int c4s = 0;
+    while ((1 << c4s) < C4) ++c4s;
+    dim3 g((unsigned)cdiv(W, 256 >> c4s), (unsigned)H, (unsigned)B);
+    maxpool_bwd_idx4_row_kernel<<<g, 256, 0, as_stream(stream)>>>(
+        reinterpret_cast<const uchar4*>(idx), dy, H, W, c4s, OH, OW, k, stride, pad, dx);
+    return check_launch("maxpool_bwd_idx");
+  }
   maxpool_bwd_idx4_kernel<<<(unsigned)cdiv(t4, 256), 256, 0, as_stream(stream)>>>(
       reinterpret_cast<const uchar4*>(idx), dy, H, W, C / 4, OH, OW, k, stride, pad, (int)t4, dx);
   return check_launch("maxpool_bwd_idx");

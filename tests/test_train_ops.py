@@ -575,6 +575,27 @@ def test_dgrad_bn_bwd_sums(cuda, cin, cout, k, stride, bhw, scale):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_in,n", [(1, 4096), (2, 1000), (3, 123457 * 4), (4, 64), (5, 4000),
+                                    (2, 4001)])
+def test_sum_multi_bit_exact(cuda, n_in, n):
+    """jabd_sum_multi_f32 (the gradient of a tensor consumed n_in times) adds
+    the inputs in order — bit-identical to ((a + b) + c) + ... in torch."""
+    import ctypes
+    from jabd_amd._lib import call
+    g = torch.Generator().manual_seed(n_in * 7 + n)
+    xs = [torch.randn(n, generator=g).to(cuda) for _ in range(n_in)]
+    out = torch.empty(n, device=cuda)
+    ptrs = (ctypes.c_void_p * n_in)(*[x.data_ptr() for x in xs])
+    call("jabd_sum_multi_f32", n_in, ptrs, n, out.data_ptr(),
+         ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    ref = xs[0].clone()
+    for x in xs[1:]:
+        ref = ref + x
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("c,k,s,bhw,act", [(64, 3, 2, (2, 66, 50), "relu"), (72, 3, 1, (3, 31, 29), "relu"),
                                            (120, 5, 1, (2, 17, 19), "hswish"),
                                            (240, 5, 2, (2, 21, 16), "hswish")])
@@ -717,7 +738,7 @@ def test_dw_bnin_kink_masks(cuda, recompute, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("bhwc", [(2, 17, 23, 64), (1, 64, 64, 8), (3, 9, 8, 12)])
+@pytest.mark.parametrize("bhwc", [(2, 17, 23, 64), (1, 64, 64, 8), (3, 9, 8, 12), (1, 9, 37, 256)])
 def test_maxpool_idx_forms_bit_identical(cuda, bhwc):
     """The training max-pool (argmax kept as a uint8 window position) gives
     the eval max-pool's values and the recomputing backward's gradient bit for
