@@ -788,13 +788,8 @@ extern "C" int jabd_heads_f32(const float* x, int64_t x_bs, int32_t x_ps, int32_
   JABD_REQUIRE(x && wt && bias && loc && conf && landm, "heads: null pointer");
   JABD_REQUIRE(C % 4 == 0 && x_ps % 4 == 0, "heads: C and pixel stride must be multiples of 4");
   JABD_REQUIRE(a_off + 2 * (int64_t)HW <= A, "heads: anchor range out of bounds");
-  // one-wave workgroups when 256-thread ones would not cover the CUs (bs1
-  // predict: 25 workgroups at 80^2): every wave is a serial chain of weight
-  // loads + FMAs, so spreading the same waves over 4x the CUs shortens the
-  // launch; the results do not depend on the grouping
-  const int nt = (int64_t)B * cdiv(HW, 256) < 512 ? 64 : 256;
-  dim3 g((unsigned)cdiv(HW, nt), (unsigned)B);
-  heads_kernel<<<g, nt, 0, as_stream(stream)>>>(
+  dim3 g((unsigned)cdiv(HW, 256), (unsigned)B);
+  heads_kernel<<<g, 256, 0, as_stream(stream)>>>(
       x, x_bs, x_ps, HW, C, wt, bias, A, a_off, softmax, loc, conf, landm);
   return check_launch("heads");
 }
