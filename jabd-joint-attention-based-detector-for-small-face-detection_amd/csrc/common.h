@@ -33,6 +33,10 @@ __device__ __forceinline__ float hsigmoid_f(float v) {
   return __builtin_amdgcn_fmed3f(fmaf(v, 1.f / 6.f, 0.5f), 0.f, 1.f);
 }
 __device__ __forceinline__ float hswish_f(float v) { return v * hsigmoid_f(v); }
+// ReLU with torch.relu's NaN rule (NaN stays NaN): one v_maximum_f32.  Every
+// kernel's ReLU goes through this, so fused and unfused forms of a layer agree
+// on NaN inputs too (fmaxf and `v > 0 ? v : 0` both map NaN to 0).
+__device__ __forceinline__ float relu_f(float v) { return __builtin_elementwise_maximum(v, 0.f); }
 
 // c + a * b per component as two packed v_pk_fma_f32 (one IEEE fma per
 // element, the same result as four fmaf; the compiler emits scalar v_fma_f32
@@ -82,7 +86,7 @@ __device__ __forceinline__ float4 dw_bn_z(float4 v, const DwBnCoef& k) {
 __device__ __forceinline__ float4 dw_bn_in(float4 v, const DwBnCoef& k, int act, float slope) {
   float4 z = dw_bn_z(v, k);
   if (act == 1) {
-    z.x = fmaxf(z.x, 0.f); z.y = fmaxf(z.y, 0.f); z.z = fmaxf(z.z, 0.f); z.w = fmaxf(z.w, 0.f);
+    z.x = relu_f(z.x); z.y = relu_f(z.y); z.z = relu_f(z.z); z.w = relu_f(z.w);
   } else if (act == 2) {
     z.x = z.x > 0.f ? z.x : z.x * slope; z.y = z.y > 0.f ? z.y : z.y * slope;
     z.z = z.z > 0.f ? z.z : z.z * slope; z.w = z.w > 0.f ? z.w : z.w * slope;

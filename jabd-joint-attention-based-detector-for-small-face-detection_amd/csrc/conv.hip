@@ -32,7 +32,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float act_apply(float v, int act, float slope) {
   switch (act) {
-    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_RELU: return relu_f(v);
     case ACT_LEAKY: return v > 0.f ? v : v * slope;
     case ACT_HSWISH: return hswish_f(v);
     case ACT_HSIGMOID: return hsigmoid_f(v);
@@ -1119,7 +1119,7 @@ __global__ __launch_bounds__(kStemThreads) void stem_kernel(const float* __restr
     for (int n = 0; n < kStemOut; ++n) o[n] = fmaf(wr[n], v[tp], o[n]);
   }
   auto f = [](float u) {
-    return ACT == ACT_HSWISH ? hswish_f(u) : ACT == ACT_RELU ? fmaxf(u, 0.f) : u;
+    return ACT == ACT_HSWISH ? hswish_f(u) : ACT == ACT_RELU ? relu_f(u) : u;
   };
   // pixel p's 4 float4 at st[4p + p/8 + q]: the pad keeps the 16 B writes of
   // 8 consecutive lanes on distinct banks

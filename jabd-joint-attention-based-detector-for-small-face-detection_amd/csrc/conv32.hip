@@ -38,7 +38,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ float act32(float v, int act, float slope) {
   switch (act) {
-    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_RELU: return relu_f(v);
     case ACT_LEAKY: return v > 0.f ? v : v * slope;
     case ACT_HSWISH: return hswish_f(v);
     case ACT_HSIGMOID: return hsigmoid_f(v);

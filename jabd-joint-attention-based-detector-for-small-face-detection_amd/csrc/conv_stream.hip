@@ -37,7 +37,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float cs_act(float v, int act, float slope) {
   switch (act) {
-    case ACT_RELU: return fmaxf(v, 0.f);
+    case ACT_RELU: return relu_f(v);
     case ACT_LEAKY: return v > 0.f ? v : v * slope;
     case ACT_HSWISH: return hswish_f(v);
     case ACT_HSIGMOID: return hsigmoid_f(v);

@@ -14,7 +14,7 @@ namespace jabd {
 
 __device__ __forceinline__ float dw_act(float v, int act, float slope) {
   switch (act) {
-    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_RELU: return relu_f(v);
     case ACT_LEAKY: return v > 0.f ? v : v * slope;
     case ACT_HSWISH: return hswish_f(v);
     default: return v;

@@ -29,7 +29,7 @@ namespace jabd {
 // ---------------------------------------------------------------------------
 template <int ACT>
 __device__ __forceinline__ float xd2_act(float v) {
-  if (ACT == ACT_RELU) return __builtin_elementwise_maximum(v, 0.f);
+  if (ACT == ACT_RELU) return relu_f(v);
   if (ACT == ACT_HSWISH) return hswish_f(v);
   return v;
 }

@@ -52,7 +52,7 @@ template <int ACT>
 __device__ __forceinline__ float xd_act(float v) {
   // one v_maximum_f32 (NaN-propagating, as torch.relu); fmaxf compiled to a
   // canonicalising v_max plus the v_max (2 VALU per element)
-  if (ACT == ACT_RELU) return __builtin_elementwise_maximum(v, 0.f);
+  if (ACT == ACT_RELU) return relu_f(v);
   if (ACT == ACT_HSWISH) return hswish_f(v);
   return v;
 }

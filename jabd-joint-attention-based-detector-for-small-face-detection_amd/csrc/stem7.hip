@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256, 2) void stem7_fwd_kernel(const ConvArgs p, int
           }
           if (ACT == ACT_RELU) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+            for (int e = 0; e < 4; ++e) v[e] = relu_f(v[e]);
           }
           *reinterpret_cast<f32x4*>(yp + 16 * u) = v;
         }

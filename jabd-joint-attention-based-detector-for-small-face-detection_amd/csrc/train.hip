@@ -18,7 +18,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float act_f(float v, int act, float slope) {
   switch (act) {
-    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_RELU: return relu_f(v);
     case ACT_LEAKY: return v > 0.f ? v : v * slope;
     case ACT_HSWISH: {
       float r = fminf(fmaxf(v + 3.f, 0.f), 6.f);

@@ -6,6 +6,7 @@ pre-packed (see `pack_conv`); every call launches on torch's current stream
 and returns without synchronising.
 """
 import ctypes
+import threading
 
 import torch
 
@@ -28,24 +29,30 @@ KINK_TAP = None
 # batch it was run in.  Off by default (batched eval is batch-invariant: an
 # image gives the same bits at any batch size); the bs1 predict path turns it
 # on for its forward (jabd_amd.predict, `with split_k():`), where the R50's
-# late 3x3 convs would otherwise fill a few dozen workgroups.
-CONV_KSPLIT = False
+# late 3x3 convs would otherwise fill a few dozen workgroups.  The setting is
+# per thread, so a threaded server running bs1 predict beside batched eval
+# cannot flip the other thread's form.
+_KSPLIT = threading.local()
+
+
+def ksplit_enabled():
+    return getattr(_KSPLIT, "on", False)
 
 
 class split_k:
-    """Context manager: split-K on (or off) for the convs launched inside."""
+    """Context manager: split-K on (or off) for the convs this thread launches
+    inside it."""
 
     def __init__(self, enabled=True):
         self.enabled = enabled
 
     def __enter__(self):
-        global CONV_KSPLIT
-        self.prev, CONV_KSPLIT = CONV_KSPLIT, self.enabled
+        self.prev = ksplit_enabled()
+        _KSPLIT.on = self.enabled
         return self
 
     def __exit__(self, *exc):
-        global CONV_KSPLIT
-        CONV_KSPLIT = self.prev
+        _KSPLIT.on = self.prev
 
 
 def tap(kind, *operands):
@@ -258,7 +265,7 @@ def conv(x, pk, stride=1, pad=0, act="none", slope=0.0, ascale=None, x2=None, x2
     a.nchw_in = 1 if nchw_in else 0
     a.reserved1 = _CONV_DBG
     ws = None
-    if CONV_KSPLIT and pk.w32 is not None and not nchw_in and y2 is None:
+    if ksplit_enabled() and pk.w32 is not None and not nchw_in and y2 is None:
         # a conv on the 32x32 kernel whose output grid cannot fill the device
         # (bs1) may split its K reduction over workgroups: give it the
         # workspace it asks for

@@ -3,6 +3,7 @@ letterbox + preprocess_input (jabd_letterbox_f32) -> RetinaFace eval forward ->
 decode + score filter + NMS (jabd_detect_f32) -> retinaface_correct_boxes +
 pixel rescale (jabd_correct_boxes_f32).  Only the kept rows leave the device.
 """
+import collections
 import os
 
 import numpy as np
@@ -18,6 +19,9 @@ from jabd_amd import hipmodule, ops
 # faulted the device (ROCm 7, tools/graph_check.py --between det); with kernel
 # nodes only, interleaved eager calls and replays agree bit for bit.
 PREDICT_GRAPH = os.environ.get("JABD_PREDICT_GRAPH", "1") != "0"
+# graphs kept per module (least recently used dropped first): each holds a
+# private memory pool with the whole activation set of its shape
+GRAPH_CACHE = int(os.environ.get("JABD_PREDICT_GRAPHS", "4"))
 
 
 class GraphedDetect:
@@ -65,14 +69,34 @@ def graphed_detect(net, x, priors, variances, conf_thres=0.5, nms_thres=0.3):
     rebuilt when the module's eval packs may have changed."""
     key = (tuple(x.shape), str(x.device), float(variances[0]), float(variances[1]),
            float(conf_thres), float(nms_thres), priors.data_ptr())
-    cache = net.__dict__.setdefault("_jabd_graphs", {})
+    cache = net.__dict__.setdefault("_jabd_graphs", collections.OrderedDict())
     g = cache.get(key)
     if g is None or g.gen != hipmodule.generation() or g.pri is not priors:
-        if len(cache) > 8:
-            cache.clear()
+        cache.pop(key, None)
+        while len(cache) >= max(1, GRAPH_CACHE):
+            cache.popitem(last=False)
         g = cache[key] = GraphedDetect(net, tuple(x.shape), priors, variances, conf_thres,
                                        nms_thres, x.device)
+    cache.move_to_end(key)
     return g(x)
+
+
+def _use_graph(net, shape, fixed_shape):
+    """Graph only a shape that will recur: letterboxed inputs (one fixed
+    shape), or an image size this module has already run once.  A folder of
+    mixed-size images (letterbox_image=False) stays on the eager path instead
+    of paying two warm-up forwards, a capture and a private pool per size."""
+    if not PREDICT_GRAPH or net.training:
+        return False
+    if fixed_shape:
+        return True
+    seen = net.__dict__.setdefault("_jabd_seen_shapes", collections.OrderedDict())
+    hit = shape in seen
+    seen[shape] = True
+    seen.move_to_end(shape)
+    while len(seen) > 64:
+        seen.popitem(last=False)
+    return hit
 
 
 def detect_image(net, image, input_shape, cfg, confidence=0.5, nms_iou=0.3,
@@ -89,7 +113,7 @@ def detect_image(net, image, input_shape, cfg, confidence=0.5, nms_iou=0.3,
     x = ops.letterbox(img, (W, H), mean=(104.0, 117.0, 123.0))   # [1, 3, H, W]
     priors = Anchors(cfg, image_size=(H, W)).get_anchors().to(device).float().contiguous()
     with torch.no_grad():
-        if PREDICT_GRAPH and not net.training:
+        if _use_graph(net, (H, W, str(device)), letterbox_image):
             priors = _cached_priors(net, cfg, H, W, device, priors)
             rows, n_keep = graphed_detect(net, x, priors, cfg["variance"], confidence, nms_iou)
         else:
@@ -106,10 +130,13 @@ def detect_image(net, image, input_shape, cfg, confidence=0.5, nms_iou=0.3,
 
 
 def _cached_priors(net, cfg, H, W, device, priors):
-    """One priors tensor per (input size, device) on the module (the graph
-    keys on its storage)."""
+    """One priors tensor per (input size, device, anchor cfg) on the module
+    (the graph keys on its storage).  The priors are a function of exactly
+    these keys (utils/anchors.py:8-42), so another cfg on the same net gets
+    its own tensor (and graph) instead of stale priors."""
     cache = net.__dict__.setdefault("_jabd_priors", {})
-    key = (H, W, str(device))
+    key = (H, W, str(device), repr(cfg.get("min_sizes")), repr(cfg.get("steps")),
+           bool(cfg.get("clip", False)))
     p = cache.get(key)
     if p is None or p.shape != priors.shape:
         p = cache[key] = priors

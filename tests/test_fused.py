@@ -252,3 +252,44 @@ def test_expand_dw_forms_bit_identical(cuda, spec, bhw):
     for other in outs[1:]:
         for a, b in zip(outs[0], other):
             assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", [BLOCKS[1], BLOCKS[2], BLOCKS[5]],
+                         ids=lambda s: "k%d_c%d_e%d_s%d" % s[:4])
+def test_expand_dw_nan_rule(cuda, spec):
+    """NaN inputs: the fused expand+depthwise kernel, the two-kernel path and
+    PyTorch put NaN at the same outputs (every ReLU keeps NaN, as torch.relu;
+    csrc/common.h relu_f), and agree elsewhere."""
+    from jabd_amd import functional as F
+    k, cin, E, s, act = spec
+    g = torch.Generator().manual_seed(31)
+    B, H, W = 2, 33, 40
+    x = torch.randn(B, cin, H, W, generator=g)
+    x[0, 3, 5, 7] = float("nan")
+    x[1, :, 20, 31] = float("nan")
+    conv1 = torch.nn.Conv2d(cin, E, 1, bias=False)
+    conv2 = torch.nn.Conv2d(E, E, k, s, k // 2, groups=E, bias=False)
+    bn1, bn2 = torch.nn.BatchNorm2d(E).eval(), torch.nn.BatchNorm2d(E).eval()
+    with torch.no_grad():
+        conv1.weight.copy_(torch.randn(conv1.weight.shape, generator=g) / cin ** 0.5)
+        conv2.weight.copy_(torch.randn(conv2.weight.shape, generator=g) / k)
+        for bn in (bn1, bn2):
+            bn.bias.copy_(0.3 * torch.randn(E, generator=g))
+        e_ref = _act(bn1(conv1(x)), act)
+        ref = _act(bn2(conv2(e_ref)), act)
+    pk = F.pack_conv(conv1.to(cuda), bn1.to(cuda))
+    dw_w, dw_b = F.pack_dw(conv2.to(cuda), bn2.to(cuda))
+    xg = x.permute(0, 2, 3, 1).contiguous().to(cuda)
+    y, _ = F.expand_dw(xg, pk, dw_w, dw_b, k, s, act=act)
+    e = F.conv(xg, pk, act=act)
+    y2, _ = F.dwconv(e, dw_w, dw_b, k, s, act=act, partials=True)
+    got = y.permute(0, 3, 1, 2).cpu()
+    got2 = y2.permute(0, 3, 1, 2).cpu()
+    nan = torch.isnan(ref)
+    assert int(nan.sum()) > 0
+    assert torch.equal(torch.isnan(got), nan)
+    assert torch.equal(torch.isnan(got2), nan)
+    assert torch.equal(torch.isnan(e.cpu()), torch.isnan(e_ref.permute(0, 2, 3, 1)))
+    assert rel_err(got[~nan], ref[~nan]) < 2e-5
+    assert rel_err(got2[~nan], ref[~nan]) < 2e-5

@@ -147,7 +147,7 @@ def test_benchmarked_batch_last_image(cuda, kind, B):
     model: R50 RetinaFace bs64, whose layer1 activations are [64,256,256,256]
     = 1.07e9 elements): images 0 and B-1 of the full batch equal bs1 runs of
     the same images bit for bit (per-image batch strides, no cross-image
-    mixing) with split-K off (functional.CONV_KSPLIT, the default); with it on
+    mixing) with split-K off (functional.split_k, off by default); with it on
     (the bs1 predict path: the R50's bs1 3x3 convs split their K sum over
     workgroups, conv32.hip m32_ksplit)
     the bs1 outputs differ only in fp32 rounding: each within the oracle bar,
@@ -161,7 +161,7 @@ def test_benchmarked_batch_last_image(cuda, kind, B):
     gen = torch.Generator(device=cuda).manual_seed(77)
     x = torch.rand((B, 3, 1024, 1024), generator=gen, device=cuda) * 255.0 - 117.0
     from jabd_amd import functional as JF
-    assert JF.CONV_KSPLIT is False   # batched eval is batch-invariant by default
+    assert not JF.ksplit_enabled()  # batched eval is batch-invariant by default
     with torch.no_grad():
         full = [t.clone() for t in mg(x)]
         with JF.split_k():

@@ -209,7 +209,9 @@ def test_graphed_detect_equals_eager(cuda, kind, size):
     """predict.py's per-image forward + decode + NMS replayed as one HIP graph
     (jabd_amd.predict.graphed_detect) gives the eager launches' kept rows bit
     for bit, on two different inputs through the same graph, and is rebuilt
-    after the packs change (load_state_dict bumps the generation)."""
+    after the packs change: load_state_dict with perturbed class-head biases
+    bumps the generation, and the replay must then equal a fresh eager run and
+    differ from the old rows."""
     import bench
     from jabd_amd import functional as F
     from jabd_amd import ops
@@ -230,7 +232,18 @@ def test_graphed_detect_equals_eager(cuda, kind, size):
         k = int(n0[0])
         assert int(n1[0]) == k and k > 0
         assert torch.equal(r0[0, :k], r1[0, :k])
-    net.load_state_dict(net.state_dict())
+    # perturbed weights (every class head's face logit +0.7): a stale graph
+    # replaying the old packs would return the old rows
+    sd = {k_: v.clone() for k_, v in net.state_dict().items()}
+    heads = [k_ for k_ in sd if "ClassHead" in k_ and k_.endswith("bias")]
+    assert heads
+    for k_ in heads:
+        sd[k_].view(-1, 2)[:, 1] += 0.7
+    net.load_state_dict(sd)
     with torch.no_grad():
+        with F.split_k():
+            r3, n3 = ops.detect(*net(x), pri, var, 0.5, 0.3)
         r2, n2 = graphed_detect(net, x, pri, var, 0.5, 0.3)
-    assert int(n2[0]) == k and torch.equal(r2[0, :k], r0[0, :k])
+    k3 = int(n3[0])
+    assert int(n2[0]) == k3 and torch.equal(r2[0, :k3], r3[0, :k3])
+    assert k3 != k or not torch.equal(r3[0, :k], r0[0, :k])
