@@ -608,6 +608,122 @@ def pmc_traffic():
         return json.load(f)
 
 
+def activation_census(kind, device, size):
+    """Pass-independent work of one training image: the
+    forward conv FLOPs and the bytes of every conv output the reference's
+    module graph holds, counted from ONE bs1 eval forward of the same
+    architecture through wrappers of the conv entry points (F.conv, F.stem,
+    F.expand_dw, F.dwconv, F.heads) — whatever the kernels fuse, each reference
+    conv is counted once:
+      * F.conv: B*OH*OW*Cout output; a K-concatenated second source (the
+        stride-2 block's 1x1 skip conv, nets/mobilenetV3.py:126-137) is a
+        second reference conv with an output of the same size;
+      * F.expand_dw: the expand 1x1 output (B*H*W*E), the depthwise output and,
+        fused, the skip branch's dw3x3/s2 output;
+      * F.heads: the loc/conf/landm rows.
+    FLOPs: 2 MACs per conv tap, depthwise included (_expdw_work's count for
+    the fused kernel)."""
+    from jabd_amd import functional as F
+    if kind == "mnv3":
+        m = build_model(device)
+    else:
+        from nets.retinaface_eca_nonlocal import RetinaFace
+        from utils.config import cfg_re50
+        torch.manual_seed(0)
+        m = RetinaFace(cfg=cfg_re50, mode="eval").eval().to(device)
+    tot = {"act_bytes": 0.0, "convs": 0, "flops": 0.0, "stem_flops": 0.0}
+    names = ("conv", "stem", "expand_dw", "dwconv", "heads")
+    orig = {n: getattr(F, n) for n in names}
+
+    def add(nel):
+        tot["act_bytes"] += 4.0 * nel
+        tot["convs"] += 1
+
+    def w_conv(xx, pk, stride=1, pad=0, **kw):
+        out = orig["conv"](xx, pk, stride=stride, pad=pad, **kw)
+        B = xx.shape[0]
+        H, W = (xx.shape[2], xx.shape[3]) if kw.get("nchw_in") else (xx.shape[1], xx.shape[2])
+        OH = (H + 2 * pad - pk.KH) // stride + 1
+        OW = (W + 2 * pad - pk.KW) // stride + 1
+        M = B * OH * OW
+        add(M * pk.Cout)
+        fl = 2.0 * M * pk.KH * pk.KW * pk.Cin * pk.Cout
+        if kw.get("x2") is not None:
+            add(M * pk.Cout)
+            fl += 2.0 * M * pk.Cin2 * pk.Cout
+        tot["flops"] += fl
+        if kw.get("nchw_in"):
+            tot["stem_flops"] += fl
+        return out
+
+    def w_stem(xx, w, bias, act):
+        y = orig["stem"](xx, w, bias, act)
+        add(y.numel())
+        fl = 2.0 * y.numel() * 27
+        tot["flops"] += fl
+        tot["stem_flops"] += fl
+        return y
+
+    def w_xd(xx, pk, w, b, k, stride, **kw):
+        out = orig["expand_dw"](xx, pk, w, b, k, stride, **kw)
+        add(xx.shape[0] * xx.shape[1] * xx.shape[2] * pk.Cout)
+        add(out[0].numel())
+        if kw.get("skip") is not None:
+            add(out[2].numel())
+        tot["flops"] += _expdw_work(xx, pk, k, stride, out[0], kw.get("skip") is not None)[0]
+        return out
+
+    def w_dw(xx, w, bias, k, stride, **kw):
+        out = orig["dwconv"](xx, w, bias, k, stride, **kw)
+        y = out[0] if isinstance(out, tuple) else out
+        add(y.numel())
+        tot["flops"] += 2.0 * y.numel() * k * k
+        return out
+
+    def w_heads(xx, wt, bias, loc, conf, landm, a_off, softmax):
+        r = orig["heads"](xx, wt, bias, loc, conf, landm, a_off, softmax)
+        npx = xx.shape[0] * xx.shape[1] * xx.shape[2]
+        n_out = wt.numel() // xx.shape[3] if wt.numel() % xx.shape[3] == 0 else 32
+        add(npx * n_out)
+        tot["flops"] += 2.0 * npx * xx.shape[3] * n_out
+        return r
+
+    for n, f in zip(names, (w_conv, w_stem, w_xd, w_dw, w_heads)):
+        setattr(F, n, f)
+    try:
+        x = torch.randn(1, 3, size, size, device=device)
+        tot["act_bytes"] += 4.0 * x.numel()   # the network input
+        with torch.no_grad():
+            m(x)
+        torch.cuda.synchronize()
+    finally:
+        for n in names:
+            setattr(F, n, orig[n])
+    del m
+    return tot
+
+
+def step_floor(kind, device, size, batch, step_ms):
+    """Pass-independent floor of one training step:
+         floor_ms = conv_flops / 157.3 TFLOP/s + 4 * act_bytes / 8 TB/s
+    with conv_flops = 3 x the forward conv FLOPs (forward, data gradient,
+    weight gradient) minus the first conv's data gradient (the image needs
+    none), and act_bytes = every reference conv output of the step's batch:
+    one write and one read in the forward, one write and one read of its
+    gradient in the backward.  Independent of how many passes the
+    implementation makes; frac_floor = floor_ms / step_ms."""
+    c = activation_census(kind, device, size)
+    conv_flops = batch * (3.0 * c["flops"] - c["stem_flops"])
+    act_bytes = batch * c["act_bytes"]
+    f_ms = conv_flops / (PEAK_FP32_MFMA_TFLOPS * 1e12) * 1e3
+    b_ms = 4.0 * act_bytes / (PEAK_HBM_GBS * 1e9) * 1e3
+    return {"formula": "conv_flops / %.1f TFLOP/s + 4 * act_bytes / %.0f TB/s"
+                       % (PEAK_FP32_MFMA_TFLOPS, PEAK_HBM_GBS / 1000),
+            "conv_flops": conv_flops, "act_bytes": act_bytes, "reference_convs": c["convs"],
+            "flop_ms": f_ms, "byte_ms": b_ms, "floor_ms": f_ms + b_ms,
+            "frac_floor": (f_ms + b_ms) / step_ms}
+
+
 def step_roofline(name, step_ms, workload):
     """Training-step roofline: the sum over the step's libjabd launches of
     max(algorithmic FLOPs / fp32 MFMA peak, algorithmic bytes / HBM peak),
@@ -875,6 +991,11 @@ def main():
             if k in tr:
                 tr[k]["roofline"] = step_roofline(
                     fn, tr[k]["ms_per_step"], f"{kind} training bs{b} {args.size}x{args.size}")
+                if rank == 0:
+                    fl = step_floor(kind, device, args.size, b, tr[k]["ms_per_step"])
+                    if tr[k]["roofline"] is None:
+                        tr[k]["roofline"] = {}
+                    tr[k]["roofline"].update(fl)
         extra["train"] = tr
     if rank == 0:
         extra["forward_gflop_per_image"] = forward_flops(model, args.size, 1) / 1e9

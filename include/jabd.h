@@ -490,11 +490,14 @@ typedef struct jabd_expdw_args {
 } jabd_expdw_args;
 int64_t jabd_expand_dw_nblk(int32_t OH, int32_t OW, int32_t k, int32_t stride);
 int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_t stream);
-/* Kernel form of jabd_expand_dw_nhwc_f32 (same results bit for bit): 1 = one
- * work item per workgroup, 2 = wave-specialised persistent workgroups, 3 =
- * persistent workgroups walking a fixed channel chunk's tiles, 0 = the
- * default (1; 2 with JABD_EXPDW_WS=1, 3 with JABD_EXPDW2=1).  Returns the
- * previous setting.  For A/B timing and the equivalence test. */
+/* Kernel form of jabd_expand_dw_nhwc_f32: 1 = one work item per workgroup,
+ * 2 = wave-specialised persistent workgroups, 3 = persistent workgroups
+ * walking a fixed channel chunk's tiles (forms 1-3: the same results bit for
+ * bit), 4 = chunk-pipelined persistent workgroups for Cin <= 80 (y and the
+ * skip branch bit-identical to 1-3, the ECA partials summed in another fixed
+ * order; geometries it does not cover run form 1), 0 = the default (1; 2
+ * with JABD_EXPDW_WS=1, 3 with JABD_EXPDW2=1, 4 with JABD_EXPDW3=1).
+ * Returns the previous setting.  For A/B timing and the equivalence tests. */
 int jabd_expand_dw_select(int32_t form);
 
 /* Per-(image, block, channel) sums of an NHWC tensor (ECA pooling of a tensor

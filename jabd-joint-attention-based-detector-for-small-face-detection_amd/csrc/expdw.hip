@@ -1049,7 +1049,7 @@ extern "C" int jabd_xd_trace_set(void* buf) {
 
 extern "C" int jabd_expand_dw_select(int32_t form) {
   const int prev = xw_form;
-  xw_form = form >= 1 && form <= 3 ? form : 0;
+  xw_form = form >= 1 && form <= 4 ? form : 0;
   return prev;
 }
 
@@ -1143,6 +1143,10 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
                   make_fastdiv((uint32_t)tiles_w)};
   JABD_REQUIRE((int64_t)a.B * a.x_bs * 4 < ((int64_t)1 << 32) - 16,
                "expand_dw: input must be < 4 GiB (buffer-descriptor offsets)");
+  if (xw_form == 0 || xw_form == 4) {   // the chunk-pipelined form: opt-in (expdw3.hip)
+    const int e = expdw3_dispatch(a, dv, tiles_img, xw_form == 4, st);
+    if (e != JABD_EINVAL) return e;   // else: not covered, the forms below
+  }
   if (x2_enabled() && !xw_enabled()) {
     const int e = expdw2_dispatch(a, dv, nitems, EC, nch, st);
     if (e != JABD_EINVAL) return e;   // else: no persistent instantiation, expdw1 below

@@ -209,5 +209,9 @@ int xd_skc(int cin);
 // no instantiation covers it; the caller then uses expdw1_kernel)
 int expdw2_dispatch(const jabd_expdw_args& a, const XdDivs& dv, int64_t nitems, int EC, int nch,
                     hipStream_t st);
+// expdw3.hip: the chunk-pipelined persistent form for input-narrow layers
+// (JABD_EINVAL when it does not cover the geometry; the caller falls back)
+int expdw3_dispatch(const jabd_expdw_args& a, const XdDivs& dv, int tiles_img, bool forced,
+                    hipStream_t st);
 
 }  // namespace jabd

@@ -252,6 +252,22 @@ def test_expand_dw_forms_bit_identical(cuda, spec, bhw):
     for other in outs[1:]:
         for a, b in zip(outs[0], other):
             assert torch.equal(a, b)
+    # the chunk-pipelined form (4, csrc/expdw3.hip; the default where it
+    # applies): y and the skip branch bit-identical, the ECA partials (a sum
+    # over the tile in another fixed order) within 2e-6 relative
+    try:
+        lib().jabd_expand_dw_select(4)
+        if s == 2:
+            o4 = F.expand_dw(x, pk, dw_w, dw_b, k, s, act=act, skip=(skw, skb))
+        else:
+            o4 = F.expand_dw(x, pk, dw_w, dw_b, k, s, act=act)
+    finally:
+        lib().jabd_expand_dw_select(0)
+    torch.cuda.synchronize()
+    assert torch.equal(o4[0], outs[0][0])
+    if s == 2:
+        assert torch.equal(o4[2], outs[0][2])
+    assert rel_err(o4[1], outs[0][1]) < 2e-6
 
 
 @pytest.mark.gpu
