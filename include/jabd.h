@@ -383,6 +383,16 @@ int jabd_conv_pack_tn32(int cout);
 int jabd_conv_pack_f32(const float* w, int32_t cout, int32_t cin, int32_t kh, int32_t kw,
                        int32_t transposed, int32_t Kc, int32_t Ntiles, float* wp, int32_t K8,
                        int32_t NT32, float* wp32, jabd_stream_t stream);
+/* Batched jabd_conv_pack_f32: every conv weight an optimizer step changed,
+ * repacked into its existing buffers in one launch (jabd_amd/optim.py, after
+ * the fused Adam step; the reference's optimizer.step(),
+ * train_mobilenetV3_ecagai.py:588).  jobs = device int64 [njobs][11] rows
+ * {w, wp, wp32 (0: none), cout, cin, kh*kw, transposed, Kc, Ntiles, K8,
+ * NT32}; starts = device int64 [njobs + 1]: starts[i] = the float4 outputs of
+ * the jobs before i (Kc*Ntiles*64 + K8*NT32*64 each), total = starts[njobs].
+ * njobs <= 1024. */
+int jabd_conv_pack_multi_f32(const int64_t* jobs, const int64_t* starts, int32_t njobs,
+                             int64_t total, jabd_stream_t stream);
 int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t stream);
 /* Training forward of a 1x1 conv followed by BatchNorm (MNv3 Block_eca
  * conv1 -> bn1, nets/mobilenetV3.py:141-143 / :160-170): the streaming 1x1

@@ -794,7 +794,69 @@ __global__ __launch_bounds__(256) void pack_w_kernel(const float* __restrict__ w
   reinterpret_cast<float4*>(wp32)[i2] = v;
 }
 
+// Batched pack: one launch for every weight an optimizer step changed.  Job
+// rows {w, wp, wp32, cout, cin, khw, transposed, Kc, Ntiles, K8, NT32};
+// starts[i] = float4 outputs of jobs < i, staged in LDS for a binary search.
+constexpr int kPackMaxJobs = 1024;
+__global__ __launch_bounds__(256) void pack_w_multi_kernel(const int64_t* __restrict__ jobs,
+                                                           const int64_t* __restrict__ starts,
+                                                           int njobs, int64_t total) {
+  __shared__ int64_t st[kPackMaxJobs + 1];
+  for (int t = threadIdx.x; t <= njobs; t += blockDim.x) st[t] = starts[t];
+  __syncthreads();
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  int lo = 0, hi = njobs - 1;  // last job with st[job] <= i
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (st[mid] <= i) lo = mid; else hi = mid - 1;
+  }
+  const int64_t* jb = jobs + (int64_t)lo * 11;
+  const float* w = reinterpret_cast<const float*>(jb[0]);
+  float* wp = reinterpret_cast<float*>(jb[1]);
+  float* wp32 = reinterpret_cast<float*>(jb[2]);
+  const int cout = (int)jb[3], cin = (int)jb[4], khw = (int)jb[5], tr = (int)jb[6];
+  const int Kc = (int)jb[7], Ntiles = (int)jb[8], NT32 = (int)jb[10];
+  const int64_t r0 = i - st[lo];
+  const int64_t n16 = (int64_t)Kc * Ntiles * 64;
+  if (r0 < n16) {
+    const int lane = (int)(r0 & 63);
+    const int64_t r = r0 >> 6;
+    const int nt = (int)(r % Ntiles), kc = (int)(r / Ntiles);
+    const int g = lane >> 4, j = lane & 15;
+    float4 v;
+    v.x = w2d_at(w, cout, cin, khw, tr, 16 * kc + 4 * g + 0, 16 * nt + j);
+    v.y = w2d_at(w, cout, cin, khw, tr, 16 * kc + 4 * g + 1, 16 * nt + j);
+    v.z = w2d_at(w, cout, cin, khw, tr, 16 * kc + 4 * g + 2, 16 * nt + j);
+    v.w = w2d_at(w, cout, cin, khw, tr, 16 * kc + 4 * g + 3, 16 * nt + j);
+    reinterpret_cast<float4*>(wp)[r0] = v;
+    return;
+  }
+  const int64_t i2 = r0 - n16;
+  const int lane = (int)(i2 & 63);
+  const int64_t r = i2 >> 6;
+  const int nt = (int)(r % NT32), k8 = (int)(r / NT32);
+  const int h = lane >> 5, j = lane & 31;
+  float4 v;
+  v.x = w2d_at(w, cout, cin, khw, tr, 8 * k8 + 4 * h + 0, 32 * nt + j);
+  v.y = w2d_at(w, cout, cin, khw, tr, 8 * k8 + 4 * h + 1, 32 * nt + j);
+  v.z = w2d_at(w, cout, cin, khw, tr, 8 * k8 + 4 * h + 2, 32 * nt + j);
+  v.w = w2d_at(w, cout, cin, khw, tr, 8 * k8 + 4 * h + 3, 32 * nt + j);
+  reinterpret_cast<float4*>(wp32)[i2] = v;
+}
+
 }  // namespace jabd
+
+extern "C" int jabd_conv_pack_multi_f32(const int64_t* jobs, const int64_t* starts,
+                                        int32_t njobs, int64_t total, jabd_stream_t stream) {
+  using namespace jabd;
+  if (njobs <= 0 || total <= 0) return JABD_OK;
+  JABD_REQUIRE(jobs && starts && njobs <= kPackMaxJobs, "conv_pack_multi: bad args (njobs %d)",
+               njobs);
+  pack_w_multi_kernel<<<(unsigned)cdiv(total, 256), 256, 0, as_stream(stream)>>>(jobs, starts,
+                                                                                njobs, total);
+  return check_launch("conv_pack_multi");
+}
 
 extern "C" int jabd_conv_pack_f32(const float* w, int32_t cout, int32_t cin, int32_t kh,
                                   int32_t kw, int32_t transposed, int32_t Kc, int32_t Ntiles,

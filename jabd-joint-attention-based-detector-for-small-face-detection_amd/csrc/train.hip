@@ -1277,11 +1277,19 @@ __global__ __launch_bounds__(256) void dw_dgrad_bn_kernel(
         a2[e] = sdzx[c + e] * invM;
       }
     }
+    // groups band-major (image, band of rows_pass strips, row): a workgroup
+    // walks spb consecutive rows of one band, so the dy rows a row shares
+    // with its neighbours are re-read from this CU's L2 instead of by
+    // workgroups on other XCDs (PMC: 1.70x the algorithmic bytes row-major)
+    const int nbands = (nstrip + rows_pass - 1) / rows_pass;
     for (int sp = 0; sp < spb; ++sp) {
-      const int64_t it = ((int64_t)blockIdx.x * spb + sp) * rows_pass + r0;
-      if (it >= items) break;
-      const int row = (int)(it / nstrip), strip = (int)(it - (int64_t)row * nstrip);
-      const int b = row / H, ih = row - b * H;
+      const int64_t grp = (int64_t)blockIdx.x * spb + sp;
+      if (grp >= items) break;
+      const int64_t bb = grp / H;
+      const int ih = (int)(grp - bb * H);
+      const int b = (int)(bb / nbands), band = (int)(bb - (int64_t)b * nbands);
+      const int strip = band * rows_pass + r0;
+      if (strip >= nstrip) continue;
       const int iw0 = strip * PW;
       const int ow0 = iw0 / S + OFF;
       float4 acc[PW];
@@ -1384,11 +1392,21 @@ __global__ __launch_bounds__(256) void dw_wgrad_strip_kernel(
   DwBnCoef bc{};
   if (IT && active) bc = dw_bn_coef(bmean, binvstd, bgamma, bbeta, cg);
   auto tf = [&](float4 v) -> float4 { return IT ? dw_bn_in(v, bc, bact, bslope) : v; };
+  // items band-major (image, band of rows_pass strips, row, strip in band):
+  // a pass of the workgroup is one row of a band and its passes walk down the
+  // band, so an input row is re-read by the next K/S output rows from this
+  // CU's L2 (row-major items re-read whole rows across XCDs: PMC 2.7x the
+  // algorithmic bytes)
+  const int nbands = (nstrip + rows_pass - 1) / rows_pass;
   const int64_t i0 = (int64_t)blockIdx.x * items_per_blk;
   const int64_t i1 = min(i0 + items_per_blk, items);
   for (int64_t it = i0 + r0; active && it < i1; it += rows_pass) {
-    const int row = (int)(it / nstrip), strip = (int)(it - (int64_t)row * nstrip);
-    const int b = row / OH, oh = row - b * OH;
+    const int64_t grp = it / rows_pass;  // it % rows_pass == r0 (items_per_blk % rows_pass == 0)
+    const int64_t bb = grp / OH;
+    const int oh = (int)(grp - bb * OH);
+    const int b = (int)(bb / nbands), band = (int)(bb - (int64_t)b * nbands);
+    const int strip = band * rows_pass + r0;
+    if (strip >= nstrip) continue;
     const int ow0 = strip * PW;
     const float4* drow = reinterpret_cast<const float4*>(dy + (((int64_t)b * OH + oh) * OW) * C) + cg;
     float4 g[PW];
@@ -2192,10 +2210,12 @@ extern "C" int jabd_dw_dgrad_f32(const float* dy, const float* w, int32_t B, int
 
 // Workgroups of dw_dgrad_bn_kernel along the strip rows: ~8192 (each walks
 // spb rows of rows_pass strips), so bn_bwd_final reads few partial rows.
-static void dgbn_plan(int B, int H, int W, int C, int& nblk, int& spb) {
+static int64_t dgbn_groups(int B, int H, int W, int C) {
   const int C4 = C / 4, lanes = C4 < 64 ? C4 : 64, rows_pass = 256 / lanes;
-  const int64_t items = (int64_t)B * H * cdiv(W, 8);
-  const int64_t groups = cdiv(items, rows_pass);
+  return (int64_t)B * cdiv(cdiv(W, 8), rows_pass) * H;  // (image, band, row)
+}
+static void dgbn_plan(int B, int H, int W, int C, int& nblk, int& spb) {
+  const int64_t groups = dgbn_groups(B, H, W, C);
   spb = (int)cdiv(groups, 8192);
   nblk = (int)cdiv(groups, spb);
 }
@@ -2225,7 +2245,7 @@ extern "C" int jabd_dw_dgrad_bn_bwd_f32(const float* dy, const float* w, int32_t
   dgbn_plan(B, H, W, C, nblk, spb);
   hipStream_t st = as_stream(stream);
   const int nstrip = (int)cdiv(W, 8);
-  const int64_t items = (int64_t)B * H * nstrip;
+  const int64_t items = dgbn_groups(B, H, W, C);  // (image, band, row) groups
   const dim3 g((unsigned)nblk, (unsigned)cdiv(C4, lanes));
   const int64_t M = (int64_t)B * H * W;
   // dz == NULL: the two-pass form (partials, then the apply with de
@@ -2285,7 +2305,7 @@ static int dw_wgrad(const float* x, const float* dy, int32_t B, int32_t H, int32
 #define WG_CASE(K_, S_, PW_)                                                                    \
   if (k == K_ && stride == S_) {                                                                \
     const int nstrip = (int)cdiv(OW, PW_);                                                      \
-    const int64_t items = (int64_t)B * OH * nstrip;                                             \
+    const int64_t items = (int64_t)B * OH * cdiv(nstrip, rows_pass) * rows_pass;               \
     int64_t per = cdiv(items, 1024);                                                            \
     per = cdiv(per, rows_pass) * rows_pass;                                                     \
     nblk = cdiv(items, per);                                                                    \

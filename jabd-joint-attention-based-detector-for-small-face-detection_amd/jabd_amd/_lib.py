@@ -154,6 +154,7 @@ SIGNATURES = {
                               c_vp, c_vp, c_vp],
     "jabd_add3_f32": [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
     "jabd_beca_ws_floats": [c_i64, c_i64, c_int],
+    "jabd_conv_pack_multi_f32": [c_vp, c_vp, c_i32, c_i64, c_vp],
     "jabd_conv_pack_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32,
                            c_i32, c_vp, c_vp],
     "jabd_beca_fwd_f32": [c_vp, c_i64, c_i64, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_vp],

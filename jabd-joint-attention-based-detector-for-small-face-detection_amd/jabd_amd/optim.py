@@ -105,4 +105,8 @@ class Adam(torch.optim.Adam):
                 # counters as an in-place torch op would, so weight caches
                 # keyed on _version (train._packed) see the new values
                 torch.autograd.graph.increment_version([t[0] for t in tensors])
+                # the training convs' packed weight copies, rebuilt in place
+                # by one launch (instead of one per weight at the next forward)
+                from . import train as _train
+                _train.repack([t[0] for t in tensors])
         return loss

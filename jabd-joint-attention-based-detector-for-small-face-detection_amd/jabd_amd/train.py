@@ -111,6 +111,61 @@ def _packed(weight, transposed):
     return pk
 
 
+_REPACK_TABLES = {}  # job-table key -> (device jobs, device starts, njobs, total)
+
+
+def repack(params):
+    """After an optimizer step changed `params` in place (and bumped their
+    versions): rewrite every cached training pack of them in its existing
+    buffers with ONE launch (jabd_conv_pack_multi_f32) and re-key the cache to
+    the new versions, instead of one jabd_conv_pack_f32 launch per weight and
+    form at the next forward.  Keeps the newest pack per form; a parameter
+    with no cached pack is packed lazily by _packed as before.  (A graph
+    retained across the step would see the new weights in its packs, as
+    autograd sees in-place parameter updates.)"""
+    rows, fixups = [], []
+    for w in params:
+        ent = _PACK.get(id(w))
+        if ent is None or ent[0]() is not w or not ent[1]:
+            continue
+        cache = ent[1]
+        newest = {}
+        for key, pk in cache.items():
+            ver, ptr, tr = key
+            if ptr == w.data_ptr() and (tr not in newest or ver > newest[tr][0]):
+                newest[tr] = (ver, pk)
+        if not newest or not w.is_contiguous() or w.dtype != torch.float32:
+            continue
+        cout, cin, kh, kw = w.shape
+        for tr, (_, pk) in newest.items():
+            k8 = pk.w32.shape[0] if pk.w32 is not None else 0
+            nt32 = pk.w32.shape[1] if pk.w32 is not None else 0
+            rows.append((w.data_ptr(), pk.w.data_ptr(), _p(pk.w32) or 0, cout, cin, kh * kw,
+                         1 if tr else 0, pk.Kc, pk.Ntiles, k8, nt32))
+        fixups.append((w, cache, newest))
+    if not rows:
+        return 0
+    key = tuple(rows)
+    tab = _REPACK_TABLES.get(key)
+    if tab is None:
+        dev = fixups[0][0].device
+        starts = [0]
+        for r in rows:
+            starts.append(starts[-1] + (r[7] * r[8] + r[9] * r[10]) * 64)
+        tab = (torch.tensor(rows, dtype=torch.int64).to(dev),
+               torch.tensor(starts, dtype=torch.int64).to(dev), len(rows), starts[-1])
+        if len(_REPACK_TABLES) > 8:
+            _REPACK_TABLES.clear()
+        _REPACK_TABLES[key] = tab
+    jobs, starts, n, total = tab
+    call("jabd_conv_pack_multi_f32", jobs.data_ptr(), starts.data_ptr(), n, total, _st())
+    for w, cache, newest in fixups:
+        cache.clear()
+        for tr, (_, pk) in newest.items():
+            cache[(w._version, w.data_ptr(), tr)] = pk
+    return len(rows)
+
+
 def _conv_args(x, pk, y, stride, pad, nchw_in=False, ascale=None, tconv=False, OH=None, OW=None):
     a = ConvArgs()
     if nchw_in:

@@ -128,3 +128,55 @@ def test_adam_steps_reach_the_training_convs(cuda):
     assert losses["torch"][0] != losses["torch"][2]  # the steps do move the loss
     for a, b in zip(losses["torch"], losses["jabd"]):
         assert abs(a - b) <= 1e-4 * abs(a), losses
+
+
+@pytest.mark.gpu
+def test_batched_repack_equals_fresh_packs(cuda):
+    """After a fused Adam step, every cached training pack of the model is
+    rewritten in place by ONE jabd_conv_pack_multi_f32 launch (train.repack):
+    each must equal a fresh jabd_conv_pack_f32 pack of the updated weight bit
+    for bit (both forms, both layouts), and the cache must be keyed on the new
+    version so the next forward reuses it without repacking."""
+    from _util import init_for_parity
+    from jabd_amd import functional as F
+    from jabd_amd import parallel, synth, train
+    from jabd_amd.optim import Adam
+    from nets.retinaface_r import RetinaFace
+    from nets.retinaface_training import MultiBoxLoss
+    from utils.anchors import Anchors
+    from utils.config import cfg_mnet
+    x = synth.images(2, 96, seed=5).to(cuda)
+    tg = [torch.from_numpy(t).to(cuda) for t in synth.targets(2, 96, seed=6)]
+    pri = Anchors(cfg_mnet, image_size=(96, 96)).get_anchors().to(cuda)
+    m = init_for_parity(RetinaFace(cfg=cfg_mnet, mode="train"), seed=8).to(cuda).train()
+    opt = Adam(m.parameters(), lr=1e-2, weight_decay=5e-4)
+    crit = MultiBoxLoss(2, 0.35, 7, cfg_mnet["variance"], True)
+    parallel.train_step(m, crit, opt, x, tg, pri)
+    torch.cuda.synchronize()
+    n = 0
+    for p in m.parameters():
+        ent = train._PACK.get(id(p))
+        if ent is None or ent[0]() is not p:
+            continue
+        for (ver, ptr, tr), pk in ent[1].items():
+            assert ver == p._version and ptr == p.data_ptr()
+            ref = F.pack_weight_device(p, tr)
+            assert torch.equal(pk.w, ref.w)
+            assert (pk.w32 is None) == (ref.w32 is None)
+            if pk.w32 is not None:
+                assert torch.equal(pk.w32, ref.w32)
+            n += 1
+    assert n > 50, n
+    # the next forward takes the repacked copies: no per-weight pack launch
+    # for a parameter (tensors derived per step, e.g. weight slices, are
+    # packed per call as before)
+    calls = []
+    orig = F.pack_weight_device
+    F.pack_weight_device = lambda w, *a, **k: calls.append(w) or orig(w, *a, **k)
+    try:
+        parallel.train_step(m, crit, opt, x, tg, pri)
+    finally:
+        F.pack_weight_device = orig
+    params = {id(p) for p in m.parameters()}
+    print("per-call packs of derived tensors:", [tuple(w.shape) for w in calls])
+    assert not [w for w in calls if id(w) in params]
