@@ -556,6 +556,21 @@ int jabd_nlm_apply_f32(const float* src, int64_t src_bs, int32_t src_ps, int32_t
 int jabd_maxpool_nhwc_f32(const float* x, int32_t B, int32_t H, int32_t W, int32_t C,
                           int32_t k, int32_t stride, int32_t pad, float* y,
                           jabd_stream_t stream);
+/* A4 SSH tail + heads of one pyramid level of the 40-channel SSH (MobileNetV3
+ * detectors; nets/layers.py:37-68 and the heads of nets/retinaface_r.py:
+ * 17-57,335-343) in one launch: given the level's first GEMM outputs c33 =
+ * relu(conv3X3) [B,H,W,>=20] (pixel stride c33_ps) and t = leaky(conv5X5_1)
+ * [B,H,W,12] (10 channels + 2 zero), computes conv7X7_2 (+leaky), conv5X5_2,
+ * conv7x7_3, relu(cat), the three 1x1 heads (+ the eval softmax) and stores
+ * loc/conf/landm rows [B,A,4|2|10] from anchor a_off.  wb: the packed,
+ * BN-folded weights, jabd_ssh_tail_weight_floats() floats: three 3x3 10->10
+ * convs [n][kh*3+kw][12] + bias [10] (conv5X5_2, conv7X7_2, conv7x7_3), then
+ * heads [32][40] + bias [32] (8 bbox, 4 class, 20 landmark rows). */
+int64_t jabd_ssh_tail_weight_floats(void);
+int jabd_ssh_tail_heads_f32(const float* c33, int64_t c33_bs, int32_t c33_ps, const float* t,
+                            int64_t t_bs, int32_t B, int32_t H, int32_t W, const float* wb,
+                            float leaky, int64_t A, int64_t a_off, int32_t softmax, float* loc,
+                            float* conf, float* landm, jabd_stream_t stream);
 int jabd_heads_f32(const float* x, int64_t x_bs, int32_t x_ps, int32_t B, int32_t HW,
                    int32_t C, const float* wt, const float* bias, int64_t A, int64_t a_off,
                    int32_t softmax, float* loc, float* conf, float* landm,

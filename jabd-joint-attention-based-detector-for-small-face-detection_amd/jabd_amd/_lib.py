@@ -155,6 +155,9 @@ SIGNATURES = {
     "jabd_add3_f32": [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
     "jabd_beca_ws_floats": [c_i64, c_i64, c_int],
     "jabd_conv_pack_multi_f32": [c_vp, c_vp, c_i32, c_i64, c_vp],
+    "jabd_ssh_tail_weight_floats": [],
+    "jabd_ssh_tail_heads_f32": [c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_f32,
+                                c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp],
     "jabd_conv_pack_f32": [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32,
                            c_i32, c_vp, c_vp],
     "jabd_beca_fwd_f32": [c_vp, c_i64, c_i64, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_i64, c_vp],
@@ -291,6 +294,7 @@ _RESTYPE = {"jabd_version": ctypes.c_char_p, "jabd_dw_nblk": ctypes.c_int64,
             "jabd_adam_num_chunks": ctypes.c_int64, "jabd_beca_ws_floats": ctypes.c_int64,
             "jabd_adaptive_pool_ws_floats": ctypes.c_int64,
             "jabd_abi_struct_size": ctypes.c_int64, "jabd_conv_workspace_size": ctypes.c_int64,
+            "jabd_ssh_tail_weight_floats": ctypes.c_int64,
             "jabd_nlm_attn_dkv_ws_floats": ctypes.c_int64}
 
 _lock = threading.Lock()

@@ -49,6 +49,9 @@ GATES_MULTI = os.environ.get("JABD_GATES_MULTI", "1") != "0"
 # Heads of >= 128-channel levels (R50) as one GEMM + scatter instead of
 # heads_kernel; JABD_HEADS_GEMM=0 for A/B.
 HEADS_GEMM = os.environ.get("JABD_HEADS_GEMM", "1") != "0"
+# JABD_SSH_TAIL=0: the 40-channel SSH's tail convs and the heads as separate
+# launches (A/B against the fused ssh.hip kernel)
+SSH_TAIL = os.environ.get("JABD_SSH_TAIL", "1") != "0"
 
 
 def _w1d(eca):
@@ -86,6 +89,17 @@ class SSHPack:
                           F.pack_conv(s.conv5X5_2[0], s.conv5X5_2[1], cin_pad=qp),
                           F.pack_conv(s.conv7X7_2[0], s.conv7X7_2[1], cin_pad=qp, cout_pad=qp),
                           F.pack_conv(s.conv7x7_3[0], s.conv7x7_3[1], cin_pad=qp))
+
+    def first(self, o, sc=None):
+        """The split form's first GEMM alone: (relu(conv3X3) [B,h,w,C/2],
+        t = leaky(conv5X5_1) [B,h,w,qp]) for the fused tail (ssh.hip)."""
+        B, h, w, _ = o.shape
+        ca = self.packs[0]
+        c33 = torch.empty((B, h, w, self.C // 2), dtype=torch.float32, device=o.device)
+        t = torch.empty((B, h, w, self.packs[1].Cin), dtype=torch.float32, device=o.device)
+        F.conv(o, ca, pad=1, act="relu", ascale=sc, out=c33, out_c0=0, y2=t,
+               nsplit=self.C // 2, act2="leaky", slope2=self.leaky)
+        return c33, t
 
     def forward(self, o, sc=None):
         """o NHWC [B,h,w,Cin] (ECA gate `sc` [B,Cin] applied on load) -> relu(cat) NHWC."""
@@ -190,6 +204,52 @@ def nlm_weights(nlm):
             d(nlm.W.weight.view(C, ch)), d(nlm.W.bias))
 
 
+def ssh_tail_pack(s, heads):
+    """Packed weights of jabd_ssh_tail_heads_f32 for one level (csrc/ssh.hip):
+    MFMA A fragments (lane = 16 g + j, float4 component e) of conv5X5_2,
+    conv7X7_2, conv7x7_3 (BN folded) per tap — W[n = j][ch = 4g + e] — their
+    biases per lane group, the heads' fragments over the k chunks (conv3X3
+    0-15, conv3X3 16-19, conv5X5_2, conv7x7_3) x 2 output tiles, and the head
+    biases.  None unless the SSH is the 40-channel one (branches 20/10/10)."""
+    if (s.conv3X3[0].in_channels != 40 or s.conv3X3[0].out_channels != 20 or
+            s.conv5X5_1[0].out_channels != 10 or tuple(heads[0].shape) != (32, 40)):
+        return None
+    dev = heads[0].device
+    j = torch.arange(16, device=dev).view(1, 16, 1)        # [g, j, e]
+    g = torch.arange(4, device=dev).view(4, 1, 1)
+    e = torch.arange(4, device=dev).view(1, 1, 4)
+    k = 4 * g + e                                          # channel of (g, e)
+    convs, cbias = [], []
+    for seq in (s.conv5X5_2, s.conv7X7_2, s.conv7x7_3):
+        sc, sh = F.bn_fold(seq[1])
+        w = (seq[0].weight.detach().float() * sc[:, None, None, None]).reshape(10, 10, 9)
+        ok = (j < 10) & (k < 10)
+        for p in range(9):
+            frag = torch.where(ok, w[j.clamp(max=9), k.clamp(max=9), p], torch.zeros((), device=dev))
+            convs.append(frag.reshape(64, 4))              # lane = 16 g + j
+        b16 = torch.zeros(16, device=dev)
+        b16[:10] = sh.detach().float()
+        cbias.append(b16.view(4, 4))
+    wh, bh = heads
+    hfr = []
+    for kc in range(4):
+        if kc == 0:
+            ch, ok = k, k < 16
+        elif kc == 1:
+            ch, ok = 16 + k, k < 4
+        else:
+            ch, ok = (20 if kc == 2 else 30) + k, k < 10
+        for nt in range(2):
+            frag = torch.where(ok & (j >= 0), wh[16 * nt + j, ch.clamp(max=39)],
+                               torch.zeros((), device=dev))
+            hfr.append(frag.reshape(64, 4))
+    wb = torch.cat([torch.cat(convs).reshape(-1), torch.cat(cbias).reshape(-1),
+                    torch.cat(hfr).reshape(-1), bh.reshape(2, 4, 4).reshape(-1)]).contiguous()
+    if wb.numel() != int(F.lib().jabd_ssh_tail_weight_floats()):
+        raise RuntimeError("ssh_tail_pack: layout mismatch with libjabd")
+    return wb
+
+
 def heads_pack(m, i):
     convs = (m.BboxHead[i].conv1x1, m.ClassHead[i].conv1x1, m.LandmarkHead[i].conv1x1)
     w = torch.cat([c.weight.detach().float().reshape(c.weight.shape[0], -1) for c in convs])
@@ -209,6 +269,9 @@ class _Head:
         self.eca_fpn = _w1d(m.eca_fpn)
         self.ssh = [s._jabd_cached(dev, lambda s=s: SSHPack(s)) for s in (m.ssh1, m.ssh2, m.ssh3)]
         self.heads = [heads_pack(m, i) for i in range(3)]
+        # the 40-channel SSH's tail + heads as one launch per level (ssh.hip)
+        self.tails = [ssh_tail_pack(s, self.heads[i]) if SSH_TAIL and p.split else None
+                      for i, (s, p) in enumerate(zip((m.ssh1, m.ssh2, m.ssh3), self.ssh))]
         # wide levels (R50: 256 channels): the three heads as one MFMA GEMM
         # plus a scatter; heads_kernel's per-position channel loop is serial
         self.heads_gemm = [
@@ -250,6 +313,12 @@ class _Head:
         scs = self._gates(levels, [self.eca_fpn] * len(levels))
         for i, o in enumerate(levels):
             _, h, w, C = o.shape
+            if self.tails[i] is not None:
+                c33, t = self.ssh[i].first(o, scs[i])
+                F.ssh_tail_heads(c33, t, self.tails[i], self.ssh[i].leaky, loc, conf, landm,
+                                 a_off, softmax)
+                a_off += 2 * h * w
+                continue
             feat = self.ssh[i].forward(o, scs[i])
             if self.heads_gemm[i] is not None:
                 F.heads_scatter(F.conv(feat, self.heads_gemm[i]), loc, conf, landm, a_off, softmax)

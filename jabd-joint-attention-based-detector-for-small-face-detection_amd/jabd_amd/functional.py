@@ -537,6 +537,20 @@ def heads(x, wt, bias, loc, conf, landm, a_off, softmax):
          landm.data_ptr(), _stream())
 
 
+def ssh_tail_heads(c33, t, wb, leaky, loc, conf, landm, a_off, softmax):
+    """The 40-channel SSH's tail + heads of one level (jabd_ssh_tail_heads_f32):
+    c33 = relu(conv3X3) [B,h,w,20], t = leaky(conv5X5_1) [B,h,w,12] -> the
+    level's loc / conf / landm rows from anchor a_off."""
+    _check("ssh_tail.c33", c33)
+    _check("ssh_tail.t", t)
+    B, h, w, _ = c33.shape
+    if tuple(t.shape) != (B, h, w, 12) or not t.is_contiguous():
+        raise ValueError(f"ssh_tail_heads: t must be contiguous [B,h,w,12], got {tuple(t.shape)}")
+    call("jabd_ssh_tail_heads_f32", c33.data_ptr(), c33.stride(0), c33.stride(2), t.data_ptr(),
+         t.stride(0), B, h, w, wb.data_ptr(), float(leaky), loc.shape[1], a_off,
+         1 if softmax else 0, loc.data_ptr(), conf.data_ptr(), landm.data_ptr(), _stream())
+
+
 def heads_scatter(y, loc, conf, landm, a_off, softmax):
     """y [B, h, w, 32] (the three heads as one 1x1 GEMM) -> loc / conf / landm rows."""
     B, h, w, _ = y.shape

@@ -82,7 +82,16 @@ def main():
         outs = o if isinstance(o, tuple) else (o,)
         return 0.0, _nb(*ins) + _nb(*outs), "x".join(str(s) for s in ins[0].shape) if ins else ""
 
+    def c_tail(o, c33, t, wb, leaky, loc, *a, **kw):
+        # conv7X7_2 on the tile + halo counted on the tile only (algorithmic),
+        # conv5X5_2, conv7x7_3 (90 -> 10 each) and the heads (40 -> 32)
+        M = c33.shape[0] * c33.shape[1] * c33.shape[2]
+        fl = 2.0 * M * (3 * 90 * 10 + 40 * 32)
+        nb = _nb(c33, t) + 4.0 * M * 32
+        return fl, nb, "M%d (3x 90->10, heads 40->32)" % M
+
     F.conv = wrap("conv", F.conv, c_conv)
+    F.ssh_tail_heads = wrap("ssh_tail", F.ssh_tail_heads, c_tail)
     F.expand_dw = wrap("expand_dw", F.expand_dw, c_xd)
     F.dwconv = wrap("dwconv", F.dwconv, c_dw)
     for n in ("stem", "channel_sums", "eca_gate", "nlm_fused", "maxpool", "heads"):
