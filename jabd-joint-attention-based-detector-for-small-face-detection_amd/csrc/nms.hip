@@ -370,6 +370,9 @@ static constexpr int kClassOff = 512;
 static constexpr int kCellOff = 1 << 17;  // 18-bit biased cell coordinates
 static constexpr int kCellLim = 1 << 14;
 static constexpr int64_t kPairsPerBox = 128;  // off-block pair capacity per box
+static constexpr int kWaveRec = 64 * (int)kPairsPerBox;  // pair records per key-order wave
+static constexpr int kLaneRec = 64;                      // of which each lane's own slots
+static constexpr int kWaveShared = kWaveRec - 64 * kLaneRec;  // and the wave's shared tail
 static constexpr int kK = 2;                  // class sub-division (neighbour range)
 static constexpr int kGridNbr = 1 + kK + kK * (2 * kK + 1);  // class pairs searched per box
 
@@ -502,10 +505,20 @@ __device__ __forceinline__ uint32_t run_hash(uint64_t k) {
 }
 
 __global__ void grid_runs_insert(const uint64_t* __restrict__ skey, int64_t total,
-                                 CellRun* __restrict__ tab, uint32_t mask) {
+                                 CellRun* __restrict__ tab, uint32_t mask, int bc,
+                                 int* __restrict__ istart) {
   const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (p >= total) return;
   const uint64_t k = skey[p];
+  // istart[x] = key position of image x's first candidate (inactive keys ~0
+  // sort last and count as image bc; istart[bc] = the number of active keys)
+  {
+    const int cur = k == kEmptyKey ? bc : (int)(k >> 56);
+    const int prv = p == 0 ? -1 : (skey[p - 1] == kEmptyKey ? bc : (int)(skey[p - 1] >> 56));
+    for (int x = prv + 1; x <= cur; ++x) istart[x] = (int)p;
+    if (p == total - 1)
+      for (int x = cur + 1; x <= bc; ++x) istart[x] = (int)total;
+  }
   if (k == kEmptyKey || (p > 0 && skey[p - 1] == k)) return;  // not a run start
   uint32_t h = run_hash(k) & mask;
   for (;;) {
@@ -549,22 +562,27 @@ __global__ __launch_bounds__(256) void grid_pairs(
     const float4* __restrict__ gbox, const float* __restrict__ garea, int64_t n, int bc,
     float inv_w, float fcell, const unsigned* __restrict__ ext,
     const CellRun* __restrict__ tab, uint32_t tmask,
-    double thr, int64_t cap, int* __restrict__ dense, uint64_t* __restrict__ diag,
-    int* __restrict__ npairs, int* __restrict__ rowcnt, int* __restrict__ prow,
-    int* __restrict__ pcol, int* __restrict__ pslot, unsigned long long* __restrict__ tested) {
+    double thr, int* __restrict__ dense, uint64_t* __restrict__ diag,
+    uint64_t* __restrict__ rec, int* __restrict__ lcnt, int* __restrict__ wcnt,
+    unsigned long long* __restrict__ tested) {
   // XCD-aware block order: hardware block id g runs on XCD g % 8; give each
   // XCD one contiguous eighth of the key order (= one image when the batch
   // holds 8), so an image's candidate arrays stay in one XCD's L2
   // (host: gridDim.x is a multiple of 8, so the map is a permutation)
+  __shared__ int s_wcnt[4];
   const int64_t g = blockIdx.x, per = gridDim.x / 8;
   const int64_t lb = (g % 8) * per + g / 8;
   const int64_t p = lb * blockDim.x + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  if (p >= total) return;
-  const uint64_t k = skey[p];
-  if (k == ~0ull) return;
-  const int b = (int)(k >> 56);
-  if (dense[b] & 11) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // this wave's private pair region (key-order wave index p / 64): no global
+  // counter, so a flush is a wave-local LDS reservation and plain stores
+  const int64_t wglob = lb * 4 + wv;
+  uint64_t* wrec = rec + wglob * kWaveRec;
+  if (lane == 0) s_wcnt[wv] = 0;
+  const uint64_t k = p < total ? skey[p] : ~0ull;
+  const int b = k != ~0ull ? (int)(k >> 56) : 0;
+  int nl = 0;  // records in this lane's own slots
+  if (k != ~0ull && !(dense[b] & 11)) {
   const int i = sval[p];
   const float4 bi = gbox[p];
   const float ai = garea[p];
@@ -580,51 +598,14 @@ __global__ __launch_bounds__(256) void grid_pairs(
   const float rlo = (float)thr * 0.99f, rhi = ratio ? 1.01f / (float)thr : 0.f;
   const float cx = (bi.x + bi.z) * 0.5f, cy = (bi.y + bi.w) * 0.5f;
   const float thrf = (float)thr;
-  const uint64_t lt = (1ull << lane) - 1;
+  const uint32_t bkt0 = (uint32_t)(b * ((n + 63) >> 6));  // this image's first row block
 
-  // Off-block pairs are buffered per lane and flushed in bursts: one counter
-  // atomic per wave reserves every lane's slots (ballot prefix sum), and the
-  // per-row slot atomics of a burst are issued back to back so their
-  // latencies overlap (a returning atomic per pair serialises the kernel).
-  constexpr int kBuf = 8;
-  int pr[kBuf], pc[kBuf], np = 0;
-  auto flush = [&]() {
-    const int lb = __builtin_amdgcn_readfirstlane(b);
-    const bool mine = b == lb;
-    int pre = 0, tot = 0;
-#pragma unroll
-    for (int bit = 0; bit < 4; ++bit) {
-      const uint64_t mb = __ballot(mine && ((np >> bit) & 1));
-      pre += __popcll(mb & lt) << bit;
-      tot += __popcll(mb) << bit;
-    }
-    int base = 0;
-    if (tot) {
-      const int leader = __ffsll((unsigned long long)__ballot(1)) - 1;
-      if (lane == leader) base = atomicAdd(&npairs[lb], tot);
-      base = __shfl(base, leader) + pre;
-    }
-    if (!mine && np) base = atomicAdd(&npairs[b], np);  // wave spans two images
-    int ps[kBuf];
-#pragma unroll
-    for (int q = 0; q < kBuf; ++q)
-      if (q < np && base + q < cap) ps[q] = atomicAdd(&rowcnt[(int64_t)b * n + pc[q]], 1);
-#pragma unroll
-    for (int q = 0; q < kBuf; ++q) {
-      if (q < np) {
-        if (base + q < cap) {
-          const int64_t o = (int64_t)b * cap + base + q;
-          prow[o] = pr[q];
-          pcol[o] = pc[q];
-          pslot[o] = ps[q];
-        } else {
-          atomicOr(&dense[b], 4);
-        }
-      }
-    }
-    np = 0;
-  };
-
+  // Off-block pairs go straight to this lane's kLaneRec slots of the wave's
+  // region (no reservation); a lane past them takes slots of the wave's
+  // shared tail by an LDS atomic.  Records are (destination block << 32) |
+  // (row << 6 | col & 63); one beyond the region sends its image to the dense
+  // producer.
+  uint64_t* lrec = wrec + lane;  // slot q of this lane: lrec[64 q]
   // own class, then the forward half of the neighbour classes:
   // (0, 1..kK) and (1..kK, -kK..kK)
   unsigned ntest = 0;
@@ -652,18 +633,42 @@ __global__ __launch_bounds__(256) void grid_pairs(
     const int X0 = (int)fmaxf(floorf((cx - rx) / sx), -lim), X1 = (int)fminf(floorf((cx + rx) / sx), lim);
     const int Y0 = (int)fmaxf(floorf((cy - ry) / sy), -lim), Y1 = (int)fminf(floorf((cy + ry) / sy), lim);
     for (int Y = Y0; Y <= Y1; ++Y) {
-      for (int X = X0; X <= X1; ++X) {
-        int q = 0;
-        const int qe = run_find(tab, tmask, grid_key(b, cw2, ch2, Y, X), q);
+      // a row of up to three cells at once: their table probes are in flight
+      // together, and their runs are walked as one candidate sequence
+      for (int Xb = X0; Xb <= X1; Xb += 3) {
+        uint4 e3[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const uint32_t h = run_hash(grid_key(b, cw2, ch2, Y, Xb + c)) & tmask;
+          e3[c] = Xb + c <= X1 ? *reinterpret_cast<const uint4*>(&tab[h])
+                               : make_uint4(~0u, ~0u, 0u, 0u);
+        }
+        int lo3[3], n3[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const uint64_t key = grid_key(b, cw2, ch2, Y, Xb + c);
+          const uint64_t kk = ((uint64_t)e3[c].y << 32) | e3[c].x;
+          lo3[c] = (int)e3[c].z;
+          n3[c] = kk == key ? (int)(e3[c].w - e3[c].z) : 0;
+          if (kk != key && kk != kEmptyKey) {  // first slot taken by another run: probe on
+            int lo = 0;
+            const int hi = run_find(tab, tmask, key, lo);
+            lo3[c] = lo;
+            n3[c] = hi >= 0 ? hi - lo : 0;
+          }
+        }
+        const int qe = n3[0] + n3[1] + n3[2];
         // candidates four at a time: their loads are in flight together
-        for (; q < qe; q += 4) {
-          if (__ballot(np > kBuf - 4)) flush();
+        for (int q = 0; q < qe; q += 4) {
           int jj[4];
           float4 bb[4];
           float aa[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            const int qq = q + u < qe ? q + u : q;
+            const int t = q + u < qe ? q + u : q;
+            const int qq = t < n3[0] ? lo3[0] + t
+                                     : (t < n3[0] + n3[1] ? lo3[1] + (t - n3[0])
+                                                          : lo3[2] + (t - n3[0] - n3[1]));
             jj[u] = sval[qq];
             bb[u] = gbox[qq];
             aa[u] = garea[qq];
@@ -674,20 +679,32 @@ __global__ __launch_bounds__(256) void grid_pairs(
             // same class: each pair once, from the lower rank
             bool hit = q + u < qe && !(nbr == 0 && j <= i);
             ntest += hit;
+#ifdef JABD_NMS_AB_NOIOU  // A/B timing build: the walk and loads alone (results wrong)
+            hit = hit && __float_as_uint(bb[u].x) == 0x7fc00001u && aa[u] == 1.f;
+#else
             if (hit) hit = iou_gt(bi.x, bi.y, bi.z, bi.w, ai, bb[u], aa[u], thr, thrf, true);
+#endif
+#ifdef JABD_NMS_AB_NOSTORE  // A/B timing build: tests kept, pair output dropped
+            ntest += hit ? 65536u : 0u;
+            hit = false;
+#endif
             if (hit) {
               const int row = i < j ? i : j, col = i < j ? j : i;
               if ((row >> 6) == (col >> 6)) {
                 atomicOr((unsigned long long*)&diag[(int64_t)b * n + row],
                          (unsigned long long)1 << (col & 63));
               } else {
-#pragma unroll
-                for (int t2 = 0; t2 < kBuf; ++t2)
-                  if (t2 == np) {
-                    pr[t2] = row;
-                    pc[t2] = col;
-                  }
-                ++np;
+                const uint64_t rv = ((uint64_t)(bkt0 + (uint32_t)(col >> 6)) << 32) |
+                                    (uint32_t)((row << 6) | (col & 63));
+                if (nl < kLaneRec) {
+                  lrec[64 * nl++] = rv;
+                } else {
+                  const int sl = atomicAdd(&s_wcnt[wv], 1);
+                  if (sl < kWaveShared)
+                    wrec[64 * kLaneRec + sl] = rv;
+                  else
+                    atomicOr(&dense[b], 4);
+                }
               }
             }
           }
@@ -695,29 +712,118 @@ __global__ __launch_bounds__(256) void grid_pairs(
       }
     }
   }
-  flush();
   // per-lane counter slots (64 per image): a single address per image would
-  // serialise ~100k L2 atomics; lanes that returned early take no part
+  // serialise ~100k L2 atomics
   if (ntest) atomicAdd(&tested[(int64_t)b * 64 + lane], (unsigned long long)ntest);
+  }
+  lcnt[wglob * 64 + lane] = nl;
+  if (lane == 0)
+    wcnt[wglob] = min(__hip_atomic_load(&s_wcnt[wv], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP),
+                      kWaveShared);
 }
 
-// CSR by destination row: each off-block pair (row suppresses col, row
-// ranked earlier, in an earlier 64-row block) is stored in col's list as
-// (row << 6) | (col & 63): csr[rowoff[col] + slot].  A row block's incoming
-// pairs are then one contiguous range (rows of a block are contiguous).
-__global__ void grid_scatter(const int* __restrict__ npairs, const int* __restrict__ dense,
-                             int64_t cap, int64_t n, const int* __restrict__ prow,
-                             const int* __restrict__ pcol, const int* __restrict__ pslot,
-                             const int* __restrict__ rowoff, int* __restrict__ csr) {
-  const int b = blockIdx.y;
-  if (dense[b]) return;
-  const int64_t np = min((int64_t)npairs[b], cap);
-  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < np;
-       s += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t o = (int64_t)b * cap + s;
-    const int col = pcol[o];
-    csr[rowoff[(int64_t)b * n + col] + pslot[o]] = (prow[o] << 6) | (col & 63);
+// Pair records -> incoming lists per destination row block (a counting sort
+// by block).  Image b's key-order waves [istart[b] / 64, ceil(istart[b+1] /
+// 64)) are split into K chunks, one workgroup each; a wave spanning two images
+// is read by both and each keeps its own records.  Count: per-chunk block
+// histograms in LDS, written as hist[(b nb + block) K + chunk]; an exclusive
+// scan of that table gives every (block, chunk) its CSR range; scatter: the
+// chunk re-reads its records and places each at its range's start + an LDS
+// counter.  Block c's incoming pairs are csr[off[(b nb + c) K], off[(b nb + c
+// + 1) K]) as (row << 6) | (col & 63), in no particular order (the scan ORs
+// them).  No global atomics: the old per-pair row-slot reservation cost the
+// pair search a device atomic round trip per flush.
+__device__ __forceinline__ void grid_chunk_waves(const int* istart, int b, int K, int k,
+                                                 int64_t& wa, int64_t& wb) {
+  const int64_t p0 = istart[b], p1 = istart[b + 1];
+  const int64_t w0 = p0 >> 6, w1 = p1 > p0 ? (p1 + 63) >> 6 : w0;
+  wa = w0 + (w1 - w0) * k / K;
+  wb = w0 + (w1 - w0) * (k + 1) / K;
+}
+
+// Every record of key-order waves [wa, wb) (each lane's own slots, then the
+// wave's shared tail), waves spread over the workgroup's nwv waves.
+// Every record of key-order waves [wa, wb) (the lanes' own slots, interleaved
+// slot-major so each slot row is one coalesced load, then the wave's shared
+// tail), waves spread over the workgroup's nwv waves.
+template <typename F>
+__device__ __forceinline__ void grid_chunk_records(const uint64_t* __restrict__ rec,
+                                                   const int* __restrict__ lcnt,
+                                                   const int* __restrict__ wcnt, int64_t wa,
+                                                   int64_t wb, int lane, int wv, int nwv, F&& f) {
+  for (int64_t w = wa + wv; w < wb; w += nwv) {
+    const uint64_t* r = rec + w * kWaveRec;
+    const int ml = lcnt[w * 64 + lane];
+    const int ms = wcnt[w];
+    int mx = ml;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+    for (int q = 0; q < mx; q += 8) {
+      uint64_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = q + u < ml ? r[(q + u) * 64 + lane] : 0ull;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (q + u < ml) f(v[u]);
+    }
+    const uint64_t* sr = r + 64 * kLaneRec;
+    for (int q = lane; q < ms; q += 64) f(sr[q]);
   }
+}
+
+static constexpr int kBucketT = 1024;
+
+__global__ __launch_bounds__(kBucketT) void grid_bucket_count(
+    const uint64_t* __restrict__ rec, const int* __restrict__ lcnt, const int* __restrict__ wcnt,
+    const int* __restrict__ istart, const int* __restrict__ dense, int64_t nb, int K,
+    int* __restrict__ hist, int* __restrict__ npairs) {
+  extern __shared__ int h[];
+  __shared__ int s_tot;
+  // image fastest in the block id: with 8 images, image b's chunks all run on
+  // XCD b, whose L2 holds the records grid_pairs wrote for it
+  const int bc = gridDim.x / K;
+  const int b = blockIdx.x % bc, k = blockIdx.x / bc, t = threadIdx.x;
+  for (int64_t i = t; i < nb; i += kBucketT) h[i] = 0;
+  if (t == 0) s_tot = 0;
+  __syncthreads();
+  int mine = 0;
+  if (!dense[b]) {
+    int64_t wa, wb;
+    grid_chunk_waves(istart, b, K, k, wa, wb);
+    const uint32_t lo = (uint32_t)(b * nb), hi = (uint32_t)(lo + nb);
+    grid_chunk_records(rec, lcnt, wcnt, wa, wb, t & 63, t >> 6, kBucketT / 64, [&](uint64_t v) {
+      const uint32_t bk = (uint32_t)(v >> 32);
+      if (bk >= lo && bk < hi) {
+        atomicAdd(&h[bk - lo], 1);
+        ++mine;
+      }
+    });
+  }
+  if (mine) atomicAdd(&s_tot, mine);
+  __syncthreads();
+  int* hb = hist + (int64_t)b * nb * K;
+  for (int64_t i = t; i < nb; i += kBucketT) hb[i * K + k] = h[i];
+  if (t == 0 && s_tot) atomicAdd(&npairs[b], s_tot);
+}
+
+__global__ __launch_bounds__(kBucketT) void grid_bucket_scatter(
+    const uint64_t* __restrict__ rec, const int* __restrict__ lcnt, const int* __restrict__ wcnt,
+    const int* __restrict__ istart, const int* __restrict__ dense, int64_t nb, int K,
+    const int* __restrict__ off, uint32_t* __restrict__ csr) {
+  extern __shared__ int h[];
+  const int bc = gridDim.x / K;
+  const int b = blockIdx.x % bc, k = blockIdx.x / bc, t = threadIdx.x;  // as grid_bucket_count
+  if (dense[b]) return;  // workgroup-uniform
+  const int* ob = off + (int64_t)b * nb * K;
+  for (int64_t i = t; i < nb; i += kBucketT) h[i] = ob[i * K + k];
+  __syncthreads();
+  int64_t wa, wb;
+  grid_chunk_waves(istart, b, K, k, wa, wb);
+  const uint32_t lo = (uint32_t)(b * nb), hi = (uint32_t)(lo + nb);
+  grid_chunk_records(rec, lcnt, wcnt, wa, wb, t & 63, t >> 6, kBucketT / 64, [&](uint64_t v) {
+    const uint32_t bk = (uint32_t)(v >> 32);
+    if (bk >= lo && bk < hi) csr[atomicAdd(&h[bk - lo], 1)] = (uint32_t)v;
+  });
 }
 
 // ---------------------------------------------------------------------------
@@ -767,8 +873,7 @@ __device__ __forceinline__ void lds_release(int* p, int v) {
 
 __global__ __launch_bounds__(64 * (kPullLoaders + 1)) void nms_scan_pull(
     const uint64_t* __restrict__ diag, const int* __restrict__ dense,
-    const int* __restrict__ rowcnt, const int* __restrict__ rowoff,
-    const uint32_t* __restrict__ csr, const int* __restrict__ sidx,
+    const int* __restrict__ boff, int K, const uint32_t* __restrict__ csr, const int* __restrict__ sidx,
     const int* __restrict__ counts, int64_t n, int img0, int64_t* __restrict__ keep,
     int64_t keep_bstride, int64_t* __restrict__ n_keep, int* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -795,7 +900,8 @@ __global__ __launch_bounds__(64 * (kPullLoaders + 1)) void nms_scan_pull(
     if (tid == 0) n_keep[b + img0] = 0;
     return;
   }
-  const int E0 = rowoff[rb0];  // CSR position of this image's first pair
+  const int* ob = boff + (int64_t)b * ((n + 63) >> 6) * K;  // block c's pairs: [ob[cK], ob[(c+1)K])
+  const int E0 = ob[0];  // CSR position of this image's first pair
 
   if (wave > 0) {  // ------------------------------------------------ loaders
 #ifdef JABD_NMS_TRACE
@@ -806,9 +912,8 @@ __global__ __launch_bounds__(64 * (kPullLoaders + 1)) void nms_scan_pull(
       const uint64_t tl0 = __builtin_readcyclecounter();
 #endif
       const int slot = c % kMetaRing;
-      const int last = min(64 * c + 64, cnt) - 1;
-      const int e0 = rowoff[rb0 + 64 * c];
-      const int e1 = rowoff[rb0 + last] + rowcnt[rb0 + last];
+      const int e0 = ob[(int64_t)c * K];
+      const int e1 = ob[(int64_t)(c + 1) * K];
       const int ne = e1 - e0;
       const bool fits = ne <= kEntRing;
       const int r = 64 * c + lane;
@@ -1113,7 +1218,10 @@ struct NmsWs {
   uint64_t* ent_bits;
   // grid path
   unsigned* ext;
-  int *dense, *npairs, *gval_in, *gval_out, *rowcnt, *rowoff, *prow, *pcol, *pslot, *csr;
+  int *dense, *npairs, *gval_in, *gval_out, *lcnt, *wcnt, *istart, *bhist, *boff;
+  uint64_t* rec;  // per key-order wave: kWaveRec pair records
+  uint32_t* csr;
+  int kchunks;    // count-sort chunks per image
   unsigned long long* tested;  // grid candidates IoU-tested per image (measurement)
   CellRun* runs;               // cell-run hash table (power-of-two slots)
   uint32_t run_mask;
@@ -1122,13 +1230,20 @@ struct NmsWs {
   int64_t cap;
 };
 
+// grid_pairs workgroups (256 keys each, a multiple of 8 for the XCD map)
+static int64_t grid_pair_blocks(int64_t keys) { return (cdiv(keys, 256) + 7) / 8 * 8; }
+// count-sort chunks per image: about 16 key-order waves each (one per wave of
+// a grid_bucket_* workgroup)
+static int grid_chunks(int64_t n) { return (int)std::min<int64_t>(std::max<int64_t>(cdiv(n, 64 * 16), 1), 256); }
+
 template <typename A>
 static void carve_nms(A& a, int64_t batch, int64_t n, NmsWs* w) {
   const int64_t bc = images_per_pass(batch, n);
   const int64_t nb = cdiv(n, 64);
   const int64_t ents = bc * 64 * (nb * (nb - 1) / 2 + 1);
   const int64_t cap = kPairsPerBox * (n > 0 ? n : 1);
-  const size_t tb = sort_temp_bytes(bc * n);
+  const int kch = grid_chunks(n);
+  const size_t tb = sort_temp_bytes(std::max(bc * n, bc * nb * kch + 1));
 #define T(type, cnt, field)                        \
   do {                                             \
     auto* ptr_ = a.template take<type>(cnt);       \
@@ -1153,12 +1268,14 @@ static void carve_nms(A& a, int64_t batch, int64_t n, NmsWs* w) {
   T(unsigned long long, bc * 64, tested);
   T(int, bc * n, gval_in);
   T(int, bc * n, gval_out);
-  T(int, bc * n, rowcnt);
-  T(int, bc * n, rowoff);
-  T(int, bc * cap, prow);
-  T(int, bc * cap, pcol);
-  T(int, bc * cap, pslot);
-  T(int, bc * cap, csr);
+  const int64_t nwaves = grid_pair_blocks(bc * n) * 4;
+  T(int, nwaves * 64, lcnt);
+  T(int, nwaves, wcnt);
+  T(int, bc + 1, istart);
+  T(int, bc * nb * kch + 1, bhist);
+  T(int, bc * nb * kch + 1, boff);
+  T(uint64_t, nwaves * kWaveRec, rec);
+  T(uint32_t, nwaves * kWaveRec, csr);
   T(float4, bc * n, gbox);
   T(float, bc * n, garea);
   int64_t slots = 1024;
@@ -1169,6 +1286,7 @@ static void carve_nms(A& a, int64_t batch, int64_t n, NmsWs* w) {
   if (w) {
     w->tmp_bytes = tb;
     w->cap = cap;
+    w->kchunks = kch;
   }
 }
 
@@ -1232,7 +1350,7 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
           {w.ext, gb * (int64_t)sizeof(unsigned) * bc * 4 * kNC, 0u},
           {w.runs, gb * (int64_t)sizeof(CellRun) * ((int64_t)w.run_mask + 1), 0xFFFFFFFFu},
           {w.diag, gb * (int64_t)sizeof(uint64_t) * bc * n, 0u},
-          {w.rowcnt, gb * (int64_t)sizeof(int) * bc * n, 0u}};
+          {w.bhist + (int64_t)bc * nb * w.kchunks, gb * (int64_t)sizeof(int), 0u}};
       if (int e = fill_ranges(fr, 11, st)) return e;
     }
     dim3 g1((unsigned)cdiv(n, 256), bc);
@@ -1274,21 +1392,26 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
           w.kout, w.gval_out, (int64_t)bc * n, w.sbox, w.sarea, n, w.gbox, w.garea);
       if (int e = check_launch("grid_gather")) return e;
       const unsigned gt = (unsigned)cdiv((int64_t)bc * n, 256);
-      grid_runs_insert<<<gt, 256, 0, st>>>(w.kout, (int64_t)bc * n, w.runs, w.run_mask);
+      grid_runs_insert<<<gt, 256, 0, st>>>(w.kout, (int64_t)bc * n, w.runs, w.run_mask, bc,
+                                           w.istart);
       if (int e = check_launch("grid_runs_insert")) return e;
       grid_runs_end<<<gt, 256, 0, st>>>(w.kout, (int64_t)bc * n, w.runs, w.run_mask);
       if (int e = check_launch("grid_runs_end")) return e;
-      grid_pairs<<<(gt + 7) / 8 * 8, 256, 0, st>>>(
+      grid_pairs<<<(unsigned)grid_pair_blocks((int64_t)bc * n), 256, 0, st>>>(
           w.kout, w.gval_out, (int64_t)bc * n, w.gbox, w.garea, n, bc, inv_w, fcell, w.ext,
-          w.runs, w.run_mask, iou_thr, w.cap, w.dense, w.diag, w.npairs, w.rowcnt, w.prow, w.pcol,
-          w.pslot, w.tested);
+          w.runs, w.run_mask, iou_thr, w.dense, w.diag, w.rec, w.lcnt, w.wcnt, w.tested);
       if (int e = check_launch("grid_pairs")) return e;
-      if (int e = scan_excl_i32(w.rowcnt, w.rowoff, (int64_t)bc * n, w.tmp, w.tmp_bytes, st))
+      const unsigned gk = (unsigned)(w.kchunks * bc);
+      const size_t hl = (size_t)nb * sizeof(int);
+      grid_bucket_count<<<gk, kBucketT, hl, st>>>(w.rec, w.lcnt, w.wcnt, w.istart, w.dense, nb, w.kchunks,
+                                             w.bhist, w.npairs);
+      if (int e = check_launch("grid_bucket_count")) return e;
+      if (int e = scan_excl_i32(w.bhist, w.boff, (int64_t)bc * nb * w.kchunks + 1, w.tmp,
+                                w.tmp_bytes, st))
         return e;
-      dim3 gs((unsigned)std::min<int64_t>(cdiv(w.cap, 256), 512), bc);
-      grid_scatter<<<gs, 256, 0, st>>>(w.npairs, w.dense, w.cap, n, w.prow, w.pcol, w.pslot,
-                                       w.rowoff, w.csr);
-      if (int e = check_launch("grid_scatter")) return e;
+      grid_bucket_scatter<<<gk, kBucketT, hl, st>>>(w.rec, w.lcnt, w.wcnt, w.istart, w.dense, nb, w.kchunks,
+                                               w.boff, w.csr);
+      if (int e = check_launch("grid_bucket_scatter")) return e;
     }
     nms_mask<<<2048, 256, 0, st>>>(w.sbox, w.sarea, w.counts, n, nb, bc, iou_thr, w.nanflag, w.dense,
                                  w.diag, w.nzcnt, w.ent_cb, w.ent_bits);
@@ -1309,7 +1432,7 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
                                      160 * 1024 - kPullStaticLds));
       }
       nms_scan_pull<<<bc, 64 * (kPullLoaders + 1), lds, st>>>(
-          w.diag, w.dense, w.rowcnt, w.rowoff, reinterpret_cast<const uint32_t*>(w.csr), w.sidx,
+          w.diag, w.dense, w.boff, w.kchunks, w.csr, w.sidx,
           w.counts, n, (int)img0, keep, n, n_keep, w.err);
       if (int e = check_launch("nms_scan_pull")) return e;
     }
