@@ -846,11 +846,19 @@ __global__ __launch_bounds__(kBucketT) void grid_bucket_scatter(
 // Every wait is bounded (kSpinMax): a broken hand-off ends the kernel with
 // *err set instead of hanging the device.
 // ---------------------------------------------------------------------------
+static constexpr int kPullWaves = 16;     // one scan wave + loaders
+#ifdef JABD_NMS_AB_SIMD0  // A/B: the scan wave alone on its SIMD (waves 4, 8, 12 idle)
+static constexpr int kPullLoaders = 12;
+__device__ __forceinline__ int loader_id(int wave) { return (wave & 3) ? wave - 1 - (wave >> 2) : -1; }
+#else
 static constexpr int kPullLoaders = 15;
+__device__ __forceinline__ int loader_id(int wave) { return wave - 1; }
+#endif
 static constexpr int kMetaRing = 32;        // row blocks staged ahead
-static constexpr int kEntRing = 8192;       // incoming pairs staged ahead (power of two)
+static constexpr int kEntRing = 16384;      // incoming pairs staged ahead (power of two)
+static constexpr int kPullLag = 8;          // a loader resolves block c once c - kPullLag are final
 static constexpr unsigned kSpinMax = 1u << 22;
-static constexpr int kPullStaticLds = kEntRing * 4 + kMetaRing * 64 * 12 + kMetaRing * 24 + 16;
+static constexpr int kPullStaticLds = kEntRing * 4 + kMetaRing * 64 * 16 + kMetaRing * 24 + 16;
 
 __device__ __forceinline__ uint32_t wave_or32(uint32_t v) {
   // inclusive OR-scan inside each 16-lane row, then across rows (gfx9 DPP)
@@ -871,7 +879,17 @@ __device__ __forceinline__ void lds_release(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-__global__ __launch_bounds__(64 * (kPullLoaders + 1)) void nms_scan_pull(
+__device__ __forceinline__ uint64_t lds_acquire64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_release64(uint64_t* p, uint64_t v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int prog_done(uint64_t v) { return (int)(uint32_t)v; }
+__device__ __forceinline__ int prog_end(uint64_t v) { return (int)(v >> 32); }
+
+__global__ __launch_bounds__(64 * kPullWaves) void nms_scan_pull(
     const uint64_t* __restrict__ diag, const int* __restrict__ dense,
     const int* __restrict__ boff, int K, const uint32_t* __restrict__ csr, const int* __restrict__ sidx,
     const int* __restrict__ counts, int64_t n, int img0, int64_t* __restrict__ keep,
@@ -880,9 +898,11 @@ __global__ __launch_bounds__(64 * (kPullLoaders + 1)) void nms_scan_pull(
   __shared__ uint32_t ents[kEntRing];
   __shared__ uint64_t mdiag[kMetaRing][64];
   __shared__ int msid[kMetaRing][64];
+  __shared__ uint32_t munres[kMetaRing][64];  // <= 64 unresolved pairs: the scan keeps them in registers
   __shared__ int mready[kMetaRing], me0[kMetaRing], mne[kMetaRing], mend[kMetaRing];
   __shared__ uint64_t mpre[kMetaRing];
-  __shared__ int s_done, s_done_e;
+  // scan progress, one 64-bit word: blocks done (low) | their pairs' ring end (high)
+  __shared__ uint64_t s_prog;
   const int b = blockIdx.x;
   if (dense[b]) return;  // workgroup-uniform: the dense-list scan owns this image
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -892,8 +912,7 @@ __global__ __launch_bounds__(64 * (kPullLoaders + 1)) void nms_scan_pull(
   const int64_t rb0 = (int64_t)b * n;
   if (tid < kMetaRing) mready[tid] = -1;
   if (tid == 0) {
-    s_done = 0;
-    s_done_e = 0;
+    s_prog = 0;
   }
   __syncthreads();
   if (cnt == 0) {
@@ -905,9 +924,11 @@ __global__ __launch_bounds__(64 * (kPullLoaders + 1)) void nms_scan_pull(
 
   if (wave > 0) {  // ------------------------------------------------ loaders
 #ifdef JABD_NMS_TRACE
-    uint64_t l_start = __builtin_readcyclecounter(), l_space = 0, l_load = 0;
+    uint64_t l_start = __builtin_readcyclecounter(), l_space = 0, l_load = 0, l_first = 0;
 #endif
-    for (int c = wave - 1; c < nbv; c += kPullLoaders) {
+    const int lid = loader_id(wave);
+    if (lid < 0) return;
+    for (int c = lid; c < nbv; c += kPullLoaders) {
 #ifdef JABD_NMS_TRACE
       const uint64_t tl0 = __builtin_readcyclecounter();
 #endif
@@ -932,8 +953,8 @@ __global__ __launch_bounds__(64 * (kPullLoaders + 1)) void nms_scan_pull(
       l_load += tl1 - tl0;
 #endif
       unsigned spin = 0;
-      while (!(lds_acquire(&s_done) > c - kMetaRing &&
-               (!fits || lds_acquire(&s_done_e) >= e1 - E0 - kEntRing))) {
+      while (!(prog_done(lds_acquire64(&s_prog)) > c - kMetaRing &&
+               (!fits || prog_end(lds_acquire64(&s_prog)) >= e1 - E0 - kEntRing))) {
         __builtin_amdgcn_s_sleep(2);
         if (++spin > kSpinMax) {
           if (lane == 0) atomicOr(err, 1);
@@ -943,44 +964,85 @@ __global__ __launch_bounds__(64 * (kPullLoaders + 1)) void nms_scan_pull(
 #ifdef JABD_NMS_TRACE
       l_space += __builtin_readcyclecounter() - tl1;
 #endif
-      // pairs whose source block is already final (< D) are resolved here
-      // against the kept bitset; only the rest (sources in the last few
-      // blocks) are compacted into the ring for the scan wave
-      const int D = lds_acquire(&s_done);
-      uint32_t plo = 0, phi = 0;
-      int nu = 0;  // wave-uniform
-      auto stage = [&](const uint32_t (&vv)[8], int q0) {
+      // phase A: the block's raw incoming pairs into the ring (a list larger
+      // than the ring stays in HBM for the scan wave)
+      if (fits) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const int q = q0 + lane + 64 * k;
-          const bool ok = q < ne;
-          const int sb = (int)(vv[k] >> 12);  // source block
-          const bool res = ok && sb < D;
-          const uint64_t w = kb[res ? sb : 0];
-          const bool hit = res && ((w >> ((vv[k] >> 6) & 63)) & 1);
-          const uint32_t bit = vv[k] & 63;
-          plo |= (hit && bit < 32) ? 1u << (bit & 31) : 0u;
-          phi |= (hit && bit >= 32) ? 1u << (bit & 31) : 0u;
-          const bool un = ok && !res;
-          const uint64_t um = __ballot(un);
-          if (un) {
-            const int pos = nu + __popcll(um & ((1ull << lane) - 1));
-            ents[(e0 - E0 + pos) & (kEntRing - 1)] = vv[k];
-          }
-          nu += __popcll(um);
+          const int q = lane + 64 * k;
+          if (q < ne) ents[(e0 - E0 + q) & (kEntRing - 1)] = v[k];
         }
-      };
-      if (fits) {
-        stage(v, 0);
         for (int q0 = 512; q0 < ne; q0 += 512) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             const int q = q0 + lane + 64 * k;
             v[k] = q < ne ? csr[e0 + q] : 0u;
           }
-          stage(v, q0);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int q = q0 + lane + 64 * k;
+            if (q < ne) ents[(e0 - E0 + q) & (kEntRing - 1)] = v[k];
+          }
         }
       }
+      // Resolution, in place over the block's ring range: pairs whose source
+      // block is final (< D) are looked up in the kept bitset here; the rest
+      // are compacted to the front of the range (and, the last time, also
+      // into munres[] when they are at most 64).
+      uint32_t plo = 0, phi = 0;
+      auto resolve = [&](int nin, int D, bool last) -> int {
+        int nu = 0;  // wave-uniform
+        for (int q0 = 0; q0 < nin; q0 += 512) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int q = q0 + lane + 64 * k;
+            v[k] = q < nin ? ents[(e0 - E0 + q) & (kEntRing - 1)] : 0u;
+          }
+          // every entry of this chunk is in registers before any compacted
+          // write (which lands at a position <= the chunk's); the kept-word
+          // lookups are all issued before the first compacted write
+          uint64_t wk[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int sb = (int)(v[k] >> 12);
+            wk[k] = kb[q0 + lane + 64 * k < nin && sb < D ? sb : 0];
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int q = q0 + lane + 64 * k;
+            const bool ok = q < nin;
+            const int sb = (int)(v[k] >> 12);  // source block
+            const bool res = ok && sb < D;
+            const bool hit = res && ((wk[k] >> ((v[k] >> 6) & 63)) & 1);
+            const uint32_t bit = v[k] & 63;
+            plo |= (hit && bit < 32) ? 1u << (bit & 31) : 0u;
+            phi |= (hit && bit >= 32) ? 1u << (bit & 31) : 0u;
+            const bool un = ok && !res;
+            const uint64_t um = __ballot(un);
+            if (un) {
+              const int pos = nu + __popcll(um & ((1ull << lane) - 1));
+              ents[(e0 - E0 + pos) & (kEntRing - 1)] = v[k];
+              if (last && pos < 64) munres[slot][pos] = v[k];
+            }
+            nu += __popcll(um);
+          }
+        }
+        return nu;
+      };
+      int nu = 0;
+      // early: everything whose source is already final
+      if (fits) nu = resolve(ne, prog_done(lds_acquire64(&s_prog)), false);
+      // late, once the scan is within kPullLag blocks: the few pairs left
+      // (sources in the last kPullLag blocks are left to the scan wave)
+      spin = 0;
+      while (prog_done(lds_acquire64(&s_prog)) < c - kPullLag) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spin > kSpinMax) {
+          if (lane == 0) atomicOr(err, 1);
+          return;
+        }
+      }
+      if (fits) nu = resolve(nu, prog_done(lds_acquire64(&s_prog)), true);
       const uint32_t rlo = wave_or32(plo), rhi = wave_or32(phi);
       mdiag[slot][lane] = dg;
       msid[slot][lane] = sd;
@@ -991,94 +1053,135 @@ __global__ __launch_bounds__(64 * (kPullLoaders + 1)) void nms_scan_pull(
         mend[slot] = e1 - E0;
       }
       if (lane == 0) lds_release(&mready[slot], c);
+#ifdef JABD_NMS_TRACE
+      if (c == lid) l_first = __builtin_readcyclecounter() - l_start;
+#endif
     }
 #ifdef JABD_NMS_TRACE
     if (lane == 0 && b == 0)
-      printf("loader %d img 0: %llu cycles, %llu loading, %llu waiting for space\n", wave,
+      printf("loader %d img 0: %llu cycles, %llu loading, %llu waiting for space, first block at %llu\n", wave,
              (unsigned long long)(__builtin_readcyclecounter() - l_start),
-             (unsigned long long)l_load, (unsigned long long)l_space);
+             (unsigned long long)l_load, (unsigned long long)l_space, (unsigned long long)l_first);
 #endif
     return;
   }
 
   // -------------------------------------------------------------- scan wave
+  // Software-pipelined: block c+1's flag and staged data are read while
+  // block c resolves (in registers: sources in the last kPullLag blocks come
+  // from kw[]), so the wave's LDS round trips overlap its own ALU work.  The
+  // flag is read first and the data after it with no wait in between: LDS
+  // executes one wave's accesses in order, so data read after a flag that is
+  // already set is the loader's (a flag not yet set discards the reads).
+  // Publishing is likewise two in-order LDS writes (kept word, then progress).
   int64_t* kout = keep + (int64_t)(b + img0) * keep_bstride;
   int nkeep = 0;
-#ifdef JABD_NMS_TRACE
-  uint64_t t_start = __builtin_readcyclecounter(), t_spin = 0, n_spin = 0;
-#endif
-  for (int c = 0; c < nbv; ++c) {
+  uint64_t kw[kPullLag];  // kept words of blocks c-1 .. c-kPullLag (wave-uniform)
+#pragma unroll
+  for (int x = 0; x < kPullLag; ++x) kw[x] = 0;
+  struct Meta {
+    int e0, ne, e_end, sd;
+    uint64_t pre, dg;
+    uint32_t uv;
+  };
+  auto read_meta = [&](int slot, Meta& m) {
+    m.e0 = me0[slot];
+    m.ne = mne[slot];  // unresolved pairs left by the loader (or -total - 1: read from HBM)
+    m.pre = mpre[slot];
+    m.e_end = mend[slot];
+    m.dg = mdiag[slot][lane];
+    m.sd = msid[slot][lane];
+    m.uv = munres[slot][lane];
+  };
+  // waits (bounded) for block c's flag, then reads its data
+  auto wait_meta = [&](int c, Meta& m) -> bool {
     const int slot = c % kMetaRing;
     unsigned spin = 0;
-#ifdef JABD_NMS_TRACE
-    const uint64_t ts = __builtin_readcyclecounter();
-    if (lds_acquire(&mready[slot]) != c) ++n_spin;
-#endif
     while (lds_acquire(&mready[slot]) != c) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spin > kSpinMax) {
-        if (lane == 0) {
-          atomicOr(err, 2);
-          n_keep[b + img0] = nkeep;
-        }
-        return;
-      }
+      if (++spin > kSpinMax) return false;
     }
+    read_meta(slot, m);
+    return true;
+  };
 #ifdef JABD_NMS_TRACE
-    t_spin += __builtin_readcyclecounter() - ts;
+  uint64_t t_start = __builtin_readcyclecounter();
+  int n_late = 0;
 #endif
-    const int e0 = me0[slot];
-    int ne = mne[slot];  // unresolved pairs left by the loader (or -total - 1: read from HBM)
+  Meta cur;
+  bool ok = wait_meta(0, cur);
+  for (int c = 0; ok && c < nbv; ++c) {
+    Meta nxt;
+    int f1 = -1;
+    if (c + 1 < nbv) {
+      const int s1 = (c + 1) % kMetaRing;
+      f1 = __hip_atomic_load(&mready[s1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      asm volatile("" ::: "memory");  // data reads stay after the flag read
+      read_meta(s1, nxt);
+    }
+    int ne = cur.ne;
     const bool fits = ne >= 0;
     if (!fits) ne = -ne - 1;
-    const uint64_t pre = mpre[slot];
-    const int e_end = mend[slot];
-    const uint64_t dg = mdiag[slot][lane];
-    const int sd = msid[slot][lane];
+    const uint32_t uv = cur.uv;
     uint32_t mlo = 0, mhi = 0;
-    auto pass = [&](const uint32_t (&v)[8], int q0) {
-      uint64_t w[8];
+    uint64_t rem = cur.pre;
+    if (fits && ne <= 64) {
+      if (ne > 0) {
+        // sources in the last kPullLag blocks: their kept words are in kw[];
+        // few hits, one bit each, gathered lane by lane
+        const int d = c - 1 - (int)(uv >> 12);
+        uint64_t w = kw[0];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) w[k] = kb[v[k] >> 12];  // src block = (v >> 6) >> 6
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const bool hit = q0 + lane + 64 * k < ne && ((w[k] >> ((v[k] >> 6) & 63)) & 1);
-        const uint32_t bit = v[k] & 63;
-        mlo |= (hit && bit < 32) ? 1u << (bit & 31) : 0u;
-        mhi |= (hit && bit >= 32) ? 1u << (bit & 31) : 0u;
-      }
-    };
-    if (fits) {
-      for (int q0 = 0; q0 < ne; q0 += 64) {  // usually one short pass
-        const int q = q0 + lane;
-        const uint32_t v = q < ne ? ents[(e0 - E0 + q) & (kEntRing - 1)] : 0u;
-        const uint64_t w = kb[v >> 12];
-        const bool hit = q < ne && ((w >> ((v >> 6) & 63)) & 1);
-        const uint32_t bit = v & 63;
-        mlo |= (hit && bit < 32) ? 1u << (bit & 31) : 0u;
-        mhi |= (hit && bit >= 32) ? 1u << (bit & 31) : 0u;
+        for (int x = 1; x < kPullLag; ++x) w = d == x ? kw[x] : w;
+        uint64_t hm = __ballot(lane < ne && ((w >> ((uv >> 6) & 63)) & 1));
+        while (hm) {
+          const int p = __ffsll((unsigned long long)hm) - 1;
+          hm &= hm - 1;
+          rem |= 1ull << (__builtin_amdgcn_readlane(uv, p) & 63);
+        }
       }
     } else {
-      // a list larger than the ring: the loader left it whole; read it from HBM
-      // in its own branch (a global load pending where the paths join would
-      // make the compiler wait vmcnt(0) there, i.e. for this wave's stores)
-      for (int q0 = 0; q0 < ne; q0 += 512) {
-        uint32_t v[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int q = q0 + lane + 64 * k;
-          v[k] = csr[e0 + (q < ne ? q : 0)];
+      if (fits) {
+        for (int q0 = 0; q0 < ne; q0 += 64) {
+          const int q = q0 + lane;
+          const uint32_t v = q < ne ? ents[(cur.e0 - E0 + q) & (kEntRing - 1)] : 0u;
+          const uint64_t w = kb[v >> 12];
+          const bool hit = q < ne && ((w >> ((v >> 6) & 63)) & 1);
+          const uint32_t bit = v & 63;
+          mlo |= (hit && bit < 32) ? 1u << (bit & 31) : 0u;
+          mhi |= (hit && bit >= 32) ? 1u << (bit & 31) : 0u;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        pass(v, q0);
+      } else {
+        // a list larger than the ring: the loader left it whole; read it from
+        // HBM in its own branch (a global load pending where the paths join
+        // would make the compiler wait vmcnt(0) there, i.e. for this wave's
+        // stores)
+        for (int q0 = 0; q0 < ne; q0 += 512) {
+          uint32_t v[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int q = q0 + lane + 64 * k;
+            v[k] = csr[cur.e0 + (q < ne ? q : 0)];
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          uint64_t w[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) w[k] = kb[v[k] >> 12];  // src block = (v >> 6) >> 6
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const bool hit = q0 + lane + 64 * k < ne && ((w[k] >> ((v[k] >> 6) & 63)) & 1);
+            const uint32_t bit = v[k] & 63;
+            mlo |= (hit && bit < 32) ? 1u << (bit & 31) : 0u;
+            mhi |= (hit && bit >= 32) ? 1u << (bit & 31) : 0u;
+          }
+        }
       }
+      rem |= ((uint64_t)wave_or32(mhi) << 32) | wave_or32(mlo);
     }
-    uint64_t rem = pre;
-    if (ne > 0) rem |= ((uint64_t)wave_or32(mhi) << 32) | wave_or32(mlo);
     const int lim = cnt - 64 * c < 64 ? cnt - 64 * c : 64;
     const uint64_t valid = lim == 64 ? ~0ull : ((1ull << lim) - 1);
-    uint64_t todo = __ballot(dg != 0) & valid;
-    const uint32_t dlo = (uint32_t)dg, dhi = (uint32_t)(dg >> 32);
+    uint64_t todo = __ballot(cur.dg != 0) & valid;
+    const uint32_t dlo = (uint32_t)cur.dg, dhi = (uint32_t)(cur.dg >> 32);
     while (todo) {  // rows with in-block suppressions, in rank order
       const int t = __ffsll((unsigned long long)todo) - 1;
       todo &= todo - 1;
@@ -1089,20 +1192,36 @@ __global__ __launch_bounds__(64 * (kPullLoaders + 1)) void nms_scan_pull(
       }
     }
     const uint64_t kept = valid & ~rem;
-    if ((kept >> lane) & 1) kout[nkeep + __popcll(kept & ((1ull << lane) - 1))] = sd;
+#ifndef JABD_NMS_AB_NOKOUT  // A/B timing build: kept rows not written (results wrong)
+    if ((kept >> lane) & 1) kout[nkeep + __popcll(kept & ((1ull << lane) - 1))] = cur.sd;
+#endif
     nkeep += __popcll(kept);
+#pragma unroll
+    for (int x = kPullLag - 1; x > 0; --x) kw[x] = kw[x - 1];
+    kw[0] = kept;
     if (lane == 0) {
       kb[c] = kept;
-      s_done_e = e_end;  // ordered before s_done by the release below
-      lds_release(&s_done, c + 1);
+      asm volatile("" ::: "memory");  // in-order LDS: the kept word lands before the progress
+      __hip_atomic_store(&s_prog, ((uint64_t)(uint32_t)cur.e_end << 32) | (uint32_t)(c + 1),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (c + 1 < nbv) {
+      if (f1 == c + 1) {
+        cur = nxt;
+      } else {
+#ifdef JABD_NMS_TRACE
+        ++n_late;
+#endif
+        ok = wait_meta(c + 1, cur);
+      }
     }
   }
+  if (!ok && lane == 0) atomicOr(err, 2);
   if (lane == 0) n_keep[b + img0] = nkeep;
 #ifdef JABD_NMS_TRACE
   if (lane == 0)
-    printf("nms_scan_pull img %d: %d blocks, %llu cycles, %llu spinning, %llu blocks waited\n", b,
-           nbv, (unsigned long long)(__builtin_readcyclecounter() - t_start),
-           (unsigned long long)t_spin, (unsigned long long)n_spin);
+    printf("nms_scan_pull img %d: %d blocks, %llu cycles, %d blocks not staged in time\n", b, nbv,
+           (unsigned long long)(__builtin_readcyclecounter() - t_start), n_late);
 #endif
 }
 
@@ -1431,7 +1550,7 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
                                      hipFuncAttributeMaxDynamicSharedMemorySize,
                                      160 * 1024 - kPullStaticLds));
       }
-      nms_scan_pull<<<bc, 64 * (kPullLoaders + 1), lds, st>>>(
+      nms_scan_pull<<<bc, 64 * kPullWaves, lds, st>>>(
           w.diag, w.dense, w.boff, w.kchunks, w.csr, w.sidx,
           w.counts, n, (int)img0, keep, n, n_keep, w.err);
       if (int e = check_launch("nms_scan_pull")) return e;

@@ -1448,6 +1448,127 @@ __global__ __launch_bounds__(256) void dw_wgrad_strip_kernel(
 }
 
 
+// 3x3 depthwise weight gradient with every input row read once per chunk of
+// R output rows: a thread owns one strip of PW output columns and one channel
+// quad and walks its chunk's rows; the rows it still needs stay in registers
+// (stride 1: the three dy rows around the current input row; stride 2: the
+// shared input row between consecutive output rows), so x and dy cross HBM
+// once per chunk (+2 / +1 halo rows) instead of once per tap row.
+// Workgroup blockIdx.x = (image, band of rows_pass strips, row chunk); the
+// partials are part[blk][tap][c] as dw_wgrad_strip_kernel's.
+template <int S, int PW, bool IT = false>
+__global__ __launch_bounds__(256) void dw_wgrad_rows_kernel(
+    const float* __restrict__ x, const float* __restrict__ dy, int H, int W, int C, int OH,
+    int OW, int nstrip, int nbands, int nchunks, int R, int lanes, float* __restrict__ part,
+    const float* __restrict__ bmean = nullptr, const float* __restrict__ binvstd = nullptr,
+    const float* __restrict__ bgamma = nullptr, const float* __restrict__ bbeta = nullptr,
+    int bact = 0, float bslope = 0.f) {
+  constexpr int K = 3;
+  constexpr int L = (PW - 1) * S + K;
+  __shared__ float4 red[256];
+  const int C4 = C >> 2;
+  const int t = threadIdx.x;
+  const int rows_pass = 256 / lanes;
+  const int r0 = t / lanes;
+  const int cg = blockIdx.y * lanes + t % lanes;
+  const int chunk = blockIdx.x % nchunks;
+  const int bb = blockIdx.x / nchunks;
+  const int b = bb / nbands, band = bb % nbands;
+  const int strip = band * rows_pass + r0;
+  const bool active = r0 < rows_pass && cg < C4 && strip < nstrip;
+  float4 acc[K * K];
+#pragma unroll
+  for (int q = 0; q < K * K; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  DwBnCoef bc{};
+  if (IT && active) bc = dw_bn_coef(bmean, binvstd, bgamma, bbeta, cg);
+  const int oh0 = chunk * R, oh1 = min(OH, oh0 + R);
+  const int ow0 = strip * PW, iw0 = ow0 * S - 1;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto load_x = [&](int ih, float4 (&xs)[L]) {
+    const bool rv = ih >= 0 && ih < H;
+    const float4* xrow = reinterpret_cast<const float4*>(x + (((int64_t)b * H + (rv ? ih : 0)) * W) * C) + cg;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const int iw = iw0 + j;
+      xs[j] = (rv && iw >= 0 && iw < W) ? (IT ? dw_bn_in(xrow[(int64_t)iw * C4], bc, bact, bslope)
+                                              : xrow[(int64_t)iw * C4])
+                                        : z;
+    }
+  };
+  auto load_g = [&](int oh, float4 (&g)[PW]) {
+    const bool rv = oh >= oh0 && oh < oh1;
+    const float4* drow = reinterpret_cast<const float4*>(dy + (((int64_t)b * OH + (rv ? oh : oh0)) * OW) * C) + cg;
+#pragma unroll
+    for (int q = 0; q < PW; ++q) g[q] = (rv && ow0 + q < OW) ? drow[(int64_t)(ow0 + q) * C4] : z;
+  };
+  // acc[kh*3 + kw] += g[q] * xs[q*S + kw]
+  auto tap_row = [&](int kh, const float4 (&g)[PW], const float4 (&xs)[L]) {
+#pragma unroll
+    for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+      for (int q = 0; q < PW; ++q) fma4(acc[kh * K + kw], g[q], xs[q * S + kw]);
+  };
+  if (active && oh0 < oh1) {
+    if constexpr (S == 1) {
+      // input row ih meets dy rows ih+1 (kh 0), ih (kh 1), ih-1 (kh 2); the
+      // three dy rows rotate through gA/gB/gC (unrolled by 3: no copies)
+      float4 gA[PW], gB[PW], gC[PW], xs[L];
+#pragma unroll
+      for (int q = 0; q < PW; ++q) gA[q] = gB[q] = z;
+      auto step = [&](int ih, const float4 (&gm1)[PW], const float4 (&g0)[PW], const float4 (&gp1)[PW]) {
+        load_x(ih, xs);
+        tap_row(0, gp1, xs);
+        tap_row(1, g0, xs);
+        tap_row(2, gm1, xs);
+      };
+      for (int ih = oh0 - 1; ih <= oh1; ih += 3) {
+        load_g(ih + 1, gC);
+        step(ih, gA, gB, gC);
+        if (ih + 1 > oh1) break;
+        load_g(ih + 2, gA);
+        step(ih + 1, gB, gC, gA);
+        if (ih + 2 > oh1) break;
+        load_g(ih + 3, gB);
+        step(ih + 2, gC, gA, gB);
+      }
+    } else {
+      // output row oh reads input rows 2oh-1, 2oh, 2oh+1; 2oh+1 is the next
+      // row's 2oh'-1 (unrolled by 2: no copies)
+      float4 xp[L], xa[L], xb[L], g[PW];
+      load_x(2 * oh0 - 1, xp);
+      for (int oh = oh0; oh < oh1; oh += 2) {
+        load_g(oh, g);
+        load_x(2 * oh, xa);
+        load_x(2 * oh + 1, xb);
+        tap_row(0, g, xp);
+        tap_row(1, g, xa);
+        tap_row(2, g, xb);
+        if (oh + 1 >= oh1) break;
+        load_g(oh + 1, g);
+        load_x(2 * oh + 2, xa);
+        load_x(2 * oh + 3, xp);
+        tap_row(0, g, xb);
+        tap_row(1, g, xa);
+        tap_row(2, g, xp);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < K * K; ++q) {
+    __syncthreads();
+    red[t] = acc[q];
+    __syncthreads();
+    if (t < lanes && cg < C4) {
+      float4 Sm = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int r = 0; r < rows_pass; ++r) {
+        const float4 a = red[r * lanes + t];
+        Sm.x += a.x; Sm.y += a.y; Sm.z += a.z; Sm.w += a.w;
+      }
+      reinterpret_cast<float4*>(part + ((int64_t)blockIdx.x * K * K + q) * C)[cg] = Sm;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // ECA-scaled operand backward.  The consumer conv saw a = x * s[b][c]; given
 // da: dx = da * s, and ds[b][c] = sum_hw da * x (block partials).
@@ -2302,8 +2423,35 @@ static int dw_wgrad(const float* x, const float* dy, int32_t B, int32_t H, int32
   const int C4 = C / 4, lanes = C4 < 64 ? C4 : 64, rows_pass = 256 / lanes;
   hipStream_t st = as_stream(stream);
   int64_t nblk = 0;
+  // 3x3: the row-walking kernel when (image, band) pairs leave room for row
+  // chunks within the 1024 partial blocks (JABD_DW_WGRAD_ROWS=0: strip kernel)
+  static const bool rows_on = [] {
+    const char* e = getenv("JABD_DW_WGRAD_ROWS");
+    return !(e && e[0] == '0');
+  }();
+#define WR_CASE(S_, PW_)                                                                        \
+  if (rows_on && k == 3 && stride == S_) {                                                      \
+    const int nstrip = (int)cdiv(OW, PW_);                                                      \
+    const int nbands = (int)cdiv(nstrip, rows_pass);                                            \
+    if ((int64_t)B * nbands <= 1024) {                                                          \
+      const int want = (int)std::max<int64_t>(1, std::min<int64_t>(OH, 1024 / ((int64_t)B * nbands))); \
+      const int R = (int)cdiv(OH, want);                                                        \
+      const int nch = (int)cdiv(OH, R);                                                         \
+      nblk = (int64_t)B * nbands * nch;                                                         \
+      dim3 g((unsigned)nblk, (unsigned)cdiv(C4, lanes));                                        \
+      if (it)                                                                                   \
+        dw_wgrad_rows_kernel<S_, PW_, true><<<g, 256, 0, st>>>(                                 \
+            x, dy, H, W, C, OH, OW, nstrip, nbands, nch, R, lanes, part, bmean, binvstd, bgamma, \
+            bbeta, bact, bslope);                                                               \
+      else                                                                                      \
+        dw_wgrad_rows_kernel<S_, PW_><<<g, 256, 0, st>>>(x, dy, H, W, C, OH, OW, nstrip, nbands, \
+                                                          nch, R, lanes, part);                 \
+    }                                                                                           \
+  }
+  WR_CASE(1, 4) WR_CASE(2, 2)
+#undef WR_CASE
 #define WG_CASE(K_, S_, PW_)                                                                    \
-  if (k == K_ && stride == S_) {                                                                \
+  if (nblk == 0 && k == K_ && stride == S_) {                                                   \
     const int nstrip = (int)cdiv(OW, PW_);                                                      \
     const int64_t items = (int64_t)B * OH * cdiv(nstrip, rows_pass) * rows_pass;               \
     int64_t per = cdiv(items, 1024);                                                            \

@@ -154,7 +154,11 @@ def test_bnactfn_grads(cuda, c, act, res):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("c,k,s,h", [(16, 3, 1, 9), (64, 3, 2, 10), (72, 5, 2, 11), (120, 5, 1, 6)])
+@pytest.mark.parametrize("c,k,s,h", [(16, 3, 1, 9), (64, 3, 2, 10), (72, 5, 2, 11), (120, 5, 1, 6),
+                                     # tall maps: the 3x3 weight gradient walks chunks of
+                                     # 5 / 4 output rows (train.hip dw_wgrad_rows_kernel),
+                                     # the last chunk short
+                                     (16, 3, 1, 703), (24, 3, 2, 701)])
 def test_dwconvfn_grads(cuda, c, k, s, h):
     from jabd_amd.train import DwConvFn
     g = torch.Generator().manual_seed(c + k)
