@@ -1111,14 +1111,12 @@ __global__ __launch_bounds__(64 * kPullWaves) void nms_scan_pull(
   Meta cur;
   bool ok = wait_meta(0, cur);
   for (int c = 0; ok && c < nbv; ++c) {
+    // (past the last block the reads are of an unused slot and dropped)
     Meta nxt;
-    int f1 = -1;
-    if (c + 1 < nbv) {
-      const int s1 = (c + 1) % kMetaRing;
-      f1 = __hip_atomic_load(&mready[s1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      asm volatile("" ::: "memory");  // data reads stay after the flag read
-      read_meta(s1, nxt);
-    }
+    const int s1 = (c + 1) % kMetaRing;
+    int f1 = __hip_atomic_load(&mready[s1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");  // data reads stay after the flag read
+    read_meta(s1, nxt);
     int ne = cur.ne;
     const bool fits = ne >= 0;
     if (!fits) ne = -ne - 1;
@@ -1205,9 +1203,19 @@ __global__ __launch_bounds__(64 * kPullWaves) void nms_scan_pull(
       __hip_atomic_store(&s_prog, ((uint64_t)(uint32_t)cur.e_end << 32) | (uint32_t)(c + 1),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    // the prefetched values are first touched here, so their LDS latency
+    // overlaps this block's work (no early wait)
+    asm volatile("" : "+v"(f1), "+v"(nxt.e0), "+v"(nxt.ne), "+v"(nxt.e_end), "+v"(nxt.sd),
+                 "+v"(nxt.pre), "+v"(nxt.dg), "+v"(nxt.uv));
+    f1 = __builtin_amdgcn_readfirstlane(f1);
     if (c + 1 < nbv) {
       if (f1 == c + 1) {
         cur = nxt;
+        cur.e0 = __builtin_amdgcn_readfirstlane(nxt.e0);  // uniform fields back to scalars
+        cur.ne = __builtin_amdgcn_readfirstlane(nxt.ne);
+        cur.e_end = __builtin_amdgcn_readfirstlane(nxt.e_end);
+        cur.pre = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(nxt.pre >> 32)) << 32) |
+                  (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)nxt.pre);  // (int result: no sign extension)
       } else {
 #ifdef JABD_NMS_TRACE
         ++n_late;
