@@ -632,7 +632,7 @@ def activation_census(kind, device, size):
         torch.manual_seed(0)
         m = RetinaFace(cfg=cfg_re50, mode="eval").eval().to(device)
     tot = {"act_bytes": 0.0, "convs": 0, "flops": 0.0, "stem_flops": 0.0}
-    names = ("conv", "stem", "expand_dw", "dwconv", "heads")
+    names = ("conv", "stem", "expand_dw", "dwconv", "heads", "ssh_tail_heads")
     orig = {n: getattr(F, n) for n in names}
 
     def add(nel):
@@ -688,7 +688,21 @@ def activation_census(kind, device, size):
         tot["flops"] += 2.0 * npx * xx.shape[3] * n_out
         return r
 
-    for n, f in zip(names, (w_conv, w_stem, w_xd, w_dw, w_heads)):
+    def w_ssh(c33, t, wb, leaky, loc, conf, landm, a_off, softmax):
+        # the fused SSH tail + heads of one level (csrc/ssh.hip): the reference's
+        # conv5X5_2, conv7X7_2, conv7x7_3 (C/4 -> C/4, 3x3) and the three 1x1 heads
+        r = orig["ssh_tail_heads"](c33, t, wb, leaky, loc, conf, landm, a_off, softmax)
+        npx = c33.shape[0] * c33.shape[1] * c33.shape[2]
+        C = 2 * c33.shape[3]
+        q = C // 4
+        n_out = loc.shape[2] + conf.shape[2] + landm.shape[2]   # per anchor
+        A = 2                                                  # anchors per position (cfg min_sizes)
+        add(npx * (3 * q + n_out * A))
+        tot["flops"] += npx * (3 * 2.0 * 9 * q * q + 2.0 * C * n_out * A)
+        tot["convs"] += 5   # (add() counted one)
+        return r
+
+    for n, f in zip(names, (w_conv, w_stem, w_xd, w_dw, w_heads, w_ssh)):
         setattr(F, n, f)
     try:
         x = torch.randn(1, 3, size, size, device=device)

@@ -180,6 +180,160 @@ __global__ __launch_bounds__(kDwThreads) void dw_kernel(const DwArgs p, int stri
   }
 }
 
+// The 3x3 training forward with BatchNorm statistics as a row walker: a
+// thread owns PW output columns x 4 channels and a chunk of R output rows,
+// and keeps the input rows it still needs in registers (stride 1: a ring of
+// three rows rotated by unrolling; stride 2: the row shared by consecutive
+// outputs), so every input row is loaded once per chunk (+2 / +1 halo rows)
+// instead of once per output row it feeds.  Each output is accumulated in
+// dw_kernel's tap order (rows outside the image skipped, in-row padding as
+// zeros): the outputs are dw_kernel's bit for bit.  Workgroup blockIdx.x =
+// band * nchunks + chunk (blocks past nbands * nchunks write zero partials,
+// so the statistics rows keep jabd_dwconv_stats_nblk's count).
+template <int S, int PW, bool IT>
+__global__ __launch_bounds__(kDwThreads) void dw_rows_kernel(const DwArgs p, int nbands,
+                                                            int nchunks, int R,
+                                                            float* __restrict__ stp,
+                                                            float* __restrict__ shift,
+                                                            const DwBnIn bi) {
+  constexpr int K = 3;
+  constexpr int SPAN = (PW - 1) * S + K;
+  const int CG = p.C >> 2;
+  const int SP = kDwThreads / CG;
+  const int tid = threadIdx.x;
+  const int cg = tid % CG, sp = tid / CG;
+  const int b = blockIdx.y;
+  const int band = blockIdx.x / nchunks, chunk = blockIdx.x % nchunks;
+  const int OWs = (p.OW + PW - 1) / PW;
+  const int strip = band * SP + sp;
+  const bool active = sp < SP && band < nbands && strip < OWs;
+  const float* xb = p.x + (int64_t)b * p.x_bs + 4 * cg;
+  float* yb = p.y + (int64_t)b * p.y_bs + 4 * cg;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 wr[K * K];
+  float4 bias = z;
+  if (sp < SP) {
+#pragma unroll
+    for (int t = 0; t < K * K; ++t) wr[t] = reinterpret_cast<const float4*>(p.w + t * p.C)[cg];
+    if (p.bias) bias = reinterpret_cast<const float4*>(p.bias)[cg];
+  }
+  DwBnCoef bc{};
+  if (IT && sp < SP) bc = dw_bn_coef(bi.mean, bi.invstd, bi.gamma, bi.beta, cg);
+  auto ldx = [&](const float* ptr) -> float4 {
+    const float4 v = *reinterpret_cast<const float4*>(ptr);
+    return IT ? dw_bn_in(v, bc, bi.act, bi.slope) : v;
+  };
+  float4 sh = z, ss = z, sq = z;
+  if (sp < SP) {  // the shift: output (0, 0) of image 0, dw_kernel's expression
+    float4 a0 = bias;
+    const float* x0 = p.x + 4 * cg;
+#pragma unroll
+    for (int kh = 0; kh < K; ++kh) {
+      const int ih = -p.pad + kh;
+      if (ih < 0 || ih >= p.H) continue;
+#pragma unroll
+      for (int kw = 0; kw < K; ++kw) {
+        const int iw = -p.pad + kw;
+        const float4 r = (iw >= 0 && iw < p.W) ? ldx(x0 + ((int64_t)ih * p.W + iw) * p.x_ps) : z;
+        a0 = f4fma(r, wr[kh * K + kw], a0);
+      }
+    }
+    sh.x = dw_act(a0.x, p.act, p.slope);
+    sh.y = dw_act(a0.y, p.act, p.slope);
+    sh.z = dw_act(a0.z, p.act, p.slope);
+    sh.w = dw_act(a0.w, p.act, p.slope);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && sp == 0) reinterpret_cast<float4*>(shift)[cg] = sh;
+  }
+  const int oh0 = chunk * R, oh1 = min(p.OH, oh0 + R);
+  const int ow0 = strip * PW, iw0 = ow0 * S - p.pad;
+  auto load_row = [&](int ih, float4 (&r)[SPAN]) {
+    const bool rv = ih >= 0 && ih < p.H;
+    const float* xr = xb + (int64_t)(rv ? ih : 0) * p.W * p.x_ps;
+#pragma unroll
+    for (int c = 0; c < SPAN; ++c) {
+      const int iw = iw0 + c;
+      r[c] = (rv && iw >= 0 && iw < p.W) ? ldx(xr + (int64_t)iw * p.x_ps) : z;
+    }
+  };
+  // output row oh from input rows ih0, ih0 + 1, ih0 + 2 (held in r0, r1, r2)
+  auto emit = [&](int oh, int ih0, const float4 (&r0)[SPAN], const float4 (&r1)[SPAN],
+                  const float4 (&r2)[SPAN]) {
+    float4 acc[PW];
+#pragma unroll
+    for (int o = 0; o < PW; ++o) acc[o] = bias;
+    auto tap_row = [&](int kh, const float4 (&r)[SPAN]) {
+      if (ih0 + kh < 0 || ih0 + kh >= p.H) return;
+#pragma unroll
+      for (int o = 0; o < PW; ++o)
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw) acc[o] = f4fma(r[o * S + kw], wr[kh * K + kw], acc[o]);
+    };
+    tap_row(0, r0);
+    tap_row(1, r1);
+    tap_row(2, r2);
+#pragma unroll
+    for (int o = 0; o < PW; ++o) {
+      if (ow0 + o >= p.OW) break;
+      float4 v;
+      v.x = dw_act(acc[o].x, p.act, p.slope);
+      v.y = dw_act(acc[o].y, p.act, p.slope);
+      v.z = dw_act(acc[o].z, p.act, p.slope);
+      v.w = dw_act(acc[o].w, p.act, p.slope);
+      *reinterpret_cast<float4*>(yb + ((int64_t)oh * p.OW + ow0 + o) * p.y_ps) = v;
+      const float4 d = make_float4(v.x - sh.x, v.y - sh.y, v.z - sh.z, v.w - sh.w);
+      ss.x += d.x; ss.y += d.y; ss.z += d.z; ss.w += d.w;
+      sq.x = fmaf(d.x, d.x, sq.x); sq.y = fmaf(d.y, d.y, sq.y);
+      sq.z = fmaf(d.z, d.z, sq.z); sq.w = fmaf(d.w, d.w, sq.w);
+    }
+  };
+  if (active && oh0 < oh1) {
+    if constexpr (S == 1) {
+      float4 rA[SPAN], rB[SPAN], rC[SPAN];
+      load_row(oh0 - p.pad, rA);
+      load_row(oh0 - p.pad + 1, rB);
+      for (int oh = oh0; oh < oh1; oh += 3) {
+        const int ih = oh - p.pad;
+        load_row(ih + 2, rC);
+        emit(oh, ih, rA, rB, rC);
+        if (oh + 1 >= oh1) break;
+        load_row(ih + 3, rA);
+        emit(oh + 1, ih + 1, rB, rC, rA);
+        if (oh + 2 >= oh1) break;
+        load_row(ih + 4, rB);
+        emit(oh + 2, ih + 2, rC, rA, rB);
+      }
+    } else {
+      float4 rP[SPAN], rA[SPAN], rB[SPAN];
+      load_row(2 * oh0 - p.pad, rP);
+      for (int oh = oh0; oh < oh1; oh += 2) {
+        const int ih = 2 * oh - p.pad;
+        load_row(ih + 1, rA);
+        load_row(ih + 2, rB);
+        emit(oh, ih, rP, rA, rB);
+        if (oh + 1 >= oh1) break;
+        load_row(ih + 3, rA);
+        load_row(ih + 4, rP);
+        emit(oh + 1, ih + 2, rB, rA, rP);
+      }
+    }
+  }
+  __shared__ float4 rs[kDwThreads], rq[kDwThreads];
+  rs[tid] = ss;
+  rq[tid] = sq;
+  __syncthreads();
+  if (tid < CG) {
+    float4 S_ = z, Q_ = z;
+    for (int q = 0; q < SP; ++q) {
+      const float4 a = rs[q * CG + tid], c = rq[q * CG + tid];
+      S_.x += a.x; S_.y += a.y; S_.z += a.z; S_.w += a.w;
+      Q_.x += c.x; Q_.y += c.y; Q_.z += c.z; Q_.w += c.w;
+    }
+    const int64_t blk = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    reinterpret_cast<float4*>(stp + blk * 2 * p.C)[tid] = S_;
+    reinterpret_cast<float4*>(stp + blk * 2 * p.C + p.C)[tid] = Q_;
+  }
+}
+
 static int64_t dw_strips_per_blk(int64_t B, int64_t OH, int64_t OW, int64_t C) {
   const int64_t SP = kDwThreads / (C / 4);
   const int64_t nstrip = OH * ((OW + kPW - 1) / kPW);
@@ -249,6 +403,32 @@ static int dwconv_stats(const jabd_dw_args* args, float* stats_part, float* shif
   const int64_t nblk = jabd_dw_nblk(a.B, a.OH, a.OW, a.C);
   dim3 grid((unsigned)nblk, (unsigned)a.B);
   hipStream_t st = as_stream(stream);
+  // 3x3: the row walker, within the same partial-block count
+  // (JABD_DW_ROWS=0: dw_kernel)
+  static const bool rows_on = [] {
+    const char* e = getenv("JABD_DW_ROWS");
+    return !(e && e[0] == '0');
+  }();
+#define DWR_CASE(S, PW)                                                                      \
+  if (rows_on && a.k == 3 && a.stride == S && a.pad == 1) {                                 \
+    const int SP = kDwThreads / (a.C / 4);                                                   \
+    const int nbands = (int)cdiv((int64_t)cdiv(a.OW, PW), SP);                               \
+    if (nbands <= nblk) {                                                                    \
+      const int want = (int)std::max<int64_t>(1, std::min<int64_t>(a.OH, nblk / nbands));    \
+      const int R = (int)cdiv(a.OH, want);                                                   \
+      const int nch = (int)cdiv(a.OH, R);                                                    \
+      if (bi)                                                                                \
+        dw_rows_kernel<S, PW, true><<<grid, kDwThreads, 0, st>>>(a, nbands, nch, R, stats_part, \
+                                                                  shift, *bi);               \
+      else                                                                                   \
+        dw_rows_kernel<S, PW, false><<<grid, kDwThreads, 0, st>>>(a, nbands, nch, R,           \
+                                                                   stats_part, shift, {});   \
+      return check_launch("dwconv_stats_rows");                                              \
+    }                                                                                        \
+  }
+  DWR_CASE(1, 4)
+  DWR_CASE(2, 2)
+#undef DWR_CASE
 #define DWS_CASE(K, S)                                                                      \
   if (a.k == K && a.stride == S) {                                                         \
     if (bi)                                                                                \

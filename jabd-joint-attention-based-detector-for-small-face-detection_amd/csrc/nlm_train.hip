@@ -157,6 +157,178 @@ __global__ __launch_bounds__(256) void nlm_bwd_attn_kernel(
   }
 }
 
+// One thread per up-sampled pixel (256 pixels per workgroup): the softmax row
+// is recomputed over all S bins in registers (K/V broadcast from LDS), and
+// the bin sums dK[s] = sum_p dL[p][s] q[p], dV[s] = sum_p P[p][s] dctx[p] go
+// through LDS in chunks of kNb bins: the pixels write their dL / P columns,
+// then thread (bin, group of 16 pixels) accumulates 16 pixels and the 16
+// groups are added in a fixed order.  No cross-lane shuffles (the quad form
+// spent its time in 32 LDS-routed butterflies per bin and wave).
+// part[b][blk][S][8] as nlm_bwd_attn_kernel's, blk = 256-pixel block.
+constexpr int kNb = 8;             // bins per LDS chunk
+constexpr int kNg = 256 / kNb;     // reducer pixel groups (of 256 / kNg pixels)
+constexpr int kNbP = 256 + 1;      // padded pixel stride of the chunk columns
+__global__ __launch_bounds__(256) void nlm_bwd_attn256_kernel(
+    const float* __restrict__ dout, int h, int w, int C, const float* __restrict__ q,
+    const float* __restrict__ kpool, const float* __restrict__ vpool, int S,
+    const float* __restrict__ wW, const float* __restrict__ wq, float* __restrict__ dq_out,
+    float* __restrict__ dxup, float* __restrict__ part, int nblk) {
+  // wW[C][4], wq[4][C], qs[256][4], dcs[256][4], dLs[kNb][kNbP], Ps[kNb][kNbP],
+  // red[kNg][kNb][8]
+  extern __shared__ float sm[];
+  const int b = blockIdx.y, t = threadIdx.x;
+  float* sWW = sm;
+  float* sWq = sWW + C * CH;
+  float* qs = sWq + CH * C;
+  float* dcs = qs + 256 * CH;
+  float* dLs = dcs + 256 * CH;
+  float* Ps = dLs + kNb * kNbP;
+  float* red = Ps + kNb * kNbP;
+  for (int i = t; i < C * CH; i += 256) {
+    sWW[i] = wW[i];
+    sWq[i] = wq[i];
+  }
+  const int pix = blockIdx.x * 256 + t;
+  const bool ok = pix < h * w;
+  const int64_t m = (int64_t)b * h * w + (ok ? pix : 0);
+  float qv[CH] = {0.f, 0.f, 0.f, 0.f};
+  if (ok) {
+    const float4 q4 = *reinterpret_cast<const float4*>(q + m * CH);
+    qv[0] = q4.x; qv[1] = q4.y; qv[2] = q4.z; qv[3] = q4.w;
+  }
+  __syncthreads();
+  const float* dop = dout + m * C;
+  float dctx[CH] = {0.f, 0.f, 0.f, 0.f};
+  if (ok)
+    for (int c = 0; c < C; c += 4) {
+      const float4 g = *reinterpret_cast<const float4*>(dop + c);
+#pragma unroll
+      for (int o = 0; o < CH; ++o)
+        dctx[o] = fmaf(g.x, sWW[(c + 0) * CH + o],
+                  fmaf(g.y, sWW[(c + 1) * CH + o],
+                  fmaf(g.z, sWW[(c + 2) * CH + o], fmaf(g.w, sWW[(c + 3) * CH + o], dctx[o]))));
+    }
+  *reinterpret_cast<float4*>(qs + t * CH) = make_float4(qv[0], qv[1], qv[2], qv[3]);
+  *reinterpret_cast<float4*>(dcs + t * CH) = make_float4(dctx[0], dctx[1], dctx[2], dctx[3]);
+  // K / V rows straight from global memory at wave-uniform addresses: scalar
+  // loads into SGPR operands (an LDS broadcast of a float4 costs the LDS a
+  // 1 KiB return per wave and bin)
+  const float4* __restrict__ K4 = reinterpret_cast<const float4*>(kpool + (int64_t)b * S * CH);
+  const float4* __restrict__ V4 = reinterpret_cast<const float4*>(vpool + (int64_t)b * S * CH);
+  auto logit = [&](const float4 k) {
+    return fmaf(qv[0], k.x, fmaf(qv[1], k.y, fmaf(qv[2], k.z, qv[3] * k.w)));
+  };
+  auto dprod = [&](const float4 v) {
+    return fmaf(dctx[0], v.x, fmaf(dctx[1], v.y, fmaf(dctx[2], v.z, dctx[3] * v.w)));
+  };
+  // four independent partial chains per reduction (two waves per SIMD do not
+  // hide a serial max / sum chain's latency)
+  float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  int s = 0;
+  for (; s + 4 <= S; s += 4)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) m4[u] = fmaxf(m4[u], logit(K4[s + u]));
+  for (; s < S; ++s) m4[0] = fmaxf(m4[0], logit(K4[s]));
+  const float mx = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
+  float d4[4] = {0.f, 0.f, 0.f, 0.f}, p4[4] = {0.f, 0.f, 0.f, 0.f};
+  for (s = 0; s + 4 <= S; s += 4)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float e = __expf(logit(K4[s + u]) - mx);
+      d4[u] += e;
+      p4[u] = fmaf(e, dprod(V4[s + u]), p4[u]);
+    }
+  for (; s < S; ++s) {
+    const float e = __expf(logit(K4[s]) - mx);
+    d4[0] += e;
+    p4[0] = fmaf(e, dprod(V4[s]), p4[0]);
+  }
+  const float den = (d4[0] + d4[1]) + (d4[2] + d4[3]);
+  const float inv = 1.f / den;
+  const float sdp = ((p4[0] + p4[1]) + (p4[2] + p4[3])) * inv;
+  float dq[CH] = {0.f, 0.f, 0.f, 0.f};
+  constexpr int ppg = 256 / kNg;
+  const int rb = t % kNb, rg = t / kNb;  // reducer: bin rb of the chunk, pixels ppg rg .. ppg rg + ppg - 1
+  for (int s0 = 0; s0 < S; s0 += kNb) {
+#pragma unroll 8
+    for (int j = 0; j < kNb; ++j) {  // (K4 / V4 rows: scalar loads batched by the unroll)
+      const int sj = s0 + j;
+      const bool sv = sj < S;
+      const float4 kk = K4[sv ? sj : 0], vv = V4[sv ? sj : 0];
+      const float P = (ok && sv) ? __expf(logit(kk) - mx) * inv : 0.f;
+      const float dL = P * (dprod(vv) - sdp);
+      dq[0] = fmaf(dL, kk.x, dq[0]);
+      dq[1] = fmaf(dL, kk.y, dq[1]);
+      dq[2] = fmaf(dL, kk.z, dq[2]);
+      dq[3] = fmaf(dL, kk.w, dq[3]);
+      dLs[j * kNbP + t] = dL;
+      Ps[j * kNbP + t] = P;
+    }
+    __syncthreads();
+    float acc[2 * CH] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int i = 0; i < ppg; ++i) {
+      const int p = rg * ppg + i;
+      const float dl = dLs[rb * kNbP + p], pp = Ps[rb * kNbP + p];
+      const float4 qq = *reinterpret_cast<const float4*>(qs + p * CH);
+      const float4 dc = *reinterpret_cast<const float4*>(dcs + p * CH);
+      acc[0] = fmaf(dl, qq.x, acc[0]); acc[1] = fmaf(dl, qq.y, acc[1]);
+      acc[2] = fmaf(dl, qq.z, acc[2]); acc[3] = fmaf(dl, qq.w, acc[3]);
+      acc[4] = fmaf(pp, dc.x, acc[4]); acc[5] = fmaf(pp, dc.y, acc[5]);
+      acc[6] = fmaf(pp, dc.z, acc[6]); acc[7] = fmaf(pp, dc.w, acc[7]);
+    }
+    float4* rr = reinterpret_cast<float4*>(red + (rg * kNb + rb) * 2 * CH);
+    rr[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    rr[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    __syncthreads();
+    if (t < kNb * 2 * CH) {  // (bin, component): the kNg groups in order
+      const int j = t / (2 * CH), o = t % (2 * CH);
+      float a = 0.f;
+#pragma unroll
+      for (int g2 = 0; g2 < kNg; ++g2) a += red[(g2 * kNb + j) * 2 * CH + o];
+      if (s0 + j < S) part[(((int64_t)b * nblk + blockIdx.x) * S + s0 + j) * 2 * CH + o] = a;
+    }
+    // (the next chunk's dLs / Ps writes come after this barrier; red is
+    // rewritten only after the next chunk's first barrier)
+    __syncthreads();
+  }
+  if (!ok) return;
+  *reinterpret_cast<float4*>(dq_out + m * CH) = make_float4(dq[0], dq[1], dq[2], dq[3]);
+  float* dx = dxup + m * C;
+  for (int c = 0; c < C; c += 4) {
+    const float4 g = *reinterpret_cast<const float4*>(dop + c);
+    float rr2[4] = {g.x, g.y, g.z, g.w};  // the "+ x" path
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int o = 0; o < CH; ++o) rr2[e] = fmaf(sWq[o * C + c + e], dq[o], rr2[e]);
+    *reinterpret_cast<float4*>(dx + c) = make_float4(rr2[0], rr2[1], rr2[2], rr2[3]);
+  }
+}
+
+// dk/dv[b][s][o] = sum over the nblk block partials (four block ranges per
+// output, added in a fixed order)
+__global__ __launch_bounds__(256) void nlm_bwd_kv_reduce4_kernel(const float* __restrict__ part,
+                                                                 int nblk, int S,
+                                                                 float* __restrict__ dk,
+                                                                 float* __restrict__ dv) {
+  __shared__ float red[4][64];
+  const int b = blockIdx.y;
+  const int o = blockIdx.x * 64 + (threadIdx.x & 63), qq = threadIdx.x >> 6;
+  const int tot = S * 2 * CH;
+  float a = 0.f;
+  if (o < tot)
+    for (int k = qq; k < nblk; k += 4) a += part[((int64_t)b * nblk + k) * tot + o];
+  red[qq][threadIdx.x & 63] = a;
+  __syncthreads();
+  if (qq == 0 && o < tot) {
+    a = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    const int s = o / (2 * CH), c = o % (2 * CH);
+    if (c < CH) dk[((int64_t)b * S + s) * CH + c] = a;
+    else dv[((int64_t)b * S + s) * CH + (c - CH)] = a;
+  }
+}
+
 __global__ void nlm_bwd_kv_reduce_kernel(const float* __restrict__ part, int nblk, int S,
                                          float* __restrict__ dk, float* __restrict__ dv) {
   const int b = blockIdx.y;
@@ -307,10 +479,31 @@ extern "C" int jabd_nlm_bwd_attn_f32(const float* dout, int32_t B, int32_t h, in
   JABD_REQUIRE(dout && q && kpool && vpool && wW && wq && dq && dxup && part && dk && dv &&
                    C % 4 == 0,
                "nlm_bwd_attn: bad args");
+  hipStream_t st = as_stream(stream);
+  // JABD_NLM_BWD_QUAD=1: the lane-quad kernel (A/B)
+  static const bool quad = [] {
+    const char* e = getenv("JABD_NLM_BWD_QUAD");
+    return e && e[0] == '1';
+  }();
+  if (!quad) {
+    const int nblk = (int)cdiv((int64_t)h * w, 256);  // within jabd.h's part size (64-pixel blocks)
+    const size_t smem = (2 * (size_t)C * CH + 2 * 256 * CH + 2 * (size_t)kNb * kNbP +
+                         kNg * (size_t)kNb * 2 * CH) * 4;
+    JABD_REQUIRE(smem <= 160 * 1024, "nlm_bwd_attn: LDS %zu > 160KiB", smem);
+    if (smem > 64 * 1024)
+      JABD_HIP(hipFuncSetAttribute((const void*)nlm_bwd_attn256_kernel,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+    dim3 g((unsigned)nblk, (unsigned)B);
+    nlm_bwd_attn256_kernel<<<g, 256, smem, st>>>(dout, h, w, C, q, kpool, vpool, S, wW, wq, dq,
+                                                 dxup, part, nblk);
+    if (int e = check_launch("nlm_bwd_attn")) return e;
+    dim3 g2((unsigned)cdiv(S * 2 * CH, 64), (unsigned)B);
+    nlm_bwd_kv_reduce4_kernel<<<g2, 256, 0, st>>>(part, nblk, S, dk, dv);
+    return check_launch("nlm_bwd_kv_reduce");
+  }
   const int nblk = (int)cdiv((int64_t)h * w, 64);  // a lane quad per pixel
   const size_t smem = (2 * (size_t)S * CH + 2 * (size_t)C * CH + 4 * (size_t)S * 2 * CH) * 4;
   JABD_REQUIRE(smem <= 64 * 1024, "nlm_bwd_attn: LDS %zu > 64KiB", smem);
-  hipStream_t st = as_stream(stream);
   dim3 g((unsigned)nblk, (unsigned)B);
   nlm_bwd_attn_kernel<<<g, 256, smem, st>>>(dout, h, w, C, q, kpool, vpool, S, wW, wq, dq, dxup,
                                             part, nblk);
