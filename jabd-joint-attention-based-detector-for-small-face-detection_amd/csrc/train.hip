@@ -1366,6 +1366,181 @@ __global__ __launch_bounds__(256) void dw_dgrad_bn_kernel(
   }
 }
 
+// dw_dgrad_bn_kernel for 3x3 as a row walker: a thread owns PW input (dx)
+// columns x 4 channels and a chunk of R dx rows and keeps the dy rows it
+// still needs in registers (stride 1: the three rows around the current dx
+// row, rotated by unrolling; stride 2: the row an even dx row shares with the
+// next odd one), so each dy row is read once per chunk instead of once per
+// dx row it feeds.  The taps are accumulated in dw_dgrad_bn_kernel's order
+// (kh ascending, rows outside dy skipped; kw ascending per column): dx / de
+// and the partials' terms are that kernel's bit for bit.  Workgroup
+// blockIdx.x = (image, band, chunk) < nwork; the remaining blocks of the
+// partial-row count write zero rows.
+template <int S, int PW, int MODE>
+__global__ __launch_bounds__(256) void dw_dgrad_bn_rows_kernel(
+    const float* __restrict__ dy, const float* __restrict__ w, int H, int W, int C, int OH, int OW,
+    int nstrip, int nbands, int nchunks, int R, int nwork, int lanes, float* __restrict__ dx,
+    const float* __restrict__ xb, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ gamma, const float* __restrict__ beta, int act, float slope,
+    float* __restrict__ part, const float* __restrict__ sdz = nullptr,
+    const float* __restrict__ sdzx = nullptr, int64_t M = 1) {
+  constexpr int K = 3, PAD = 1;
+  constexpr int OFF = floordiv_c(PAD - K + 1, S);
+  constexpr int L = (PW - 1 + PAD - S * OFF) / S + 1;
+  __shared__ float4 rs[256], rq[256];
+  const int C4 = C >> 2;
+  const int t = threadIdx.x;
+  const int rows_pass = 256 / lanes;
+  const int r0 = t / lanes;
+  const int cg = blockIdx.y * lanes + t % lanes;
+  const int chunk = blockIdx.x % nchunks;
+  const int bb = blockIdx.x / nchunks;
+  const int b = bb / nbands, band = bb % nbands;
+  const int strip = band * rows_pass + r0;
+  const bool tv = r0 < rows_pass && cg < C4 && (int)blockIdx.x < nwork && strip < nstrip;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 sS = z, sQ = z;
+  if (tv) {
+    const int c = cg * 4;
+    const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+    const float4 is = *reinterpret_cast<const float4*>(invstd + c);
+    const float4 gm = *reinterpret_cast<const float4*>(gamma + c);
+    const float4 bt = *reinterpret_cast<const float4*>(beta + c);
+    float a1[4] = {}, a2[4] = {};
+    if (MODE == 2) {
+      const float invM = 1.f / (float)M;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a1[e] = sdz[c + e] * invM;
+        a2[e] = sdzx[c + e] * invM;
+      }
+    }
+    float4 wk[K * K];
+#pragma unroll
+    for (int q = 0; q < K * K; ++q) wk[q] = reinterpret_cast<const float4*>(w + q * C)[cg];
+    const int iw0 = strip * PW;
+    const int ow0 = iw0 / S + OFF;
+    const int ih0 = chunk * R, ih1 = min(H, ih0 + R);
+    auto load_dy = [&](int oh, float4 (&seg)[L]) {
+      const bool rv = oh >= 0 && oh < OH;
+      const float4* drow =
+          reinterpret_cast<const float4*>(dy + (((int64_t)b * OH + (rv ? oh : 0)) * OW) * C) + cg;
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const int ow = ow0 + j;
+        seg[j] = (rv && ow >= 0 && ow < OW) ? drow[(int64_t)ow * C4] : z;
+      }
+    };
+    // one dx row from the dy rows of taps kh (valid ones only, kh ascending)
+    auto finish = [&](int ih, float4 (&acc)[PW]) {
+      const int64_t rb = (((int64_t)b * H + ih) * W) * C4 + cg;
+      float4* xrow = reinterpret_cast<float4*>(dx) + rb;
+      const float4* brow = reinterpret_cast<const float4*>(xb) + rb;
+#pragma unroll
+      for (int q = 0; q < PW; ++q) {
+        if (iw0 + q >= W) break;
+        if (MODE == 0) xrow[(int64_t)(iw0 + q) * C4] = acc[q];
+        const float4 xv = brow[(int64_t)(iw0 + q) * C4];
+        const float xh[4] = {(xv.x - mu.x) * is.x, (xv.y - mu.y) * is.y, (xv.z - mu.z) * is.z,
+                             (xv.w - mu.w) * is.w};
+        const float gg[4] = {acc[q].x, acc[q].y, acc[q].z, acc[q].w};
+        const float gmm[4] = {gm.x, gm.y, gm.z, gm.w}, btt[4] = {bt.x, bt.y, bt.z, bt.w};
+        const float iss[4] = {is.x, is.y, is.z, is.w};
+        float dzv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dzv[e] = gg[e] * act_d(fmaf(xh[e], gmm[e], btt[e]), act, slope);
+        if (MODE == 2) {
+          float o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = gmm[e] * iss[e] * (dzv[e] - a1[e] - xh[e] * a2[e]);
+          xrow[(int64_t)(iw0 + q) * C4] = make_float4(o[0], o[1], o[2], o[3]);
+          continue;
+        }
+        sS.x += dzv[0]; sS.y += dzv[1]; sS.z += dzv[2]; sS.w += dzv[3];
+        sQ.x = fmaf(dzv[0], xh[0], sQ.x); sQ.y = fmaf(dzv[1], xh[1], sQ.y);
+        sQ.z = fmaf(dzv[2], xh[2], sQ.z); sQ.w = fmaf(dzv[3], xh[3], sQ.w);
+      }
+    };
+    auto tap = [&](int kh, const float4 (&seg)[L], float4 (&acc)[PW]) {
+#pragma unroll
+      for (int q = 0; q < PW; ++q)
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw) {
+          if (((q + PAD - kw) % S + S) % S) continue;  // parity (iw0 % S == 0)
+          const int j = (q + PAD - kw - S * OFF) / S;
+          fma4(acc[q], seg[j], wk[kh * K + kw]);
+        }
+    };
+    if (ih0 < ih1) {
+      if constexpr (S == 1) {
+        // dx row ih: kh 0, 1, 2 read dy rows ih+1, ih, ih-1
+        float4 gA[L], gB[L], gC[L];
+        load_dy(ih0 - 1, gA);
+        load_dy(ih0, gB);
+        auto row = [&](int ih, const float4 (&gm1)[L], const float4 (&g0)[L],
+                       const float4 (&gp1)[L]) {
+          float4 acc[PW];
+#pragma unroll
+          for (int q = 0; q < PW; ++q) acc[q] = z;
+          if (ih + 1 < OH) tap(0, gp1, acc);
+          if (ih < OH) tap(1, g0, acc);
+          if (ih >= 1 && ih - 1 < OH) tap(2, gm1, acc);
+          finish(ih, acc);
+        };
+        for (int ih = ih0; ih < ih1; ih += 3) {
+          load_dy(ih + 1, gC);
+          row(ih, gA, gB, gC);
+          if (ih + 1 >= ih1) break;
+          load_dy(ih + 2, gA);
+          row(ih + 1, gB, gC, gA);
+          if (ih + 2 >= ih1) break;
+          load_dy(ih + 3, gB);
+          row(ih + 2, gC, gA, gB);
+        }
+      } else {
+        // even dx row 2m: kh 1 reads dy row m; odd row 2m+1: kh 0 reads m+1,
+        // kh 2 reads m
+        float4 gP[L], gN[L];
+        int have = -1;  // dy row held in gP
+        for (int ih = ih0; ih < ih1; ++ih) {
+          float4 acc[PW];
+#pragma unroll
+          for (int q = 0; q < PW; ++q) acc[q] = z;
+          const int m = ih >> 1;
+          if ((ih & 1) == 0) {
+            if (have != m) load_dy(m, gP);
+            have = m;
+            if (m < OH) tap(1, gP, acc);
+          } else {
+            if (have != m) load_dy(m, gP);
+            load_dy(m + 1, gN);
+            if (m + 1 < OH) tap(0, gN, acc);
+            if (m < OH) tap(2, gP, acc);
+#pragma unroll
+            for (int j = 0; j < L; ++j) gP[j] = gN[j];
+            have = m + 1;
+          }
+          finish(ih, acc);
+        }
+      }
+    }
+  }
+  if (MODE == 2) return;
+  rs[t] = sS;
+  rq[t] = sQ;
+  __syncthreads();
+  if (t < lanes && cg < C4) {
+    float4 S_ = z, Q_ = z;
+    for (int r = 0; r < rows_pass; ++r) {
+      const float4 a = rs[r * lanes + t], q = rq[r * lanes + t];
+      S_.x += a.x; S_.y += a.y; S_.z += a.z; S_.w += a.w;
+      Q_.x += q.x; Q_.y += q.y; Q_.z += q.z; Q_.w += q.w;
+    }
+    reinterpret_cast<float4*>(part + (int64_t)blockIdx.x * 2 * C)[cg] = S_;
+    reinterpret_cast<float4*>(part + (int64_t)blockIdx.x * 2 * C + C)[cg] = Q_;
+  }
+}
+
 // part[blk][tap][c] = sum over this block's output strips of dy * x(tap)
 // IT: x(tap) = act(bn(xs)) of the stored pre-BN tensor xs, recomputed on load
 // with dwconv.hip's BN-input forward expression (common.h dw_bn_in; in-bounds
@@ -2371,6 +2546,47 @@ extern "C" int jabd_dw_dgrad_bn_bwd_f32(const float* dy, const float* w, int32_t
   const int64_t M = (int64_t)B * H * W;
   // dz == NULL: the two-pass form (partials, then the apply with de
   // recomputed; MODE 1 + 2), else de is stored to dz and applied (MODE 0)
+  // 3x3 row walker, opt-in (JABD_DW_DGRAD_ROWS=1): measured slower than the
+  // strip-row kernel at every C4 shape (b1 s2 1803 -> 2640 us, b3 647 -> 1017,
+  // b7 181 -> 205: ~200 VGPRs, two waves per SIMD, where the strip-row
+  // kernel's dy re-reads hit L2)
+  static const bool rows_on = [] {
+    const char* e = getenv("JABD_DW_DGRAD_ROWS");
+    return e && e[0] == '1';
+  }();
+  const int rows_pass = 256 / lanes;
+#define DGR_CASE(S_, PW_)                                                                      \
+  if (rows_on && k == 3 && stride == S_) {                                                     \
+    const int ns = (int)cdiv(W, PW_);                                                          \
+    const int nbands = (int)cdiv(ns, rows_pass);                                               \
+    if ((int64_t)B * nbands <= nblk) {                                                         \
+      const int want = (int)std::max<int64_t>(1, std::min<int64_t>(H, nblk / ((int64_t)B * nbands))); \
+      const int R = (int)cdiv(H, want);                                                        \
+      const int nch = (int)cdiv(H, R);                                                         \
+      const int nwork = B * nbands * nch;                                                      \
+      if (dz)                                                                                  \
+        dw_dgrad_bn_rows_kernel<S_, PW_, 0><<<g, 256, 0, st>>>(                                \
+            dy, w, H, W, C, OH, OW, ns, nbands, nch, R, nwork, lanes, dz, x, mean, invstd,     \
+            gamma, beta, act, slope, part);                                                    \
+      else                                                                                     \
+        dw_dgrad_bn_rows_kernel<S_, PW_, 1><<<g, 256, 0, st>>>(                                \
+            dy, w, H, W, C, OH, OW, ns, nbands, nch, R, nwork, lanes, nullptr, x, mean, invstd, \
+            gamma, beta, act, slope, part);                                                    \
+      if (int e = check_launch("dw_dgrad_bn_rows")) return e;                                  \
+      bn_bwd_final_kernel<<<(unsigned)cdiv(C, kFinLanes), kFinThreads, 0, st>>>(part, nblk, C, \
+                                                                                dbeta, dgamma); \
+      if (int e = check_launch("bn_bwd_final")) return e;                                      \
+      if (!dz) {                                                                               \
+        dw_dgrad_bn_rows_kernel<S_, PW_, 2><<<g, 256, 0, st>>>(                                \
+            dy, w, H, W, C, OH, OW, ns, nbands, nch, R, nwork, lanes, dx, x, mean, invstd,     \
+            gamma, beta, act, slope, nullptr, dbeta, dgamma, M);                               \
+        return check_launch("dw_dgrad_bn_rows_apply");                                         \
+      }                                                                                        \
+      goto apply;                                                                              \
+    }                                                                                          \
+  }
+  DGR_CASE(1, 4) DGR_CASE(2, 8)
+#undef DGR_CASE
 #define DGB_CASE(K_, S_)                                                                       \
   if (k == K_ && stride == S_) {                                                               \
     if (dz)                                                                                    \
@@ -2396,6 +2612,7 @@ extern "C" int jabd_dw_dgrad_bn_bwd_f32(const float* dy, const float* w, int32_t
   }
   DGB_CASE(3, 1) DGB_CASE(3, 2) DGB_CASE(5, 1) DGB_CASE(5, 2)
 #undef DGB_CASE
+apply:
   int elanes;
   const dim3 grid = ew_grid(M, C, elanes);
   bn_bwd_apply_kernel<false, false><<<grid, kRedThreads, 0, st>>>(dz, C, 0, x, C, nullptr, 0, M, C,

@@ -350,7 +350,9 @@ def test_bnactfn_grads_wide(cuda, c, act, h, w):
 @pytest.mark.gpu
 @pytest.mark.parametrize("c,k,s,bhw,act", [(64, 3, 2, (4, 64, 48), "relu"), (72, 5, 1, (3, 37, 29), "relu"),
                                            (240, 3, 2, (2, 30, 34), "hswish"),
-                                           (480, 3, 1, (3, 32, 48), "hswish"), (16, 3, 1, (2, 9, 5), "relu")])
+                                           (480, 3, 1, (3, 32, 48), "hswish"), (16, 3, 1, (2, 9, 5), "relu"),
+                                           # a tall map: more rows than partial blocks
+                                           (16, 3, 1, (2, 5000, 40), "relu")])
 @pytest.mark.parametrize("recompute", [True, False])
 def test_dw_dgrad_bn_fused(cuda, c, k, s, bhw, act, recompute, monkeypatch):
     """MNv3 block backward through bn1 + act -> depthwise conv: the fused
