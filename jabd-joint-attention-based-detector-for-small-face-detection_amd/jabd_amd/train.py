@@ -55,6 +55,12 @@ BN_BWD_EPI = __import__("os").environ.get("JABD_BN_BWD_EPI", "1") != "0"
 # saves; 3x3/s1 (4.5 loads per element) and 5x5 (3.4-10) turn VALU-bound
 # and lose (r03 C4 profile).
 DW_BNIN = __import__("os").environ.get("JABD_DW_BNIN", "1") != "0"
+# JABD_DW_BNIN_S1=1: the 3x3 stride-1 blocks take bn1 + act on load as well
+# (their forward and weight-gradient kernels are row walkers now, ~1.6 loads
+# per input element).  Measured neutral (C4 52.8 vs 52.9 ms/step: the saved
+# apply pass is spent in the walkers' VALU), so off by default; it does save
+# the stored e of those blocks.
+DW_BNIN_S1 = __import__("os").environ.get("JABD_DW_BNIN_S1", "0") == "1"
 # JABD_DGBN_RECOMPUTE=0: bn1's backward stores de and applies from it instead
 # of recomputing de in a second depthwise pass (A/B)
 DGBN_RECOMPUTE = __import__("os").environ.get("JABD_DGBN_RECOMPUTE", "1") != "0"
@@ -1201,7 +1207,7 @@ class MNv3BlockFn(torch.autograd.Function):
             e_pre, bst1 = _conv_fwd_bn_stats(s, blk.conv1.weight, blk.bn1)
         else:
             e_pre, bst1 = _conv_fwd(s, blk.conv1.weight), None
-        if DW_BN_FUSE and DW_BNIN and k == 3 and stride == 2:
+        if DW_BN_FUSE and DW_BNIN and k == 3 and (stride == 2 or DW_BNIN_S1):
             # bn1 + act applied on conv2's loads: e is never written
             if bst1 is None:
                 bst1 = _bn_stats(e_pre, blk.bn1)
