@@ -371,6 +371,10 @@ static constexpr int kCellOff = 1 << 17;  // 18-bit biased cell coordinates
 static constexpr int kCellLim = 1 << 14;
 static constexpr int64_t kPairsPerBox = 128;  // off-block pair capacity per box
 static constexpr int kWaveRec = 64 * (int)kPairsPerBox;  // pair records per key-order wave
+#ifndef JABD_NMS_CAND
+#define JABD_NMS_CAND 4
+#endif
+static constexpr int kCand = JABD_NMS_CAND;              // candidate loads in flight per lane
 static constexpr int kLaneRec = 64;                      // of which each lane's own slots
 static constexpr int kWaveShared = kWaveRec - 64 * kLaneRec;  // and the wave's shared tail
 static constexpr int kK = 2;                  // class sub-division (neighbour range)
@@ -471,18 +475,16 @@ __global__ void grid_keys(const float4* __restrict__ sbox, const float* __restri
   val[o] = (int)r;
 }
 
-// candidate data in key order: gbox[q] = sbox[rank sval[q]] (+ area)
+// candidate data in key order: gbox[q] = sbox[rank sval[q]] (areas are
+// recomputed from the box where needed: nms_gather's expression)
 __global__ void grid_gather(const uint64_t* __restrict__ skey, const int* __restrict__ sval,
-                            int64_t total, const float4* __restrict__ sbox,
-                            const float* __restrict__ sarea, int64_t n, float4* __restrict__ gbox,
-                            float* __restrict__ garea) {
+                            int64_t total, const float4* __restrict__ sbox, int64_t n,
+                            float4* __restrict__ gbox) {
   const int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (q >= total) return;
   const uint64_t k = skey[q];
   if (k == ~0ull) return;
-  const int64_t o = (int64_t)(k >> 56) * n + sval[q];
-  gbox[q] = sbox[o];
-  garea[q] = sarea[o];
+  gbox[q] = sbox[(int64_t)(k >> 56) * n + sval[q]];
 }
 
 // Cell runs: after the sort, the boxes of one (image, classes, cell) key are
@@ -520,6 +522,7 @@ __global__ void grid_runs_insert(const uint64_t* __restrict__ skey, int64_t tota
       for (int x = cur + 1; x <= bc; ++x) istart[x] = (int)total;
   }
   if (k == kEmptyKey || (p > 0 && skey[p - 1] == k)) return;  // not a run start
+  tab += (k >> 56) * ((int64_t)mask + 1);  // this image's table
   uint32_t h = run_hash(k) & mask;
   for (;;) {
     const unsigned long long prev = atomicCAS(&tab[h].key, kEmptyKey, (unsigned long long)k);
@@ -552,6 +555,7 @@ __global__ void grid_runs_end(const uint64_t* __restrict__ skey, int64_t total,
   if (p >= total) return;
   const uint64_t k = skey[p];
   if (k == kEmptyKey || (p + 1 < total && skey[p + 1] == k)) return;  // not a run end
+  tab += (k >> 56) * ((int64_t)mask + 1);
   uint32_t h = run_hash(k) & mask;
   while (tab[h].key != k) h = (h + 1) & mask;
   tab[h].hi = (int)(p + 1);
@@ -559,7 +563,7 @@ __global__ void grid_runs_end(const uint64_t* __restrict__ skey, int64_t total,
 
 __global__ __launch_bounds__(256) void grid_pairs(
     const uint64_t* __restrict__ skey, const int* __restrict__ sval, int64_t total,
-    const float4* __restrict__ gbox, const float* __restrict__ garea, int64_t n, int bc,
+    const float4* __restrict__ gbox, int64_t n, int bc,
     float inv_w, float fcell, const unsigned* __restrict__ ext,
     const CellRun* __restrict__ tab, uint32_t tmask,
     double thr, int* __restrict__ dense, uint64_t* __restrict__ diag,
@@ -585,7 +589,7 @@ __global__ __launch_bounds__(256) void grid_pairs(
   if (k != ~0ull && !(dense[b] & 11)) {
   const int i = sval[p];
   const float4 bi = gbox[p];
-  const float ai = garea[p];
+  const float ai = (bi.z - bi.x) * (bi.w - bi.y);  // nms_gather's area expression (exact)
   const int cw = (int)((k >> 46) & (kNC - 1)), ch = (int)((k >> 36) & (kNC - 1));
   const unsigned* ew = ext + (int64_t)b * 4 * kNC;
   const unsigned* eh = ew + kNC;
@@ -599,6 +603,7 @@ __global__ __launch_bounds__(256) void grid_pairs(
   const float cx = (bi.x + bi.z) * 0.5f, cy = (bi.y + bi.w) * 0.5f;
   const float thrf = (float)thr;
   const uint32_t bkt0 = (uint32_t)(b * ((n + 63) >> 6));  // this image's first row block
+  tab += (int64_t)b * ((int64_t)tmask + 1);  // this image's run table (resident in its XCD's L2)
 
   // Off-block pairs go straight to this lane's kLaneRec slots of the wave's
   // region (no reservation); a lane past them takes slots of the wave's
@@ -658,31 +663,31 @@ __global__ __launch_bounds__(256) void grid_pairs(
           }
         }
         const int qe = n3[0] + n3[1] + n3[2];
-        // candidates four at a time: their loads are in flight together
-        for (int q = 0; q < qe; q += 4) {
-          int jj[4];
-          float4 bb[4];
-          float aa[4];
+        // candidates kCand at a time: their loads are in flight together (the
+        // area is recomputed from the box: nms_gather's expression, exact)
+        for (int q = 0; q < qe; q += kCand) {
+          int jj[kCand];
+          float4 bb[kCand];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
+          for (int u = 0; u < kCand; ++u) {
             const int t = q + u < qe ? q + u : q;
             const int qq = t < n3[0] ? lo3[0] + t
                                      : (t < n3[0] + n3[1] ? lo3[1] + (t - n3[0])
                                                           : lo3[2] + (t - n3[0] - n3[1]));
             jj[u] = sval[qq];
             bb[u] = gbox[qq];
-            aa[u] = garea[qq];
           }
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
+          for (int u = 0; u < kCand; ++u) {
             const int j = jj[u];
+            const float aa_u = (bb[u].z - bb[u].x) * (bb[u].w - bb[u].y);
             // same class: each pair once, from the lower rank
             bool hit = q + u < qe && !(nbr == 0 && j <= i);
             ntest += hit;
 #ifdef JABD_NMS_AB_NOIOU  // A/B timing build: the walk and loads alone (results wrong)
-            hit = hit && __float_as_uint(bb[u].x) == 0x7fc00001u && aa[u] == 1.f;
+            hit = hit && __float_as_uint(bb[u].x) == 0x7fc00001u && aa_u == 1.f;
 #else
-            if (hit) hit = iou_gt(bi.x, bi.y, bi.z, bi.w, ai, bb[u], aa[u], thr, thrf, true);
+            if (hit) hit = iou_gt(bi.x, bi.y, bi.z, bi.w, ai, bb[u], aa_u, thr, thrf, true);
 #endif
 #ifdef JABD_NMS_AB_NOSTORE  // A/B timing build: tests kept, pair output dropped
             ntest += hit ? 65536u : 0u;
@@ -856,7 +861,10 @@ __device__ __forceinline__ int loader_id(int wave) { return wave - 1; }
 #endif
 static constexpr int kMetaRing = 32;        // row blocks staged ahead
 static constexpr int kEntRing = 16384;      // incoming pairs staged ahead (power of two)
-static constexpr int kPullLag = 8;          // a loader resolves block c once c - kPullLag are final
+#ifndef JABD_NMS_LAG
+#define JABD_NMS_LAG 8
+#endif
+static constexpr int kPullLag = JABD_NMS_LAG;         // a loader resolves block c once c - kPullLag are final
 static constexpr unsigned kSpinMax = 1u << 22;
 static constexpr int kPullStaticLds = kEntRing * 4 + kMetaRing * 64 * 16 + kMetaRing * 24 + 16;
 
@@ -1353,7 +1361,6 @@ struct NmsWs {
   CellRun* runs;               // cell-run hash table (power-of-two slots)
   uint32_t run_mask;
   float4* gbox;
-  float* garea;
   int64_t cap;
 };
 
@@ -1404,10 +1411,11 @@ static void carve_nms(A& a, int64_t batch, int64_t n, NmsWs* w) {
   T(uint64_t, nwaves * kWaveRec, rec);
   T(uint32_t, nwaves * kWaveRec, csr);
   T(float4, bc * n, gbox);
-  T(float, bc * n, garea);
+  // one run table per image (its own XCD's L2 holds it: 2 MiB at n = 100k),
+  // power-of-two slots >= 1.25 n (load factor <= 0.8 even if every box is a run)
   int64_t slots = 1024;
-  while (slots < 2 * bc * n) slots <<= 1;  // load factor <= 1/2
-  T(CellRun, slots, runs);
+  while (slots * 4 < 5 * n) slots <<= 1;
+  T(CellRun, bc * slots, runs);
 #undef T
   if (w) w->run_mask = (uint32_t)(slots - 1);
   if (w) {
@@ -1475,7 +1483,7 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
           {w.npairs, gb * (int64_t)sizeof(int) * bc, 0u},
           {w.tested, gb * (int64_t)sizeof(unsigned long long) * bc * 64, 0u},
           {w.ext, gb * (int64_t)sizeof(unsigned) * bc * 4 * kNC, 0u},
-          {w.runs, gb * (int64_t)sizeof(CellRun) * ((int64_t)w.run_mask + 1), 0xFFFFFFFFu},
+          {w.runs, gb * (int64_t)sizeof(CellRun) * bc * ((int64_t)w.run_mask + 1), 0xFFFFFFFFu},
           {w.diag, gb * (int64_t)sizeof(uint64_t) * bc * n, 0u},
           {w.bhist + (int64_t)bc * nb * w.kchunks, gb * (int64_t)sizeof(int), 0u}};
       if (int e = fill_ranges(fr, 11, st)) return e;
@@ -1516,7 +1524,7 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
                                w.tmp, w.tmp_bytes, st))
         return e;
       grid_gather<<<(unsigned)cdiv((int64_t)bc * n, 256), 256, 0, st>>>(
-          w.kout, w.gval_out, (int64_t)bc * n, w.sbox, w.sarea, n, w.gbox, w.garea);
+          w.kout, w.gval_out, (int64_t)bc * n, w.sbox, n, w.gbox);
       if (int e = check_launch("grid_gather")) return e;
       const unsigned gt = (unsigned)cdiv((int64_t)bc * n, 256);
       grid_runs_insert<<<gt, 256, 0, st>>>(w.kout, (int64_t)bc * n, w.runs, w.run_mask, bc,
@@ -1525,7 +1533,7 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
       grid_runs_end<<<gt, 256, 0, st>>>(w.kout, (int64_t)bc * n, w.runs, w.run_mask);
       if (int e = check_launch("grid_runs_end")) return e;
       grid_pairs<<<(unsigned)grid_pair_blocks((int64_t)bc * n), 256, 0, st>>>(
-          w.kout, w.gval_out, (int64_t)bc * n, w.gbox, w.garea, n, bc, inv_w, fcell, w.ext,
+          w.kout, w.gval_out, (int64_t)bc * n, w.gbox, n, bc, inv_w, fcell, w.ext,
           w.runs, w.run_mask, iou_thr, w.dense, w.diag, w.rec, w.lcnt, w.wcnt, w.tested);
       if (int e = check_launch("grid_pairs")) return e;
       const unsigned gk = (unsigned)(w.kchunks * bc);
