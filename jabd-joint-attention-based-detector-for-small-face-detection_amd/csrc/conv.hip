@@ -1063,8 +1063,10 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
 // ---------------------------------------------------------------------------
 // MobileNetV3 stem: conv3x3/s2/p1, 3 -> 16 channels, read straight from the
 // NCHW network input (layout conversion fused), folded BN + activation,
-// NHWC output.  One thread per output pixel.
-//  - all 27 input values are loaded up front (27 loads in flight per lane);
+// NHWC output.  One thread per output column, kStemRows output rows.
+//  - all (2 kStemRows + 1) x 9 input values are loaded up front (the input
+//    row shared by two output rows once: 45 loads for 2 pixels instead of
+//    54; 2 rows per thread measured 245 -> 226 us at bs32 1024^2);
 //  - the 27x16 weights and the bias are read at wave-uniform addresses, so
 //    they arrive through scalar loads and feed the FMAs as SGPR operands; an
 //    empty asm with a memory clobber between taps keeps the compiler from
@@ -1077,6 +1079,10 @@ extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t st
 namespace jabd {
 constexpr int kStemOut = 16;
 constexpr int kStemThreads = 128;
+#ifndef STEM_ROWS
+#define STEM_ROWS 2
+#endif
+constexpr int kStemRows = STEM_ROWS;  // output rows per thread
 
 template <int ACT>
 __global__ __launch_bounds__(kStemThreads) void stem_kernel(const float* __restrict__ x, int H,
@@ -1085,17 +1091,20 @@ __global__ __launch_bounds__(kStemThreads) void stem_kernel(const float* __restr
                                                             const float* __restrict__ bias,
                                                             float* __restrict__ y) {
   __shared__ float4 st[kStemThreads / 64][64 * kStemOut / 4 + 64 / 8];  // +1 float4 per 8 px
-  const int b = blockIdx.z, oh = blockIdx.y;
+  const int b = blockIdx.z, oh0 = blockIdx.y * kStemRows;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ow0 = blockIdx.x * kStemThreads + wave * 64;  // this wave's first pixel
   const int ow = ow0 + lane;
   const bool pv = ow < OW;
   const float* xb = x + (int64_t)b * 3 * H * W;
   const int64_t HW = (int64_t)H * W;
-  float v[27];
+  // the 2 kStemRows + 1 input rows of this thread's kStemRows output rows
+  // (rows shared by neighbouring output rows are loaded once)
+  constexpr int IR = 2 * kStemRows + 1;
+  float v[IR][9];
 #pragma unroll
-  for (int kh = 0; kh < 3; ++kh) {
-    const int ih = 2 * oh - 1 + kh;
+  for (int r = 0; r < IR; ++r) {
+    const int ih = 2 * oh0 - 1 + r;
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
       const int iw = 2 * ow - 1 + kw;
@@ -1104,38 +1113,45 @@ __global__ __launch_bounds__(kStemThreads) void stem_kernel(const float* __restr
 #pragma unroll
       for (int ci = 0; ci < 3; ++ci) {
         const float t = xp[ci * HW];
-        v[(kh * 3 + kw) * 3 + ci] = ok ? t : 0.f;
+        v[r][kw * 3 + ci] = ok ? t : 0.f;
       }
     }
-  }
-  float o[kStemOut];
-#pragma unroll
-  for (int n = 0; n < kStemOut; ++n) o[n] = bias[n];
-#pragma unroll
-  for (int tp = 0; tp < 27; ++tp) {
-    asm volatile("" ::: "memory");
-    const float* wr = w + tp * kStemOut;
-#pragma unroll
-    for (int n = 0; n < kStemOut; ++n) o[n] = fmaf(wr[n], v[tp], o[n]);
   }
   auto f = [](float u) {
     return ACT == ACT_HSWISH ? hswish_f(u) : ACT == ACT_RELU ? relu_f(u) : u;
   };
-  // pixel p's 4 float4 at st[4p + p/8 + q]: the pad keeps the 16 B writes of
-  // 8 consecutive lanes on distinct banks
   float4* sw = st[wave];
 #pragma unroll
-  for (int q = 0; q < kStemOut / 4; ++q)
-    sw[4 * lane + (lane >> 3) + q] =
-        make_float4(f(o[4 * q]), f(o[4 * q + 1]), f(o[4 * q + 2]), f(o[4 * q + 3]));
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private region
-  float4* yw = reinterpret_cast<float4*>(y + (((int64_t)b * OH + oh) * OW + ow0) * kStemOut);
-  const int npx = min(64, OW - ow0);
+  for (int ro = 0; ro < kStemRows; ++ro) {
+    const int oh = oh0 + ro;
+    if (oh >= OH) break;
+    float o[kStemOut];
 #pragma unroll
-  for (int q = 0; q < kStemOut / 4; ++q) {
-    const int i = q * 64 + lane;  // float4 index in the wave's block
-    const int p = i >> 2;
-    if (p < npx) yw[i] = sw[i + (p >> 3)];
+    for (int n = 0; n < kStemOut; ++n) o[n] = bias[n];
+#pragma unroll
+    for (int tp = 0; tp < 27; ++tp) {
+      asm volatile("" ::: "memory");
+      const float* wr = w + tp * kStemOut;
+      const float xv = v[2 * ro + tp / 9][tp % 9];   // tap (kh, kw, ci) = tp
+#pragma unroll
+      for (int n = 0; n < kStemOut; ++n) o[n] = fmaf(wr[n], xv, o[n]);
+    }
+    // pixel p's 4 float4 at st[4p + p/8 + q]: the pad keeps the 16 B writes of
+    // 8 consecutive lanes on distinct banks
+#pragma unroll
+    for (int q = 0; q < kStemOut / 4; ++q)
+      sw[4 * lane + (lane >> 3) + q] =
+          make_float4(f(o[4 * q]), f(o[4 * q + 1]), f(o[4 * q + 2]), f(o[4 * q + 3]));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private region
+    float4* yw = reinterpret_cast<float4*>(y + (((int64_t)b * OH + oh) * OW + ow0) * kStemOut);
+    const int npx = min(64, OW - ow0);
+#pragma unroll
+    for (int q = 0; q < kStemOut / 4; ++q) {
+      const int i = q * 64 + lane;  // float4 index in the wave's block
+      const int p = i >> 2;
+      if (p < npx) yw[i] = sw[i + (p >> 3)];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next row's writes
   }
 }
 }  // namespace jabd
@@ -1145,7 +1161,7 @@ extern "C" int jabd_stem_nchw_f32(const float* x, int32_t B, int32_t H, int32_t 
                                   jabd_stream_t stream) {
   JABD_REQUIRE(x && w && bias && y && B > 0 && H > 0 && W > 0, "stem: bad args");
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
-  dim3 g((unsigned)cdiv(OW, kStemThreads), (unsigned)OH, (unsigned)B);
+  dim3 g((unsigned)cdiv(OW, kStemThreads), (unsigned)cdiv(OH, kStemRows), (unsigned)B);
   JABD_REQUIRE(act == ACT_HSWISH || act == ACT_RELU || act == ACT_NONE, "stem: act %d", act);
   hipStream_t st = as_stream(stream);
   if (act == ACT_HSWISH)
