@@ -994,8 +994,12 @@ def main():
             extra["variants"] = {k: variant_forward(k, device, args.size, args.batch, 5)
                                  for k in ("beca", "small")}
     if not args.no_train:
+        # every rank runs the conv-timer step: it is a full training step whose
+        # backward all-reduces the gradients, so all ranks must take it (a
+        # rank-0-only extra step would leave its RCCL all-reduces unmatched);
+        # only rank 0 reports it
         tr = {"C4_mnv3": train_bench("mnv3", args.batch, args.size, args.train_steps, 3, device,
-                                     dist, rank, conv_roofline_steps=1 if rank == 0 else 0)}
+                                     dist, rank, conv_roofline_steps=1)}
         if world == 1 and args.r50_batch > 0:
             tr["C3_r50"] = train_bench("r50", args.r50_batch, args.size, max(2, args.train_steps // 2),
                                        2, device, None, rank, conv_roofline_steps=1)
