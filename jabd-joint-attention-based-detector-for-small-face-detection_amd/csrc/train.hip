@@ -1803,6 +1803,9 @@ __global__ void eca_gate_bwd_kernel(const float* __restrict__ part, int nblk, in
   const int h = (k - 1) / 2;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float ds = 0.f;
+    // blocks in order (up to 64 partials per channel: the unroll keeps 8 of
+    // the loads in flight instead of one L2 round trip per add)
+#pragma unroll 8
     for (int q = 0; q < nblk; ++q) ds += part[((int64_t)b * nblk + q) * C + c];
     const float sv = s[(int64_t)b * C + c];
     float gd;
@@ -1831,6 +1834,9 @@ __global__ void eca_gate_bwd_kernel(const float* __restrict__ part, int nblk, in
   if (threadIdx.x < k) {
     const int t = threadIdx.x;
     float acc = 0.f;
+    // (in-order fma chain; the unroll only lets the LDS reads run ahead of
+    // it: up to C = 960 iterations, each waiting on its read otherwise)
+#pragma unroll 8
     for (int c = 0; c < C; ++c) {
       const int cc = c + t - h;
       if (cc >= 0 && cc < C) acc = fmaf(dz[c], mu[cc], acc);
@@ -2381,6 +2387,8 @@ __global__ __launch_bounds__(256) void wgrad_eca_reduce_kernel(
   for (int n = t; n < Cout; n += blockDim.x) {
     const float wn = w[(int64_t)n * E + c];
     float acc = 0.f;
+    // images in order (the unroll lets their loads run ahead of the chain)
+#pragma unroll 8
     for (int b = 0; b < B; ++b) {
       const float* pb = part + (int64_t)b * cpi * EN + (int64_t)c * Cout + n;
       float g0 = 0.f, g1 = 0.f;
@@ -2399,6 +2407,7 @@ __global__ __launch_bounds__(256) void wgrad_eca_reduce_kernel(
   __syncthreads();
   for (int b = t; b < B; b += blockDim.x) {
     float sm = 0.f;
+#pragma unroll 8
     for (int n = 0; n < Cout; ++n) sm += prod[b * Cout + n];
     ds[(int64_t)b * E + c] = sm;
   }
