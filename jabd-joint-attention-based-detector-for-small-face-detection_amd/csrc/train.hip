@@ -886,6 +886,9 @@ __global__ __launch_bounds__(256) void wgrad_reduce2_kernel(const float* __restr
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (r < rows && o < KN) {
     int64_t c = r;
+    // two iterations' loads in flight (same accumulation order; 10.2 -> 8.4
+    // us per call over C4's 71 calls per step)
+#pragma unroll 2
     for (; c + 3 * rows < nchunk; c += 4 * rows) {
       s0 += part[c * KN + o];
       s1 += part[(c + rows) * KN + o];
