@@ -138,6 +138,21 @@ struct Sizer {
   }
 };
 
+// n / d for 0 <= n < 2^31 by multiply-high and shift with a host-built
+// divisor (a runtime-divisor integer division is ~15-40 instructions)
+struct FastDiv {
+  uint32_t m, l, d;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  const uint64_t m = ((((uint64_t)1 << l) - d) << 32) / d + 1;
+  return FastDiv{(uint32_t)m, l, d};
+}
+__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
+  return (int)((__umulhi((uint32_t)n, f.m) + (uint32_t)n) >> f.l);
+}
+
 }  // namespace jabd
 
 #define JABD_REQUIRE(cond, ...)      \

@@ -121,18 +121,7 @@ struct XdItem {
 // n / d for 0 <= n < 2^31 by multiply-high and shift (host-built divisor):
 // the per-item decode would otherwise run three ~40-instruction integer
 // divisions on the scalar unit.
-struct FastDiv {
-  uint32_t m, l, d;
-};
-static FastDiv make_fastdiv(uint32_t d) {
-  uint32_t l = 0;
-  while ((1ull << l) < d) ++l;
-  const uint64_t m = ((((uint64_t)1 << l) - d) << 32) / d + 1;
-  return FastDiv{(uint32_t)m, l, d};
-}
-__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
-  return (int)((__umulhi((uint32_t)n, f.m) + (uint32_t)n) >> f.l);
-}
+// (FastDiv / make_fastdiv / fdiv: common.h)
 struct XdDivs {
   FastDiv nch, tiles_img, tiles_w;
 };

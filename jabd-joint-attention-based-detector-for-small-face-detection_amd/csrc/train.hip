@@ -736,9 +736,15 @@ struct WvPitch {
   static constexpr int v = (KT % 32 == 16) ? KT : KT + 16;
 };
 
+// host-built divisors of the im2col decode (OH*OW, OW, Cin, KW)
+struct WgDivs {
+  FastDiv ohw, ow, cin, kw;
+};
+
 template <int KT, int NT>
 __global__ __launch_bounds__(256) void conv_wgrad_v_kernel(const ConvArgs p, int px_per_wg,
-                                                           int fast1x1, float* __restrict__ part) {
+                                                           int fast1x1, float* __restrict__ part,
+                                                           const WgDivs dv) {
   constexpr int LDA = WvPitch<KT>::v, LDN = WvPitch<NT>::v;
   constexpr int QA = KT / 16, QD = NT / 16;  // float4 loads per thread per stage
   constexpr int NBK = KT / 16, NBN = NT / 16, NB = NBK * NBN;
@@ -768,15 +774,15 @@ __global__ __launch_bounds__(256) void conv_wgrad_v_kernel(const ConvArgs p, int
         if (fast1x1) {
           v = *reinterpret_cast<const float4*>(p.x + (int64_t)m * p.x_ps + p.x_c0 + k);
           if (p.ascale) {
-            const int b = m / OHW;
+            const int b = fdiv(m, dv.ohw);
             const float4 s4 = *reinterpret_cast<const float4*>(p.ascale + (int64_t)b * p.ascale_bs + k);
             v.x *= s4.x; v.y *= s4.y; v.z *= s4.z; v.w *= s4.w;
           }
         } else {
-          const int b = m / OHW, rr = m - b * OHW;
-          const int oh = rr / p.OW, ow = rr - oh * p.OW;
-          const int tap = k / p.Cin, ci = k - tap * p.Cin;
-          const int kh = tap / p.KW, kw = tap - kh * p.KW;
+          const int b = fdiv(m, dv.ohw), rr = m - b * OHW;
+          const int oh = fdiv(rr, dv.ow), ow = rr - oh * p.OW;
+          const int tap = fdiv(k, dv.cin), ci = k - tap * p.Cin;
+          const int kh = fdiv(tap, dv.kw), kw = tap - kh * p.KW;
           const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
           if (ih >= 0 && ih < p.H && iw >= 0 && iw < p.W) {
             v = *reinterpret_cast<const float4*>(p.x + (int64_t)b * p.x_bs +
@@ -1015,7 +1021,8 @@ constexpr int kWg32Px = 32;  // pixels per stage
 template <int KT, int NT>
 __global__ __launch_bounds__(256, 2) void conv_wgrad32_kernel(const ConvArgs p, int px_per_wg,
                                                               int fast1x1,
-                                                              float* __restrict__ part) {
+                                                              float* __restrict__ part,
+                                                              const WgDivs dv) {
   constexpr int TK = KT / 64, TNn = NT / 64;          // 32x32 blocks per wave (k, n)
   constexpr int QA = kWg32Px * KT / 4 / 256, QD = kWg32Px * NT / 4 / 256;
   __shared__ float Xs[kWg32Px * KT];
@@ -1031,6 +1038,23 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad32_kernel(const ConvArgs p, 
   const int OHW = p.OH * p.OW;
 
   float4 ra[QA], rd[QD];
+  // the A elements' im2col k decomposition is fixed for the launch (this
+  // thread's channel column does not move between stages): decoded once here,
+  // not per stage (a runtime-divisor division inside the stage loop's guarded
+  // block cannot be hoisted by the compiler)
+  int a_ci[QA], a_kh[QA], a_kw[QA];
+#pragma unroll
+  for (int q = 0; q < QA; ++q) {
+    const int k = k0 + ((q * 256 + t) % (KT / 4)) * 4;
+    a_ci[q] = k;
+    a_kh[q] = a_kw[q] = 0;
+    if (!fast1x1 && k < K) {
+      const int tap = fdiv(k, dv.cin);
+      a_ci[q] = k - tap * p.Cin;
+      a_kh[q] = fdiv(tap, dv.kw);
+      a_kw[q] = tap - a_kh[q] * p.KW;
+    }
+  }
   auto load_stage = [&](int px0) {
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
@@ -1039,18 +1063,18 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad32_kernel(const ConvArgs p, 
       const int m = px0 + px, k = k0 + c4;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (m < mend && k < K) {
-        const int b = m / OHW;
-        int ci = k;
+        int b = 0;
+        const int ci = a_ci[q];
         int64_t off;
         bool ok = true;
         if (fast1x1) {
           off = (int64_t)m * p.x_ps + p.x_c0 + k;
+          if (p.ascale) b = fdiv(m, dv.ohw);
         } else {
+          b = fdiv(m, dv.ohw);
           const int rr = m - b * OHW;
-          const int oh = rr / p.OW, ow = rr - oh * p.OW;
-          const int tap = k / p.Cin;
-          ci = k - tap * p.Cin;
-          const int kh = tap / p.KW, kw = tap - kh * p.KW;
+          const int oh = fdiv(rr, dv.ow), ow = rr - oh * p.OW;
+          const int kh = a_kh[q], kw = a_kw[q];
           const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
           ok = ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
           off = (int64_t)b * p.x_bs + ((int64_t)ih * p.W + iw) * p.x_ps + p.x_c0 + ci;
@@ -2243,6 +2267,8 @@ extern "C" int jabd_bn_act_bwd_ex_f32(const float* dy, int32_t lddy, int32_t dyc
 static void wgrad_launch_parts(const ConvArgs& a, int64_t per, int64_t nch, float* part,
                                hipStream_t st) {
   const int K = a.KH * a.KW * a.Cin;
+  const WgDivs dv{make_fastdiv((uint32_t)((int64_t)a.OH * a.OW)), make_fastdiv((uint32_t)a.OW),
+                  make_fastdiv((uint32_t)a.Cin), make_fastdiv((uint32_t)a.KW)};
   if (wgrad_vec_ok(a) && wgrad32_ok(a)) {
     const int tk = wg32_tile(K), tn = wg32_tile(a.Cout);
     const int fast = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.H == a.OH &&
@@ -2250,7 +2276,7 @@ static void wgrad_launch_parts(const ConvArgs& a, int64_t per, int64_t nch, floa
     dim3 g((unsigned)cdiv(K, tk), (unsigned)cdiv(a.Cout, tn), (unsigned)nch);
 #define W32_CASE(KT_, NT_)                                                        \
   if (tk == KT_ && tn == NT_)                                                     \
-    conv_wgrad32_kernel<KT_, NT_><<<g, 256, 0, st>>>(a, (int)per, fast, part);
+    conv_wgrad32_kernel<KT_, NT_><<<g, 256, 0, st>>>(a, (int)per, fast, part, dv);
     W32_CASE(64, 64) W32_CASE(64, 128) W32_CASE(128, 64) W32_CASE(128, 128)
 #undef W32_CASE
   } else if (wgrad_vec_ok(a)) {
@@ -2260,7 +2286,7 @@ static void wgrad_launch_parts(const ConvArgs& a, int64_t per, int64_t nch, floa
     dim3 g((unsigned)cdiv(K, tk), (unsigned)cdiv(a.Cout, tn), (unsigned)nch);
 #define WV_CASE(KT_, NT_)                                                         \
   if (tk == KT_ && tn == NT_)                                                     \
-    conv_wgrad_v_kernel<KT_, NT_><<<g, 256, 0, st>>>(a, (int)per, fast, part);
+    conv_wgrad_v_kernel<KT_, NT_><<<g, 256, 0, st>>>(a, (int)per, fast, part, dv);
     WV_CASE(16, 16) WV_CASE(16, 32) WV_CASE(16, 64)
     WV_CASE(32, 16) WV_CASE(32, 32) WV_CASE(32, 64)
     WV_CASE(64, 16) WV_CASE(64, 32) WV_CASE(64, 64)
