@@ -1018,15 +1018,19 @@ static int wv_tile(int64_t n) { return n <= 16 ? 16 : (n <= 32 ? 32 : 64); }
 // ---------------------------------------------------------------------------
 constexpr int kWg32Px = 32;  // pixels per stage
 
-template <int KT, int NT>
+
+template <int KT, int NT, bool DB>
 __global__ __launch_bounds__(256, 2) void conv_wgrad32_kernel(const ConvArgs p, int px_per_wg,
                                                               int fast1x1,
                                                               float* __restrict__ part,
                                                               const WgDivs dv) {
   constexpr int TK = KT / 64, TNn = NT / 64;          // 32x32 blocks per wave (k, n)
   constexpr int QA = kWg32Px * KT / 4 / 256, QD = kWg32Px * NT / 4 / 256;
-  __shared__ float Xs[kWg32Px * KT];
-  __shared__ float Ds[kWg32Px * NT];
+  // DB: two LDS stage buffers — stage s+1 is stored while no wave can still
+  // be reading its buffer (read in stage s-1, before the last barrier): one
+  // barrier per stage instead of two
+  __shared__ float XsA[(DB ? 2 : 1) * kWg32Px * KT];
+  __shared__ float DsA[(DB ? 2 : 1) * kWg32Px * NT];
   const int K = p.KH * p.KW * p.Cin;
   const int k0 = blockIdx.x * KT, n0 = blockIdx.y * NT;
   const int chunk = blockIdx.z;
@@ -1110,6 +1114,44 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad32_kernel(const ConvArgs p, 
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[u][v][r] = 0.f;
 
+  if constexpr (DB) {
+  auto store_stage = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < QA; ++q)
+      reinterpret_cast<float4*>(XsA + buf * kWg32Px * KT)[q * 256 + t] = ra[q];
+#pragma unroll
+    for (int q = 0; q < QD; ++q)
+      reinterpret_cast<float4*>(DsA + buf * kWg32Px * NT)[q * 256 + t] = rd[q];
+  };
+  load_stage(mbeg);
+  store_stage(0);
+  __syncthreads();
+  int cb = 0;
+  for (int px0 = mbeg; px0 < mend; px0 += kWg32Px, cb ^= 1) {
+    const bool more = px0 + kWg32Px < mend;
+    if (more) load_stage(px0 + kWg32Px);
+    const float* Xs = XsA + cb * kWg32Px * KT;
+    const float* Ds = DsA + cb * kWg32Px * NT;
+#pragma unroll 4
+    for (int pp = 0; pp < kWg32Px / 2; ++pp) {
+      const int row = 2 * pp + h;
+      float a[TK], b[TNn];
+#pragma unroll
+      for (int u = 0; u < TK; ++u) a[u] = Xs[row * KT + wk + 32 * u + j];
+#pragma unroll
+      for (int v = 0; v < TNn; ++v) b[v] = Ds[row * NT + wn + 32 * v + j];
+#pragma unroll
+      for (int u = 0; u < TK; ++u)
+#pragma unroll
+        for (int v = 0; v < TNn; ++v)
+          acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[v], acc[u][v], 0, 0, 0);
+    }
+    if (more) store_stage(cb ^ 1);
+    __syncthreads();
+  }
+  } else {
+  float* Xs = XsA;
+  float* Ds = DsA;
   load_stage(mbeg);
   for (int px0 = mbeg; px0 < mend; px0 += kWg32Px) {
 #pragma unroll
@@ -1135,6 +1177,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad32_kernel(const ConvArgs p, 
           acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[v], acc[u][v], 0, 0, 0);
     }
     __syncthreads();
+  }
   }
   // acc[u][v][r]: k = k0 + wk + 32u + 8(r>>2) + 4h + (r&3), n = n0 + wn + 32v + j
   float* pc = part + (int64_t)chunk * K * p.Cout;
@@ -2274,9 +2317,15 @@ static void wgrad_launch_parts(const ConvArgs& a, int64_t per, int64_t nch, floa
     const int fast = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.H == a.OH &&
                      a.W == a.OW;
     dim3 g((unsigned)cdiv(K, tk), (unsigned)cdiv(a.Cout, tn), (unsigned)nch);
-#define W32_CASE(KT_, NT_)                                                        \
-  if (tk == KT_ && tn == NT_)                                                     \
-    conv_wgrad32_kernel<KT_, NT_><<<g, 256, 0, st>>>(a, (int)per, fast, part, dv);
+    // double-buffered stages for the 1x1 layers (tools/wgdb_ab.sh: 1x1 shapes
+    // +0-19%, the 3x3 ones 5% slower with the doubled LDS)
+#define W32_CASE(KT_, NT_)                                                              \
+  if (tk == KT_ && tn == NT_) {                                                         \
+    if (fast)                                                                           \
+      conv_wgrad32_kernel<KT_, NT_, true><<<g, 256, 0, st>>>(a, (int)per, fast, part, dv);  \
+    else                                                                                \
+      conv_wgrad32_kernel<KT_, NT_, false><<<g, 256, 0, st>>>(a, (int)per, fast, part, dv); \
+  }
     W32_CASE(64, 64) W32_CASE(64, 128) W32_CASE(128, 64) W32_CASE(128, 128)
 #undef W32_CASE
   } else if (wgrad_vec_ok(a)) {
