@@ -42,6 +42,12 @@ import torch  # noqa: E402
 METRIC = "images/sec at 1024x1024 bs32 (1/2/4/8 GPU); boxes/sec NMS"
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak (spec)
+# process-group backend of the N>1 path: RCCL ("nccl") on the GPU node; "gloo"
+# rehearses the same control flow (tests/test_bench_dist.py)
+DIST_BACKEND = os.environ.get("JABD_DIST_BACKEND", "nccl")
+# 1: the training legs shard one global synthetic batch over the ranks and
+# report the job's loss per step and every rank's parameter checksum
+GLOBAL_DATA = os.environ.get("JABD_BENCH_GLOBAL_DATA", "0") == "1"
 
 
 def parse():
@@ -198,41 +204,15 @@ def o1_activation_c2(device, x, steps, warmup):
                     "stats non-trivial)"}
 
 
-def forward_flops(model, size, batch):
-    """Algorithmic FLOPs (2*MAC) of the whole forward, from the layer shapes."""
-    from jabd_amd import functional as F
-    tot = [0.0]
-    orig_conv, orig_dw, orig_xd = F.conv, F.dwconv, F.expand_dw
-
-    def c(xx, pk, stride=1, pad=0, **kw):
-        out = orig_conv(xx, pk, stride=stride, pad=pad, **kw)
-        tot[0] += 2.0 * out.shape[0] * out.shape[1] * out.shape[2] * (
-            pk.KH * pk.KW * pk.Cin + pk.Cin2) * pk.Cout
-        return out
-
-    def d(xx, w, b, k, stride, **kw):
-        y, p = orig_dw(xx, w, b, k, stride, **kw)
-        tot[0] += 2.0 * y.numel() * k * k
-        return y, p
-
-    def xd(xx, pk, w, b, k, stride, **kw):
-        out = orig_xd(xx, pk, w, b, k, stride, **kw)
-        y = out[0]
-        # the reference's expand conv runs over the input pixels only once
-        B, H, W, C = xx.shape
-        tot[0] += 2.0 * B * H * W * C * pk.Cout + 2.0 * y.numel() * k * k
-        if kw.get("skip") is not None:  # the fused skip branch's dw3x3/s2
-            tot[0] += 2.0 * y.shape[0] * y.shape[1] * y.shape[2] * C * 9
-        return out
-
-    F.conv, F.dwconv, F.expand_dw = c, d, xd
-    try:
-        with torch.no_grad():
-            model(torch.zeros(1, 3, size, size, device="cuda"))
-        torch.cuda.synchronize()
-    finally:
-        F.conv, F.dwconv, F.expand_dw = orig_conv, orig_dw, orig_xd
-    return tot[0]
+def forward_flops(size, batch, device):
+    """Algorithmic FLOPs (2*MAC) of the JABD-MobileNetV3 eval forward: the
+    same census as the training floor (activation_census: every conv-like
+    launch -- stem, convs, fused expand+depthwise incl. its skip branch,
+    depthwise convs, heads and the fused SSH tail's three 3x3 convs and three
+    heads), so the bench line carries one forward GFLOP/image (VERDICT r05
+    item 8).  Not counted: the NLM attention (S = 225 bins x C = 4 channels per
+    pixel, < 0.1% of the forward) and elementwise work."""
+    return batch * activation_census("mnv3", device, size)["flops"]
 
 
 NMS_OPS_PER_PAIR = 13  # fp32 ops of one exact IoU test: 4 min/max, 2 sub, 2 clamp, mul, 2 add/sub, div, cmp
@@ -504,17 +484,36 @@ def train_bench(kind, batch, size, steps, warmup, device, dist, rank, conv_roofl
     opt = optim.Adam(model.parameters(), 1e-3, weight_decay=5e-4)  # fused HIP step
     crit = MultiBoxLoss(2, 0.35, 7, cfg["variance"], True)
     pri = Anchors(cfg, image_size=(size, size)).get_anchors().to(device)
-    x = synth.images(batch, size, seed=1234 + rank, device=device)
-    tg = [torch.from_numpy(t).to(device) for t in synth.targets(batch, size, seed=4321 + rank)]
+    world = dist.get_world_size() if dist else 1
+    if GLOBAL_DATA:
+        # every rank synthesises the same global batch and takes its shard
+        # (parallel.shard, DataParallel's scatter): the job then sees one
+        # global batch, comparable with a one-process run of it
+        gx = synth.images(batch * world, size, seed=1234, device=device)
+        gt = [torch.from_numpy(t).to(device) for t in synth.targets(batch * world, size, seed=4321)]
+        x, tg = parallel.shard(gx, gt, rank, world)
+        x = x.contiguous()
+        del gx, gt
+    else:
+        x = synth.images(batch, size, seed=1234 + rank, device=device)
+        tg = [torch.from_numpy(t).to(device) for t in synth.targets(batch, size, seed=4321 + rank)]
     reducer = parallel.GradAllReduce(model) if dist else None
+    trace = []
+
+    def step():
+        loss, _ = parallel.train_step(model, crit, opt, x, tg, pri, reducer=reducer)
+        if GLOBAL_DATA:
+            trace.append(loss)
+        return loss
+
     for _ in range(warmup):
-        parallel.train_step(model, crit, opt, x, tg, pri, reducer=reducer)
+        step()
     torch.cuda.synchronize()
     conv = None
     if conv_roofline_steps:
         with TrainConvTimer() as tm:
             for _ in range(conv_roofline_steps):
-                parallel.train_step(model, crit, opt, x, tg, pri, reducer=reducer)
+                step()
         c_ms, c_gf, c_n = tm.summary(conv_roofline_steps)
         ach = c_gf / c_ms  # GFLOP/ms = TFLOP/s
         conv = {"bound": "mfma", "kernel": f"training-step conv stack: forward, data-gradient "
@@ -529,7 +528,7 @@ def train_bench(kind, batch, size, steps, warmup, device, dist, rank, conv_roofl
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        loss, _ = parallel.train_step(model, crit, opt, x, tg, pri, reducer=reducer)
+        loss = step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -538,13 +537,28 @@ def train_bench(kind, batch, size, steps, warmup, device, dist, rank, conv_roofl
         t = torch.tensor([el], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    world = dist.get_world_size() if dist else 1
+        # the job's loss of the last step: each rank's loss is its shard's part
+        # of the global-batch loss (global positive counts), so the sum over
+        # ranks is DataParallel's loss (outside the timed region)
+        loss = loss.detach().clone()
+        dist.all_reduce(loss)
     mem = torch.cuda.max_memory_allocated(device) / 2**30
+    extra = {}
+    if GLOBAL_DATA:
+        tr = torch.stack(trace).double()
+        ck = torch.stack([p.detach().double().sum() for p in model.parameters()]).sum().reshape(1)
+        if dist:
+            dist.all_reduce(tr)
+            cks = [torch.zeros_like(ck) for _ in range(world)]
+            dist.all_gather(cks, ck)
+            ck = torch.cat(cks)
+        extra = {"loss_trace": tr.cpu().tolist(), "param_checksums": ck.cpu().tolist()}
     del model, opt, x, tg
     torch.cuda.empty_cache()
     out = {"images_per_sec": batch * steps * world / el, "ms_per_step": el / steps * 1e3,
            "per_gpu_batch": batch, "global_batch": batch * world, "image_size": size,
            "steps": steps, "warmup": warmup, "loss_last": float(loss), "max_mem_gib": mem}
+    out.update(extra)
     if conv is not None:
         out["conv_roofline"] = conv
     return out
@@ -924,8 +938,11 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        # ranks beyond the visible devices share them (a gloo rehearsal of the
+        # N>1 path on a one-GPU box); on the 8-GPU node this is rank -> GPU
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(DIST_BACKEND)
     device = torch.device("cuda", local)
     from jabd_amd import synth
     model = build_model(device)
@@ -1016,7 +1033,7 @@ def main():
                     tr[k]["roofline"].update(fl)
         extra["train"] = tr
     if rank == 0:
-        extra["forward_gflop_per_image"] = forward_flops(model, args.size, 1) / 1e9
+        extra["forward_gflop_per_image"] = forward_flops(args.size, 1, device) / 1e9
         if not args.no_nms:
             extra["nms"] = nms_bench(device)
             extra["augment"] = augment_bench(device)

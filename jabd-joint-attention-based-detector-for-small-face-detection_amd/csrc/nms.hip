@@ -377,6 +377,12 @@ static constexpr int kWaveRec = 64 * (int)kPairsPerBox;  // pair records per key
 static constexpr int kCand = JABD_NMS_CAND;              // candidate loads in flight per lane
 static constexpr int kLaneRec = 64;                      // of which each lane's own slots
 static constexpr int kWaveShared = kWaveRec - 64 * kLaneRec;  // and the wave's shared tail
+// Past its wave's region a pair goes to its image's overflow region (one
+// global atomic per record: only a cluster's waves get there), kOvfPerBox
+// records per row; an image only falls back to the dense producer past that.
+// (A few hundred mutually overlapping boxes of one face put ~n_c^2 / 2 pairs
+// into the handful of key-order waves that hold their cell run.)
+static constexpr int64_t kOvfPerBox = 16;
 static constexpr int kK = 2;                  // class sub-division (neighbour range)
 static constexpr int kGridNbr = 1 + kK + kK * (2 * kK + 1);  // class pairs searched per box
 
@@ -568,6 +574,7 @@ __global__ __launch_bounds__(256) void grid_pairs(
     const CellRun* __restrict__ tab, uint32_t tmask,
     double thr, int* __restrict__ dense, uint64_t* __restrict__ diag,
     uint64_t* __restrict__ rec, int* __restrict__ lcnt, int* __restrict__ wcnt,
+    uint64_t* __restrict__ ovf, int* __restrict__ ocnt, int64_t ovcap,
     unsigned long long* __restrict__ tested) {
   // XCD-aware block order: hardware block id g runs on XCD g % 8; give each
   // XCD one contiguous eighth of the key order (= one image when the batch
@@ -614,7 +621,8 @@ __global__ __launch_bounds__(256) void grid_pairs(
   // own class, then the forward half of the neighbour classes:
   // (0, 1..kK) and (1..kK, -kK..kK)
   unsigned ntest = 0;
-  for (int nbr = 0; nbr < kGridNbr; ++nbr) {
+  bool full = false;  // the image's pair capacity is exhausted (it falls back to dense)
+  for (int nbr = 0; nbr < kGridNbr && !full; ++nbr) {
     int cw2, ch2;
     if (nbr <= kK) {
       cw2 = cw;
@@ -637,7 +645,7 @@ __global__ __launch_bounds__(256) void grid_pairs(
     const float lim = (float)(kCellLim + 1);
     const int X0 = (int)fmaxf(floorf((cx - rx) / sx), -lim), X1 = (int)fminf(floorf((cx + rx) / sx), lim);
     const int Y0 = (int)fmaxf(floorf((cy - ry) / sy), -lim), Y1 = (int)fminf(floorf((cy + ry) / sy), lim);
-    for (int Y = Y0; Y <= Y1; ++Y) {
+    for (int Y = Y0; Y <= Y1 && !full; ++Y) {
       // a row of up to three cells at once: their table probes are in flight
       // together, and their runs are walked as one candidate sequence
       for (int Xb = X0; Xb <= X1; Xb += 3) {
@@ -665,7 +673,7 @@ __global__ __launch_bounds__(256) void grid_pairs(
         const int qe = n3[0] + n3[1] + n3[2];
         // candidates kCand at a time: their loads are in flight together (the
         // area is recomputed from the box: nms_gather's expression, exact)
-        for (int q = 0; q < qe; q += kCand) {
+        for (int q = 0; q < qe && !full; q += kCand) {
           int jj[kCand];
           float4 bb[kCand];
 #pragma unroll
@@ -705,10 +713,18 @@ __global__ __launch_bounds__(256) void grid_pairs(
                   lrec[64 * nl++] = rv;
                 } else {
                   const int sl = atomicAdd(&s_wcnt[wv], 1);
-                  if (sl < kWaveShared)
+                  if (sl < kWaveShared) {
                     wrec[64 * kLaneRec + sl] = rv;
-                  else
-                    atomicOr(&dense[b], 4);
+                  } else {
+                    const int64_t so = atomicAdd(&ocnt[b], 1);
+                    if (so < ovcap) {
+                      ovf[(int64_t)b * ovcap + so] = rv;
+                    } else {
+                      // the image goes dense: this lane's walk ends here
+                      atomicOr(&dense[b], 4);
+                      full = true;
+                    }
+                  }
                 }
               }
             }
@@ -776,10 +792,22 @@ __device__ __forceinline__ void grid_chunk_records(const uint64_t* __restrict__ 
   }
 }
 
+// Image b's overflow records (grid_pairs past a wave's region), split over
+// its K chunks by index: count and scatter see the same partition.
+template <typename F>
+__device__ __forceinline__ void grid_chunk_overflow(const uint64_t* __restrict__ ovf,
+                                                    const int* __restrict__ ocnt, int64_t ovcap,
+                                                    int b, int K, int k, int t, int nt, F&& f) {
+  const int64_t m = min((int64_t)ocnt[b], ovcap);
+  const uint64_t* ob = ovf + (int64_t)b * ovcap;
+  for (int64_t q = m * k / K + t; q < m * (k + 1) / K; q += nt) f(ob[q]);
+}
+
 static constexpr int kBucketT = 1024;
 
 __global__ __launch_bounds__(kBucketT) void grid_bucket_count(
     const uint64_t* __restrict__ rec, const int* __restrict__ lcnt, const int* __restrict__ wcnt,
+    const uint64_t* __restrict__ ovf, const int* __restrict__ ocnt, int64_t ovcap,
     const int* __restrict__ istart, const int* __restrict__ dense, int64_t nb, int K,
     int* __restrict__ hist, int* __restrict__ npairs) {
   extern __shared__ int h[];
@@ -796,13 +824,15 @@ __global__ __launch_bounds__(kBucketT) void grid_bucket_count(
     int64_t wa, wb;
     grid_chunk_waves(istart, b, K, k, wa, wb);
     const uint32_t lo = (uint32_t)(b * nb), hi = (uint32_t)(lo + nb);
-    grid_chunk_records(rec, lcnt, wcnt, wa, wb, t & 63, t >> 6, kBucketT / 64, [&](uint64_t v) {
+    auto count = [&](uint64_t v) {
       const uint32_t bk = (uint32_t)(v >> 32);
       if (bk >= lo && bk < hi) {
         atomicAdd(&h[bk - lo], 1);
         ++mine;
       }
-    });
+    };
+    grid_chunk_records(rec, lcnt, wcnt, wa, wb, t & 63, t >> 6, kBucketT / 64, count);
+    grid_chunk_overflow(ovf, ocnt, ovcap, b, K, k, t, kBucketT, count);
   }
   if (mine) atomicAdd(&s_tot, mine);
   __syncthreads();
@@ -813,6 +843,7 @@ __global__ __launch_bounds__(kBucketT) void grid_bucket_count(
 
 __global__ __launch_bounds__(kBucketT) void grid_bucket_scatter(
     const uint64_t* __restrict__ rec, const int* __restrict__ lcnt, const int* __restrict__ wcnt,
+    const uint64_t* __restrict__ ovf, const int* __restrict__ ocnt, int64_t ovcap,
     const int* __restrict__ istart, const int* __restrict__ dense, int64_t nb, int K,
     const int* __restrict__ off, uint32_t* __restrict__ csr) {
   extern __shared__ int h[];
@@ -825,10 +856,12 @@ __global__ __launch_bounds__(kBucketT) void grid_bucket_scatter(
   int64_t wa, wb;
   grid_chunk_waves(istart, b, K, k, wa, wb);
   const uint32_t lo = (uint32_t)(b * nb), hi = (uint32_t)(lo + nb);
-  grid_chunk_records(rec, lcnt, wcnt, wa, wb, t & 63, t >> 6, kBucketT / 64, [&](uint64_t v) {
+  auto place = [&](uint64_t v) {
     const uint32_t bk = (uint32_t)(v >> 32);
     if (bk >= lo && bk < hi) csr[atomicAdd(&h[bk - lo], 1)] = (uint32_t)v;
-  });
+  };
+  grid_chunk_records(rec, lcnt, wcnt, wa, wb, t & 63, t >> 6, kBucketT / 64, place);
+  grid_chunk_overflow(ovf, ocnt, ovcap, b, K, k, t, kBucketT, place);
 }
 
 // ---------------------------------------------------------------------------
@@ -1122,8 +1155,14 @@ __global__ __launch_bounds__(64 * kPullWaves) void nms_scan_pull(
     // (past the last block the reads are of an unused slot and dropped)
     Meta nxt;
     const int s1 = (c + 1) % kMetaRing;
+    // flag, then an LDS-only acquire fence, then the slot's data: the
+    // fence pairs with the loader's release (lds_release) when f1 == c + 1
+    // and keeps the data reads after the flag read.  "workgroup-one-as"
+    // orders LDS with respect to LDS only, so the AMDGPU memory model needs
+    // no s_waitcnt for it (one wave's LDS operations complete in order);
+    // the flag and data reads stay in flight together
     int f1 = __hip_atomic_load(&mready[s1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    asm volatile("" ::: "memory");  // data reads stay after the flag read
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup-one-as");
     read_meta(s1, nxt);
     int ne = cur.ne;
     const bool fits = ne >= 0;
@@ -1207,7 +1246,9 @@ __global__ __launch_bounds__(64 * kPullWaves) void nms_scan_pull(
     kw[0] = kept;
     if (lane == 0) {
       kb[c] = kept;
-      asm volatile("" ::: "memory");  // in-order LDS: the kept word lands before the progress
+      // release (LDS only, as above: no wait for this wave's kout stores):
+      // a loader that acquires s_prog >= c + 1 sees kb[c]
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup-one-as");
       __hip_atomic_store(&s_prog, ((uint64_t)(uint32_t)cur.e_end << 32) | (uint32_t)(c + 1),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
@@ -1353,8 +1394,10 @@ struct NmsWs {
   uint64_t* ent_bits;
   // grid path
   unsigned* ext;
-  int *dense, *npairs, *gval_in, *gval_out, *lcnt, *wcnt, *istart, *bhist, *boff;
+  int *dense, *npairs, *gval_in, *gval_out, *lcnt, *wcnt, *istart, *bhist, *boff, *ocnt;
   uint64_t* rec;  // per key-order wave: kWaveRec pair records
+  uint64_t* ovf;  // per image: ovcap overflow pair records
+  int64_t ovcap;
   uint32_t* csr;
   int kchunks;    // count-sort chunks per image
   unsigned long long* tested;  // grid candidates IoU-tested per image (measurement)
@@ -1409,7 +1452,10 @@ static void carve_nms(A& a, int64_t batch, int64_t n, NmsWs* w) {
   T(int, bc * nb * kch + 1, bhist);
   T(int, bc * nb * kch + 1, boff);
   T(uint64_t, nwaves * kWaveRec, rec);
-  T(uint32_t, nwaves * kWaveRec, csr);
+  const int64_t ovcap = kOvfPerBox * (n > 0 ? n : 1);
+  T(uint64_t, bc * ovcap, ovf);
+  T(int, bc, ocnt);
+  T(uint32_t, nwaves * kWaveRec + bc * ovcap, csr);
   T(float4, bc * n, gbox);
   // one run table per image (its own XCD's L2 holds it: 2 MiB at n = 100k),
   // power-of-two slots >= 1.25 n (load factor <= 0.8 even if every box is a run)
@@ -1422,6 +1468,7 @@ static void carve_nms(A& a, int64_t batch, int64_t n, NmsWs* w) {
     w->tmp_bytes = tb;
     w->cap = cap;
     w->kchunks = kch;
+    w->ovcap = ovcap;
   }
 }
 
@@ -1474,7 +1521,7 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
     }
     {  // every counter / table this pass starts from, one launch
       const int64_t gb = grid ? 1 : 0;  // the grid path's tables
-      const FillRange fr[11] = {
+      const FillRange fr[12] = {
           {w.counts, (int64_t)sizeof(int) * bc, 0u},
           {w.nanflag, (int64_t)sizeof(int) * bc, 0u},
           {w.err, (int64_t)sizeof(int), 0u},
@@ -1485,8 +1532,9 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
           {w.ext, gb * (int64_t)sizeof(unsigned) * bc * 4 * kNC, 0u},
           {w.runs, gb * (int64_t)sizeof(CellRun) * bc * ((int64_t)w.run_mask + 1), 0xFFFFFFFFu},
           {w.diag, gb * (int64_t)sizeof(uint64_t) * bc * n, 0u},
-          {w.bhist + (int64_t)bc * nb * w.kchunks, gb * (int64_t)sizeof(int), 0u}};
-      if (int e = fill_ranges(fr, 11, st)) return e;
+          {w.bhist + (int64_t)bc * nb * w.kchunks, gb * (int64_t)sizeof(int), 0u},
+          {w.ocnt, gb * (int64_t)sizeof(int) * bc, 0u}};
+      if (int e = fill_ranges(fr, 12, st)) return e;
     }
     dim3 g1((unsigned)cdiv(n, 256), bc);
     int sorted = -1;
@@ -1534,18 +1582,21 @@ int nms_core(const float* boxes, int64_t box_stride, int64_t box_bstride,
       if (int e = check_launch("grid_runs_end")) return e;
       grid_pairs<<<(unsigned)grid_pair_blocks((int64_t)bc * n), 256, 0, st>>>(
           w.kout, w.gval_out, (int64_t)bc * n, w.gbox, n, bc, inv_w, fcell, w.ext,
-          w.runs, w.run_mask, iou_thr, w.dense, w.diag, w.rec, w.lcnt, w.wcnt, w.tested);
+          w.runs, w.run_mask, iou_thr, w.dense, w.diag, w.rec, w.lcnt, w.wcnt, w.ovf, w.ocnt,
+          w.ovcap, w.tested);
       if (int e = check_launch("grid_pairs")) return e;
       const unsigned gk = (unsigned)(w.kchunks * bc);
       const size_t hl = (size_t)nb * sizeof(int);
-      grid_bucket_count<<<gk, kBucketT, hl, st>>>(w.rec, w.lcnt, w.wcnt, w.istart, w.dense, nb, w.kchunks,
-                                             w.bhist, w.npairs);
+      grid_bucket_count<<<gk, kBucketT, hl, st>>>(w.rec, w.lcnt, w.wcnt, w.ovf, w.ocnt, w.ovcap,
+                                                  w.istart, w.dense, nb, w.kchunks, w.bhist,
+                                                  w.npairs);
       if (int e = check_launch("grid_bucket_count")) return e;
       if (int e = scan_excl_i32(w.bhist, w.boff, (int64_t)bc * nb * w.kchunks + 1, w.tmp,
                                 w.tmp_bytes, st))
         return e;
-      grid_bucket_scatter<<<gk, kBucketT, hl, st>>>(w.rec, w.lcnt, w.wcnt, w.istart, w.dense, nb, w.kchunks,
-                                               w.boff, w.csr);
+      grid_bucket_scatter<<<gk, kBucketT, hl, st>>>(w.rec, w.lcnt, w.wcnt, w.ovf, w.ocnt, w.ovcap,
+                                                    w.istart, w.dense, nb, w.kchunks, w.boff,
+                                                    w.csr);
       if (int e = check_launch("grid_bucket_scatter")) return e;
     }
     nms_mask<<<2048, 256, 0, st>>>(w.sbox, w.sarea, w.counts, n, nb, bc, iou_thr, w.nanflag, w.dense,

@@ -117,7 +117,8 @@ def _packed(weight, transposed):
     return pk
 
 
-_REPACK_TABLES = {}  # job-table key -> (device jobs, device starts, njobs, total)
+_REPACK_TABLES = {}  # job-table key -> [(device jobs, device starts, njobs, total)] per launch
+REPACK_MAX_JOBS = 1024  # kPackMaxJobs in csrc/conv32.hip
 
 
 def repack(params):
@@ -152,19 +153,24 @@ def repack(params):
     if not rows:
         return 0
     key = tuple(rows)
-    tab = _REPACK_TABLES.get(key)
-    if tab is None:
+    tabs = _REPACK_TABLES.get(key)
+    if tabs is None:
+        # the kernel takes at most REPACK_MAX_JOBS jobs per launch (its job
+        # starts live in LDS): larger models launch once per chunk of rows
         dev = fixups[0][0].device
-        starts = [0]
-        for r in rows:
-            starts.append(starts[-1] + (r[7] * r[8] + r[9] * r[10]) * 64)
-        tab = (torch.tensor(rows, dtype=torch.int64).to(dev),
-               torch.tensor(starts, dtype=torch.int64).to(dev), len(rows), starts[-1])
+        tabs = []
+        for c0 in range(0, len(rows), REPACK_MAX_JOBS):
+            chunk = rows[c0:c0 + REPACK_MAX_JOBS]
+            starts = [0]
+            for r in chunk:
+                starts.append(starts[-1] + (r[7] * r[8] + r[9] * r[10]) * 64)
+            tabs.append((torch.tensor(chunk, dtype=torch.int64).to(dev),
+                         torch.tensor(starts, dtype=torch.int64).to(dev), len(chunk), starts[-1]))
         if len(_REPACK_TABLES) > 8:
             _REPACK_TABLES.clear()
-        _REPACK_TABLES[key] = tab
-    jobs, starts, n, total = tab
-    call("jabd_conv_pack_multi_f32", jobs.data_ptr(), starts.data_ptr(), n, total, _st())
+        _REPACK_TABLES[key] = tabs
+    for jobs, starts, n, total in tabs:
+        call("jabd_conv_pack_multi_f32", jobs.data_ptr(), starts.data_ptr(), n, total, _st())
     for w, cache, newest in fixups:
         cache.clear()
         for tr, (_, pk) in newest.items():

@@ -276,12 +276,14 @@ def test_nms_c5_full_config(cuda):
 @pytest.mark.parametrize("thr", [0.3, 0.9])
 def test_nms_pair_capacity_dense_fallback(cuda, thr):
     """Image 0 is one tight cluster of 24k near-identical boxes: every pair is a
-    grid candidate (n^2/2 = 2.9e8 pairs vs the workspace's 128 per box =
-    3.1e6, csrc/nms.hip kPairsPerBox), so its mask must come from the dense
-    fallback producer; image 1 (ordinary clustered boxes) stays on the grid
-    producer in the same call.  Both bit-exact vs the oracle.  (24k rows: the
-    grid producer runs for images above csrc/nms.hip's 20480-row dense
-    limit.)"""
+    grid candidate (n^2/2 = 2.9e8 pairs vs the image's pair capacity: each
+    64-key wave's 8192 records plus the image's overflow region of 16 per row,
+    csrc/nms.hip kPairsPerBox / kOvfPerBox: 3.5e6 in all), so its mask must
+    come from the dense fallback producer; image 1 (ordinary clustered boxes)
+    stays on the grid producer in the same call.  Both bit-exact vs the
+    oracle, and the producers are the ones named (jabd_nms_pair_stats).
+    (24k rows: the grid producer runs for images above csrc/nms.hip's
+    20480-row dense limit.)"""
     from jabd_amd import ops, synth
     n = 24_000
     rng = np.random.default_rng(17)
@@ -295,5 +297,37 @@ def test_nms_pair_capacity_dense_fallback(cuda, thr):
     keep, nk = ops.batched_nms(torch.from_numpy(bx).to(cuda), torch.from_numpy(sc).to(cuda), thr)
     keep, nk = keep.cpu().numpy(), nk.cpu().numpy()
     refs = _oracle_nms_many(bx, sc, thr)
+    for b in range(2):
+        assert np.array_equal(keep[b, : nk[b]], refs[b]), b
+    _, _, _, dense = ops.batched_nms_stats(torch.from_numpy(bx).to(cuda),
+                                           torch.from_numpy(sc).to(cuda), thr)
+    assert dense.tolist() == [True, False]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ncl", [300, 700])
+def test_nms_cluster_stays_on_grid(cuda, ncl):
+    """A mid-size cluster: ncl near-identical boxes of one face in
+    a 24k-row image of ordinary clustered boxes.  They share one cell run of
+    the grid key order, so the first key-order wave of the run holds 64 boxes
+    that each pair with nearly every later cluster box: about 64 * (ncl - 32)
+    off-block records (17k at 300, 43k at 700) against the wave's 8192.  The
+    excess spills into the image's overflow region (csrc/nms.hip kOvfPerBox)
+    and the image stays on the grid producer (before the spill it went dense:
+    an O(n^2) mask for the whole image); bit-exact vs the oracle."""
+    from jabd_amd import ops, synth
+    n = 24_000
+    b1, s1 = synth.nms_boxes(2, n, seed=29)
+    bx, sc = b1.copy(), s1.copy()
+    rng = np.random.default_rng(ncl)
+    rows = rng.choice(n, ncl, replace=False)
+    ctr = np.array([0.3, 0.6]) + rng.normal(0, 0.001, (ncl, 2))
+    wh = 0.08 * (1 + rng.uniform(0, 0.02, (ncl, 2)))
+    bx[0, rows] = np.concatenate([ctr - wh / 2, ctr + wh / 2], 1).astype(np.float32)
+    keep, nk, tested, dense = ops.batched_nms_stats(torch.from_numpy(bx).to(cuda),
+                                                    torch.from_numpy(sc).to(cuda), 0.5)
+    assert dense.tolist() == [False, False]
+    keep, nk = keep.cpu().numpy(), nk.cpu().numpy()
+    refs = _oracle_nms_many(bx, sc, 0.5)
     for b in range(2):
         assert np.array_equal(keep[b, : nk[b]], refs[b]), b

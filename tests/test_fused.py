@@ -252,8 +252,8 @@ def test_expand_dw_forms_bit_identical(cuda, spec, bhw):
     for other in outs[1:]:
         for a, b in zip(outs[0], other):
             assert torch.equal(a, b)
-    # the chunk-pipelined form (4, csrc/expdw3.hip; the default where it
-    # applies): y and the skip branch bit-identical, the ECA partials (a sum
+    # the chunk-pipelined form (4, csrc/expdw3.hip; opt-in: JABD_EXPDW3=1
+    # or select(4), measured slower than expdw1): y and the skip branch bit-identical, the ECA partials (a sum
     # over the tile in another fixed order) within 2e-6 relative
     try:
         lib().jabd_expand_dw_select(4)

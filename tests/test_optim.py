@@ -131,9 +131,12 @@ def test_adam_steps_reach_the_training_convs(cuda):
 
 
 @pytest.mark.gpu
-def test_batched_repack_equals_fresh_packs(cuda):
+@pytest.mark.parametrize("max_jobs", [1024, 16])
+def test_batched_repack_equals_fresh_packs(cuda, max_jobs, monkeypatch):
     """After a fused Adam step, every cached training pack of the model is
-    rewritten in place by ONE jabd_conv_pack_multi_f32 launch (train.repack):
+    rewritten in place by ONE jabd_conv_pack_multi_f32 launch (train.repack;
+    max_jobs 16: the same rows split over several launches, as a model with
+    more packs than the kernel's 1024-job table takes them):
     each must equal a fresh jabd_conv_pack_f32 pack of the updated weight bit
     for bit (both forms, both layouts), and the cache must be keyed on the new
     version so the next forward reuses it without repacking."""
@@ -145,6 +148,8 @@ def test_batched_repack_equals_fresh_packs(cuda):
     from nets.retinaface_training import MultiBoxLoss
     from utils.anchors import Anchors
     from utils.config import cfg_mnet
+    monkeypatch.setattr(train, "REPACK_MAX_JOBS", max_jobs)
+    monkeypatch.setattr(train, "_REPACK_TABLES", {})
     x = synth.images(2, 96, seed=5).to(cuda)
     tg = [torch.from_numpy(t).to(cuda) for t in synth.targets(2, 96, seed=6)]
     pri = Anchors(cfg_mnet, image_size=(96, 96)).get_anchors().to(cuda)

@@ -347,12 +347,23 @@ def test_bnactfn_grads_wide(cuda, c, act, h, w):
            ["dx", "dgamma", "dbeta"])
 
 
+def _act_masked(z, zmask, act):
+    """act(z) in float64 whose derivative takes its region from zmask (the
+    HIP kernel's own fp32 pre-activation), PyTorch's *_backward conventions:
+    relu' = [z > 0]; hardswish' = 0 below -3, z/3 + 1/2 on [-3, 3], 1 above."""
+    if act == "relu":
+        return torch.where(zmask > 0, z, z * 0)
+    return torch.where(zmask < -3, z * 0, torch.where(zmask <= 3, z * (z + 3) / 6, z))
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("c,k,s,bhw,act", [(64, 3, 2, (4, 64, 48), "relu"), (72, 5, 1, (3, 37, 29), "relu"),
                                            (240, 3, 2, (2, 30, 34), "hswish"),
                                            (480, 3, 1, (3, 32, 48), "hswish"), (16, 3, 1, (2, 9, 5), "relu"),
-                                           # a tall map: more rows than partial blocks
-                                           (16, 3, 1, (2, 5000, 40), "relu")])
+                                           # tall maps: more rows than partial blocks; stride 2
+                                           # with an odd height (chunks starting on odd rows)
+                                           (16, 3, 1, (2, 5000, 40), "relu"),
+                                           (16, 3, 2, (2, 8201, 40), "hswish")])
 @pytest.mark.parametrize("recompute", [True, False])
 def test_dw_dgrad_bn_fused(cuda, c, k, s, bhw, act, recompute, monkeypatch):
     """MNv3 block backward through bn1 + act -> depthwise conv: the fused
@@ -361,8 +372,21 @@ def test_dw_dgrad_bn_fused(cuda, c, k, s, bhw, act, recompute, monkeypatch):
     the depthwise gradient bit-identical, dgamma / dbeta / dx within fp32
     reassociation of the partial sums; and both against float64 autograd.
     recompute: de not stored, recomputed by a second depthwise pass that
-    writes dx (dz == NULL)."""
+    writes dx (dz == NULL).
+
+    The float64 reference takes its activation region from the HIP
+    backward's own fp32 pre-activation (fma((x - mean) * invstd, g, b),
+    tests/_kinks._bn_z), bounded like tests/_kinks.py: at most
+    max(8, 2e-4 * numel) elements may sit on a different side of a kink than
+    in float64, each within 1e-5 of it.  Why: in the
+    (16, 3, 2, (2, 8201, 40), hswish) case one element of channel 10 has
+    z = 3.0000000215 in float64 and 2.9999998 in fp32; Hardswish's derivative
+    jumps from 1.5 to 1 at z = 3, and that single flip alone moves dx by
+    1.597e-3 of its max (the value round 5 measured on the GPU) and
+    dbeta[10] from -119.9910 to -119.9819 — reproduced on the CPU by the
+    float64 reference with the fp32 mask, no kernel involved."""
     from jabd_amd import train as T
+    from _kinks import _bn_z, _region, _kink_dist, _FAMILY
     monkeypatch.setattr(T, "DGBN_RECOMPUTE", recompute)
     B, H, W = bhw
     g = torch.Generator().manual_seed(c + k * 10 + s)
@@ -373,13 +397,6 @@ def test_dw_dgrad_bn_fused(cuda, c, k, s, bhw, act, recompute, monkeypatch):
     OH = (H + 2 * (k // 2) - k) // s + 1
     OW = (W + 2 * (k // 2) - k) // s + 1
     dy = torch.randn(B, OH, OW, c, generator=g)
-    # float64 reference: e = act(bn(x_bn)) (batch statistics), d = dwconv(e)
-    xr = _nchw(x_bn).double().requires_grad_()
-    gr, br = gamma.double().requires_grad_(), beta.double().requires_grad_()
-    e = tF.batch_norm(xr, None, None, gr, br, True, 0.0, 1e-5)
-    e = tF.relu(e) if act == "relu" else tF.hardswish(e)
-    d = tF.conv2d(e, w.double(), None, s, k // 2, 1, c)
-    d.backward(_nchw(dy).double())
     dev = torch.device(cuda)
     bn = torch.nn.BatchNorm2d(c).to(dev)
     with torch.no_grad():
@@ -396,6 +413,21 @@ def test_dw_dgrad_bn_fused(cuda, c, k, s, bhw, act, recompute, monkeypatch):
     assert torch.equal(dw1, dw2)
     for a, b in ((dx1, dx2), (dg1, dg2), (db1, db2)):
         assert rel_err(a.cpu(), b.cpu()) < 1e-5
+    # float64 reference: e = act(bn(x_bn)) (batch statistics), d = dwconv(e),
+    # the activation's region from the HIP pre-activation
+    zh = _nchw(_bn_z(x_bn, st[2], st[3], gamma, beta, None)).double()
+    xr = _nchw(x_bn).double().requires_grad_()
+    gr, br = gamma.double().requires_grad_(), beta.double().requires_grad_()
+    z = tF.batch_norm(xr, None, None, gr, br, True, 0.0, 1e-5)
+    fam = _FAMILY[act]
+    flips = _region(fam, zh) != _region(fam, z.detach())
+    nflip = int(flips.sum())
+    assert nflip <= max(8, 2e-4 * flips.numel()), nflip
+    if nflip:
+        assert float(_kink_dist(fam, z.detach()[flips]).max()) < 1e-5
+    e = _act_masked(z, zh, act)
+    d = tF.conv2d(e, w.double(), None, s, k // 2, 1, c)
+    d.backward(_nchw(dy).double())
     _check([_nchw(dx1.cpu()), dg1.cpu(), db1.cpu()], [xr.grad, gr.grad, br.grad],
            ["dx", "dgamma", "dbeta"])
 
