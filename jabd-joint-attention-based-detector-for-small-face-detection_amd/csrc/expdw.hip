@@ -34,10 +34,17 @@ constexpr int xd1_min_wg() {
   return (SKIP && NW == 4 && 4 * bytes <= 160 * 1024) ? 4 : 2;
 }
 
+// KCC: the number of 16-channel input stages when known at compile time
+// (Cin <= 32: the stage loop unrolls away with its next-stage addressing),
+// 0 = p.Kc at run time.  Taken where it measured faster (tools/ab_xd.sh,
+// two rounds): Cin 16 E16 k3 s1 246 vs 258 us, the Cin 24 k5 s2 skip form
+// 305-313 vs 324-327 us; the Cin 16 k3 s2 skip form measured 506-514 vs
+// 491-498 us with it and keeps the run-time count.
 template <int K, int S, int TH, int TW, int EC, int ACT, int KP, bool SKIP = false, int NW = 4,
-          int SKC = 160>
+          int SKC = 160, int KCC = 0>
 __global__ __launch_bounds__(64 * NW, (xd1_min_wg<K, S, TH, TW, EC, SKIP, NW, SKC>())) void expdw1_kernel(const jabd_expdw_args p, const XdDivs dv,
                                                        int nitems) {
+  const int Kc = KCC ? KCC : p.Kc;
   using C = XdCfg<K, S, TH, TW, EC>;
   constexpr int T = 64 * NW;                  // threads
   constexpr int NPF = (C::IPAD * 4 + T - 1) / T;
@@ -123,12 +130,12 @@ __global__ __launch_bounds__(64 * NW, (xd1_min_wg<K, S, TH, TW, EC, SKIP, NW, SK
   for (int u = 0; u < BPW; ++u) acc[u] = bias4;
 #pragma unroll
   for (int s = 0; s < KP; ++s)
-    if (s < p.Kc) load_stage(s, pf[s]);
-  for (int kc0 = 0; kc0 < p.Kc; kc0 += KP) {
+    if (s < Kc) load_stage(s, pf[s]);
+  for (int kc0 = 0; kc0 < Kc; kc0 += KP) {
 #pragma unroll
     for (int s = 0; s < KP; ++s) {
       const int kc = kc0 + s;
-      if (kc >= p.Kc) break;
+      if (kc >= Kc) break;
       f32x4 a = wpk[(kc * p.Ntiles + ntc) * 64 + lane];
 #pragma unroll
       for (int u = 0; u < NPF; ++u) {
@@ -143,7 +150,7 @@ __global__ __launch_bounds__(64 * NW, (xd1_min_wg<K, S, TH, TW, EC, SKIP, NW, SK
       asm volatile("" : "+v"(a));
       lds_barrier();
       if (kc == 0) XD_T(2);
-      if (kc + KP < p.Kc) load_stage(kc + KP, pf[s]);
+      if (kc + KP < Kc) load_stage(kc + KP, pf[s]);
       // fused skip branch (stride 2, first chunk's workgroups): this stage's
       // 16 channels for output pixel t & 63, channel quad t >> 6 (waves 0-3), taps from LDS
       const int sc = 16 * kc + 4 * (t >> 6);
@@ -1175,6 +1182,9 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
     if (S_ == 2 && a.sy && nw == 8)                                                           \
       expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1, true, 8><<<(unsigned)nitems, 512, 0, st>>>( \
           a, dv, (int)nitems);                                                                \
+    else if (S_ == 2 && a.sy && skc == 40 && a.Kc == 2)                                       \
+      expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1, true, 4, 40, 2><<<(unsigned)nitems, 256, 0, st>>>( \
+          a, dv, (int)nitems);                                                                \
     else if (S_ == 2 && a.sy && skc == 40)                                                    \
       expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1, true, 4, 40><<<(unsigned)nitems, 256, 0, st>>>( \
           a, dv, (int)nitems);                                                                \
@@ -1187,10 +1197,16 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
     else if (nw == 8)                                                                         \
       expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1, false, 8><<<(unsigned)nitems, 512, 0, st>>>( \
           a, dv, (int)nitems);                                                                \
-    else if (a.Kc == 1 || xd_kp() == 1)                                                       \
+    else if (a.Kc == 1)                                                                       \
+      expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1, false, 4, 160, 1><<<(unsigned)nitems, 256, 0, st>>>( \
+          a, dv, (int)nitems);                                                                \
+    else if (a.Kc == 2)                                                                       \
+      expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 2, false, 4, 160, 2><<<(unsigned)nitems, 256, 0, st>>>( \
+          a, dv, (int)nitems);                                                                \
+    else if (xd_kp() == 1)                                                                    \
       expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 1><<<(unsigned)nitems, 256, 0, st>>>(       \
           a, dv, (int)nitems);                                                                \
-    else if (a.Kc == 2 || xd_kp() == 2)                                                       \
+    else if (xd_kp() == 2)                                                                    \
       expdw1_kernel<K_, S_, TH_, TW_, EC_, ACT_, 2><<<(unsigned)nitems, 256, 0, st>>>(       \
           a, dv, (int)nitems);                                                                \
     else                                                                                      \

@@ -383,6 +383,13 @@ static constexpr int kWaveShared = kWaveRec - 64 * kLaneRec;  // and the wave's 
 // (A few hundred mutually overlapping boxes of one face put ~n_c^2 / 2 pairs
 // into the handful of key-order waves that hold their cell run.)
 static constexpr int64_t kOvfPerBox = 16;
+// JABD_NMS_OVF_PER_BOX overrides it (read on every carve, so a test can turn
+// the overflow region off between calls; the size query and the call it
+// sizes must see the same value)
+static int64_t nms_ovf_per_box() {
+  const char* e = getenv("JABD_NMS_OVF_PER_BOX");
+  return e ? std::max<int64_t>(0, atoll(e)) : kOvfPerBox;
+}
 static constexpr int kK = 2;                  // class sub-division (neighbour range)
 static constexpr int kGridNbr = 1 + kK + kK * (2 * kK + 1);  // class pairs searched per box
 
@@ -1452,7 +1459,7 @@ static void carve_nms(A& a, int64_t batch, int64_t n, NmsWs* w) {
   T(int, bc * nb * kch + 1, bhist);
   T(int, bc * nb * kch + 1, boff);
   T(uint64_t, nwaves * kWaveRec, rec);
-  const int64_t ovcap = kOvfPerBox * (n > 0 ? n : 1);
+  const int64_t ovcap = nms_ovf_per_box() * (n > 0 ? n : 1);
   T(uint64_t, bc * ovcap, ovf);
   T(int, bc, ocnt);
   T(uint32_t, nwaves * kWaveRec + bc * ovcap, csr);

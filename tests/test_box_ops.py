@@ -324,10 +324,16 @@ def test_nms_cluster_stays_on_grid(cuda, ncl):
     ctr = np.array([0.3, 0.6]) + rng.normal(0, 0.001, (ncl, 2))
     wh = 0.08 * (1 + rng.uniform(0, 0.02, (ncl, 2)))
     bx[0, rows] = np.concatenate([ctr - wh / 2, ctr + wh / 2], 1).astype(np.float32)
-    keep, nk, tested, dense = ops.batched_nms_stats(torch.from_numpy(bx).to(cuda),
-                                                    torch.from_numpy(sc).to(cuda), 0.5)
-    assert dense.tolist() == [False, False]
-    keep, nk = keep.cpu().numpy(), nk.cpu().numpy()
     refs = _oracle_nms_many(bx, sc, 0.5)
-    for b in range(2):
-        assert np.array_equal(keep[b, : nk[b]], refs[b]), b
+    # without the overflow region (JABD_NMS_OVF_PER_BOX=0) the cluster's wave
+    # overflows and image 0 goes dense: the case exercises the spill
+    for ovf, want in (("0", [True, False]), (None, [False, False])):
+        with pytest.MonkeyPatch.context() as mp:
+            if ovf is not None:
+                mp.setenv("JABD_NMS_OVF_PER_BOX", ovf)
+            keep, nk, tested, dense = ops.batched_nms_stats(torch.from_numpy(bx).to(cuda),
+                                                            torch.from_numpy(sc).to(cuda), 0.5)
+        assert dense.tolist() == want, (ovf, dense)
+        keep, nk = keep.cpu().numpy(), nk.cpu().numpy()
+        for b in range(2):
+            assert np.array_equal(keep[b, : nk[b]], refs[b]), (ovf, b)

@@ -189,7 +189,13 @@ def run_xd(shape, reps):
     wd = torch.randn(k * k, E, device=dev, generator=g) / k
     bd = torch.randn(E, device=dev, generator=g) * 0.1
     pk = F.PackedConv(we, be, 1, 1, cin)
-    y, part = F.expand_dw(x, pk, wd, bd, k, stride, act=act)
+    # XD_SKIP_BRANCH=1: stride-2 layers carry the block's fused dw3x3/s2 skip
+    # branch, as in the C2 forward (nets/mobilenetV3.py:126-137)
+    skip = None
+    if stride == 2 and os.environ.get("XD_SKIP_BRANCH") == "1":
+        skip = (torch.randn(9, cin, device=dev, generator=g) / 3,
+                torch.randn(cin, device=dev, generator=g) * 0.1)
+    y, part = F.expand_dw(x, pk, wd, bd, k, stride, act=act, skip=skip)[:2]
     dbg = int(os.environ.get("XD_DBG", "0"))
     if dbg:
         F._XD_DBG = dbg
@@ -200,13 +206,13 @@ def run_xd(shape, reps):
     err = float((y - r).abs().max() / r.abs().max())
     perr = float((part.sum(1) - r.sum((1, 2))).abs().max() / r.sum((1, 2)).abs().max())
     for _ in range(3):
-        F.expand_dw(x, pk, wd, bd, k, stride, act=act)
+        F.expand_dw(x, pk, wd, bd, k, stride, act=act, skip=skip)
     s = torch.cuda.Event(enable_timing=True)
     e = torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     s.record()
     for _ in range(reps):
-        F.expand_dw(x, pk, wd, bd, k, stride, act=act)
+        F.expand_dw(x, pk, wd, bd, k, stride, act=act, skip=skip)
     e.record()
     torch.cuda.synchronize()
     t = s.elapsed_time(e) / reps * 1e3
