@@ -131,12 +131,29 @@ __global__ __launch_bounds__(64 * NW, (xd1_min_wg<K, S, TH, TW, EC, SKIP, NW, SK
 #pragma unroll
   for (int s = 0; s < KP; ++s)
     if (s < Kc) load_stage(s, pf[s]);
+  // Cin 24 (two input stages, KCC == 2): the last stage holds 8 channels.
+  // The packed fragments put channel 4g + e of a stage in MFMA e (lane group
+  // g), so each of its four MFMAs would contract 2 real channels and 2 zeros;
+  // the tail stage instead runs 2 MFMAs over channels 4e + g (e = 0, 1): A
+  // from the packed array's lane group e, component g (two scalar loads), B
+  // one float of quad plane e per lane.  A quarter of the layer's MFMAs; the
+  // sum over k is taken in another order.  (Cin 40 with a run-time stage
+  // count measured +5% on the 3x3/s2 skip form: not taken there.)
+  const bool tail8 = KCC == 2 && (p.Cin & 15) == 8;
   for (int kc0 = 0; kc0 < Kc; kc0 += KP) {
 #pragma unroll
     for (int s = 0; s < KP; ++s) {
       const int kc = kc0 + s;
       if (kc >= Kc) break;
-      f32x4 a = wpk[(kc * p.Ntiles + ntc) * 64 + lane];
+      const bool tl = tail8 && kc == Kc - 1;
+      f32x4 a;
+      if (tl) {
+        const float* wf = reinterpret_cast<const float*>(p.we) +
+                          ((int64_t)(kc * p.Ntiles + ntc) * 64 + j) * 4 + g;
+        a = (f32x4){wf[0], wf[64], 0.f, 0.f};
+      } else {
+        a = wpk[(kc * p.Ntiles + ntc) * 64 + lane];
+      }
 #pragma unroll
       for (int u = 0; u < NPF; ++u) {
         if (u * 16 * NW + spx0 < C::IPAD)
@@ -178,7 +195,19 @@ __global__ __launch_bounds__(64 * NW, (xd1_min_wg<K, S, TH, TW, EC, SKIP, NW, SK
       }
       // a wave whose 16-channel tile lies past E skips its MFMAs (wave-uniform;
       // its accumulators are masked in the epilogue)
-      if (ntv && !(XD_SKIP & 1)) {
+      if (ntv && !(XD_SKIP & 1) && tl) {
+#pragma unroll
+        for (int u = 0; u < BPW; ++u) {
+          const int blk = wave + NW * u;
+          if (blk < C::NBLK) {
+            const int pb = blk / C::NNT;
+            const float b0 = lds[(pb * 16 + j) * 4 + g];
+            const float b1 = lds[(C::IPAD + pb * 16 + j) * 4 + g];
+            acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b0, acc[u], 0, 0, 0);
+            acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b1, acc[u], 0, 0, 0);
+          }
+        }
+      } else if (ntv && !(XD_SKIP & 1)) {
 #pragma unroll
         for (int u = 0; u < BPW; ++u) {
           const int blk = wave + NW * u;

@@ -219,7 +219,14 @@ def test_expand_dw_forms_bit_identical(cuda, spec, bhw):
     every output with the same operation sequence: y, the ECA partials and
     the fused skip branch must be bit-identical.  (4, 96, 80)
     gives several items per persistent workgroup (the expanded-buffer and
-    tap/partial rings wrap), (1, 1, 2) a grid smaller than the CU count."""
+    tap/partial rings wrap), (1, 1, 2) a grid smaller than the CU count.
+
+    Exception (round 6): for Cin 24 (two input stages) the default kernel
+    runs the 8-channel last input stage as 2 MFMAs over channels 4e + g
+    instead of 4 over channels 4g + e (csrc/expdw.hip, tail8), so its k sum
+    is taken in another order: there forms 2 / 3 / 4 stay bit-identical to
+    each other, form 1 agrees with them within 1e-6 and its skip branch
+    (no MFMA) bit for bit."""
     from jabd_amd import functional as F
     from jabd_amd._lib import lib
     k, cin, E, s, act = spec
@@ -249,8 +256,13 @@ def test_expand_dw_forms_bit_identical(cuda, spec, bhw):
     finally:
         lib().jabd_expand_dw_select(0)
     torch.cuda.synchronize()
-    for other in outs[1:]:
-        for a, b in zip(outs[0], other):
+    tail8 = cin == 24
+    for a, b in zip(outs[1], outs[2]):
+        assert torch.equal(a, b)
+    for i, (a, b) in enumerate(zip(outs[0], outs[1])):
+        if tail8 and i < 2:
+            assert rel_err(a, b) < 1e-6, rel_err(a, b)
+        else:
             assert torch.equal(a, b)
     # the chunk-pipelined form (4, csrc/expdw3.hip; opt-in: JABD_EXPDW3=1
     # or select(4), measured slower than expdw1): y and the skip branch bit-identical, the ECA partials (a sum
@@ -264,10 +276,10 @@ def test_expand_dw_forms_bit_identical(cuda, spec, bhw):
     finally:
         lib().jabd_expand_dw_select(0)
     torch.cuda.synchronize()
-    assert torch.equal(o4[0], outs[0][0])
+    assert torch.equal(o4[0], outs[1][0])
     if s == 2:
-        assert torch.equal(o4[2], outs[0][2])
-    assert rel_err(o4[1], outs[0][1]) < 2e-6
+        assert torch.equal(o4[2], outs[1][2])
+    assert rel_err(o4[1], outs[1][1]) < 2e-6
 
 
 @pytest.mark.gpu
