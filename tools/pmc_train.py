@@ -24,21 +24,28 @@ import json
 # serve two calls: their algorithmic bytes are the two calls' sum)
 FAMILIES = {
     "dw_dgrad_bn (jabd_dw_dgrad_bn_bwd_f32)": (["jabd_dw_dgrad_bn_bwd_f32"], ["dw_dgrad_bn_kernel"]),
-    "bn_act_bwd (jabd_bn_act_bwd_ex_f32 + jabd_bn_act_bwd_f32)":
-        (["jabd_bn_act_bwd_ex_f32", "jabd_bn_act_bwd_f32"],
-         ["bn_bwd_part_kernel", "bn_bwd_apply_kernel", "bn_bwd_final_kernel"]),
+    "bn_act_bwd (jabd_bn_act_bwd_ex_f32 + jabd_bn_act_bwd_f32 + _rows)":
+        (["jabd_bn_act_bwd_ex_f32", "jabd_bn_act_bwd_f32", "jabd_bn_act_bwd_rows_f32"],
+         ["bn_bwd_part_kernel", "bn_bwd_apply_kernel", "bn_bwd_final_kernel", "bn_rows_sum_kernel"]),
     "conv_wgrad (jabd_conv_wgrad_f32 + _eca)": (["jabd_conv_wgrad_f32", "jabd_conv_wgrad_eca_f32"],
                                                ["conv_wgrad32_kernel", "conv_wgrad_v_kernel",
                                                 "wgrad_reduce2_kernel", "wgrad_img_reduce",
                                                 "wgrad_eca_reduce"]),
-    "conv2d_nhwc (jabd_conv2d_nhwc_f32)": (["jabd_conv2d_nhwc_f32"],
-                                          ["conv1x1_m32_kernel", "conv1x1_kernel",
-                                           "conv1x1_stream_kernel", "conv3x3_tile_kernel",
-                                           "conv_gemm_kernel", "stem7_fwd_kernel"]),
-    "nlm_bwd_attn (jabd_nlm_bwd_attn_f32)": (["jabd_nlm_bwd_attn_f32"], ["nlm_bwd_attn_kernel"]),
+    # the GEMM kernels serve the plain conv call and its statistics / BatchNorm-backward forms
+    "conv2d_nhwc (jabd_conv2d_nhwc_f32 + _bn_stats + _bn_bwd_sums)":
+        (["jabd_conv2d_nhwc_f32", "jabd_conv1x1_bn_stats_f32", "jabd_conv_bn_stats_f32",
+          "jabd_conv_bn_bwd_sums_f32"],
+         ["conv1x1_m32_kernel", "conv1x1_kernel", "conv1x1_stream_kernel", "conv3x3_tile_kernel",
+          "conv_gemm_kernel", "stem7_fwd_kernel", "m32_ksplit_reduce", "bn_rows_chunk_kernel"]),
+    "nlm_bwd_attn (jabd_nlm_bwd_attn_f32)": (["jabd_nlm_bwd_attn_f32"], ["nlm_bwd_attn"]),
     "bn_act_fwd (jabd_bn_act_fwd_f32 + _sum)": (["jabd_bn_act_fwd_f32", "jabd_bn_act_fwd_sum_f32"],
                                                ["bn_act_fwd_kernel", "bn_act_fwd_sum_kernel"]),
-    "dw_wgrad (jabd_dw_wgrad_f32)": (["jabd_dw_wgrad_f32"], ["dw_wgrad_strip_kernel"]),
+    "bn_stats (jabd_bn_stats_f32)": (["jabd_bn_stats_f32"], ["bn_stats_part_kernel"]),
+    "dw_wgrad (jabd_dw_wgrad_f32 + _bnin)": (["jabd_dw_wgrad_f32", "jabd_dw_wgrad_bnin_f32"],
+                                            ["dw_wgrad_strip_kernel", "dw_wgrad_rows_kernel"]),
+    "dwconv_stats (jabd_dwconv_stats_f32 + _bnin + jabd_dwconv_nhwc_f32)":
+        (["jabd_dwconv_stats_f32", "jabd_dwconv_bnin_stats_f32", "jabd_dwconv_nhwc_f32"],
+         ["dw_rows_kernel", "dw_kernel<", "bn_stats_final_kernel"]),
 }
 
 
