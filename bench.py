@@ -82,11 +82,12 @@ def build_model(device):
     return m.eval().to(device)
 
 
-def _expdw_work(xx, pk, k, stride, y, skip=False):
+def _expdw_work(xx, pk, k, stride, y, skip=False, pre=None):
     """(FLOPs, algorithmic bytes) of one fused expand+depthwise launch: the
     expand GEMM over every input pixel plus the k x k depthwise MACs; bytes =
     input read once + output written once + weights (+ the fused stride-2
-    skip branch's dw3x3 MACs and output)."""
+    skip branch's dw3x3 MACs and output; + the previous block's fused project,
+    pre: its 1x1 GEMM over every input pixel and its residual read)."""
     B, H, W, C = xx.shape
     E = pk.Cout
     flops = 2.0 * B * H * W * C * E + 2.0 * y.numel() * k * k
@@ -95,6 +96,10 @@ def _expdw_work(xx, pk, k, stride, y, skip=False):
         npx = y.shape[0] * y.shape[1] * y.shape[2]
         flops += 2.0 * npx * C * 9
         nbytes += 4.0 * npx * C
+    if pre is not None:
+        ppk = pre[0]
+        flops += 2.0 * B * H * W * ppk.Cin * ppk.Cout
+        nbytes += 4.0 * (pre[2].numel() + ppk.Cin * ppk.Cout)
     return flops, nbytes
 
 
@@ -133,7 +138,8 @@ def conv_roofline(model, x, steps):
         s.record()
         out = orig_xd(xx, pk, w, b, k, stride, **kw)
         e.record()
-        recs.append((s, e) + _expdw_work(xx, pk, k, stride, out[0], kw.get("skip") is not None))
+        recs.append((s, e) + _expdw_work(xx, pk, k, stride, out[0], kw.get("skip") is not None,
+                                         kw.get("pre")))
         return out
 
     F.conv, F.expand_dw = timed_conv, timed_xd
@@ -680,11 +686,14 @@ def activation_census(kind, device, size):
 
     def w_xd(xx, pk, w, b, k, stride, **kw):
         out = orig["expand_dw"](xx, pk, w, b, k, stride, **kw)
+        if kw.get("pre") is not None:   # the previous block's project output (kept on chip)
+            add(xx.numel())
         add(xx.shape[0] * xx.shape[1] * xx.shape[2] * pk.Cout)
         add(out[0].numel())
         if kw.get("skip") is not None:
             add(out[2].numel())
-        tot["flops"] += _expdw_work(xx, pk, k, stride, out[0], kw.get("skip") is not None)[0]
+        tot["flops"] += _expdw_work(xx, pk, k, stride, out[0], kw.get("skip") is not None,
+                                    kw.get("pre"))[0]
         return out
 
     def w_dw(xx, w, bias, k, stride, **kw):

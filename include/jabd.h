@@ -497,6 +497,15 @@ typedef struct jabd_expdw_args {
    * sy_bs) by the first expanded-channel chunk's workgroups
    * (nets/mobilenetV3.py:126-137, the K-concat source of the project GEMM). */
   const float* sw; const float* sb; float* sy; int64_t sy_bs; int32_t sy_ps, reserved1;
+  /* optional (pw NULL: none; stride 2 with the skip branch, Cin <= 16): the
+   * previous block's project fused in front of the expand.  x is then that
+   * block's depthwise output d, and the kernel expands
+   *   x' = pact( Wp (pg[b] * d) + pb + pres )      (nets/mobilenetV3.py:144-150)
+   * per input-tile pixel (zero outside the image): Wp packed as `we` ([1][1][64]
+   * float4, Cin -> Cin), pb [Cin], pg [B][Cin] (image stride pg_bs: the ECA
+   * gate), pres the block input (the identity residual; x's strides).  x' is
+   * never written: the block pair's activation between them stays on chip. */
+  const void* pw; const float* pb; const float* pg; const float* pres; int32_t pg_bs, pact;
 } jabd_expdw_args;
 int64_t jabd_expand_dw_nblk(int32_t OH, int32_t OW, int32_t k, int32_t stride);
 int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_t stream);

@@ -40,10 +40,19 @@ constexpr int xd1_min_wg() {
 // two rounds): Cin 16 E16 k3 s1 246 vs 258 us, the Cin 24 k5 s2 skip form
 // 305-313 vs 324-327 us; the Cin 16 k3 s2 skip form measured 506-514 vs
 // 491-498 us with it and keeps the run-time count.
+// PRE (KCC == 1, Cin <= 16): the previous block's project in front of the
+// expand (jabd_expdw_args.pw): the staged tile is that block's depthwise
+// output d; its 1x1 GEMM (the ECA gate folded into the packed weights, one
+// 16-channel stage, one n-tile: 4 MFMAs per 16-pixel block), bias, the
+// identity residual and the activation turn it into the block output in LDS,
+// which the expand (and the skip branch) then read.  The block output never
+// goes to HBM: its project launch (a write + a read of it) disappears, for a
+// second input read (the residual) and a quarter more MFMAs here.
 template <int K, int S, int TH, int TW, int EC, int ACT, int KP, bool SKIP = false, int NW = 4,
-          int SKC = 160, int KCC = 0>
+          int SKC = 160, int KCC = 0, bool PRE = false>
 __global__ __launch_bounds__(64 * NW, (xd1_min_wg<K, S, TH, TW, EC, SKIP, NW, SKC>())) void expdw1_kernel(const jabd_expdw_args p, const XdDivs dv,
                                                        int nitems) {
+  static_assert(!PRE || (KCC == 1 && KP == 1), "PRE: one input stage");
   const int Kc = KCC ? KCC : p.Kc;
   using C = XdCfg<K, S, TH, TW, EC>;
   constexpr int T = 64 * NW;                  // threads
@@ -96,6 +105,17 @@ __global__ __launch_bounds__(64 * NW, (xd1_min_wg<K, S, TH, TW, EC, SKIP, NW, SK
   const int chl = 4 * c4;
   const bool chv = it.c0 + chl < p.E;
   const float4 bias2 = *reinterpret_cast<const float4*>(p.bd + (chv ? it.c0 + chl : 0));
+  // PRE: packed project weights of lane (j, g) (component e: input channel
+  // 4g + e, output channel j) scaled by this image's gate; bias of output
+  // channels 4g .. 4g + 3 (the lane's accumulator rows)
+  f32x4 apre = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float4 bpre = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (PRE) {
+    const f32x4 w = reinterpret_cast<const f32x4*>(p.pw)[lane];
+    const float4 gt = *reinterpret_cast<const float4*>(p.pg + (int64_t)it.b * p.pg_bs + 4 * g);
+    apre = (f32x4){w.x * gt.x, w.y * gt.y, w.z * gt.z, w.w * gt.w};
+    bpre = *reinterpret_cast<const float4*>(p.pb + 4 * g);
+  }
   // input stage loads through a buffer descriptor: an out-of-range slot gets
   // voffset 0xFFFFFFF0 and reads zeros (host: x < 4 GiB)
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
@@ -167,6 +187,52 @@ __global__ __launch_bounds__(64 * NW, (xd1_min_wg<K, S, TH, TW, EC, SKIP, NW, SK
       asm volatile("" : "+v"(a));
       lds_barrier();
       if (kc == 0) XD_T(2);
+      if constexpr (PRE) {
+        // block output = pact(Wp (g d) + pb + res) on the staged tile, back into
+        // the same quad planes (lane (j, g) of block pb: pixel 16 pb + j,
+        // channels 4g .. 4g + 3); zero outside the image (the expand input's
+        // padding) and on the pad pixels past IPX
+        constexpr int BPP = (C::NPB + NW - 1) / NW;
+        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(p.pres), (short)0, (int)(uint32_t)((int64_t)p.B * p.x_bs * 4),
+            0x00020000);
+        f32x4 pacc[BPP];
+        float4 res[BPP];
+        bool pin[BPP];
+#pragma unroll
+        for (int u = 0; u < BPP; ++u) {
+          const int pb = wave + NW * u;
+          const int px = pb * 16 + j;
+          const int r = px / C::IW, c = px - r * C::IW;
+          const int ih = it.ih0 + r, iw = it.iw0 + c;
+          pin[u] = pb < C::NPB && px < C::IPX &&
+                   (interior || ((unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W));
+          const uint32_t off =
+              pin[u] ? (uint32_t)(it.b * p.x_bs + (ih * p.W + iw) * p.x_ps + 4 * g) * 4u : 0xFFFFFFF0u;
+          res[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0));
+          pacc[u] = (f32x4){bpre.x, bpre.y, bpre.z, bpre.w};
+          if (pb < C::NPB) {
+            const f32x4 bv = *reinterpret_cast<const f32x4*>(lds + (g * C::IPAD + px) * 4);
+            pacc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(apre.x, bv.x, pacc[u], 0, 0, 0);
+            pacc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(apre.y, bv.y, pacc[u], 0, 0, 0);
+            pacc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(apre.z, bv.z, pacc[u], 0, 0, 0);
+            pacc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(apre.w, bv.w, pacc[u], 0, 0, 0);
+          }
+        }
+        lds_barrier();  // every wave's reads of d done
+#pragma unroll
+        for (int u = 0; u < BPP; ++u) {
+          const int pb = wave + NW * u;
+          if (pb >= C::NPB) continue;
+          float4 v = make_float4(pacc[u][0] + res[u].x, pacc[u][1] + res[u].y,
+                                 pacc[u][2] + res[u].z, pacc[u][3] + res[u].w);
+          if (p.pact == ACT_RELU) v = xd_act4<ACT_RELU>(v);
+          else if (p.pact == ACT_HSWISH) v = xd_act4<ACT_HSWISH>(v);
+          if (!pin[u]) v = make_float4(0.f, 0.f, 0.f, 0.f);
+          *reinterpret_cast<float4*>(lds + (g * C::IPAD + pb * 16 + j) * 4) = v;
+        }
+        lds_barrier();
+      }
       if (kc + KP < Kc) load_stage(kc + KP, pf[s]);
       // fused skip branch (stride 2, first chunk's workgroups): this stage's
       // 16 channels for output pixel t & 63, channel quad t >> 6 (waves 0-3), taps from LDS
@@ -1179,6 +1245,25 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
                   make_fastdiv((uint32_t)tiles_w)};
   JABD_REQUIRE((int64_t)a.B * a.x_bs * 4 < ((int64_t)1 << 32) - 16,
                "expand_dw: input must be < 4 GiB (buffer-descriptor offsets)");
+  if (a.pw) {  // the previous block's project fused in front (one form)
+    JABD_REQUIRE(a.pb && a.pg && a.pres && a.pg_bs >= a.Cin &&
+                     (a.pact == ACT_NONE || a.pact == ACT_RELU || a.pact == ACT_HSWISH),
+                 "expand_dw: bad fused-project arguments");
+    JABD_REQUIRE(a.k == 3 && a.stride == 2 && EC == 32 && a.sy && a.Cin == 16 && a.Kc == 1 &&
+                     a.x_ps == 16 && skc == 40 && nw == 4,
+                 "expand_dw: the fused previous project takes the 3x3/s2 Cin-16 skip form only");
+#define XP_LAUNCH(ACT_)                                                                       \
+  expdw1_kernel<3, 2, 8, 8, 32, ACT_, 1, true, 4, 40, 1, true><<<(unsigned)nitems, 256, 0, st>>>( \
+      a, dv, (int)nitems)
+    if (a.act == ACT_RELU)
+      XP_LAUNCH(ACT_RELU);
+    else if (a.act == ACT_HSWISH)
+      XP_LAUNCH(ACT_HSWISH);
+    else
+      XP_LAUNCH(ACT_NONE);
+#undef XP_LAUNCH
+    return check_launch("expand_dw (fused project)");
+  }
   if (xw_form == 0 || xw_form == 4) {   // the chunk-pipelined form: opt-in (expdw3.hip)
     const int e = expdw3_dispatch(a, dv, tiles_img, xw_form == 4, st);
     if (e != JABD_EINVAL) return e;   // else: not covered, the forms below

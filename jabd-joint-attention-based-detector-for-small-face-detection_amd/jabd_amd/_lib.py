@@ -83,6 +83,7 @@ class ExpDwArgs(ctypes.Structure):
         ("part", c_vp),
         ("sw", c_vp), ("sb", c_vp), ("sy", c_vp), ("sy_bs", c_i64), ("sy_ps", c_i32),
         ("reserved1", c_i32),
+        ("pw", c_vp), ("pb", c_vp), ("pg", c_vp), ("pres", c_vp), ("pg_bs", c_i32), ("pact", c_i32),
     ]
 
 

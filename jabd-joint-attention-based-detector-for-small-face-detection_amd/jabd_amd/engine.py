@@ -34,6 +34,10 @@ FUSE_EXPAND_DW = os.environ.get("JABD_FUSE_EXPAND_DW", "1") != "0"
 # ... and the stride-2 blocks' dw3x3 skip branch into that kernel (it stages
 # the same input tile); JABD_FUSE_SKIP=0 runs it as its own dw launch.
 FUSE_SKIP = os.environ.get("JABD_FUSE_SKIP", "1") != "0"
+# ... and a 16 -> 16 identity-residual block's project into the next block's
+# fused kernel when that is the 3x3/s2 Cin-16 skip form (JABD-MNv3 blocks 1 -> 2:
+# the 512^2 x 16 block output stays on chip); JABD_FUSE_PRE=0: separate launches
+FUSE_PRE = os.environ.get("JABD_FUSE_PRE", "1") != "0"
 # JABD_EVAL_STREAMS=2: eval batches of EVAL_SPLIT_MIN+ images run as image
 # groups on their own HIP streams (Engine.run).  Off by default: at bs32
 # 1024^2 two streams are +1.7% with weights_init's near-zero activations but
@@ -375,9 +379,38 @@ class _MNv3Block:
             return M.beca_gate(d, self.eca)
         return None
 
-    def forward(self, x):
+    def can_defer(self):
+        """This block's project can run inside the next block's fused kernel:
+        ECA gate, identity residual, a 16 -> 16 1x1 with a folded bias."""
+        pk = self.project
+        return (FUSE_PRE and FUSE_EXPAND_DW and self.gate == "eca" and self.kind == "identity" and
+                pk.KH == 1 and pk.KW == 1 and pk.Cin == 16 and pk.Cout == 16 and not pk.Cin2 and
+                pk.bias is not None)
+
+    def takes_pre(self):
+        """The fused kernel can take the previous block's project: the 3x3/s2
+        skip form over 16 input channels, and nothing after it reads this
+        block's input (its skip branch runs inside that kernel)."""
+        return (FUSE_EXPAND_DW and FUSE_SKIP and self.stride == 2 and self.k == 3 and
+                self.skip_dw is not None and self.kind in ("dw_concat", "dw_residual") and
+                self.expand.Cin == 16 and self.expand.KH == 1 and not self.expand.Cin2)
+
+    def front(self, x):
+        """Expand + depthwise + ECA gate of this block; its project is handed
+        to the next block's kernel: (d, (project, gate, residual, act))."""
+        d, part = F.expand_dw(x, self.expand, self.dw_w, self.dw_b, self.k, self.stride,
+                              act=self.act, partials=True)
+        return d, (self.project, self._scale(d, part), x, self.act)
+
+    def forward(self, x, pre=None):
         t = None
-        if FUSE_EXPAND_DW:
+        if pre is not None:  # x: the previous block's (d, project) from front()
+            d_prev, pspec = x, pre
+            r = F.expand_dw(d_prev, self.expand, self.dw_w, self.dw_b, self.k, self.stride,
+                            act=self.act, partials=self.gate == "eca", skip=self.skip_dw,
+                            pre=pspec)
+            d, part, t = r
+        elif FUSE_EXPAND_DW:
             fuse_skip = FUSE_SKIP and self.skip_dw is not None and self.stride == 2
             r = F.expand_dw(x, self.expand, self.dw_w, self.dw_b, self.k, self.stride,
                             act=self.act, partials=self.gate == "eca",
@@ -526,8 +559,15 @@ class Engine:
                 s = F.stem(x, self.stem[0], self.stem[1], "hswish")
                 feats = []
                 for layer in self.layers:
-                    for blk in layer:
-                        s = blk.forward(s)
+                    pre = None
+                    for i, blk in enumerate(layer):
+                        nxt = layer[i + 1] if i + 1 < len(layer) else None
+                        if pre is None and nxt is not None and blk.can_defer() and \
+                                nxt.takes_pre():
+                            s, pre = blk.front(s)   # s: this block's d, for the next kernel
+                            continue
+                        s = blk.forward(s, pre=pre)
+                        pre = None
                     feats.append(s)
             else:
                 s = F.conv(x, self.stem, stride=2, pad=3, act="relu", nchw_in=True)

@@ -323,11 +323,15 @@ def dwconv(x, w, bias, k, stride, act="none", slope=0.0, partials=False):
 _XD_DBG = 0  # kernel-phase skip mask for tools/convbench.py timing experiments only
 
 
-def expand_dw(x, pk, w, bias, k, stride, act="none", partials=True, skip=None):
+def expand_dw(x, pk, w, bias, k, stride, act="none", partials=True, skip=None, pre=None):
     """Fused expand 1x1 (PackedConv pk, folded BN) + act -> depthwise k x k
     (pad k//2, folded BN) + act; returns (y, ECA partials [B, nblk, E]).
     skip = (w [9][Cin], bias [Cin]) (stride 2): the block's dw3x3/s2 skip
-    branch computed from the same input tile; returns (y, partials, t)."""
+    branch computed from the same input tile; returns (y, partials, t).
+    pre = (pk_prev, gate [B, Cin], res, act_prev): x is the previous block's
+    depthwise output and that block's project act_prev(pk_prev(gate * x) +
+    res) runs inside the kernel in front of the expand (the 3x3/s2 Cin-16
+    skip form; jabd_expdw_args.pw)."""
     _check("expand_dw.x", x)
     B, H, W, C = x.shape
     if pk.KH != 1 or pk.KW != 1 or pk.Cin != C or pk.Cin2:
@@ -355,6 +359,19 @@ def expand_dw(x, pk, w, bias, k, stride, act="none", partials=True, skip=None):
         t = torch.empty((B, OH, OW, C), dtype=torch.float32, device=x.device)
         a.sw, a.sb = skip[0].data_ptr(), skip[1].data_ptr()
         a.sy, a.sy_bs, a.sy_ps = t.data_ptr(), t.stride(0), C
+    if pre is not None:
+        ppk, pg, pres, pact = pre
+        if (ppk.KH != 1 or ppk.KW != 1 or ppk.Cin != C or ppk.Cout != C or ppk.Cin2 or
+                ppk.bias is None or ppk.Kc != 1 or ppk.Ntiles != 1):
+            raise ValueError("expand_dw: pre must be a plain Cin -> Cin 1x1 conv with a bias")
+        _check("expand_dw.pre.res", pres)
+        if tuple(pres.shape) != tuple(x.shape) or pres.stride() != x.stride():
+            raise ValueError("expand_dw: the pre residual must have x's shape and strides")
+        if pg.shape != (B, C) or not pg.is_contiguous():
+            raise ValueError("expand_dw: the pre gate must be a contiguous [B, Cin] tensor")
+        a.pw, a.pb, a.pg, a.pres = ppk.w.data_ptr(), ppk.bias.data_ptr(), pg.data_ptr(), \
+            pres.data_ptr()
+        a.pg_bs, a.pact = pg.stride(0), ACT[pact]
     call("jabd_expand_dw_nhwc_f32", ctypes.byref(a), _stream())
     return (y, part, t) if skip is not None else (y, part)
 

@@ -321,3 +321,78 @@ def test_expand_dw_nan_rule(cuda, spec):
     assert torch.equal(torch.isnan(e.cpu()), torch.isnan(e_ref.permute(0, 2, 3, 1)))
     assert rel_err(got[~nan], ref[~nan]) < 2e-5
     assert rel_err(got2[~nan], ref[~nan]) < 2e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hw", [(37, 29), (64, 64), (18, 17)])
+@pytest.mark.parametrize("act", ["relu", "hswish"])
+def test_expand_dw_fused_previous_project(cuda, hw, act):
+    """Blocks 1 -> 2 of JABD-MNv3 (nets/mobilenetV3.py:144-150, 452-456): block
+    1's project (16 -> 16 1x1 + folded BN, ECA gate, identity residual, act)
+    run inside block 2's fused kernel (jabd_expdw_args.pw) against the same
+    ops launched separately (F.conv, then F.expand_dw on its output): y, the
+    ECA partials and the fused skip branch within fp32 reassociation (the
+    project's k sum is taken in the MFMA's order instead of the streaming
+    kernel's)."""
+    from jabd_amd import functional as F
+    H, W = hw
+    B, C, E = 2, 16, 64
+    g = torch.Generator().manual_seed(H * 7 + W)
+
+    def conv_bn(cin, cout, k, s, groups=1):
+        c = torch.nn.Conv2d(cin, cout, k, s, k // 2, groups=groups, bias=False)
+        bn = torch.nn.BatchNorm2d(cout)
+        with torch.no_grad():
+            c.weight.copy_(torch.randn(c.weight.shape, generator=g) / c.weight[0].numel() ** 0.5)
+            bn.weight.copy_(1 + 0.2 * torch.randn(cout, generator=g))
+            bn.bias.copy_(0.3 * torch.randn(cout, generator=g))
+            bn.running_mean.copy_(0.1 * torch.randn(cout, generator=g))
+            bn.running_var.copy_(0.5 + torch.rand(cout, generator=g))
+        return c.eval().to(cuda), bn.eval().to(cuda)
+
+    p_conv, p_bn = conv_bn(C, C, 1, 1)
+    e_conv, e_bn = conv_bn(C, E, 1, 1)
+    d_conv, d_bn = conv_bn(E, E, 3, 2, groups=E)
+    s_conv, s_bn = conv_bn(C, C, 3, 2, groups=C)
+    pk_p = F.pack_conv(p_conv, p_bn)
+    pk_e = F.pack_conv(e_conv, e_bn)
+    dw_w, dw_b = F.pack_dw(d_conv, d_bn)
+    skw, skb = F.pack_dw(s_conv, s_bn)
+    d0 = torch.randn(B, H, W, C, generator=g).relu().to(cuda)   # block 1's depthwise output
+    x0 = torch.randn(B, H, W, C, generator=g).to(cuda)          # block 1's input (residual)
+    gate = torch.rand(B, C, generator=g).to(cuda)
+    out0 = F.conv(d0, pk_p, act=act, ascale=gate, res=x0)
+    ref = F.expand_dw(out0, pk_e, dw_w, dw_b, 3, 2, act=act, skip=(skw, skb))
+    got = F.expand_dw(d0, pk_e, dw_w, dw_b, 3, 2, act=act, skip=(skw, skb),
+                      pre=(pk_p, gate, x0, act))
+    torch.cuda.synchronize()
+    for name, a, b in zip(("y", "partials", "skip"), got, ref):
+        assert rel_err(a, b) < 1e-5, (name, rel_err(a, b))
+
+
+@pytest.mark.gpu
+def test_engine_fused_previous_project(cuda, monkeypatch):
+    """The eval plan takes the fused-project form for JABD-MNv3 blocks 1 -> 2
+    (engine.FUSE_PRE) and agrees with the separate launches (FUSE_PRE off)."""
+    from jabd_amd import engine, functional as F
+    from test_model import _mnv3
+    m = _mnv3().to(cuda).eval()
+    x = torch.randn(2, 3, 160, 128, generator=torch.Generator().manual_seed(3)).to(cuda)
+    calls = []
+    orig = F.expand_dw
+
+    def spy(*a, **kw):
+        calls.append(kw.get("pre") is not None)
+        return orig(*a, **kw)
+
+    monkeypatch.setattr(F, "expand_dw", spy)
+    with torch.no_grad():
+        monkeypatch.setattr(engine, "FUSE_PRE", True)
+        got = m(x)
+        assert calls.count(True) == 1, calls
+        monkeypatch.setattr(engine, "FUSE_PRE", False)
+        calls.clear()
+        ref = m(x)
+        assert not any(calls)
+    for a, b in zip(got, ref):
+        assert rel_err(a, b) < 1e-5, rel_err(a, b)

@@ -70,7 +70,13 @@ def main():
         E = y.shape[3]
         Min = xx.shape[0] * xx.shape[1] * xx.shape[2]
         fl = 2.0 * Min * pk.Cin * E + 2.0 * M * E * k * k
-        return fl, _nb(xx, y), "Min%d Cin%d E%d k%d s%d" % (Min, pk.Cin, E, k, stride)
+        nb = _nb(xx, y)
+        pre = kw.get("pre")
+        if pre is not None:   # the previous block's project fused in front
+            fl += 2.0 * Min * pre[0].Cin * pre[0].Cout
+            nb += _nb(pre[2])
+        return fl, nb, "Min%d Cin%d E%d k%d s%d%s" % (Min, pk.Cin, E, k, stride,
+                                                      " +proj" if pre is not None else "")
 
     def c_dw(o, xx, w, b, k, stride, **kw):
         y = o[0]
