@@ -373,11 +373,11 @@ __global__ __launch_bounds__(64 * NW, (xd1_min_wg<K, S, TH, TW, EC, SKIP, NW, SK
     // xor 12, 20 (the even-popcount quad permutations) and 32; EC = 16 ->
     // xor 4, 8, 16, 32.  Fixed order: deterministic.  Lanes 0..NC4-1 then
     // hold channel quads 0..NC4-1.
-    constexpr int NX = C::NC4 == 8 ? 3 : 4;
-    constexpr int X8[3] = {12, 20, 32}, X4[4] = {4, 8, 16, 32};
+    constexpr int NX = C::NC4 == 16 ? 2 : C::NC4 == 8 ? 3 : 4;
+    constexpr int X8[3] = {12, 20, 32}, X4[4] = {4, 8, 16, 32}, X16[2] = {16, 32};
 #pragma unroll
     for (int r = 0; r < NX; ++r) {
-      const int off = C::NC4 == 8 ? X8[r] : X4[r];
+      const int off = C::NC4 == 16 ? X16[r] : C::NC4 == 8 ? X8[r] : X4[r];
       psum.x += __shfl_xor(psum.x, off);
       psum.y += __shfl_xor(psum.y, off);
       psum.z += __shfl_xor(psum.z, off);
@@ -1252,6 +1252,29 @@ extern "C" int jabd_expand_dw_nhwc_f32(const jabd_expdw_args* args, jabd_stream_
     JABD_REQUIRE(a.k == 3 && a.stride == 2 && EC == 32 && a.sy && a.Cin == 16 && a.Kc == 1 &&
                      a.x_ps == 16 && skc == 40 && nw == 4,
                  "expand_dw: the fused previous project takes the 3x3/s2 Cin-16 skip form only");
+    // E <= 64: all expanded channels in one 8-wave workgroup (the project and
+    // the input tiles once per tile instead of once per 32-channel chunk);
+    // JABD_EXPDW_PRE_EC=32 keeps 32-channel chunks (A/B)
+    static int pre_ec = -1;
+    if (pre_ec < 0) {
+      const char* e = getenv("JABD_EXPDW_PRE_EC");
+      pre_ec = e && e[0] == '3' ? 32 : 64;
+    }
+    if (pre_ec == 64 && a.E <= 64) {
+      const XdDivs dv1{make_fastdiv(1u), dv.tiles_img, dv.tiles_w};
+      const int64_t n1 = cdiv(ntiles, 8) * 8;
+#define XP_LAUNCH(ACT_)                                                                        \
+  expdw1_kernel<3, 2, 8, 8, 64, ACT_, 1, true, 8, 40, 1, true><<<(unsigned)n1, 512, 0, st>>>( \
+      a, dv1, (int)n1)
+      if (a.act == ACT_RELU)
+        XP_LAUNCH(ACT_RELU);
+      else if (a.act == ACT_HSWISH)
+        XP_LAUNCH(ACT_HSWISH);
+      else
+        XP_LAUNCH(ACT_NONE);
+#undef XP_LAUNCH
+      return check_launch("expand_dw (fused project, one chunk)");
+    }
 #define XP_LAUNCH(ACT_)                                                                       \
   expdw1_kernel<3, 2, 8, 8, 32, ACT_, 1, true, 4, 40, 1, true><<<(unsigned)nitems, 256, 0, st>>>( \
       a, dv, (int)nitems)

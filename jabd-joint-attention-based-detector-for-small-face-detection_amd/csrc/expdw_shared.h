@@ -100,7 +100,7 @@ struct XdCfg {
   static_assert(TW % PW == 0 && 256 % NC4 == 0, "tile shape");
   static_assert(LDS * 4 <= 160 * 1024 && LDS_PM * 4 <= 160 * 1024, "LDS");
   static_assert((K * K + 1) * NC4 <= 256, "dw taps: one float4 per thread");
-  static_assert(NC4 == 4 || NC4 == 8, "dw_lane: 16- or 32-channel chunks");
+  static_assert(NC4 == 4 || NC4 == 8 || NC4 == 16, "dw_lane: 16-, 32- or 64-channel chunks");
 };
 
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() is also a
@@ -179,6 +179,14 @@ __device__ __forceinline__ bool xd_item(const jabd_expdw_args& p, int i, const X
 // picks the strip row.  Returns (channel quad, strip within the wave's slice).
 template <int NC4>
 __device__ __forceinline__ void dw_lane(int l, int& c4, int& sl) {
+  // EC = 64 (16 channel quads): quad l & 15, strip l >> 4; a 16-lane read
+  // group is one strip's 16 quads, banks 4 (q QP + px) mod 64 = 4q + const
+  // (QP odd): distinct
+  if (NC4 == 16) {
+    c4 = l & 15;
+    sl = l >> 4;
+    return;
+  }
   const int h = l >> 5, q = (l >> 2) & 7, par = __builtin_popcount(q) & 1, k = q >> 1;
   if (NC4 == 8) {
     c4 = (l & 3) + 4 * par;
