@@ -780,6 +780,11 @@ static bool use_conv32(const ConvArgs& a) {
   }
   if (!a.w32 || a.tn32 <= 0 || a.ntiles32 % a.tn32 || a.ntiles32 * 32 < a.Cout) return false;
   if (v >= 0) return v == 1;
+  // K 64 / 128 1x1s into >= 64 channels: the 32x32 kernel's streaming form
+  // (conv1x1_m32s_kernel; R50 l1.c3-shaped GEMM 2190 -> 2005 us vs conv.hip)
+  if (a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && !a.x2 && !a.ascale && !a.y2 &&
+      !a.tconv && (a.Cin == 64 || a.Cin == 128) && a.Cout >= 64)
+    return true;
   const int K = a.KH * a.KW * a.Cin + (a.x2 ? a.Cin2 : 0);
   if (a.KH * a.KW > 1) return a.Cout >= 64 && K >= 288;
   return a.Cout >= 96 && K >= 96;

@@ -58,13 +58,159 @@ __device__ __forceinline__ void wave_lds_sync32() {
 constexpr int kG = kBK / 8;      // 8-channel groups per stage
 constexpr int kGateLds = 1024;   // ECA gate channels staged in LDS
 
+// The TM = 1 epilogue of one 32-pixel x 32*TN-channel wave tile (shared by
+// conv1x1_m32_kernel and the streaming form conv1x1_m32s_kernel, so both
+// produce the same bits): lane (h, j) holds pixel pm / output pixel om (-1:
+// past M) and the accumulators acc[u][4c + e] of channels
+// (nb*TN + u)*32 + 8c + 4h + e; ep is the wave's private LDS slice
+// (32 x kEpiPitch floats); srow the tile's statistics row (ST / BB).
+constexpr int kEpiPitch = 36;
+// EPI: what the host guarantees about the plain epilogue terms — kEpiRt
+// reads bias / residual / activation from p at run time; kEpiNone: no bias,
+// no residual, identity activation (the statistics / BatchNorm-backward forms
+// and plain data gradients); kEpiRes: the residual only.  The run-time form
+// inlines every activation (incl. the sigmoid's division) at each of the 64
+// element sites: ~5.6k instructions per kernel instead of ~1.5k.
+enum { kEpiRt = 0, kEpiNone = 1, kEpiRes = 2 };
+template <int TN, bool ST, bool BB, int EPI = kEpiRt>
+__device__ __forceinline__ void m32_epilogue_tm1(const ConvArgs& p, const f32x16 (&acc)[TN],
+                                                 int pm, int om, int nb, int srow, float* ep,
+                                                 float* __restrict__ part, const BnEpi& bb,
+                                                 int lane) {
+  const bool has_bias = EPI == kEpiRt && p.bias;
+  const bool has_res = EPI == kEpiRes || (EPI == kEpiRt && p.res);
+  const int h = lane >> 5, j = lane & 31;
+  const int ep_px = lane >> 3, ep_q = lane & 7;
+  // the tile's pixel rows (pm < 0: past M) for the 8-pixel store groups
+  int mrow[4], prow[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    prow[r] = __shfl(pm, ep_px + 8 * r);
+    mrow[r] = __shfl(om, ep_px + 8 * r);
+  }
+#pragma unroll
+  for (int u = 0; u < TN; ++u) {
+    const int nb0 = (nb * TN + u) * 32;
+    if (nb0 >= p.Cout) break;  // wave-uniform
+    const int n = nb0 + 4 * ep_q;
+    float4 ss = make_float4(0.f, 0.f, 0.f, 0.f), sq = ss, sh = ss;
+    float4 bmu = sh, bis = sh, bgm = sh, bbt = sh;
+    float4 bx[4];
+    if constexpr (BB) {  // issued before the LDS round trip: in flight across it
+      if (n < p.Cout) {
+        bmu = *reinterpret_cast<const float4*>(bb.mean + n);
+        bis = *reinterpret_cast<const float4*>(bb.invstd + n);
+        bgm = *reinterpret_cast<const float4*>(bb.gamma + n);
+        bbt = *reinterpret_cast<const float4*>(bb.beta + n);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)   // the BatchNorm input at the tile's pixels, in flight
+        bx[r] = (prow[r] >= 0 && n < p.Cout)
+                    ? *reinterpret_cast<const float4*>(bb.x + (int64_t)mrow[r] * bb.x_ps + n)
+                    : sh;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      *reinterpret_cast<float4*>(ep + j * kEpiPitch + 8 * c + 4 * h) =
+          make_float4(acc[u][4 * c], acc[u][4 * c + 1], acc[u][4 * c + 2],
+                      acc[u][4 * c + 3]);
+    wave_lds_sync32();
+    if constexpr (ST) sh = *reinterpret_cast<const float4*>(ep + 4 * ep_q);  // pixel 0
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int px = ep_px + 8 * r;
+      if (prow[r] < 0 || n >= p.Cout) continue;
+      float4 v = *reinterpret_cast<const float4*>(ep + px * kEpiPitch + 4 * ep_q);
+      if constexpr (BB) {
+        // as bn_bwd_part / bn_bwd_apply (train.hip): xhat, act'(xhat gamma + beta)
+        const float xv[4] = {bx[r].x, bx[r].y, bx[r].z, bx[r].w};
+        const float mu[4] = {bmu.x, bmu.y, bmu.z, bmu.w}, is[4] = {bis.x, bis.y, bis.z, bis.w};
+        const float gm[4] = {bgm.x, bgm.y, bgm.z, bgm.w}, bt[4] = {bbt.x, bbt.y, bbt.z, bbt.w};
+        const float gv[4] = {v.x, v.y, v.z, v.w};
+        float dzs[4], dzx[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xh = (xv[e] - mu[e]) * is[e];
+          const float z = fmaf(xh, gm[e], bt[e]);
+          const float d = bb.act == ACT_RELU ? (z > 0.f ? 1.f : 0.f)
+                          : bb.act == ACT_LEAKY ? (z > 0.f ? 1.f : bb.slope) : 1.f;
+          dzs[e] = gv[e] * d;
+          dzx[e] = dzs[e] * xh;
+        }
+        ss.x += dzs[0]; ss.y += dzs[1]; ss.z += dzs[2]; ss.w += dzs[3];
+        sq.x += dzx[0]; sq.y += dzx[1]; sq.z += dzx[2]; sq.w += dzx[3];
+      }
+      if constexpr (ST) {
+        const float dx = v.x - sh.x, dy = v.y - sh.y, dz = v.z - sh.z, dw = v.w - sh.w;
+        ss.x += dx; ss.y += dy; ss.z += dz; ss.w += dw;
+        sq.x = fmaf(dx, dx, sq.x); sq.y = fmaf(dy, dy, sq.y);
+        sq.z = fmaf(dz, dz, sq.z); sq.w = fmaf(dw, dw, sq.w);
+      }
+      if (has_bias) {
+        const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
+        v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
+      }
+      if (has_res) {
+        const float4 rr = *reinterpret_cast<const float4*>(p.res + (int64_t)mrow[r] * p.res_ps +
+                                                           p.res_c0 + n);
+        v.x += rr.x; v.y += rr.y; v.z += rr.z; v.w += rr.w;
+      }
+      if constexpr (EPI == kEpiRt) {
+        v.x = act32(v.x, p.act, p.slope);
+        v.y = act32(v.y, p.act, p.slope);
+        v.z = act32(v.z, p.act, p.slope);
+        v.w = act32(v.w, p.act, p.slope);
+      }
+      *reinterpret_cast<float4*>(p.y + (int64_t)mrow[r] * p.y_ps + p.y_c0 + n) = v;
+    }
+    if constexpr (BB) {
+#pragma unroll
+      for (int off = 8; off <= 32; off <<= 1) {
+        ss.x += __shfl_xor(ss.x, off); ss.y += __shfl_xor(ss.y, off);
+        ss.z += __shfl_xor(ss.z, off); ss.w += __shfl_xor(ss.w, off);
+        sq.x += __shfl_xor(sq.x, off); sq.y += __shfl_xor(sq.y, off);
+        sq.z += __shfl_xor(sq.z, off); sq.w += __shfl_xor(sq.w, off);
+      }
+      if (ep_px == 0 && (int64_t)srow * 32 < p.M && n < p.Cout) {
+        const int ldc = p.Ntiles * 32;
+        float* pr = bb.rows + (int64_t)srow * 2 * ldc + n;
+        *reinterpret_cast<float4*>(pr) = ss;
+        *reinterpret_cast<float4*>(pr + ldc) = sq;
+      }
+    }
+    if constexpr (ST) {
+      // the 8 lanes of one channel quad (lane xor 8, 16, 32), fixed order
+#pragma unroll
+      for (int off = 8; off <= 32; off <<= 1) {
+        ss.x += __shfl_xor(ss.x, off); ss.y += __shfl_xor(ss.y, off);
+        ss.z += __shfl_xor(ss.z, off); ss.w += __shfl_xor(ss.w, off);
+        sq.x += __shfl_xor(sq.x, off); sq.y += __shfl_xor(sq.y, off);
+        sq.z += __shfl_xor(sq.z, off); sq.w += __shfl_xor(sq.w, off);
+      }
+      const int64_t cnt = min<int64_t>(32, p.M - (int64_t)srow * 32);
+      if (ep_px == 0 && cnt > 0 && n < p.Cout) {
+        const float inv = 1.f / (float)cnt;
+        const int ldc = p.Ntiles * 32;
+        float* pr = part + (int64_t)srow * 2 * ldc + n;
+        *reinterpret_cast<float4*>(pr) =
+            make_float4(fmaf(ss.x, inv, sh.x), fmaf(ss.y, inv, sh.y), fmaf(ss.z, inv, sh.z),
+                        fmaf(ss.w, inv, sh.w));
+        *reinterpret_cast<float4*>(pr + ldc) =
+            make_float4(fmaxf(sq.x - ss.x * ss.x * inv, 0.f), fmaxf(sq.y - ss.y * ss.y * inv, 0.f),
+                        fmaxf(sq.z - ss.z * ss.z * inv, 0.f), fmaxf(sq.w - ss.w * ss.w * inv, 0.f));
+      }
+    }
+    wave_lds_sync32();
+  }
+}
+
 // Workgroup = 4 waves stacked along M (BM = 128*TM pixels) x BN = 32*TN
 // channels.  Tiles never straddle an image when `per_img` (ECA gate folded
 // into the staged weights), else M is tiled flat.
 // KXK: k x k implicit GEMM (tap-major K; every 32-channel stage lies inside
 // one tap, host guarantees Cin % 32 == 0, no K-concat source); stride-1
 // transposed form (tconv) for the data gradient.
-template <int TM, int TN, bool KXK, bool AS, bool ST = false, bool BB = false>
+template <int TM, int TN, bool KXK, bool AS, bool ST = false, bool BB = false, int EPI = kEpiRt>
 // AS: the ECA gate (ascale) is set — staged in LDS, applied at the weight store.
 // ST (TM = 1, training forward, no bias / residual / act): the epilogue also
 // writes the following BatchNorm's statistics per 32-pixel wave tile, row
@@ -93,7 +239,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
   constexpr int NBT = (NB4 + 255) / 256;       // ... per thread
   // the TM = 1 epilogue reuses the weight buffers: per wave a 32-pixel x
   // 32-channel block, pitch 36 floats (kEpiPitch)
-  constexpr int kEpiPitch = 36, kEpi4 = 4 * 32 * kEpiPitch / 4;
+  constexpr int kEpi4 = 4 * 32 * kEpiPitch / 4;
   constexpr int SB4 = (TM == 1 && kEpi4 > 2 * NB4) ? kEpi4 : 2 * NB4;
   __shared__ float4 sB_[SB4];
   float4 (*sB)[NB4] = reinterpret_cast<float4 (*)[NB4]>(sB_);
@@ -351,130 +497,9 @@ __global__ __launch_bounds__(256, 2) void conv1x1_m32_kernel(const ConvArgs p, i
   // direct stores.  Same values and operations either way, so the same bits.
   if constexpr (TM == 1) {
     float* ep = reinterpret_cast<float*>(sB_) + wave * 32 * kEpiPitch;
-    const int ep_px = lane >> 3, ep_q = lane & 7;
     const int srow = mb * 4 + wave;  // ST: this wave tile's statistics row (flat M tiling)
-#pragma unroll
-    for (int t = 0; t < TM; ++t) {
-      // the tile's pixel rows (pm < 0: past M) for the 8-pixel store groups
-      int mrow[4], prow[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        prow[r] = __shfl(pm[t], ep_px + 8 * r);
-        mrow[r] = __shfl(om[t], ep_px + 8 * r);
-      }
-#pragma unroll
-      for (int u = 0; u < TN; ++u) {
-        const int nb0 = (nb * TN + u) * 32;
-        if (nb0 >= p.Cout) break;  // wave-uniform
-        const int n = nb0 + 4 * ep_q;
-        float4 ss = make_float4(0.f, 0.f, 0.f, 0.f), sq = ss, sh = ss;
-        float4 bmu = sh, bis = sh, bgm = sh, bbt = sh;
-        float4 bx[4];
-        if constexpr (BB) {  // issued before the LDS round trip: in flight across it
-          if (n < p.Cout) {
-            bmu = *reinterpret_cast<const float4*>(bb.mean + n);
-            bis = *reinterpret_cast<const float4*>(bb.invstd + n);
-            bgm = *reinterpret_cast<const float4*>(bb.gamma + n);
-            bbt = *reinterpret_cast<const float4*>(bb.beta + n);
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r)   // the BatchNorm input at the tile's pixels, in flight
-            bx[r] = (prow[r] >= 0 && n < p.Cout)
-                        ? *reinterpret_cast<const float4*>(bb.x + (int64_t)mrow[r] * bb.x_ps + n)
-                        : sh;
-        }
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          *reinterpret_cast<float4*>(ep + j * kEpiPitch + 8 * c + 4 * h) =
-              make_float4(acc[t][u][4 * c], acc[t][u][4 * c + 1], acc[t][u][4 * c + 2],
-                          acc[t][u][4 * c + 3]);
-        wave_lds_sync32();
-        if constexpr (ST) sh = *reinterpret_cast<const float4*>(ep + 4 * ep_q);  // pixel 0
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int px = ep_px + 8 * r;
-          if (prow[r] < 0 || n >= p.Cout) continue;
-          float4 v = *reinterpret_cast<const float4*>(ep + px * kEpiPitch + 4 * ep_q);
-          if constexpr (BB) {
-            // as bn_bwd_part / bn_bwd_apply (train.hip): xhat, act'(xhat gamma + beta)
-            const float xv[4] = {bx[r].x, bx[r].y, bx[r].z, bx[r].w};
-            const float mu[4] = {bmu.x, bmu.y, bmu.z, bmu.w}, is[4] = {bis.x, bis.y, bis.z, bis.w};
-            const float gm[4] = {bgm.x, bgm.y, bgm.z, bgm.w}, bt[4] = {bbt.x, bbt.y, bbt.z, bbt.w};
-            const float gv[4] = {v.x, v.y, v.z, v.w};
-            float dzs[4], dzx[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float xh = (xv[e] - mu[e]) * is[e];
-              const float z = fmaf(xh, gm[e], bt[e]);
-              const float d = bb.act == ACT_RELU ? (z > 0.f ? 1.f : 0.f)
-                              : bb.act == ACT_LEAKY ? (z > 0.f ? 1.f : bb.slope) : 1.f;
-              dzs[e] = gv[e] * d;
-              dzx[e] = dzs[e] * xh;
-            }
-            ss.x += dzs[0]; ss.y += dzs[1]; ss.z += dzs[2]; ss.w += dzs[3];
-            sq.x += dzx[0]; sq.y += dzx[1]; sq.z += dzx[2]; sq.w += dzx[3];
-          }
-          if constexpr (ST) {
-            const float dx = v.x - sh.x, dy = v.y - sh.y, dz = v.z - sh.z, dw = v.w - sh.w;
-            ss.x += dx; ss.y += dy; ss.z += dz; ss.w += dw;
-            sq.x = fmaf(dx, dx, sq.x); sq.y = fmaf(dy, dy, sq.y);
-            sq.z = fmaf(dz, dz, sq.z); sq.w = fmaf(dw, dw, sq.w);
-          }
-          if (p.bias) {
-            const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
-            v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
-          }
-          if (p.res) {
-            const float4 rr = *reinterpret_cast<const float4*>(p.res + (int64_t)mrow[r] * p.res_ps +
-                                                               p.res_c0 + n);
-            v.x += rr.x; v.y += rr.y; v.z += rr.z; v.w += rr.w;
-          }
-          v.x = act32(v.x, p.act, p.slope);
-          v.y = act32(v.y, p.act, p.slope);
-          v.z = act32(v.z, p.act, p.slope);
-          v.w = act32(v.w, p.act, p.slope);
-          *reinterpret_cast<float4*>(p.y + (int64_t)mrow[r] * p.y_ps + p.y_c0 + n) = v;
-        }
-        if constexpr (BB) {
-#pragma unroll
-          for (int off = 8; off <= 32; off <<= 1) {
-            ss.x += __shfl_xor(ss.x, off); ss.y += __shfl_xor(ss.y, off);
-            ss.z += __shfl_xor(ss.z, off); ss.w += __shfl_xor(ss.w, off);
-            sq.x += __shfl_xor(sq.x, off); sq.y += __shfl_xor(sq.y, off);
-            sq.z += __shfl_xor(sq.z, off); sq.w += __shfl_xor(sq.w, off);
-          }
-          if (ep_px == 0 && (int64_t)srow * 32 < p.M && n < p.Cout) {
-            const int ldc = p.Ntiles * 32;
-            float* pr = bb.rows + (int64_t)srow * 2 * ldc + n;
-            *reinterpret_cast<float4*>(pr) = ss;
-            *reinterpret_cast<float4*>(pr + ldc) = sq;
-          }
-        }
-        if constexpr (ST) {
-          // the 8 lanes of one channel quad (lane xor 8, 16, 32), fixed order
-#pragma unroll
-          for (int off = 8; off <= 32; off <<= 1) {
-            ss.x += __shfl_xor(ss.x, off); ss.y += __shfl_xor(ss.y, off);
-            ss.z += __shfl_xor(ss.z, off); ss.w += __shfl_xor(ss.w, off);
-            sq.x += __shfl_xor(sq.x, off); sq.y += __shfl_xor(sq.y, off);
-            sq.z += __shfl_xor(sq.z, off); sq.w += __shfl_xor(sq.w, off);
-          }
-          const int64_t cnt = min<int64_t>(32, p.M - (int64_t)srow * 32);
-          if (ep_px == 0 && cnt > 0 && n < p.Cout) {
-            const float inv = 1.f / (float)cnt;
-            const int ldc = p.Ntiles * 32;
-            float* pr = part + (int64_t)srow * 2 * ldc + n;
-            *reinterpret_cast<float4*>(pr) =
-                make_float4(fmaf(ss.x, inv, sh.x), fmaf(ss.y, inv, sh.y), fmaf(ss.z, inv, sh.z),
-                            fmaf(ss.w, inv, sh.w));
-            *reinterpret_cast<float4*>(pr + ldc) =
-                make_float4(fmaxf(sq.x - ss.x * ss.x * inv, 0.f), fmaxf(sq.y - ss.y * ss.y * inv, 0.f),
-                            fmaxf(sq.z - ss.z * ss.z * inv, 0.f), fmaxf(sq.w - ss.w * ss.w * inv, 0.f));
-          }
-        }
-        wave_lds_sync32();
-      }
-    }
+    m32_epilogue_tm1<TN, ST, BB, (ST || BB) ? kEpiNone : EPI>(p, acc[0], pm[0], om[0], nb, srow,
+                                                                ep, part, bb, lane);
     return;
   }
   // TM = 2: acc[t][u][4c + e] = Y[pixel pm[t]][nb*BN + 32u + 8c + 4h + e]
@@ -539,6 +564,94 @@ __global__ __launch_bounds__(256) void m32_ksplit_reduce(const ConvArgs p, int k
   *reinterpret_cast<float4*>(p.y + m * p.y_ps + p.y_c0 + n) = v;
 }
 
+// Streaming form of the 1x1 / stride-1 GEMM for short K (Cin = 32 KS, KS 2
+// or 4): the R50 bottleneck convs with K 64 / 128 (l1.c3 64 -> 256 and its
+// statistics form, l1.c1 of block 1, the data gradients into 256 / 512
+// channels, l2.c3 128 -> 512).  A conv1x1_m32_kernel workgroup of such a
+// layer lives through only 2-4 K stages, so its pixel loads, the weight
+// staging and its barrier, and the epilogue's stores run back to back with
+// little MFMA work to hide them: those layers sat at 40-57% of the MFMA peak
+// while moving 2-3 TB/s.  Here a persistent workgroup copies its N block's
+// weights (all of K: KS x TN x 4 KiB) into LDS once; each wave then walks
+// 32-pixel tiles (tile = 4 wgm + wave + k * 4 gm) with no workgroup barrier,
+// refilling a K group's registers with the next tile's pixels as soon as its
+// MFMAs are issued, so a whole tile of loads is in flight behind the current
+// tile's MFMAs and epilogue.  Same MFMA order and the same epilogue
+// (m32_epilogue_tm1) as conv1x1_m32_kernel<1, TN>: bit-identical outputs and
+// statistics / BatchNorm-backward rows.
+template <int TN, int KS, bool ST, bool BB, int EPI>
+__global__ __launch_bounds__(256) void conv1x1_m32s_kernel(const ConvArgs p, int nblk_n,
+                                                            float* __restrict__ part,
+                                                            const BnEpi bb) {
+  constexpr int NW4 = KS * kG * TN * 64;  // float4 of the resident weights
+  extern __shared__ __attribute__((aligned(16))) float4 m32s_lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = lane >> 5, j = lane & 31;
+  // XCD-paired N blocks: workgroups bid, bid + 8, ... (one XCD) take the
+  // nblk_n N blocks of the same pixel tiles (gridDim = gm * nblk_n, gm a
+  // multiple of 8), so a tile's pixels are read through one L2 and its
+  // output rows are written from one XCD
+  const int xcd = blockIdx.x & 7, rr = blockIdx.x >> 3;
+  const int nb = rr % nblk_n, wgm = (rr / nblk_n) * 8 + xcd;
+  const int gm = gridDim.x / nblk_n;
+  {
+    const float4* wg = reinterpret_cast<const float4*>(p.w);
+    for (int f = threadIdx.x; f < NW4; f += 256) {
+      const int k8 = f / (TN * 64), rem = f - k8 * (TN * 64);
+      m32s_lds[f] = wg[((int64_t)k8 * p.Ntiles + nb * TN + (rem >> 6)) * 64 + (rem & 63)];
+    }
+  }
+  __syncthreads();
+  float* ep = reinterpret_cast<float*>(m32s_lds + NW4) + wave * 32 * kEpiPitch;
+  const int64_t ntiles = (p.M + 31) >> 5;
+  const int64_t step = (int64_t)gm * 4;
+  const float* xb = p.x + p.x_c0 + 4 * h;
+  auto load = [&](int64_t T, int s, int q) {
+    const int64_t m = T * 32 + j;
+    return m < p.M ? *reinterpret_cast<const float4*>(xb + m * p.x_ps + s * kBK + 8 * q)
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  float4 a[KS][kG];
+  int64_t T = (int64_t)wgm * 4 + wave;
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int q = 0; q < kG; ++q) a[s][q] = load(T, s, q);
+  for (; T < ntiles; T += step) {
+    const int64_t Tn = T + step;
+    f32x16 acc[TN];
+#pragma unroll
+    for (int u = 0; u < TN; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int q = 0; q < kG; ++q) {
+        float4 bw[TN];
+#pragma unroll
+        for (int u = 0; u < TN; ++u) bw[u] = m32s_lds[((s * kG + q) * TN + u) * 64 + lane];
+#pragma unroll
+        for (int u = 0; u < TN; ++u)
+          acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(bw[u].x, a[s][q].x, acc[u], 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < TN; ++u)
+          acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(bw[u].y, a[s][q].y, acc[u], 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < TN; ++u)
+          acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(bw[u].z, a[s][q].z, acc[u], 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < TN; ++u)
+          acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(bw[u].w, a[s][q].w, acc[u], 0, 0, 0);
+        a[s][q] = load(Tn, s, q);  // the next tile's pixels, in flight from here
+      }
+    const int64_t m = T * 32 + j;
+    const int pm = m < p.M ? (int)m : -1;
+    m32_epilogue_tm1<TN, ST, BB, EPI>(p, acc, pm, pm, nb, (int)T, ep, part, bb, lane);
+  }
+}
+
 // K split of a forward launch (k x k, or 1x1 with its K-concatenated second
 // source) whose grid (`grid` workgroups) cannot fill the device — R50 layer3/4
 // at bs1: enough splits for ~512 workgroups, each keeping >= 4 stages of 32
@@ -598,9 +711,92 @@ static int launch_m32_as(const ConvArgs& a, hipStream_t st) {
     m32_ksplit_reduce<<<(unsigned)cdiv(n4, 256), 256, 0, st>>>(a, ks, part);
     return check_launch("m32_ksplit_reduce");
   }
+  if constexpr (TM == 1 && !AS) {  // the epilogue terms specialised (m32_epilogue_tm1)
+    if (!a.bias && a.act == ACT_NONE) {
+      if (a.res)
+        conv1x1_m32_kernel<1, TN, KXK, false, false, false, kEpiRes>
+            <<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, per_img, -1, 1, nullptr, BnEpi{});
+      else
+        conv1x1_m32_kernel<1, TN, KXK, false, false, false, kEpiNone>
+            <<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, per_img, -1, 1, nullptr, BnEpi{});
+      return check_launch("conv1x1_m32");
+    }
+  }
   conv1x1_m32_kernel<TM, TN, KXK, AS><<<(unsigned)grid, 256, 0, st>>>(a, (int)mt_img, per_img, -1,
                                                                      1, nullptr, BnEpi{});
   return check_launch("conv1x1_m32");
+}
+
+// conv1x1_m32s_kernel launch: a persistent grid of (CUs x resident
+// workgroups) rounded to whole N blocks.  JABD_M32S=0 keeps every layer on
+// conv1x1_m32_kernel (A/B).
+static bool m32s_on() {
+  static const bool on = [] {
+    const char* e = getenv("JABD_M32S");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+template <int TN, int KS, bool ST, bool BB, int EPI>
+static int launch_m32s(const ConvArgs& a, float* part, const BnEpi& bb, hipStream_t st) {
+  auto kern = conv1x1_m32s_kernel<TN, KS, ST, BB, EPI>;
+  const size_t lds = (size_t)KS * kG * TN * 64 * 16 + (size_t)4 * 32 * kEpiPitch * 4;
+  static int slots = 0;  // CUs x resident workgroups of this instance
+  if (slots <= 0) {
+    int dev = 0, ncu = 0, occ = 0;
+    JABD_HIP(hipGetDevice(&dev));
+    JABD_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    JABD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, lds));
+    JABD_REQUIRE(occ >= 1, "conv32 stream: no resident workgroup (%zu B LDS)", lds);
+    slots = ncu * occ;
+  }
+  const int nblk_n = a.Ntiles / TN;
+  const int64_t ntiles = cdiv(a.M, (int64_t)32);
+  int64_t gm = std::min<int64_t>(cdiv(ntiles, 4), slots / nblk_n);
+  gm = std::max<int64_t>(8, gm / 8 * 8);  // whole XCD rounds (see the kernel)
+  kern<<<(unsigned)(gm * nblk_n), 256, lds, st>>>(a, nblk_n, part, bb);
+  return check_launch("conv1x1_m32s");
+}
+
+// The streaming form for a 1x1 / stride-1 layer with K = 64 or 128 (a: the
+// w32 view, Ntiles = ntiles32); form 0 plain, 1 statistics (ST), 2
+// BatchNorm-backward sums (BB).  -1: not served.
+static int m32s_dispatch(const ConvArgs& a, int tn32, float* part, const BnEpi& bb, int form,
+                         hipStream_t st) {
+  if (!m32s_on() || a.KH != 1 || a.KW != 1 || a.stride != 1 || a.pad != 0 || a.tconv ||
+      a.nchw_in || a.x2 || a.ascale || a.y2 || a.Cin % kBK || a.M >= ((int64_t)1 << 31) - 64)
+    return -1;
+  const int KS = a.Cin / kBK;
+  if (KS != 2 && KS != 4) return -1;
+  int TN = tn32;
+  while (KS * TN > 8 && TN % 2 == 0) TN /= 2;  // resident weights <= 32 KiB
+  if (TN < 1 || KS * TN > 8 || a.Ntiles % TN) return -1;
+  // the plain form's epilogue terms, specialised when the layer has none or
+  // only a residual (the R50 data gradients)
+  const bool plain_none = !a.bias && !a.res && a.act == ACT_NONE;
+  const bool plain_res = !a.bias && a.res && a.act == ACT_NONE;
+#define M32S(TN_, KS_)                                                                 \
+  return form == 1   ? launch_m32s<TN_, KS_, true, false, kEpiNone>(a, part, bb, st)   \
+         : form == 2 ? launch_m32s<TN_, KS_, false, true, kEpiNone>(a, part, bb, st)   \
+         : plain_none ? launch_m32s<TN_, KS_, false, false, kEpiNone>(a, part, bb, st) \
+         : plain_res  ? launch_m32s<TN_, KS_, false, false, kEpiRes>(a, part, bb, st)  \
+                      : launch_m32s<TN_, KS_, false, false, kEpiRt>(a, part, bb, st);
+  if (KS == 2) {
+    switch (TN) {
+      case 1: M32S(1, 2)
+      case 2: M32S(2, 2)
+      case 3: M32S(3, 2)
+      case 4: M32S(4, 2)
+      default: return -1;
+    }
+  }
+  switch (TN) {
+    case 1: M32S(1, 4)
+    case 2: M32S(2, 4)
+    default: return -1;
+  }
+#undef M32S
 }
 
 // Forward conv on the 32x32 kernel with the BatchNorm statistics rows (ST):
@@ -625,6 +821,10 @@ int conv_m32_stats_dispatch(const ConvArgs& a0, bool kxk, float* part, const BnE
   ConvArgs a = a0;
   a.w = a0.w32;
   a.Ntiles = a0.ntiles32;
+  if (!kxk) {
+    const int r = m32s_dispatch(a, a0.tn32, part, bb, bb.rows ? 2 : 1, st);
+    if (r >= 0) return r;
+  }
 #define MS(TN_) return kxk ? launch_m32_stats<TN_, true>(a, part, bb, st) : launch_m32_stats<TN_, false>(a, part, bb, st);
   switch (a0.tn32) {
     case 1: MS(1)
@@ -715,6 +915,10 @@ int conv1x1_m32_dispatch(const ConvArgs& a0, hipStream_t st, bool kxk) {
   ConvArgs a = a0;
   a.w = a0.w32;
   a.Ntiles = a0.ntiles32;
+  if (!kxk) {  // K 64 / 128: the streaming form (no K split at <= 4 stages)
+    const int r = m32s_dispatch(a, a0.tn32, nullptr, BnEpi{}, 0, st);
+    if (r >= 0) return r;
+  }
 #define M32(TM_, TN_) \
   return kxk ? launch_m32<TM_, TN_, true>(a, st) : launch_m32<TM_, TN_, false>(a, st);
   if (m32_tn_launch(a0) == 1 && a0.tn32 > 1) M32(1, 1)

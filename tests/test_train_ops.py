@@ -571,6 +571,70 @@ def test_conv_bn_stats32(cuda, cin, cout, k, stride, bhw, scale):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,bhw", [
+    (64, 256, (2, 40, 36)), (64, 64, (3, 17, 19)), (128, 512, (2, 21, 18)), (64, 96, (1, 9, 7)),
+    (128, 128, (2, 33, 31)), (64, 32, (1, 5, 3)), (128, 256, (1, 1, 1))])
+def test_conv1x1_stream32_forms(cuda, cin, cout, bhw):
+    """The streaming 1x1 GEMM (conv32.hip conv1x1_m32s_kernel: K = 64 / 128,
+    weights resident in LDS, persistent waves over 32-pixel tiles) in each of
+    its epilogue forms against float64 torch: plain (no terms), bias + ReLU
+    (run-time epilogue), a data gradient with the residual, the BatchNorm
+    statistics form and the BatchNorm-backward sums form; ragged last tiles,
+    one pixel, and N not a multiple of 128 (TN 1-3)."""
+    from jabd_amd import train as T
+    B, H, W = bhw
+    g = torch.Generator().manual_seed(cin * 7 + cout)
+    x = (torch.randn(B, H, W, cin, generator=g) + 1.0) * 3.0
+    w = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    b = torch.randn(cout, generator=g)
+    r = torch.randn(B, H, W, cout, generator=g)
+    dev = torch.device(cuda)
+    xg, wg, bg, rg = x.to(dev), w.to(dev), b.to(dev), r.to(dev)
+    ref = x.double().reshape(-1, cin) @ w.double().reshape(cout, cin).t()
+    ref = ref.reshape(B, H, W, cout)
+    y0 = T._conv_fwd(xg, wg, None, 1, 0)
+    pk = T._packed(wg, transposed=False)
+    a = T._conv_args(xg, pk, torch.empty(B, H, W, cout, device=dev), 1, 0)
+    a.bias, a.act = bg.data_ptr(), T.ACT["relu"]   # bias + ReLU: the run-time epilogue
+    yb = torch.empty(B, H, W, cout, device=dev)
+    a.y = yb.data_ptr()
+    T.call("jabd_conv2d_nhwc_f32", T.ctypes.byref(a), T._st())
+    bn = torch.nn.BatchNorm2d(cout).to(dev)
+    ys, st = T._conv_fwd_stats(xg, wg, bn, 1, 0)
+    # data gradient cout <- cin with the residual (the R50 conv1 data gradient's form)
+    wt = w.reshape(cout, cin).t().contiguous().reshape(cin, cout, 1, 1).to(dev)
+    dy = torch.randn(B, H, W, cin, generator=g)
+    dres = T._dgrad_1x1_res(dy.to(dev), wt, rg)
+    torch.cuda.synchronize()
+    tol = 1e-5
+    assert rel_err(y0.cpu().double(), ref) < tol
+    assert rel_err(yb.cpu().double(), (ref + b.double()).clamp_min(0)) < tol
+    assert rel_err(ys.cpu().double(), ref) < tol
+    assert st is not None
+    y64 = ys.cpu().double()   # the statistics of the output the kernel wrote
+    mu64, var64 = y64.mean((0, 1, 2)), y64.var((0, 1, 2), unbiased=False)
+    assert float(((st[0].cpu().double() - mu64).abs() / (mu64 ** 2 + var64).sqrt()).max()) < 1e-6
+    var = st[1].cpu().double() ** -2 - bn.eps
+    assert float(((var - var64).abs() / (var64 + bn.eps)).max()) < 1e-5
+    dref = (dy.double().reshape(-1, cin) @ w.double().reshape(cout, cin).t()).reshape(B, H, W, cout)
+    assert rel_err(dres.cpu().double(), dref + r.double()) < tol
+    # BatchNorm-backward sums form: the data gradient is the dy of a BN + ReLU over cout
+    xb = (torch.randn(B, H, W, cout, generator=g) + 0.5).to(dev)
+    xm = xb.reshape(-1, cout).double()
+    stb = ((1 + 0.3 * torch.randn(cout, generator=g)).to(dev),
+           (0.2 * torch.randn(cout, generator=g)).to(dev),
+           xm.mean(0).float(), (xm.var(0, unbiased=False) + 1e-5).rsqrt().float())
+    d1, part = T._dgrad_bn_sums(dy.to(dev), wt, 1, 0, H, W, xb, stb, "relu")
+    assert part is not None
+    r1 = T._bn_bwd_rows(d1, xb, stb, "relu", part)
+    r2 = T._bn_bwd(d1, xb, stb, "relu")
+    torch.cuda.synchronize()
+    assert rel_err(d1.cpu().double(), dref) < tol
+    for a1, a2, name in zip(r1[:3], r2[:3], ("dx", "dgamma", "dbeta")):
+        assert rel_err(a1.cpu(), a2.cpu()) < 1e-5, name
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cin,cout,k,stride,bhw,scale", [
     (64, 256, 1, 1, (2, 40, 36), 1.0), (128, 512, 1, 1, (3, 17, 19), 50.0),
     (64, 64, 3, 1, (2, 33, 31), 1.0), (128, 128, 3, 1, (1, 9, 7), 50.0),
