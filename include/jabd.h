@@ -427,6 +427,22 @@ int jabd_conv_bn_bwd_sums_f32(const jabd_conv_args* args, const float* x, int32_
                               const float* mean, const float* invstd, const float* gamma,
                               const float* beta, int32_t act, float slope, float* part,
                               int64_t part_floats, jabd_stream_t stream);
+/* The residual-ReLU form of the above (the R50 bottleneck's bn3 backward,
+ * out = relu(bn3(x) + identity), nets/resnet_pytorch_r.py:139-143; it
+ * replaces the bn3 part of jabd_bn_act_bwd_ex_f32 and its reduction pass):
+ * args is a bias-free, act-free 1x1 / stride-1 data gradient (the NEXT
+ * block's conv1 data gradient, whose output is this block's dout) with an
+ * optional residual args->res (that block's identity-branch gradient); the
+ * GEMM writes dz = (dgrad + res) * [mask > 0] — mask is the saved block
+ * output `out` (pixel stride mask_ps) — and the per-32-pixel-tile sums of
+ * dz and dz xhat (x: bn3's input, pixel stride x_ps) into part, sized by
+ * jabd_conv_bn_bwd_part_floats of the same args without the residual.
+ * jabd_bn_act_bwd_rows_f32(part, dz, x, ..., act = none) finishes bn3's
+ * backward; dz itself is the identity branch's gradient. */
+int jabd_conv_bn_bwd_sums_res_f32(const jabd_conv_args* args, const float* x, int32_t x_ps,
+                                  const float* mask, int32_t mask_ps, const float* mean,
+                                  const float* invstd, float* part, int64_t part_floats,
+                                  jabd_stream_t stream);
 int jabd_bn_act_bwd_rows_f32(float* part, const float* dy, const float* x, int64_t M,
                              int32_t C, const float* mean, const float* invstd,
                              const float* gamma, const float* beta, int32_t act, float slope,

@@ -997,6 +997,40 @@ extern "C" int jabd_conv_bn_bwd_sums_f32(const jabd_conv_args* args, const float
   return r < 0 ? JABD_EINVAL : r;
 }
 
+// The residual-ReLU form (R50 bn3): a bias-free 1x1 data gradient y = dx +
+// args->res whose output is the dy of out = relu(bn(x) + identity); the
+// GEMM writes dz = y * [out > 0] (out = mask, the block output saved by the
+// forward) and the per-32-pixel-tile sums of dz and dz * xhat into part, in
+// jabd_conv_bn_bwd_sums_f32's layout (jabd_bn_act_bwd_rows_f32 with act none
+// finishes the BatchNorm backward from them).
+extern "C" int jabd_conv_bn_bwd_sums_res_f32(const jabd_conv_args* args, const float* x,
+                                             int32_t x_ps, const float* mask, int32_t mask_ps,
+                                             const float* mean, const float* invstd, float* part,
+                                             int64_t part_floats, jabd_stream_t stream) {
+  ConvArgs a;
+  bool fast1x1 = false, vec4 = false, kxk = false;
+  {
+    const int e = conv_setup(args, a, fast1x1, vec4);
+    if (e != JABD_OK) return e;
+  }
+  ConvArgs ab = a;  // the form check without the residual
+  ab.res = nullptr;
+  JABD_REQUIRE(conv_m32_bb_form(ab, fast1x1, vec4, kxk) && !kxk,
+               "conv_bn_bwd_sums_res: layer not served (1x1 / stride-1 32x32 form only)");
+  JABD_REQUIRE(!a.res || (a.res_ps % 4 == 0 && a.res_c0 % 4 == 0),
+               "conv_bn_bwd_sums_res: residual rows must be float4-aligned");
+  JABD_REQUIRE(x && mask && mean && invstd && part && x_ps % 4 == 0 && x_ps >= a.Cout &&
+                   mask_ps % 4 == 0 && mask_ps >= a.Cout,
+               "conv_bn_bwd_sums_res: bad BatchNorm arguments");
+  const int64_t need = cdiv(a.M, (int64_t)32) * 2 * a.Cout + 2 * bn_rows_sum_doubles(a.M, a.Cout);
+  JABD_REQUIRE(part_floats >= need && ((uintptr_t)part & 15) == 0,
+               "conv_bn_bwd_sums_res: part holds %lld floats, %lld needed (16-byte aligned)",
+               (long long)part_floats, (long long)need);
+  BnEpi bb{x, mean, invstd, nullptr, nullptr, part, x_ps, ACT_NONE, 0.f, mask, mask_ps};
+  const int r = conv_m32_stats_dispatch(a, false, nullptr, bb, as_stream(stream));
+  return r < 0 ? JABD_EINVAL : r;
+}
+
 extern "C" int jabd_conv2d_nhwc_f32(const jabd_conv_args* args, jabd_stream_t stream) {
   ConvArgs a;
   bool fast1x1 = false, vec4 = false;

@@ -95,19 +95,28 @@ __device__ __forceinline__ void m32_epilogue_tm1(const ConvArgs& p, const f32x16
     const int n = nb0 + 4 * ep_q;
     float4 ss = make_float4(0.f, 0.f, 0.f, 0.f), sq = ss, sh = ss;
     float4 bmu = sh, bis = sh, bgm = sh, bbt = sh;
-    float4 bx[4];
+    float4 bx[4], bmk[4];
     if constexpr (BB) {  // issued before the LDS round trip: in flight across it
       if (n < p.Cout) {
         bmu = *reinterpret_cast<const float4*>(bb.mean + n);
         bis = *reinterpret_cast<const float4*>(bb.invstd + n);
-        bgm = *reinterpret_cast<const float4*>(bb.gamma + n);
-        bbt = *reinterpret_cast<const float4*>(bb.beta + n);
+        if (!bb.mask) {  // (the mask form takes no gamma / beta)
+          bgm = *reinterpret_cast<const float4*>(bb.gamma + n);
+          bbt = *reinterpret_cast<const float4*>(bb.beta + n);
+        }
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r)   // the BatchNorm input at the tile's pixels, in flight
         bx[r] = (prow[r] >= 0 && n < p.Cout)
                     ? *reinterpret_cast<const float4*>(bb.x + (int64_t)mrow[r] * bb.x_ps + n)
                     : sh;
+      if (bb.mask) {  // mask form: the act's saved output, in flight as well
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          bmk[r] = (prow[r] >= 0 && n < p.Cout)
+                       ? *reinterpret_cast<const float4*>(bb.mask + (int64_t)mrow[r] * bb.mask_ps + n)
+                       : sh;
+      }
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c)
@@ -121,6 +130,25 @@ __device__ __forceinline__ void m32_epilogue_tm1(const ConvArgs& p, const f32x16
       const int px = ep_px + 8 * r;
       if (prow[r] < 0 || n >= p.Cout) continue;
       float4 v = *reinterpret_cast<const float4*>(ep + px * kEpiPitch + 4 * ep_q);
+      if (BB && bb.mask) {
+        // dz = (y + res) * [mask > 0], written instead of y; as bn_bwd_part's
+        // sums of dz and dz * xhat
+        if (p.res) {
+          const float4 rr = *reinterpret_cast<const float4*>(p.res + (int64_t)mrow[r] * p.res_ps +
+                                                             p.res_c0 + n);
+          v.x += rr.x; v.y += rr.y; v.z += rr.z; v.w += rr.w;
+        }
+        v.x *= bmk[r].x > 0.f ? 1.f : 0.f;
+        v.y *= bmk[r].y > 0.f ? 1.f : 0.f;
+        v.z *= bmk[r].z > 0.f ? 1.f : 0.f;
+        v.w *= bmk[r].w > 0.f ? 1.f : 0.f;
+        const float xh0 = (bx[r].x - bmu.x) * bis.x, xh1 = (bx[r].y - bmu.y) * bis.y;
+        const float xh2 = (bx[r].z - bmu.z) * bis.z, xh3 = (bx[r].w - bmu.w) * bis.w;
+        ss.x += v.x; ss.y += v.y; ss.z += v.z; ss.w += v.w;
+        sq.x += v.x * xh0; sq.y += v.y * xh1; sq.z += v.z * xh2; sq.w += v.w * xh3;
+        *reinterpret_cast<float4*>(p.y + (int64_t)mrow[r] * p.y_ps + p.y_c0 + n) = v;
+        continue;
+      }
       if constexpr (BB) {
         // as bn_bwd_part / bn_bwd_apply (train.hip): xhat, act'(xhat gamma + beta)
         const float xv[4] = {bx[r].x, bx[r].y, bx[r].z, bx[r].w};

@@ -181,6 +181,8 @@ SIGNATURES = {
     "jabd_conv_bn_bwd_part_floats": [ctypes.POINTER(ConvArgs)],
     "jabd_conv_bn_bwd_sums_f32": [ctypes.POINTER(ConvArgs), c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
                                   c_i32, c_f32, c_vp, c_i64, c_vp],
+    "jabd_conv_bn_bwd_sums_res_f32": [ctypes.POINTER(ConvArgs), c_vp, c_i32, c_vp, c_i32, c_vp,
+                                      c_vp, c_vp, c_i64, c_vp],
     "jabd_bn_act_bwd_rows_f32": [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32,
                                  c_f32, c_vp, c_vp, c_vp, c_vp],
     "jabd_conv_bn_stats_f32": [ctypes.POINTER(ConvArgs), c_vp, c_i64, c_vp, c_vp, c_vp, c_vp,

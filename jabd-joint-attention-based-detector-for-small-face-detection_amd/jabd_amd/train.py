@@ -1091,6 +1091,31 @@ def _dgrad_1x1_res(dy, weight, res):
     return dx
 
 
+def _dgrad_1x1_res_bn3(dy, weight, res, out, x3, st3):
+    """_dgrad_1x1_res whose output is the dout of the previous bottleneck's
+    out = relu(bn3(x3) + identity): the GEMM writes dz = (dgrad + res) *
+    [out > 0] and bn3's backward sums (jabd_conv_bn_bwd_sums_res_f32).
+    Returns (dz, part), or (dx, None) — the plain data gradient — when the
+    form does not serve the conv."""
+    pk = _packed(weight, transposed=True)
+    B, H, W, _ = dy.shape
+    dx = torch.empty((B, H, W, pk.Cout), dtype=torch.float32, device=dy.device)
+    a = _conv_args(dy, pk, dx, 1, 0)
+    nf = int(lib().jabd_conv_bn_bwd_part_floats(ctypes.byref(a)))
+    if res is not None:
+        a.res, a.res_bs, a.res_ps, a.res_c0 = res.data_ptr(), res.stride(0), res.shape[3], 0
+    if nf <= 0 or not (out.is_contiguous() and x3.is_contiguous() and
+                       (res is None or res.is_contiguous())):
+        call("jabd_conv2d_nhwc_f32", ctypes.byref(a), _st())
+        return dx, None
+    _, _, mean, invstd = st3
+    part = torch.empty(nf, dtype=torch.float32, device=dy.device)
+    call("jabd_conv_bn_bwd_sums_res_f32", ctypes.byref(a), x3.data_ptr(), x3.shape[3],
+         out.data_ptr(), out.shape[3], mean.data_ptr(), invstd.data_ptr(), part.data_ptr(), nf,
+         _st())
+    return dx, part
+
+
 def _dw_fwd(x, weight, stride):
     C, _, k, _ = weight.shape
     wt = F.transpose(weight.detach().reshape(C, k * k))  # tap-major [k*k][C]
@@ -1413,7 +1438,9 @@ class R50BlockFn(torch.autograd.Function):
     parameters in _r50_params order."""
 
     @staticmethod
-    def forward(ctx, blk, x, *params):
+    def forward(ctx, blk, prev, info, x, *params):
+        """prev: the link record of the bottleneck whose output x is (None:
+        x came from elsewhere); info: this block's record, filled here."""
         stride = blk.stride
         B, H, W, _ = x.shape
         # each conv's GEMM epilogue also takes its BatchNorm's batch statistics
@@ -1434,6 +1461,11 @@ class R50BlockFn(torch.autograd.Function):
         out, st3 = _bn_fwd(t3p, blk.bn3, "relu", res=idn, stats=bs3)
         ctx.blk, ctx.st = blk, (st1, st2, st3)
         ctx.hw = (H, W)
+        ctx.prev, ctx.info = prev, info
+        if info is not None:
+            # what the next bottleneck's conv1 data gradient needs to hand this
+            # block dz and bn3's sums instead of dout (R50_BN3_LINK)
+            info.update(x3=t3p, st3=st3, rows=None, dz=None)
         ctx.save_for_backward(x, t1p, t1, t2p, t2, t3p, idn, *saved)
         return out
 
@@ -1445,7 +1477,17 @@ class R50BlockFn(torch.autograd.Function):
         x, t1p, t1, t2p, t2, t3p, idn, *sv = ctx.saved_tensors
         st1, st2, st3 = ctx.st
         dout = dout.contiguous()
-        dp3, dg3, db3, dres = _bn_bwd(dout, t3p, st3, "relu", res=idn, want_dres=True)
+        info = ctx.info
+        if info is not None and info["rows"] is not None and info["dz"] == dout.data_ptr():
+            # the next block's conv1 data gradient already wrote dz = dout *
+            # [out > 0] and bn3's sums: only the apply pass is left, and dz
+            # is the identity branch's gradient
+            dp3, dg3, db3, _ = _bn_bwd_rows(dout, t3p, st3, "none", info["rows"])
+            dres = dout
+        else:
+            dp3, dg3, db3, dres = _bn_bwd(dout, t3p, st3, "relu", res=idn, want_dres=True)
+        if info is not None:
+            info.clear()
         dW3 = _wgrad(t2, dp3, blk.conv3.weight, 1, 0)
         # the data-gradient GEMMs also take the next BatchNorm backward's sums
         dt2, pt2 = _dgrad_bn_sums(dp3, blk.conv3.weight, 1, 0, t2.shape[1], t2.shape[2], t2p,
@@ -1467,8 +1509,14 @@ class R50BlockFn(torch.autograd.Function):
             grads += (dWs, dgs, dbs)
         else:
             ds_skip = dres
-        dx = _dgrad_1x1_res(dp1, blk.conv1.weight, ds_skip)
-        return (None, dx) + grads
+        prev = ctx.prev
+        if prev is not None and prev.get("x3") is not None:
+            dx, rows = _dgrad_1x1_res_bn3(dp1, blk.conv1.weight, ds_skip, x, prev["x3"],
+                                          prev["st3"])
+            prev["rows"], prev["dz"] = rows, (dx.data_ptr() if rows is not None else None)
+        else:
+            dx = _dgrad_1x1_res(dp1, blk.conv1.weight, ds_skip)
+        return (None, None, None, dx) + grads
 
 
 def _r50_params(blk):
@@ -1491,11 +1539,25 @@ def _r50_fused_ok(blk, x):
 
 # JABD_R50_FUSED=0: the bottleneck as per-op autograd nodes (A/B)
 R50_FUSED = __import__("os").environ.get("JABD_R50_FUSED", "1") != "0"
+# JABD_R50_BN3_LINK=0: every bottleneck takes its bn3 backward from dout
+# (jabd_bn_act_bwd_ex_f32's two passes) instead of from the dz + sums the
+# next bottleneck's conv1 data gradient writes (A/B)
+R50_BN3_LINK = __import__("os").environ.get("JABD_R50_BN3_LINK", "1") != "0"
 
 
 def _r50_block(blk, x):
     if _r50_fused_ok(blk, x):
-        return R50BlockFn.apply(blk, x.contiguous(), *_r50_params(blk))
+        x = x.contiguous()
+        # link to the producing bottleneck when x IS its output object (its
+        # only consumer is this block: the _train_forward chain; a fork or
+        # any other use gives a different object)
+        rec = getattr(x, "_jabd_r50_link", None) if R50_BN3_LINK else None
+        prev = rec[1] if rec is not None and rec[0]() is x else None
+        info = {} if R50_BN3_LINK else None
+        out = R50BlockFn.apply(blk, prev, info, x, *_r50_params(blk))
+        if info is not None:
+            out._jabd_r50_link = (weakref.ref(out), info)
+        return out
     t = bn_act(conv(x, blk.conv1), blk.bn1, "relu")
     t = bn_act(conv(t, blk.conv2, blk.stride, 1), blk.bn2, "relu")
     t = conv(t, blk.conv3)

@@ -134,8 +134,16 @@ class Kinks:
         self.rec.append((_FAMILY[kind], cands))
 
     def __call__(self, kind, *a):
+        # the recording device only for this call (a module default left at
+        # "cuda" would move later tests' _bn_z results off the CPU)
         global _DEV
-        _DEV = self.device
+        prev, _DEV = _DEV, self.device
+        try:
+            return self._call(kind, *a)
+        finally:
+            _DEV = prev
+
+    def _call(self, kind, *a):
         if kind == "stats":
             return
         if kind == "bn":

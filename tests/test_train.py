@@ -220,6 +220,55 @@ def test_train_r50_blocks_parity(cuda):
 
 
 @pytest.mark.gpu
+def test_train_r50_bn3_link(cuda, monkeypatch):
+    """bn3's backward taken from the next bottleneck's conv1 data gradient
+    (jabd_conv_bn_bwd_sums_res_f32 writes dz = dout * [out > 0] and the
+    BatchNorm sums; JABD_R50_BN3_LINK) against the unlinked form
+    (jabd_bn_act_bwd_ex_f32 on dout) over layer1.0 (downsample) -> layer1.1
+    -> layer1.2 -> layer2.0 (stride-2 downsample): the three links are
+    taken, and every gradient and the input gradient agree to fp32
+    reassociation."""
+    from jabd_amd import train as T
+    from nets.retinaface_eca_nonlocal import RetinaFace
+    from utils.config import cfg_re50
+    m = init_for_parity(RetinaFace(cfg=cfg_re50, mode="train"), seed=5)
+    body = m.to(cuda).train().body
+    blocks = (body.layer1[0], body.layer1[1], body.layer1[2], body.layer2[0])
+    x0 = torch.randn(2, 37, 29, 64, generator=torch.Generator().manual_seed(4)).to(cuda)
+    w = None
+    calls = []
+    real = T._dgrad_1x1_res_bn3
+
+    def spy(*a):
+        r = real(*a)
+        calls.append(r[1] is not None)
+        return r
+    monkeypatch.setattr(T, "_dgrad_1x1_res_bn3", spy)
+    res = {}
+    for link in (True, False):
+        monkeypatch.setattr(T, "R50_BN3_LINK", link)
+        body.zero_grad()
+        x = x0.clone().requires_grad_(True)
+        with T._BatchCounts():
+            s = x
+            for blk in blocks:
+                s = T._r50_block(blk, s)
+        if w is None:
+            w = torch.randn(s.shape, generator=torch.Generator().manual_seed(6)).to(cuda)
+        (s * w).sum().backward()
+        torch.cuda.synchronize()
+        res[link] = (s.detach().clone(), x.grad.clone(),
+                     {k: p.grad.clone() for k, p in body.named_parameters() if p.grad is not None})
+    assert calls == [True, True, True], calls
+    assert torch.equal(res[True][0], res[False][0])
+    assert rel_err(res[True][1], res[False][1]) < 1e-5
+    g1, g0 = res[True][2], res[False][2]
+    assert len(g1) == len(g0) > 30
+    bad = [(rel_err(g1[k], g0[k]), k) for k in g0 if rel_err(g1[k], g0[k]) > 1e-5]
+    assert not bad, sorted(bad)[-5:]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["mnv3", "r50"])
 def test_train_head_parity(cuda, kind):
     """ECA -> FPN(+NLM) -> SSH -> heads sub-graph alone (backbone features as
