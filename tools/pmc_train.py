@@ -34,8 +34,8 @@ FAMILIES = {
     # the GEMM kernels serve the plain conv call and its statistics / BatchNorm-backward forms
     "conv2d_nhwc (jabd_conv2d_nhwc_f32 + _bn_stats + _bn_bwd_sums)":
         (["jabd_conv2d_nhwc_f32", "jabd_conv1x1_bn_stats_f32", "jabd_conv_bn_stats_f32",
-          "jabd_conv_bn_bwd_sums_f32"],
-         ["conv1x1_m32_kernel", "conv1x1_kernel", "conv1x1_stream_kernel", "conv3x3_tile_kernel",
+          "jabd_conv_bn_bwd_sums_f32", "jabd_conv_bn_bwd_sums_res_f32"],
+         ["conv1x1_m32_kernel", "conv1x1_m32s_kernel", "conv1x1_kernel", "conv1x1_stream_kernel", "conv3x3_tile_kernel",
           "conv_gemm_kernel", "stem7_fwd_kernel", "m32_ksplit_reduce", "bn_rows_chunk_kernel"]),
     "nlm_bwd_attn (jabd_nlm_bwd_attn_f32)": (["jabd_nlm_bwd_attn_f32"], ["nlm_bwd_attn"]),
     "bn_act_fwd (jabd_bn_act_fwd_f32 + _sum)": (["jabd_bn_act_fwd_f32", "jabd_bn_act_fwd_sum_f32"],

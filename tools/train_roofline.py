@@ -75,7 +75,7 @@ def _ptr_args(name, args, sigs):
                         out.append(v)
             continue
         if (name, i) in (("jabd_conv_bn_stats_f32", 1), ("jabd_conv_bn_bwd_sums_f32", 9),
-                         ("jabd_bn_act_bwd_rows_f32", 0)):   # the epilogue rows: workspace
+                         ("jabd_conv_bn_bwd_sums_res_f32", 7), ("jabd_bn_act_bwd_rows_f32", 0)):   # the epilogue rows: workspace
             continue
         if t is ctypes.c_void_p:
             nxt = types[i + 1] if i + 1 < len(types) else None
@@ -92,7 +92,8 @@ _INT_TYPES = (ctypes.c_int32, ctypes.c_int, ctypes.c_int64)
 
 def _flops(name, args, sigs=None):
     if name in ("jabd_conv2d_nhwc_f32", "jabd_conv_wgrad_f32", "jabd_conv1x1_bn_stats_f32",
-                "jabd_conv_wgrad_eca_f32", "jabd_conv_bn_stats_f32", "jabd_conv_bn_bwd_sums_f32"):
+                "jabd_conv_wgrad_eca_f32", "jabd_conv_bn_stats_f32", "jabd_conv_bn_bwd_sums_f32",
+                "jabd_conv_bn_bwd_sums_res_f32"):
         a = args[0]._obj if hasattr(args[0], "_obj") else None
         if a is None:
             return 0.0
