@@ -797,6 +797,17 @@ static int m32s_dispatch(const ConvArgs& a, int tn32, float* part, const BnEpi& 
     return -1;
   const int KS = a.Cin / kBK;
   if (KS != 2 && KS != 4) return -1;
+  // K = 128: the plain form only by default (JABD_M32S_KS4 = mask of forms: bit 0 plain, 1
+  // statistics, 2 BatchNorm-backward).  There TN = 2 (32 KiB of resident weights) re-reads the
+  // pixels N / 64 times; the statistics form measured 463 (tile kernel) vs 479 us (l2.c3 at
+  // bs16) and the C3 step 517.0-517.6 (plain only) vs 517.9-518.7 ms (all forms), r06/ab/ks4
+  {
+    static const int ks4 = [] {
+      const char* e = getenv("JABD_M32S_KS4");
+      return e ? atoi(e) : 1;
+    }();
+    if (KS == 4 && !((ks4 >> form) & 1)) return -1;
+  }
   int TN = tn32;
   while (KS * TN > 8 && TN % 2 == 0) TN /= 2;  // resident weights <= 32 KiB
   if (TN < 1 || KS * TN > 8 || a.Ntiles % TN) return -1;
