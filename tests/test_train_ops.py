@@ -576,8 +576,9 @@ def test_conv_bn_stats32(cuda, cin, cout, k, stride, bhw, scale):
     (128, 128, (2, 33, 31)), (64, 32, (1, 5, 3)), (128, 256, (1, 1, 1))])
 def test_conv1x1_stream32_forms(cuda, cin, cout, bhw):
     """The streaming 1x1 GEMM (conv32.hip conv1x1_m32s_kernel: K = 64 / 128,
-    weights resident in LDS, persistent waves over 32-pixel tiles) in each of
-    its epilogue forms against float64 torch: plain (no terms), bias + ReLU
+    weights resident in LDS, persistent waves over 32-pixel tiles; at K = 128
+    only the plain form, the others on the tile kernel) in each of its
+    epilogue forms against float64 torch: plain (no terms), bias + ReLU
     (run-time epilogue), a data gradient with the residual, the BatchNorm
     statistics form and the BatchNorm-backward sums form; ragged last tiles,
     one pixel, and N not a multiple of 128 (TN 1-3)."""
