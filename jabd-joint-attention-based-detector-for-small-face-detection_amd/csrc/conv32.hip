@@ -806,7 +806,11 @@ static int m32s_dispatch(const ConvArgs& a, int tn32, float* part, const BnEpi& 
       const char* e = getenv("JABD_M32S_KS4");
       return e ? atoi(e) : 1;
     }();
-    if (KS == 4 && !((ks4 >> form) & 1)) return -1;
+    static const int ks2 = [] {  // the same mask for K = 64 (all forms by default)
+      const char* e = getenv("JABD_M32S_KS2");
+      return e ? atoi(e) : 7;
+    }();
+    if (!(((KS == 4 ? ks4 : ks2) >> form) & 1)) return -1;
   }
   int TN = tn32;
   while (KS * TN > 8 && TN % 2 == 0) TN /= 2;  // resident weights <= 32 KiB
