@@ -678,15 +678,17 @@ def test_dgrad_bn_bwd_sums(cuda, cin, cout, k, stride, bhw, scale):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n_in,n", [(1, 4096), (2, 1000), (3, 123457 * 4), (4, 64), (5, 4000),
-                                    (2, 4001)])
-def test_sum_multi_bit_exact(cuda, n_in, n):
+@pytest.mark.parametrize("n_in,n,off", [(1, 4096, 0), (2, 1000, 0), (3, 123457 * 4, 0), (4, 64, 0),
+                                        (5, 4000, 0), (2, 4001, 0), (3, 4096, 1)])
+def test_sum_multi_bit_exact(cuda, n_in, n, off):
     """jabd_sum_multi_f32 (the gradient of a tensor consumed n_in times) adds
-    the inputs in order — bit-identical to ((a + b) + c) + ... in torch."""
+    the inputs in order — bit-identical to ((a + b) + c) + ... in torch, on
+    the 16-byte-lane path (aligned, n % 4 == 0) and the scalar one (n % 4 or
+    an input off 16-byte alignment)."""
     import ctypes
     from jabd_amd._lib import call
     g = torch.Generator().manual_seed(n_in * 7 + n)
-    xs = [torch.randn(n, generator=g).to(cuda) for _ in range(n_in)]
+    xs = [torch.randn(n + off, generator=g).to(cuda)[off:] for _ in range(n_in)]
     out = torch.empty(n, device=cuda)
     ptrs = (ctypes.c_void_p * n_in)(*[x.data_ptr() for x in xs])
     call("jabd_sum_multi_f32", n_in, ptrs, n, out.data_ptr(),
