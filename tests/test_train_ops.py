@@ -682,9 +682,8 @@ def test_dgrad_bn_bwd_sums(cuda, cin, cout, k, stride, bhw, scale):
                                         (5, 4000, 0), (2, 4001, 0), (3, 4096, 1)])
 def test_sum_multi_bit_exact(cuda, n_in, n, off):
     """jabd_sum_multi_f32 (the gradient of a tensor consumed n_in times) adds
-    the inputs in order — bit-identical to ((a + b) + c) + ... in torch, on
-    the 16-byte-lane path (aligned, n % 4 == 0) and the scalar one (n % 4 or
-    an input off 16-byte alignment)."""
+    the inputs in order — bit-identical to ((a + b) + c) + ... in torch,
+    incl. inputs off 16-byte alignment."""
     import ctypes
     from jabd_amd._lib import call
     g = torch.Generator().manual_seed(n_in * 7 + n)
